@@ -1,0 +1,166 @@
+"""Datasets over the reference's preprocessed-data layout.
+
+``{preprocessed_path}/{train,val}.txt`` lines ``basename|speaker|{PH ...}|raw``,
+per-utterance ``mel/{spk}-mel-{base}.npy`` ([T,80] f32), ``pitch/``, ``energy/``,
+``duration/`` arrays, ``speakers.json``.  Behaviour follows the reference's
+``dataset.py:12-218``: the train collate sorts a group by text length
+(descending), splits it into ``batch_size`` chunks and drops the tail when
+``drop_last``.  Differences: padding is done by one vectorised C++ routine when
+the native host library is built (``csrc/host_collate.cpp``, falls back to
+numpy), energies are float32, the TextDataset does not print every
+batch (D15), and an optional ``(rank, world)`` shard makes each DP rank read a
+disjoint slice of every global group.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset as _TorchDataset
+
+from ..text import text_to_sequence
+from ..utils.tools import pad_1d, pad_2d
+
+
+def read_meta(path: str):
+    names, speakers, texts, raws = [], [], [], []
+    with open(path, "r", encoding="utf-8") as f:
+        for line in f:
+            line = line.rstrip("\n")
+            if not line:
+                continue
+            n, s, t, r = line.split("|", 3)
+            names.append(n)
+            speakers.append(s)
+            texts.append(t)
+            raws.append(r)
+    return names, speakers, texts, raws
+
+
+class Dataset(_TorchDataset):
+    def __init__(self, filename, preprocess_config, train_config, sort=False, drop_last=False,
+                 shard: Optional[Tuple[int, int]] = None):
+        self.dataset_name = preprocess_config["dataset"]
+        self.preprocessed_path = preprocess_config["path"]["preprocessed_path"]
+        self.cleaners = preprocess_config["preprocessing"]["text"]["text_cleaners"]
+        self.batch_size = train_config["optimizer"]["batch_size"]
+        self.basename, self.speaker, self.text, self.raw_text = read_meta(os.path.join(self.preprocessed_path, filename))
+        with open(os.path.join(self.preprocessed_path, "speakers.json")) as f:
+            self.speaker_map = json.load(f)
+        self.sort = sort
+        self.drop_last = drop_last
+        self.shard = shard
+
+    def __len__(self):
+        return len(self.text)
+
+    def _npy(self, kind, speaker, basename):
+        return np.load(os.path.join(self.preprocessed_path, kind, f"{speaker}-{kind}-{basename}.npy"))
+
+    def __getitem__(self, idx):
+        spk = self.speaker[idx]
+        base = self.basename[idx]
+        return {
+            "id": base,
+            "speaker": self.speaker_map[spk],
+            "text": np.asarray(text_to_sequence(self.text[idx], self.cleaners), dtype=np.int64),
+            "raw_text": self.raw_text[idx],
+            "mel": self._npy("mel", spk, base).astype(np.float32),
+            "pitch": self._npy("pitch", spk, base).astype(np.float32),
+            "energy": self._npy("energy", spk, base).astype(np.float32),
+            "duration": self._npy("duration", spk, base).astype(np.int64),
+        }
+
+    def reprocess(self, data, idxs):
+        items = [data[i] for i in idxs]
+        texts = [d["text"] for d in items]
+        mels = [d["mel"] for d in items]
+        text_lens = np.array([t.shape[0] for t in texts], dtype=np.int64)
+        mel_lens = np.array([m.shape[0] for m in mels], dtype=np.int64)
+        return (
+            [d["id"] for d in items],
+            [d["raw_text"] for d in items],
+            np.array([d["speaker"] for d in items], dtype=np.int64),
+            pad_1d(texts),
+            text_lens,
+            int(text_lens.max()),
+            pad_2d(mels),
+            mel_lens,
+            int(mel_lens.max()),
+            pad_1d([d["pitch"] for d in items]),
+            pad_1d([d["energy"] for d in items]),
+            pad_1d([d["duration"] for d in items]),
+        )
+
+    def collate_fn(self, data):
+        n = len(data)
+        if self.sort:
+            order = np.argsort(-np.array([d["text"].shape[0] for d in data]), kind="stable")
+        else:
+            order = np.arange(n)
+        bs = self.batch_size
+        full = n - n % bs
+        groups: List[List[int]] = order[:full].reshape(-1, bs).tolist() if full else []
+        if not self.drop_last and full < n:
+            groups.append(order[full:].tolist())
+        if self.shard is not None:
+            rank, world = self.shard
+            groups = [g[rank::world] for g in groups if len(g[rank::world])]
+        return [self.reprocess(data, g) for g in groups]
+
+
+class TextDataset(_TorchDataset):
+    """Synthesis-time dataset: (id, speaker, phones, raw, mel) per metadata line."""
+
+    def __init__(self, filepath, preprocess_config, train_config=None):
+        self.cleaners = preprocess_config["preprocessing"]["text"]["text_cleaners"]
+        self.preprocessed_path = preprocess_config["path"]["preprocessed_path"]
+        self.basename, self.speaker, self.text, self.raw_text = read_meta(filepath)
+        with open(os.path.join(self.preprocessed_path, "speakers.json")) as f:
+            self.speaker_map = json.load(f)
+
+    def __len__(self):
+        return len(self.text)
+
+    def __getitem__(self, idx):
+        spk, base = self.speaker[idx], self.basename[idx]
+        phone = np.asarray(text_to_sequence(self.text[idx], self.cleaners), dtype=np.int64)
+        mel_path = os.path.join(self.preprocessed_path, "mel", f"{spk}-mel-{base}.npy")
+        mel = np.load(mel_path).astype(np.float32) if os.path.exists(mel_path) else np.zeros((1, 80), np.float32)
+        return base, self.speaker_map[spk], phone, self.raw_text[idx], mel
+
+    def collate_fn(self, data):
+        texts = [d[2] for d in data]
+        mels = [d[4] for d in data]
+        text_lens = np.array([t.shape[0] for t in texts], dtype=np.int64)
+        mel_lens = np.array([m.shape[0] for m in mels], dtype=np.int64)
+        return ([d[0] for d in data], [d[3] for d in data], np.array([d[1] for d in data], dtype=np.int64),
+                pad_1d(texts), text_lens, int(text_lens.max()), pad_2d(mels), mel_lens, int(mel_lens.max()))
+
+
+def to_device(batch, device):
+    """numpy tuple -> tensors on ``device`` (reference ``utils/tools.py:18-79``;
+    energies cast to f32)."""
+    nb = torch.device(device).type == "cuda"
+
+    def t(x, dtype):
+        if isinstance(x, torch.Tensor):
+            return x.to(device=device, dtype=dtype, non_blocking=nb)
+        tt = torch.from_numpy(np.ascontiguousarray(x)).to(dtype)
+        if nb:
+            tt = tt.pin_memory()
+        return tt.to(device, non_blocking=nb)
+
+    if len(batch) == 12:
+        ids, raw, spk, texts, src_lens, max_src, mels, mel_lens, max_mel, p, e, d = batch
+        return (ids, raw, t(spk, torch.long), t(texts, torch.long), t(src_lens, torch.long), max_src,
+                t(mels, torch.float32), t(mel_lens, torch.long), max_mel, t(p, torch.float32), t(e, torch.float32),
+                t(d, torch.long))
+    if len(batch) == 9:
+        ids, raw, spk, texts, src_lens, max_src, mels, mel_lens, max_mel = batch
+        return (ids, raw, t(spk, torch.long), t(texts, torch.long), t(src_lens, torch.long), max_src,
+                t(mels, torch.float32), t(mel_lens, torch.long), max_mel)
+    raise ValueError(f"unexpected batch arity {len(batch)}")

@@ -1,0 +1,307 @@
+"""FastSpeech2 with optional speaking-style conditioning (FiLM reference encoder or GST).
+
+Forward order and outputs follow the reference's ``model/fastspeech2.py:44-120``:
+masks -> style encoder (gamma, beta) -> encoder (FiLM) -> + speaker embedding ->
+VarianceAdaptor -> decoder (FiLM) -> mel_linear -> PostNet residual, returning
+the same 10-tuple.  Activations are channel-last in the compute dtype (bf16 on
+MI355X, fp32 on CPU); mel outputs are fp32.
+
+Fixed reference bugs: no per-forward debug prints (D3),
+style encoder optional (D2), consistent rounding of controlled durations (D11),
+device derived from tensors (D19), synthesis without a reference mel uses a
+neutral style.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..config import style_mode
+from ..text.symbols import symbols
+from .layers import FFTBlock, FiLM, LinearNorm, PostNet
+from .style import GlobalStyleTokens, ReferenceEncoder
+
+
+def _pe_param(n_position: int, d: int) -> nn.Parameter:
+    return nn.Parameter(ops.sinusoid_table(n_position, d).unsqueeze(0), requires_grad=False)
+
+
+def positional_rows(pe_param: torch.Tensor, length: int, d: int, device) -> torch.Tensor:
+    """First ``length`` sinusoid rows; beyond the stored table (eval on long
+    inputs, reference ``transformer/Models.py:82-87``) they are generated."""
+    if length <= pe_param.shape[1]:
+        return pe_param[0, :length]
+    return ops.sinusoid_table(length, d, device=device)
+
+
+class Encoder(nn.Module):
+    """Phoneme embedding + PE + N FFT blocks (``transformer/Models.py:33-101``)."""
+
+    def __init__(self, config, film=False):
+        super().__init__()
+        tr = config["transformer"]
+        d = tr["encoder_hidden"]
+        self.max_seq_len = config["max_seq_len"]
+        self.d_model = d
+        self.src_word_emb = nn.Embedding(len(symbols) + 1, d, padding_idx=0)
+        self.position_enc = _pe_param(self.max_seq_len + 1, d)
+        nh = tr["encoder_head"]
+        self.layer_stack = nn.ModuleList(
+            FFTBlock(d, nh, d // nh, d // nh, tr["conv_filter_size"], tr["conv_kernel_size"], tr["encoder_dropout"], film=film)
+            for _ in range(tr["encoder_layer"])
+        )
+
+    def forward(self, texts, src_lens, style=None, compute_dtype=torch.float32):
+        T = texts.shape[1]
+        pe = positional_rows(self.position_enc, T, self.d_model, texts.device).to(compute_dtype)
+        x = ops.embed_add_pe(texts, self.src_word_emb.weight.to(compute_dtype), pe)
+        for layer in self.layer_stack:
+            x = layer(x, src_lens, style)
+        return x
+
+
+class Decoder(nn.Module):
+    """PE + N FFT blocks; training truncates to ``max_seq_len`` frames
+    (``transformer/Models.py:104-170``)."""
+
+    def __init__(self, config, film=False):
+        super().__init__()
+        tr = config["transformer"]
+        d = tr["decoder_hidden"]
+        self.max_seq_len = config["max_seq_len"]
+        self.d_model = d
+        self.position_enc = _pe_param(self.max_seq_len + 1, d)
+        nh = tr["decoder_head"]
+        self.layer_stack = nn.ModuleList(
+            FFTBlock(d, nh, d // nh, d // nh, tr["conv_filter_size"], tr["conv_kernel_size"], tr["decoder_dropout"], film=film)
+            for _ in range(tr["decoder_layer"])
+        )
+
+    def forward(self, x, mel_lens, style=None):
+        M = x.shape[1]
+        if self.training and M > self.max_seq_len:
+            M = self.max_seq_len
+            x = x[:, :M]
+            mel_lens = mel_lens.clamp(max=M)
+        pe = positional_rows(self.position_enc, M, self.d_model, x.device).to(x.dtype)
+        x = x + pe.unsqueeze(0)
+        for layer in self.layer_stack:
+            x = layer(x, mel_lens, style)
+        return x, mel_lens
+
+
+class VariancePredictor(nn.Module):
+    """[Conv1d k3 -> ReLU -> LN -> Dropout] x2 -> [FiLM] -> Linear(1) -> mask
+    (``model/modules.py:204-259``)."""
+
+    def __init__(self, model_config, film=False):
+        super().__init__()
+        d_in = model_config["transformer"]["encoder_hidden"]
+        vp = model_config["variance_predictor"]
+        fs, k, self.dropout = vp["filter_size"], vp["kernel_size"], vp["dropout"]
+        from collections import OrderedDict
+
+        from .layers import ConvHolder
+
+        self.conv_layer = nn.Sequential(OrderedDict([
+            ("conv1d_1", ConvHolder(d_in, fs, k)),
+            ("relu_1", nn.ReLU()),
+            ("layer_norm_1", nn.LayerNorm(fs)),
+            ("dropout_1", nn.Dropout(self.dropout)),
+            ("conv1d_2", ConvHolder(fs, fs, k)),
+            ("relu_2", nn.ReLU()),
+            ("layer_norm_2", nn.LayerNorm(fs)),
+            ("dropout_2", nn.Dropout(self.dropout)),
+        ]))
+        if film:
+            self.film = FiLM()
+        self.linear_layer = nn.Linear(fs, 1)
+
+    def forward(self, x, lengths, style=None):
+        cl = self.conv_layer
+        h = cl.conv1d_1(x, act="relu")
+        h = ops.add_layernorm(h, None, cl.layer_norm_1.weight, cl.layer_norm_1.bias,
+                              post_drop=self.dropout, training=self.training)
+        h = cl.conv1d_2(h, act="relu")
+        fp = self.film.pack(style) if (style is not None and hasattr(self, "film")) else None
+        h = ops.add_layernorm(h, None, cl.layer_norm_2.weight, cl.layer_norm_2.bias,
+                              post_drop=self.dropout, training=self.training, film_params=fp)
+        out = ops.linear(h, self.linear_layer.weight, self.linear_layer.bias).float().squeeze(-1)
+        if lengths is not None:
+            out = out.masked_fill(ops.lengths_to_mask(lengths, out.shape[1]), 0.0)
+        return out
+
+
+def _apply_control(pred, control):
+    if isinstance(control, torch.Tensor):
+        control = control.to(pred.device, pred.dtype)
+        if control.dim() == 2 and control.shape[1] != pred.shape[1]:
+            control = F.pad(control, (0, pred.shape[1] - control.shape[1]), value=1.0)[:, : pred.shape[1]]
+        return pred * control
+    return pred * control if control != 1.0 else pred
+
+
+class VarianceAdaptor(nn.Module):
+    """Duration / pitch / energy predictors, bucketized embeddings and the
+    length regulator (``model/modules.py:20-165``).  Only the duration predictor
+    receives the style FiLM (``modules.py:121``; D7 preserved).  Controls may be
+    scalars or per-phoneme ``[B, T]`` tensors (word-level control, the reference
+    ``notebooks/control.ipynb`` cells 17-23)."""
+
+    def __init__(self, preprocess_config, model_config, film=False):
+        super().__init__()
+        self.duration_predictor = VariancePredictor(model_config, film)
+        self.pitch_predictor = VariancePredictor(model_config, film)
+        self.energy_predictor = VariancePredictor(model_config, film)
+        pp = preprocess_config["preprocessing"]
+        self.pitch_feature_level = pp["pitch"]["feature"]
+        self.energy_feature_level = pp["energy"]["feature"]
+        ve = model_config["variance_embedding"]
+        n_bins = ve["n_bins"]
+        stats = _load_stats(preprocess_config)
+        p_min, p_max = stats["pitch"][:2]
+        e_min, e_max = stats["energy"][:2]
+        self.pitch_bins = nn.Parameter(_bins(p_min, p_max, n_bins, ve["pitch_quantization"]), requires_grad=False)
+        self.energy_bins = nn.Parameter(_bins(e_min, e_max, n_bins, ve["energy_quantization"]), requires_grad=False)
+        d = model_config["transformer"]["encoder_hidden"]
+        self.pitch_embedding = nn.Embedding(n_bins, d)
+        self.energy_embedding = nn.Embedding(n_bins, d)
+
+    def _variance(self, predictor, bins, table, x, target, lengths, control):
+        pred = predictor(x, lengths)
+        if target is not None:
+            values = target
+        else:
+            pred = _apply_control(pred, control)
+            values = pred
+        x = ops.bucketize_embed_add(x, values, bins, table.weight.to(x.dtype))
+        return pred, x
+
+    def forward(self, x, src_lens, mel_lens=None, max_len=None, pitch_target=None, energy_target=None,
+                duration_target=None, p_control=1.0, e_control=1.0, d_control=1.0, style=None):
+        log_d = self.duration_predictor(x, src_lens, style)
+        p_pred = e_pred = None
+        if self.pitch_feature_level == "phoneme_level":
+            p_pred, x = self._variance(self.pitch_predictor, self.pitch_bins, self.pitch_embedding, x, pitch_target, src_lens, p_control)
+        if self.energy_feature_level == "phoneme_level":
+            e_pred, x = self._variance(self.energy_predictor, self.energy_bins, self.energy_embedding, x, energy_target, src_lens, e_control)
+
+        if duration_target is not None:
+            d_rounded = duration_target
+            x, mel_len = ops.length_regulate(x, duration_target, max_len)
+            if mel_lens is not None:
+                mel_len = mel_lens
+        else:
+            d_pred = torch.clamp(torch.round(torch.exp(log_d) - 1.0), min=0.0)
+            d_rounded = torch.clamp(torch.round(_apply_control(d_pred, d_control)), min=0.0)
+            d_rounded = d_rounded.masked_fill(ops.lengths_to_mask(src_lens, d_rounded.shape[1]), 0.0)
+            x, mel_len = ops.length_regulate(x, d_rounded.long(), None)
+
+        if self.pitch_feature_level == "frame_level":
+            p_pred, x = self._variance(self.pitch_predictor, self.pitch_bins, self.pitch_embedding, x, pitch_target, mel_len, p_control)
+        if self.energy_feature_level == "frame_level":
+            e_pred, x = self._variance(self.energy_predictor, self.energy_bins, self.energy_embedding, x, energy_target, mel_len, e_control)
+        return x, p_pred, e_pred, log_d, d_rounded, mel_len
+
+
+def _bins(lo, hi, n_bins, quant):
+    if quant == "log":
+        return torch.exp(torch.linspace(math.log(lo), math.log(hi), n_bins - 1))
+    return torch.linspace(lo, hi, n_bins - 1)
+
+
+def _load_stats(preprocess_config):
+    path = os.path.join(preprocess_config["path"]["preprocessed_path"], "stats.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    # normalised features without stats: z-scores in a generous range
+    return {"pitch": [-4.0, 12.0, 0.0, 1.0], "energy": [-2.0, 10.0, 0.0, 1.0]}
+
+
+def _n_speakers(preprocess_config):
+    path = os.path.join(preprocess_config["path"]["preprocessed_path"], "speakers.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return len(json.load(f))
+    return int(preprocess_config.get("n_speakers", 1))
+
+
+class FastSpeech2(nn.Module):
+    def __init__(self, preprocess_config, model_config):
+        super().__init__()
+        self.model_config = model_config
+        self.style = style_mode(model_config)
+        film = self.style != "none"
+        self.encoder = Encoder(model_config, film=film)
+        if self.style == "film":
+            self.reference_encoder = ReferenceEncoder(preprocess_config, model_config)
+        elif self.style == "gst":
+            self.gst = GlobalStyleTokens(preprocess_config, model_config)
+        self.variance_adaptor = VarianceAdaptor(preprocess_config, model_config, film=film)
+        self.decoder = Decoder(model_config, film=film)
+        n_mel = preprocess_config["preprocessing"]["mel"]["n_mel_channels"]
+        self.mel_linear = nn.Linear(model_config["transformer"]["decoder_hidden"], n_mel)
+        self.postnet = PostNet(n_mel)
+        self.speaker_emb = None
+        if model_config["multi_speaker"]:
+            self.speaker_emb = nn.Embedding(_n_speakers(preprocess_config), model_config["transformer"]["encoder_hidden"])
+        self.compute_dtype = torch.float32
+
+    # ------------------------------------------------------------------ helpers
+    def set_compute_dtype(self, dtype):
+        self.compute_dtype = dtype
+        return self
+
+    def style_encoder(self):
+        return getattr(self, "reference_encoder", None) or getattr(self, "gst", None)
+
+    def film_scalars(self):
+        """Stacked s_gamma/s_beta parameters (reference ``utils/model.py:53-59``)."""
+        ps = [p for n, p in self.named_parameters() if ("s_gamma" in n or "s_beta" in n)]
+        return torch.cat(ps) if ps else None
+
+    def compute_style(self, mels, mel_lens, max_mel_len, batch, device, style_weights=None):
+        enc = self.style_encoder()
+        if enc is None:
+            return None
+        if style_weights is not None and self.style == "gst":
+            g, b = self.gst.from_token_weights(style_weights.to(device))
+        elif mels is None:
+            d = self.model_config["transformer"]["encoder_hidden"]
+            z = torch.zeros(batch, d, device=device, dtype=self.compute_dtype)
+            return (z, z)
+        else:
+            g, b = enc(mels.to(self.compute_dtype), mel_lens, max_mel_len)
+        return (g.to(self.compute_dtype), b.to(self.compute_dtype))
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None, max_mel_len=None,
+                p_targets=None, e_targets=None, d_targets=None, p_control=1.0, e_control=1.0, d_control=1.0,
+                style_weights=None):
+        dev = texts.device
+        cd = self.compute_dtype
+        if mels is not None and max_mel_len is None:
+            max_mel_len = mels.shape[1]
+        style = self.compute_style(mels, mel_lens, max_mel_len, texts.shape[0], dev, style_weights)
+        x = self.encoder(texts, src_lens, style, cd)
+        if self.speaker_emb is not None:
+            x = x + self.speaker_emb(speakers).to(cd).unsqueeze(1)
+        training_lr = d_targets is not None
+        x, p_pred, e_pred, log_d, d_rounded, mel_lens_out = self.variance_adaptor(
+            x, src_lens, mel_lens, max_mel_len if training_lr else None, p_targets, e_targets, d_targets,
+            p_control, e_control, d_control, style,
+        )
+        x, dec_lens = self.decoder(x, mel_lens_out, style)
+        mel = ops.linear(x, self.mel_linear.weight, self.mel_linear.bias).float()
+        post = self.postnet(mel.to(cd)).float() + mel
+        src_masks = ops.lengths_to_mask(src_lens, texts.shape[1])
+        mel_masks = ops.lengths_to_mask(dec_lens, mel.shape[1])
+        return (mel, post, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_lens_out)

@@ -1,0 +1,156 @@
+"""Building blocks of the FastSpeech2 family, channel-last and op-dispatched.
+
+Parameter *names and shapes* follow the reference exactly so that reference
+checkpoints load, e.g.
+``slf_attn.w_qs.weight (256,256)``, ``pos_ffn.w_1.weight (1024,256,9)``,
+``film.s_gamma (1,)``.  ``nn.Linear``/``nn.Conv1d``/``nn.LayerNorm`` are used
+only as parameter containers (names + PyTorch default init); every forward goes
+through ``speakingstyle_amd.ops`` which runs the HIP kernels on the GPU.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+FiLMParams = Optional[Tuple[torch.Tensor, torch.Tensor]]  # (gamma [B,C], beta [B,C])
+
+
+class FiLM(nn.Module):
+    """Learnable-scale FiLM: (s_g*g + 1)*x + s_b*b (reference ``model/blocks.py:43-62``)."""
+
+    def __init__(self):
+        super().__init__()
+        self.s_gamma = nn.Parameter(torch.ones(1))
+        self.s_beta = nn.Parameter(torch.ones(1))
+
+    def pack(self, style: FiLMParams):
+        if style is None:
+            return None
+        g, b = style
+        return (g, b, self.s_gamma, self.s_beta)
+
+
+class LinearNorm(nn.Module):
+    """Xavier-initialised Linear, no bias by default (reference ``model/blocks.py:65-78``)."""
+
+    def __init__(self, in_features, out_features, bias=False):
+        super().__init__()
+        self.linear = nn.Linear(in_features, out_features, bias)
+        nn.init.xavier_uniform_(self.linear.weight)
+        if bias:
+            nn.init.zeros_(self.linear.bias)
+
+    def forward(self, x):
+        return ops.linear(x, self.linear.weight, self.linear.bias)
+
+
+class ConvHolder(nn.Module):
+    """Parameter container named ``conv`` (reference ``ConvNorm`` / ``Conv``)."""
+
+    def __init__(self, cin, cout, k, dilation=1, bias=True):
+        super().__init__()
+        self.conv = nn.Conv1d(cin, cout, k, padding=dilation * (k - 1) // 2, dilation=dilation, bias=bias)
+        self.pad = dilation * (k - 1) // 2
+        self.dil = dilation
+
+    def forward(self, x, act=None):
+        return ops.conv1d(x, self.conv.weight, self.conv.bias, self.pad, self.dil, act)
+
+
+class MultiHeadAttention(nn.Module):
+    """Self-attention + output projection + residual + post-LN.
+
+    Reference: ``transformer/SubLayers.py:8-57``.  The three projections run as
+    one fused [3*H*dk x d] GEMM; the core is the fused flash-style attention op.
+    """
+
+    def __init__(self, n_head, d_model, d_k, d_v, dropout=0.1):
+        super().__init__()
+        assert d_k == d_v
+        self.n_head, self.d_k = n_head, d_k
+        self.w_qs = nn.Linear(d_model, n_head * d_k)
+        self.w_ks = nn.Linear(d_model, n_head * d_k)
+        self.w_vs = nn.Linear(d_model, n_head * d_v)
+        self.layer_norm = nn.LayerNorm(d_model)
+        self.fc = nn.Linear(n_head * d_v, d_model)
+        self.dropout = dropout
+
+    def forward(self, x, lengths):
+        w = torch.cat([self.w_qs.weight, self.w_ks.weight, self.w_vs.weight], 0)
+        b = torch.cat([self.w_qs.bias, self.w_ks.bias, self.w_vs.bias], 0)
+        qkv = ops.linear(x, w, b)
+        o = ops.attention(qkv, lengths, self.n_head)
+        a = ops.linear(o, self.fc.weight, self.fc.bias)
+        # LN(dropout(fc(o)) + x), then the FFT block's pad mask-fill (Layers.py:27-28)
+        return ops.add_layernorm(
+            a, x, self.layer_norm.weight, self.layer_norm.bias,
+            pre_drop=self.dropout, training=self.training, lengths=lengths,
+        )
+
+
+class PositionwiseFeedForward(nn.Module):
+    """Conv1d(k0) -> ReLU -> Conv1d(k1) -> dropout -> +res -> LN (``SubLayers.py:60-93``)."""
+
+    def __init__(self, d_in, d_hid, kernel_size: Sequence[int], dropout=0.1):
+        super().__init__()
+        self.w_1 = nn.Conv1d(d_in, d_hid, kernel_size[0], padding=(kernel_size[0] - 1) // 2)
+        self.w_2 = nn.Conv1d(d_hid, d_in, kernel_size[1], padding=(kernel_size[1] - 1) // 2)
+        self.layer_norm = nn.LayerNorm(d_in)
+        self.dropout = dropout
+        self.k = tuple(kernel_size)
+
+    def forward(self, x, lengths, film_params=None):
+        h = ops.conv1d(x, self.w_1.weight, self.w_1.bias, (self.k[0] - 1) // 2, 1, "relu")
+        z = ops.conv1d(h, self.w_2.weight, self.w_2.bias, (self.k[1] - 1) // 2, 1, None)
+        return ops.add_layernorm(
+            z, x, self.layer_norm.weight, self.layer_norm.bias,
+            pre_drop=self.dropout, training=self.training, film_params=film_params, lengths=lengths,
+        )
+
+
+class FFTBlock(nn.Module):
+    """MHA -> mask -> FFN -> [FiLM] -> mask (``transformer/Layers.py:11-37``)."""
+
+    def __init__(self, d_model, n_head, d_k, d_v, d_inner, kernel_size, dropout=0.1, film=True):
+        super().__init__()
+        self.slf_attn = MultiHeadAttention(n_head, d_model, d_k, d_v, dropout=dropout)
+        self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout=dropout)
+        if film:
+            self.film = FiLM()
+
+    def forward(self, x, lengths, style: FiLMParams = None):
+        x = self.slf_attn(x, lengths)
+        fp = self.film.pack(style) if (style is not None and hasattr(self, "film")) else None
+        return self.pos_ffn(x, lengths, fp)
+
+
+class PostNet(nn.Module):
+    """5 x (Conv1d k5 + BatchNorm1d), tanh on the first 4, dropout 0.5 always in
+    training (``transformer/Layers.py:78-148``).  BatchNorm statistics are taken
+    over all B*M rows including padding (reference semantics)."""
+
+    def __init__(self, n_mel_channels=80, emb=512, k=5, n=5):
+        super().__init__()
+        chans = [n_mel_channels] + [emb] * (n - 1) + [n_mel_channels]
+        self.convolutions = nn.ModuleList(
+            nn.Sequential(ConvHolder(chans[i], chans[i + 1], k), nn.BatchNorm1d(chans[i + 1])) for i in range(n)
+        )
+
+    def forward(self, x):
+        h = x
+        last = len(self.convolutions) - 1
+        for i, seq in enumerate(self.convolutions):
+            conv, bn = seq[0], seq[1]
+            h = conv(h)
+            B, L, C = h.shape
+            h2 = F.batch_norm(h.reshape(B * L, C), bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                              self.training, bn.momentum, bn.eps).reshape(B, L, C)
+            if i < last:
+                h2 = torch.tanh(h2)
+            h = F.dropout(h2, 0.5, self.training)
+        return h

@@ -1,0 +1,139 @@
+"""Speaking-style encoders producing FiLM (gamma, beta).
+
+* ``ReferenceEncoder`` -- the reference's FiLM variant (``model/modules.py:307-406``):
+  3 x (Conv1d k3 -> ReLU -> LN -> Dropout) on the mel, + PE(1024), LinearNorm
+  1024->256, 4 FFT blocks (8 heads, d_k 32, FFN k=[3,3], no FiLM), mean over time
+  (dividing by the padded length), LinearNorm 256->512 -> (gamma, beta).
+* ``GlobalStyleTokens`` -- the GST path that the reference only declares in a
+  commented-out config block (``config/BC2013/model.yaml:33-39``) and in its
+  README research goal: Wang et al. 2018 reference encoder (6 x Conv2d 3x3/s2 +
+  BN + ReLU -> GRU) + multi-head attention over a bank of style tokens.  The
+  resulting style embedding is projected to the same FiLM (gamma, beta), so it
+  drives exactly the FiLM sites the reference uses.  ``from_token_weights`` gives
+  direct token-weight style control at synthesis (no reference audio).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .layers import ConvHolder, FFTBlock, LinearNorm
+
+
+class ReferenceEncoder(nn.Module):
+    def __init__(self, preprocess_config, model_config, mean_over_valid: bool = False):
+        super().__init__()
+        rc = model_config["reference_encoder"]
+        n_mel = preprocess_config["preprocessing"]["mel"]["n_mel_channels"]
+        self.max_seq_len = model_config["max_seq_len"] + 1  # reference quirk: 1001
+        k = rc["conv_kernel_size"]
+        self.filter_size = fs = rc["conv_filter_size"]
+        self.d_model = d = rc["encoder_hidden"]
+        nh = rc["encoder_head"]
+        self.dropout = rc["dropout"]
+        self.mean_over_valid = mean_over_valid
+        self.layer_stack = nn.ModuleList(
+            nn.Sequential(ConvHolder(n_mel if i == 0 else fs, fs, k), nn.ReLU(), nn.LayerNorm(fs), nn.Dropout(self.dropout))
+            for i in range(rc["conv_layer"])
+        )
+        self.position_enc = nn.Parameter(ops.sinusoid_table(self.max_seq_len, fs).unsqueeze(0), requires_grad=False)
+        self.fftb_linear = LinearNorm(fs, d)
+        self.fftb_stack = nn.ModuleList(
+            FFTBlock(d, nh, d // nh, d // nh, fs, [k, k], dropout=self.dropout, film=False) for _ in range(rc["encoder_layer"])
+        )
+        self.feature_wise_affine = LinearNorm(d, 2 * d)
+
+    def forward(self, mel, mel_lens, max_len=None):
+        h = mel
+        M = h.shape[1]
+        for seq in self.layer_stack:
+            conv, ln = seq[0], seq[2]
+            h = conv(h, act="relu")
+            h = ops.add_layernorm(h, None, ln.weight, ln.bias, post_drop=self.dropout, training=self.training)
+        # pad frames are zeroed once after the whole conv stack (modules.py:370-371)
+        h = h.masked_fill(ops.lengths_to_mask(mel_lens, M).unsqueeze(-1), 0.0)
+        if (not self.training) and M > self.max_seq_len:
+            pe = ops.sinusoid_table(M, self.filter_size, device=h.device)
+        else:
+            M = min(M, self.max_seq_len)
+            h = h[:, :M]
+            pe = self.position_enc[0, :M]
+        lens = mel_lens.clamp(max=M)
+        h = h + pe.to(h.dtype).unsqueeze(0)
+        h = self.fftb_linear(h)
+        for blk in self.fftb_stack:
+            h = blk(h, lens, None)
+        if self.mean_over_valid:
+            pooled = h.float().sum(1) / lens.clamp(min=1).unsqueeze(1).float()
+        else:
+            pooled = h.float().mean(1)
+        gb = self.feature_wise_affine(pooled.to(h.dtype))
+        return gb[:, : self.d_model], gb[:, self.d_model:]
+
+
+class GlobalStyleTokens(nn.Module):
+    def __init__(self, preprocess_config, model_config):
+        super().__init__()
+        g = model_config["gst"]
+        n_mel = preprocess_config["preprocessing"]["mel"]["n_mel_channels"]
+        filters = [1] + list(g["conv_filters"])
+        self.convs = nn.ModuleList(nn.Conv2d(filters[i], filters[i + 1], 3, 2, 1) for i in range(len(filters) - 1))
+        self.bns = nn.ModuleList(nn.BatchNorm2d(c) for c in filters[1:])
+        freq = n_mel
+        for _ in range(len(filters) - 1):
+            freq = (freq - 3 + 2) // 2 + 1
+        self.gru = nn.GRU(filters[-1] * freq, g["gru_hidden"], batch_first=True)
+        self.n_head = g["attn_head"]
+        self.token_size = g["token_size"]
+        assert self.token_size % self.n_head == 0
+        self.embed = nn.Parameter(torch.randn(g["n_style_token"], self.token_size // self.n_head) * 0.5)
+        self.w_query = nn.Linear(g["gru_hidden"], self.token_size, bias=False)
+        self.w_key = nn.Linear(self.token_size // self.n_head, self.token_size, bias=False)
+        self.w_value = nn.Linear(self.token_size // self.n_head, self.token_size, bias=False)
+        d = model_config["transformer"]["encoder_hidden"]
+        self.d_model = d
+        self.feature_wise_affine = LinearNorm(self.token_size, 2 * d)
+
+    def reference_embedding(self, mel, mel_lens):
+        x = mel.float().unsqueeze(1)  # [B,1,T,n_mel]
+        lens = mel_lens.clone()
+        for conv, bn in zip(self.convs, self.bns):
+            x = F.relu(bn(conv(x)))
+            lens = (lens - 1) // 2 + 1
+        B, C, T, Fq = x.shape
+        x = x.permute(0, 2, 1, 3).reshape(B, T, C * Fq)
+        out, _ = self.gru(x)
+        idx = (lens.clamp(min=1, max=T) - 1).view(B, 1, 1).expand(-1, 1, out.shape[-1])
+        return out.gather(1, idx).squeeze(1)  # last valid GRU state [B, H]
+
+    def token_attention(self, query):
+        """query [B, token_size] -> style embedding [B, token_size] and weights [B, heads, n_tok]."""
+        keys = torch.tanh(self.embed)  # [N, ts/h]
+        B = query.shape[0]
+        q = query.view(B, self.n_head, 1, -1)
+        k = self.w_key(keys).view(-1, self.n_head, self.token_size // self.n_head).transpose(0, 1)  # [h,N,d]
+        v = self.w_value(keys).view(-1, self.n_head, self.token_size // self.n_head).transpose(0, 1)
+        s = torch.matmul(q, k.transpose(-1, -2).unsqueeze(0)) / (k.shape[-1] ** 0.5)  # [B,h,1,N]
+        w = torch.softmax(s, -1)
+        o = torch.matmul(w, v.unsqueeze(0)).reshape(B, self.token_size)
+        return o, w.squeeze(2)
+
+    def _film(self, style_emb):
+        gb = self.feature_wise_affine(style_emb)
+        return gb[:, : self.d_model], gb[:, self.d_model:]
+
+    def forward(self, mel, mel_lens, max_len=None):
+        ref = self.reference_embedding(mel, mel_lens)
+        style, _ = self.token_attention(self.w_query(ref))
+        return self._film(style.to(mel.dtype))
+
+    def from_token_weights(self, weights):
+        """weights [B, n_tok] (or [B, heads, n_tok]) -> FiLM params; style without audio."""
+        keys = torch.tanh(self.embed)
+        v = self.w_value(keys).view(-1, self.n_head, self.token_size // self.n_head).transpose(0, 1)  # [h,N,d]
+        if weights.dim() == 2:
+            weights = weights.unsqueeze(1).expand(-1, self.n_head, -1)
+        o = torch.einsum("bhn,hnd->bhd", weights.float(), v.float()).reshape(weights.shape[0], self.token_size)
+        return self._film(o)

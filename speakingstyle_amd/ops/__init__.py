@@ -1,0 +1,93 @@
+"""Op dispatch: HIP/CDNA4 kernels on the GPU, plain PyTorch on the CPU.
+
+There is exactly one code path per device.  On a CUDA(=HIP) device every op in
+this module runs the hand-written kernels of ``csrc/`` (through
+``speakingstyle_amd.ops.hip``); if the kernel library is missing on a GPU box
+the first op raises instead of silently falling back.  On the CPU the torch
+reference implementations (``ops.reference``) run -- they are also the test
+oracle.  ``set_backend("reference")`` forces the torch path everywhere (debug /
+A-B only).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_FORCED = os.environ.get("SSAMD_BACKEND")  # "reference" | "hip" | None
+
+
+def set_backend(name: Optional[str]):
+    global _FORCED
+    assert name in (None, "reference", "hip")
+    _FORCED = name
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    if _FORCED == "reference":
+        return False
+    if t.device.type != "cuda":
+        if _FORCED == "hip":
+            raise RuntimeError("hip backend forced but tensor is on CPU")
+        return False
+    return True
+
+
+def _hip():
+    from . import hip  # noqa: WPS433  (lazy: loads libssamd_kernels.so)
+
+    return hip
+
+
+lengths_to_mask = ref.lengths_to_mask
+sinusoid_table = ref.sinusoid_table
+
+
+def linear(x, w, b=None, act=None):
+    if use_hip(x):
+        return _hip().linear(x, w, b, act)
+    return ref.linear(x, w, b, act)
+
+
+def conv1d(x, w, b=None, pad=0, dil=1, act=None):
+    if use_hip(x):
+        return _hip().conv1d(x, w, b, pad, dil, act)
+    return ref.conv1d(x, w, b, pad, dil, act)
+
+
+def attention(qkv, lengths, n_head):
+    if use_hip(qkv):
+        return _hip().attention(qkv, lengths, n_head)
+    return ref.attention(qkv, lengths, n_head)
+
+
+def add_layernorm(a, residual, ln_w, ln_b, **kw):
+    if use_hip(a):
+        return _hip().add_layernorm(a, residual, ln_w, ln_b, **kw)
+    return ref.add_layernorm(a, residual, ln_w, ln_b, **kw)
+
+
+def length_regulate(x, durations, max_len):
+    if use_hip(x):
+        return _hip().length_regulate(x, durations, max_len)
+    return ref.length_regulate(x, durations, max_len)
+
+
+def embed_add_pe(ids, table, pe, extra=None):
+    """table[ids] + pe[:L] (+ extra[B,C] broadcast) -> compute dtype."""
+    if use_hip(ids):
+        return _hip().embed_add_pe(ids, table, pe, extra)
+    out = torch.nn.functional.embedding(ids, table) + pe[: ids.shape[1]].unsqueeze(0).to(table.dtype)
+    if extra is not None:
+        out = out + extra.unsqueeze(1)
+    return out
+
+
+def bucketize_embed_add(x, values, bins, table):
+    """x + table[bucketize(values, bins)]."""
+    if use_hip(x):
+        return _hip().bucketize_embed_add(x, values, bins, table)
+    return x + ref.bucketize_embed(values, bins, table).to(x.dtype)

@@ -1,0 +1,83 @@
+"""Grapheme-to-phoneme for synthesis (reference ``synthesize.py:26-90``).
+
+The reference uses a lexicon file first and falls back to ``g2p_en`` (English) /
+``pypinyin`` (Mandarin).  Neither package is available offline, so the fallback
+here spells unknown English words with ARPAbet letter names (deterministic,
+always in-vocabulary) and maps unknown Mandarin syllables to ``sp``.
+"""
+import re
+from string import punctuation
+
+from . import text_to_sequence
+
+_LETTER_NAMES = {
+    "a": "EY1", "b": "B IY1", "c": "S IY1", "d": "D IY1", "e": "IY1", "f": "EH1 F", "g": "JH IY1",
+    "h": "EY1 CH", "i": "AY1", "j": "JH EY1", "k": "K EY1", "l": "EH1 L", "m": "EH1 M", "n": "EH1 N",
+    "o": "OW1", "p": "P IY1", "q": "K Y UW1", "r": "AA1 R", "s": "EH1 S", "t": "T IY1", "u": "Y UW1",
+    "v": "V IY1", "w": "D AH1 B AH0 L Y UW0", "x": "EH1 K S", "y": "W AY1", "z": "Z IY1",
+}
+
+
+def read_lexicon(path):
+    lex = {}
+    with open(path, encoding="utf-8") as f:
+        for line in f:
+            parts = re.split(r"\s+", line.strip())
+            if len(parts) < 2:
+                continue
+            word = parts[0].lower()
+            lex.setdefault(word, parts[1:])
+    return lex
+
+
+def english_word_phones(word, lexicon):
+    w = word.lower()
+    if w in lexicon:
+        return list(lexicon[w])
+    phones = []
+    for ch in w:
+        phones += _LETTER_NAMES.get(ch, "").split()
+    return phones
+
+
+def english_to_phones(text, lexicon=None):
+    lexicon = lexicon or {}
+    text = text.rstrip(punctuation)
+    phones = []
+    for w in re.split(r"([,;.\-\?\!\s+])", text):
+        if not w or w.isspace():
+            continue
+        if re.fullmatch(r"[,;.\-\?\!]", w):
+            phones.append("sp")
+            continue
+        phones += english_word_phones(w, lexicon)
+    return phones
+
+
+def word_groups(text, lexicon=None):
+    """Per-word phoneme counts (for word-level prosody control, cf. the
+    reference notebook ``control.ipynb`` cells 17-23)."""
+    lexicon = lexicon or {}
+    groups = []
+    for w in re.split(r"([,;.\-\?\!\s+])", text.rstrip(punctuation)):
+        if not w or w.isspace():
+            continue
+        if re.fullmatch(r"[,;.\-\?\!]", w):
+            groups.append((w, ["sp"]))
+        else:
+            groups.append((w, english_word_phones(w, lexicon)))
+    return groups
+
+
+def preprocess_english(text, cleaners, lexicon=None):
+    phones = english_to_phones(text, lexicon)
+    return text_to_sequence("{" + " ".join(phones) + "}", cleaners), phones
+
+
+def preprocess_mandarin(pinyin_syllables, cleaners, lexicon=None):
+    """``pinyin_syllables``: list like ['ni3', 'hao3'] (pypinyin output)."""
+    lexicon = lexicon or {}
+    phones = []
+    for p in pinyin_syllables:
+        phones += lexicon.get(p, ["sp"])
+    return text_to_sequence("{" + " ".join(phones) + "}", cleaners), phones
