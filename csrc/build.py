@@ -1,0 +1,81 @@
+#!/usr/bin/env python
+"""Build the HIP/CDNA4 kernel library for gfx950.
+
+Every ``csrc/*.hip`` is compiled with ``hipcc --offload-arch=gfx950 -O3`` into
+an object, then linked into ``speakingstyle_amd/_lib/libssamd_kernels.so`` (the
+in-tree location the Python bindings load; the .so is git-ignored but travels
+to the GPU box with the repository snapshot).  ``csrc/host_*.cpp`` form the
+native host-runtime library ``libssamd_host.so`` (g++, no GPU code).
+
+Usage: python csrc/build.py [--jobs N] [--debug] [--clean]
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT_DIR = os.path.join(ROOT, "speakingstyle_amd", "_lib")
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+KLIB = os.path.join(OUT_DIR, "libssamd_kernels.so")
+HLIB = os.path.join(OUT_DIR, "libssamd_host.so")
+ARCH = os.environ.get("SSAMD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("command failed: %s\n%s" % (" ".join(cmd), r.stdout))
+    return r.stdout
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(jobs=8, debug=False, clean=False, verbose=False):
+    os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    headers = glob.glob(os.path.join(HERE, "*.h"))
+    srcs = sorted(glob.glob(os.path.join(HERE, "*.hip")))
+    opt = ["-O1", "-g"] if debug else ["-O3"]
+    flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+             "-Wno-unused-variable", "-munsafe-fp-atomics", "-I", HERE] + opt
+
+    def compile_one(src):
+        obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+        if clean or _stale(obj, [src] + headers):
+            _run([HIPCC, "-c", src, "-o", obj] + flags)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    if clean or _stale(KLIB, objs):
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", KLIB] + objs)
+
+    hsrcs = sorted(glob.glob(os.path.join(HERE, "host_*.cpp")))
+    if hsrcs and (clean or _stale(HLIB, hsrcs + headers)):
+        _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", HLIB] + hsrcs)
+    if verbose:
+        print("built", KLIB, HLIB if hsrcs else "")
+    return KLIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--clean", action="store_true")
+    a = ap.parse_args()
+    try:
+        build(a.jobs, a.debug, a.clean, verbose=True)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

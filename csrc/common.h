@@ -1,0 +1,54 @@
+// Shared device helpers for the gfx950 (MI355X, CDNA4) kernels.
+// Wave64 everywhere: lane = threadIdx.x & 63; reductions use 64-wide shuffles.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define SSAMD_API extern "C" __attribute__((visibility("default")))
+
+typedef unsigned short bf16_t;  // raw bf16 storage
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef float float4v __attribute__((ext_vector_type(4)));
+typedef float float16v __attribute__((ext_vector_type(16)));
+
+static __device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+static __device__ __forceinline__ bf16_t f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+static __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static __device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based uniform RNG for dropout: no state, the backward pass regenerates
+// the exact forward mask from (seed, element index).  PCG-style output hash.
+static __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+static __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
+  uint32_t h = hash_u32((uint32_t)idx ^ hash_u32((uint32_t)seed ^ (uint32_t)(idx >> 32) * 0x9E3779B9U)
+                        ^ (uint32_t)(seed >> 32));
+  return (h >> 8) * (1.0f / 16777216.0f);
+}
+// keep-scale for element idx: 0 (dropped) or 1/(1-p)
+static __device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, float p) {
+  if (p <= 0.f) return 1.f;
+  return uniform01(seed, idx) >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,439 @@
+// Implicit-GEMM Conv1d / Linear on CDNA4 MFMA (bf16 in, fp32 accumulate), channel-last.
+//
+// Forward / data-gradient ("TN" form, both operands K-contiguous):
+//   Y[m, n] = epi( sum_k A[m, k] * Bt[n, k] )
+//   m = (b, t) over B*L rows;  k = tap * Cin + cin;
+//   A[m, k] = X[b, t + tap*dil - pad, cin]   (zero outside [0, L): per-sequence padding)
+// A Linear layer is the ks = 1, pad = 0 case.  The data gradient of a conv is the
+// same kernel on dY with the flipped/transposed weight and pad' = (ks-1)*dil - pad.
+// Epilogue (fused, coalesced through LDS): + bias[n] -> activation (relu / lrelu 0.1
+// / tanh) -> * (aux > 0) (ReLU backward) -> + residual -> zero rows t >= len[b]
+// -> bf16 or fp32 store.
+//
+// Weight gradient ("rows-reduction" form):
+//   G[n, k] = sum_m dY[m, n] * Acol[m, k]      (split over m into fp32 slabs)
+// both operands are read with the reduction index m on the row axis, so the MFMA
+// fragments come from LDS through ds_read_b64_tr_b16 (hardware transpose read).
+// A reduce kernel sums the slabs and writes dW in the PyTorch [Cout, Cin, ks] layout.
+//
+// Tiling: 128x128 output tile per 256-thread block (4 waves as 2x2, 64x64 per wave =
+// 4x4 v_mfma_f32_16x16x32_bf16 accumulators), BK = 64, LDS double buffer with
+// register staging (one barrier per K-step), XOR-swizzled LDS images (conflict-free
+// ds_read_b128 / tr reads), XCD-aware bijective block remap so that the 8 blocks
+// that share an A panel run on one XCD's L2.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int NT = 256;
+constexpr int CSTRIDE = 132;  // fp32 epilogue staging row stride (conflict-free writes)
+
+struct ConvGeom {
+  int B, L, Cin, ks, dil, pad;  // A operand geometry
+  int M, N, K;                  // GEMM sizes (M = B*L, K = ks*Cin)
+};
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // bijective: consecutive remapped ids land on the same XCD (round-robin dispatch)
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, k = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+// swizzled byte offset of 16-B chunk `c` (0..7) of row `row` in a [rows][64 bf16] image
+__device__ __forceinline__ int swz128(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ short8 load_a_chunk(const bf16_t* __restrict__ X, const ConvGeom& g, int m, int bb, int tt,
+                                               int k, float invCin) {
+  short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (m < g.M && k < g.K) {
+    const int tap = (int)(((float)k + 0.5f) * invCin);
+    const int cin = k - tap * g.Cin;
+    const int ts = tt + tap * g.dil - g.pad;
+    if (ts >= 0 && ts < g.L) v = *reinterpret_cast<const short8*>(X + ((long)bb * g.L + ts) * g.Cin + cin);
+  }
+  return v;
+}
+
+template <bool OUT_F32>
+__global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          const float* __restrict__ bias, const bf16_t* __restrict__ aux,
+                                                          const bf16_t* __restrict__ resid,
+                                                          const int64_t* __restrict__ lens, void* __restrict__ Yv,
+                                                          ConvGeom g, int act, int ldy) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + BN - 1) / BN;
+  const int nM = (g.M + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, nN * nM);
+  const int tn = wg % nN, tm = wg / nN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const float invCin = 1.f / (float)g.Cin;
+
+  // staging assignment: chunk e = tid + 256*i, row = e/8, c = e%8 (i = 0..3)
+  int a_b[4], a_t[4], a_m[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (tid >> 3) + 32 * i;
+    a_m[i] = m0 + row;
+    const int mm = a_m[i] < g.M ? a_m[i] : 0;
+    a_b[i] = mm / g.L;
+    a_t[i] = mm - a_b[i] * g.L;
+  }
+  const int cchunk = tid & 7;
+
+  float4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  short8 ra[4], rb[4];
+  auto gload = [&](int kt) {
+    const int k = kt * BK + cchunk * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ra[i] = load_a_chunk(X, g, a_m[i], a_b[i], a_t[i], k, invCin);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (n < g.N && k < g.K) v = *reinterpret_cast<const short8*>(W + (long)n * g.K + k);
+      rb[i] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* As = smem + buf * (2 * BM * BK * 2);
+    char* Bs = As + BM * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<short8*>(As + swz128(row, cchunk)) = ra[i];
+      *reinterpret_cast<short8*>(Bs + swz128(row, cchunk)) = rb[i];
+    }
+  };
+
+  const int nk = (g.K + BK - 1) / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* As = smem + buf * (2 * BM * BK * 2);
+    const char* Bs = As + BM * BK * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      short8 fa[4], fb[4];
+      const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i] = *reinterpret_cast<const short8*>(As + swz128(wm * 64 + i * 16 + (lane & 15), c));
+        fb[i] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + i * 16 + (lane & 15), c));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage fp32 tile in LDS, then coalesced 8-wide row segments
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * 64 + j * 16 + (lane & 15);
+        Cs[row * CSTRIDE + col] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int seg = tid & 15;  // 8 columns each
+  for (int rr = tid >> 4; rr < BM; rr += NT / 16) {
+    const int m = m0 + rr;
+    if (m >= g.M) break;
+    const int nb = n0 + seg * 8;
+    if (nb >= g.N) continue;
+    const int bb = m / g.L, tt = m - bb * g.L;
+    const bool valid = lens == nullptr || tt < (int)lens[bb];
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = Cs[rr * CSTRIDE + seg * 8 + q];
+    const bool full = nb + 8 <= g.N;
+    if (bias) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += (full || nb + q < g.N) ? bias[nb + q] : 0.f;
+    }
+    if (act == ACT_RELU) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+    } else if (act == ACT_LRELU) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+    } else if (act == ACT_TANH) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = tanhf(v[q]);
+    }
+    const long off = (long)m * ldy + nb;
+    if (full && (ldy % 8) == 0) {
+      if (aux) {
+        short8 x = *reinterpret_cast<const short8*>(aux + off);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
+      }
+      if (resid) {
+        short8 x = *reinterpret_cast<const short8*>(resid + off);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += bf2f((bf16_t)x[q]);
+      }
+      if (!valid) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = 0.f;
+      }
+      if constexpr (OUT_F32) {
+        float4* Y = reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off);
+        Y[0] = make_float4(v[0], v[1], v[2], v[3]);
+        Y[1] = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        short8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = (short)f2bf(v[q]);
+        *reinterpret_cast<short8*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
+      }
+    } else {
+      for (int q = 0; q < 8; ++q) {
+        if (nb + q >= g.N) break;
+        float x = v[q];
+        if (aux && !(bf2f(aux[off + q]) > 0.f)) x = 0.f;
+        if (resid) x += bf2f(resid[off + q]);
+        if (!valid) x = 0.f;
+        if constexpr (OUT_F32) reinterpret_cast<float*>(Yv)[off + q] = x;
+        else reinterpret_cast<bf16_t*>(Yv)[off + q] = f2bf(x);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Weight gradient.  Tile: 128 (n = cout) x 128 (k = tap*Cin + cin), reduction over
+// rows m in steps of RB = 64.  LDS image per operand: [64 rows][128 cols] bf16,
+// 256-B rows, 8-B column chunks XOR-swizzled by f(row) = ((row&3) | ((row>>3)&1)<<2) << 2
+// so the 32 lanes of a half-wave hit 32 distinct 8-B slots in ds_read_b64_tr_b16.
+// ----------------------------------------------------------------------------
+constexpr int RB = 64;
+
+__device__ __forceinline__ int swz_tr(int row, int cc /*8-B chunk 0..31*/) {
+  const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
+  return row * 256 + ((cc ^ f) << 3);
+}
+
+__device__ __forceinline__ short4v ds_read_tr(const char* p) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+__global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
+                                                           float* __restrict__ slabs, ConvGeom g, int rows_per_split) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + 127) / 128;  // cout tiles
+  const int nK = (g.K + 127) / 128;  // k tiles
+  const int tile = blockIdx.x % (nN * nK);
+  const int split = blockIdx.x / (nN * nK);
+  const int tn = tile / nK, tk = tile % nK;
+  const int n0 = tn * 128, k0 = tk * 128;
+  const int r_begin = split * rows_per_split;
+  const int r_end = min(g.M, r_begin + rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const float invCin = 1.f / (float)g.Cin;
+
+  float4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  // staging: each operand tile = 64 rows x 128 cols bf16 = 1024 x 16-B chunks; 4 per thread
+  // chunk e = tid + 256*i: row = e / 16, c16 = e % 16 (16-B chunk = two 8-B chunks)
+  const int c16 = tid & 15;
+  const int k_ld = k0 + c16 * 8;
+  int tap = 0, cin = 0;
+  const bool k_ok = k_ld < g.K;
+  if (k_ok) {
+    tap = (int)(((float)k_ld + 0.5f) * invCin);
+    cin = k_ld - tap * g.Cin;
+  }
+  const int n_ld = n0 + c16 * 8;
+  short8 rx[4], ry[4];
+  auto gload = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + (tid >> 4) + 16 * i;
+      short8 vx = {0, 0, 0, 0, 0, 0, 0, 0}, vy = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < r_end) {
+        if (n_ld < g.N) vy = *reinterpret_cast<const short8*>(dY + (long)m * g.N + n_ld);
+        if (k_ok) {
+          const int bb = m / g.L, tt = m - bb * g.L;
+          const int ts = tt + tap * g.dil - g.pad;
+          if (ts >= 0 && ts < g.L) vx = *reinterpret_cast<const short8*>(X + ((long)bb * g.L + ts) * g.Cin + cin);
+        }
+      }
+      rx[i] = vx;
+      ry[i] = vy;
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* Ys = smem + buf * (2 * RB * 256);
+    char* Xs = Ys + RB * 256;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 4) + 16 * i;
+      *reinterpret_cast<short8*>(Ys + swz_tr(row, c16 * 2)) = ry[i];
+      *reinterpret_cast<short8*>(Xs + swz_tr(row, c16 * 2)) = rx[i];
+    }
+  };
+
+  const int nsteps = (r_end - r_begin + RB - 1) / RB;
+  if (nsteps > 0) {
+    gload(r_begin);
+    lstore(0);
+  }
+  __syncthreads();
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) gload(r_begin + (s + 1) * RB);
+    const char* Ys = smem + buf * (2 * RB * 256);
+    const char* Xs = Ys + RB * 256;
+#pragma unroll
+    for (int kk = 0; kk < RB / 32; ++kk) {
+      short8 fa[4], fb[4];
+      const int rbase = kk * 32 + grp * 8 + q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ca = (wn * 64 + i * 16) / 4 + p;  // 8-B chunk of the A (dY) column block
+        const int cb = (wk * 64 + i * 16) / 4 + p;
+        short4v a0 = ds_read_tr(Ys + swz_tr(rbase, ca));
+        short4v a1 = ds_read_tr(Ys + swz_tr(rbase + 4, ca));
+        short4v b0 = ds_read_tr(Xs + swz_tr(rbase, cb));
+        short4v b1 = ds_read_tr(Xs + swz_tr(rbase + 4, cb));
+        fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        fb[i] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // partial slab [split][N][K] fp32
+  float* S = slabs + (long)split * g.N * g.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
+        if (n < g.N && k < g.K) S[(long)n * g.K + k] = acc[i][j][r];
+      }
+}
+
+// dW[n][cin][tap] = sum_s slab[s][n][tap*Cin + cin]   (PyTorch Conv1d / Linear layout)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ dW,
+                                                           int splits, int N, int Cin, int ks) {
+  const long K = (long)Cin * ks;
+  const long total = (long)N * K;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int sp = 0; sp < splits; ++sp) s += slabs[(long)sp * total + e];
+    const long n = e / K;
+    const int k = (int)(e - n * K);
+    const int tap = k / Cin, cin = k - tap * Cin;
+    dW[(n * Cin + cin) * ks + tap] = s;
+  }
+}
+
+// db[n] = sum_m dY[m, n]  (column sums; fp32 atomics after block reduction)
+__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ dY, float* __restrict__ db, long M,
+                                                     int N, int rows_per_block) {
+  const long r0 = (long)blockIdx.y * rows_per_block;
+  const long r1 = min(M, r0 + rows_per_block);
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+    float s = 0.f;
+    for (long r = r0; r < r1; ++r) s += bf2f(dY[r * N + n]);
+    atomicAdd(db + n, s);
+  }
+}
+
+}  // namespace
+
+static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N) {
+  ConvGeom g;
+  g.B = B; g.L = L; g.Cin = Cin; g.ks = ks; g.dil = dil; g.pad = pad;
+  g.M = B * L; g.N = N; g.K = ks * Cin;
+  return g;
+}
+
+SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
+                              const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
+                              int ks, int dil, int pad, int N, int act, int ldy, hipStream_t s) {
+  if (Cin % 8 != 0) return -2;
+  if ((long)B * L == 0 || N == 0) return 0;
+  ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
+  const int nwg = ((g.M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const size_t lds = (size_t)BM * CSTRIDE * 4;  // >= 2 stages x (A+B) = 64 KiB
+  if (out_f32)
+    hipLaunchKernelGGL(conv_gemm_kernel<true>, dim3(nwg), dim3(NT), lds, s, X, W, bias, aux, resid, lens, Y, g, act, ldy);
+  else
+    hipLaunchKernelGGL(conv_gemm_kernel<false>, dim3(nwg), dim3(NT), lds, s, X, W, bias, aux, resid, lens, Y, g, act,
+                       ldy);
+  return (int)hipGetLastError();
+}
+
+// Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.
+SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, int B, int L,
+                               int Cin, int ks, int dil, int pad, int N, int max_splits, hipStream_t s) {
+  if (Cin % 8 != 0 || N % 8 != 0) return -2;
+  ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
+  const long slab = (long)N * g.K;
+  if (g.M == 0) {
+    hipMemsetAsync(dW, 0, slab * sizeof(float), s);
+    return (int)hipGetLastError();
+  }
+  const int tiles = ((N + 127) / 128) * ((g.K + 127) / 128);
+  int splits = (1536 + tiles - 1) / tiles;
+  const int max_by_rows = (g.M + 511) / 512;
+  if (splits > max_by_rows) splits = max_by_rows;
+  if (splits > max_splits) splits = max_splits;
+  if ((long)splits * slab > ws_floats) splits = (int)(ws_floats / slab);
+  if (splits < 1) return -3;
+  int rows_per_split = (g.M + splits - 1) / splits;
+  rows_per_split = (rows_per_split + RB - 1) / RB * RB;
+  splits = (g.M + rows_per_split - 1) / rows_per_split;
+  hipLaunchKernelGGL(conv_wgrad_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, g,
+                     rows_per_split);
+  const long total = slab;
+  int blocks = (int)min((total + 255) / 256, 8192L);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, splits, N, Cin, ks);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_colsum(const bf16_t* dY, float* db, long M, int N, hipStream_t s) {
+  hipMemsetAsync(db, 0, (size_t)N * sizeof(float), s);
+  if (M == 0) return (int)hipGetLastError();
+  const int rpb = 256;
+  dim3 grid((N + 255) / 256, (int)((M + rpb - 1) / rpb));
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, dY, db, M, N, rpb);
+  return (int)hipGetLastError();
+}

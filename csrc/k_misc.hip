@@ -1,0 +1,337 @@
+// Memory-bound glue kernels: length regulator, embeddings, fused loss, clip + Adam.
+#include "common.h"
+
+namespace {
+
+// ----------------------------------------------------------------------------
+// LengthRegulator (reference model/modules.py:168-201): sync-free.
+//   cum[b, i] = sum_{j<=i} d[b, j]   (inclusive prefix sum, computed in-kernel per block)
+//   frame f of item b copies phoneme p = #{i : cum[b,i] <= f} (f < mel_len[b]) else zeros,
+//   then optionally adds a positional row pe[f] (decoder input, Models.py:154-162).
+// Grid (ceil(M / 64), B), 256 threads; each half-wave moves one 512-B row (C=256)
+// with 16-B vector loads; cum is staged once per block in LDS.
+// ----------------------------------------------------------------------------
+constexpr int LR_ROWS = 64;
+
+__device__ int block_prefix_durations(const int64_t* d, int T, int* cum) {
+  // serial-per-thread chunks + wave scan; T is small (<= a few hundred)
+  for (int i = threadIdx.x; i < T; i += blockDim.x) cum[i] = (int)max((int64_t)0, d[i]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int i = 0; i < T; ++i) { s += cum[i]; cum[i] = s; }
+  }
+  __syncthreads();
+  return T > 0 ? cum[T - 1] : 0;
+}
+
+__global__ void __launch_bounds__(256) lr_fwd_kernel(const bf16_t* __restrict__ x, const int64_t* __restrict__ dur,
+                                                     const bf16_t* __restrict__ pe, bf16_t* __restrict__ out,
+                                                     int T, int M, int C) {
+  extern __shared__ int cum[];
+  const int b = blockIdx.y;
+  const int total = block_prefix_durations(dur + (long)b * T, T, cum);
+  const int vec = C / 8;  // 16-B chunks per row
+  for (int e = threadIdx.x; e < LR_ROWS * vec; e += blockDim.x) {
+    const int r = e / vec, c8 = e % vec;
+    const int f = blockIdx.x * LR_ROWS + r;
+    if (f >= M) break;
+    short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (f < total) {
+      int lo = 0, hi = T;  // first i with cum[i] > f
+      while (lo < hi) { int mid = (lo + hi) >> 1; if (cum[mid] <= f) lo = mid + 1; else hi = mid; }
+      v = *reinterpret_cast<const short8*>(x + ((long)b * T + lo) * C + c8 * 8);
+    }
+    if (pe) {
+      short8 p = *reinterpret_cast<const short8*>(pe + (long)f * C + c8 * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (short)f2bf(bf2f((bf16_t)v[i]) + bf2f((bf16_t)p[i]));
+    }
+    *reinterpret_cast<short8*>(out + ((long)b * M + f) * C + c8 * 8) = v;
+  }
+}
+
+// dx[b, p] = sum over the frames f in [cum[p-1], cum[p]) with f < M of dout[b, f]
+__global__ void __launch_bounds__(256) lr_bwd_kernel(const bf16_t* __restrict__ dout, const int64_t* __restrict__ dur,
+                                                     bf16_t* __restrict__ dx, int T, int M, int C) {
+  extern __shared__ int cum[];
+  const int b = blockIdx.y;
+  block_prefix_durations(dur + (long)b * T, T, cum);
+  const int vec = C / 8;
+  for (int e = threadIdx.x; e < LR_ROWS * vec; e += blockDim.x) {
+    const int r = e / vec, c8 = e % vec;
+    const int p = blockIdx.x * LR_ROWS + r;
+    if (p >= T) break;
+    const int f0 = p ? cum[p - 1] : 0;
+    const int f1 = min(cum[p], M);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int f = f0; f < f1; ++f) {
+      short8 v = *reinterpret_cast<const short8*>(dout + ((long)b * M + f) * C + c8 * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += bf2f((bf16_t)v[i]);
+    }
+    short8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(acc[i]);
+    *reinterpret_cast<short8*>(dx + ((long)b * T + p) * C + c8 * 8) = o;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Embedding gather + add (phoneme embedding + PE, Models.py:56-62,89-91; pitch /
+// energy bucketized embeddings, modules.py:83-101).
+//   mode 0: out[r] = table[ids[r]] + pe[r % L]            (ids int64)
+//   mode 1: out[r] = x[r] + table[bucketize(vals[r], bins)]  (torch.bucketize, right=False)
+// Backward: dtable[id] += dout[r] with fp32 atomics on 256-B row segments.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ int bucketize_lower(float v, const float* bins, int nb) {
+  int lo = 0, hi = nb;  // number of bins strictly less than v
+  while (lo < hi) { int mid = (lo + hi) >> 1; if (bins[mid] < v) lo = mid + 1; else hi = mid; }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) embed_fwd_kernel(int mode, const int64_t* __restrict__ ids,
+                                                        const float* __restrict__ vals, const float* __restrict__ bins,
+                                                        int nbins, const bf16_t* __restrict__ table,
+                                                        const bf16_t* __restrict__ addend, int L,
+                                                        bf16_t* __restrict__ out, int* __restrict__ idx_out, long rows,
+                                                        int C) {
+  const int vec = C / 8;
+  const long total = rows * vec;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / vec;
+    const int c8 = (int)(e % vec);
+    int id;
+    if (mode == 0) id = (int)ids[r];
+    else id = bucketize_lower(vals[r], bins, nbins);
+    if (idx_out && c8 == 0) idx_out[r] = id;
+    short8 t = *reinterpret_cast<const short8*>(table + (long)id * C + c8 * 8);
+    const bf16_t* ad = mode == 0 ? addend + (long)(r % L) * C : addend + r * C;
+    short8 p = *reinterpret_cast<const short8*>(ad + c8 * 8);
+    short8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(bf2f((bf16_t)t[i]) + bf2f((bf16_t)p[i]));
+    *reinterpret_cast<short8*>(out + r * C + c8 * 8) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) embed_bwd_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ dout,
+                                                        float* __restrict__ dtable, long rows, int C) {
+  const long total = rows * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / C;
+    const int c = (int)(e % C);
+    const float g = bf2f(dout[e]);
+    if (g != 0.f) atomicAdd(dtable + (long)idx[r] * C + c, g);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Fused masked L1 pair (model/loss.py:74-75): sums |p1-t| and |p2-t| over valid
+// frames (f < mel_len[b]) without masked_select compaction.
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) l1pair_fwd_kernel(const float* __restrict__ p1, const float* __restrict__ p2,
+                                                         const float* __restrict__ tgt, const int64_t* __restrict__ lens,
+                                                         int M, int Mt, int C, float* __restrict__ sums, long rows) {
+  float s1 = 0.f, s2 = 0.f;
+  const long total = rows * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / C;
+    const int c = (int)(e % C);
+    const int b = (int)(r / M), f = (int)(r % M);
+    if (f >= lens[b]) continue;
+    const float t = tgt[((long)b * Mt + f) * C + c];
+    s1 += fabsf(p1[e] - t);
+    s2 += fabsf(p2[e] - t);
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  __shared__ float red[2][4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][wave] = s1; red[1][wave] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(sums, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(sums + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+__global__ void __launch_bounds__(256) l1pair_bwd_kernel(const float* __restrict__ p1, const float* __restrict__ p2,
+                                                         const float* __restrict__ tgt, const int64_t* __restrict__ lens,
+                                                         int M, int Mt, int C, const float* __restrict__ gscale,
+                                                         const float* __restrict__ count, float* __restrict__ g1,
+                                                         float* __restrict__ g2, long rows) {
+  const float inv = 1.f / fmaxf(*count, 1.f);
+  const float s1 = gscale[0] * inv, s2 = gscale[1] * inv;
+  const long total = rows * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / C;
+    const int c = (int)(e % C);
+    const int b = (int)(r / M), f = (int)(r % M);
+    float a = 0.f, bb = 0.f;
+    if (f < lens[b]) {
+      const float t = tgt[((long)b * Mt + f) * C + c];
+      const float d1 = p1[e] - t, d2 = p2[e] - t;
+      a = d1 > 0.f ? s1 : (d1 < 0.f ? -s1 : 0.f);
+      bb = d2 > 0.f ? s2 : (d2 < 0.f ? -s2 : 0.f);
+    }
+    g1[e] = a;
+    g2[e] = bb;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Global-norm clip + Adam over the flat fp32 arena (model/optimizer.py:10-15,
+// train.py:97).  Pass 1: sum of squares -> ws[0] (fp32 atomics after wave+block
+// reduction).  Pass 2: coef = min(1, clip / (sqrt(ss) + 1e-6)); a non-finite norm
+// skips the update (and counts it) -- no host synchronisation anywhere.
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g, long n, float* __restrict__ out) {
+  float s = 0.f;
+  const long n4 = n / 4;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 v = g4[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    s += g[i] * g[i];
+  s = wave_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n,
+                                                   const float* __restrict__ ss, float clip, float lr, float b1,
+                                                   float b2, float eps, float wd, float bc1, float bc2_sqrt,
+                                                   float* __restrict__ norm_out, long long* __restrict__ skipped) {
+  const float norm = sqrtf(*ss);
+  if (!isfinite(norm)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) { *norm_out = norm; *skipped += 1; }
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *norm_out = norm;
+  const float coef = clip > 0.f ? fminf(1.f, clip / (norm + 1e-6f)) : 1.f;
+  const float step = lr / bc1;
+  const long n4 = n / 4;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
+    float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = ga[k] * coef + wd * pa[k];
+      ma[k] = b1 * ma[k] + (1.f - b1) * gk;
+      va[k] = b2 * va[k] + (1.f - b2) * gk * gk;
+      pa[k] -= step * ma[k] / (sqrtf(va[k]) / bc2_sqrt + eps);
+    }
+    p4[i] = pp; m4[i] = mm; v4[i] = vv;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gk = g[i] * coef + wd * p[i];
+    m[i] = b1 * m[i] + (1.f - b1) * gk;
+    v[i] = b2 * v[i] + (1.f - b2) * gk * gk;
+    p[i] -= step * m[i] / (sqrtf(v[i]) / bc2_sqrt + eps);
+  }
+}
+
+}  // namespace
+
+static int grid_for(long work, int per_thread = 1) {
+  long blocks = (work / per_thread + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  return (int)(blocks > 4096 ? 4096 : blocks);
+}
+
+SSAMD_API int ssamd_lr_fwd(const bf16_t* x, const int64_t* dur, const bf16_t* pe, bf16_t* out, int B, int T, int M,
+                           int C, hipStream_t s) {
+  if (C % 8) return -1;
+  if (B == 0 || M == 0) return 0;
+  hipLaunchKernelGGL(lr_fwd_kernel, dim3(cdiv(M, LR_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, x, dur, pe, out, T,
+                     M, C);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_lr_bwd(const bf16_t* dout, const int64_t* dur, bf16_t* dx, int B, int T, int M, int C,
+                           hipStream_t s) {
+  if (C % 8) return -1;
+  if (B == 0 || T == 0) return 0;
+  hipLaunchKernelGGL(lr_bwd_kernel, dim3(cdiv(T, LR_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, dout, dur, dx, T,
+                     M, C);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_embed_fwd(int mode, const int64_t* ids, const float* vals, const float* bins, int nbins,
+                              const bf16_t* table, const bf16_t* addend, int L, bf16_t* out, int* idx_out, long rows,
+                              int C, hipStream_t s) {
+  if (C % 8) return -1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(rows * (C / 8))), dim3(256), 0, s, mode, ids, vals, bins, nbins,
+                     table, addend, L, out, idx_out, rows, C);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_embed_bwd(const int* idx, const bf16_t* dout, float* dtable, long rows, int C, hipStream_t s) {
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(rows * C)), dim3(256), 0, s, idx, dout, dtable, rows, C);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_l1pair_fwd(const float* p1, const float* p2, const float* tgt, const int64_t* lens, int B, int M,
+                               int Mt, int C, float* sums, hipStream_t s) {
+  long rows = (long)B * M;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(l1pair_fwd_kernel, dim3(grid_for(rows * C, 4)), dim3(256), 0, s, p1, p2, tgt, lens, M, Mt, C,
+                     sums, rows);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_l1pair_bwd(const float* p1, const float* p2, const float* tgt, const int64_t* lens, int B, int M,
+                               int Mt, int C, const float* gscale, const float* count, float* g1, float* g2,
+                               hipStream_t s) {
+  long rows = (long)B * M;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(l1pair_bwd_kernel, dim3(grid_for(rows * C, 4)), dim3(256), 0, s, p1, p2, tgt, lens, M, Mt, C,
+                     gscale, count, g1, g2, rows);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_clip_adam(float* p, const float* g, float* m, float* v, long n, float* ws, float clip, float lr,
+                              float b1, float b2, float eps, float wd, int step, float* norm_out, long long* skipped,
+                              hipStream_t s) {
+  hipMemsetAsync(ws, 0, sizeof(float), s);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, 16)), dim3(256), 0, s, g, n, ws);
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2 = 1.f - powf(b2, (float)step);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 8)), dim3(256), 0, s, p, g, m, v, n, ws, clip, lr, b1, b2, eps, wd,
+                     bc1, sqrtf(bc2), norm_out, skipped);
+  return (int)hipGetLastError();
+}
+
+namespace {
+__global__ void __launch_bounds__(256) relu_mask_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                        bf16_t* __restrict__ out, long n) {
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    short8 a = reinterpret_cast<const short8*>(dy)[i];
+    short8 b = reinterpret_cast<const short8*>(y)[i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = bf2f((bf16_t)b[k]) > 0.f ? a[k] : (short)0;
+    reinterpret_cast<short8*>(out)[i] = a;
+  }
+  for (long i = n8 * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = bf2f(y[i]) > 0.f ? dy[i] : (bf16_t)0;
+}
+}  // namespace
+
+SSAMD_API int ssamd_relu_mask(const bf16_t* dy, const bf16_t* y, bf16_t* out, long n, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(n, 8)), dim3(256), 0, s, dy, y, out, n);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,262 @@
+// Fused residual + LayerNorm + dropout + FiLM + pad-mask (forward / backward).
+//
+//   out = rowmask( FiLM( post_drop( LN( pre_drop(a) + res ) ) ) )
+//   FiLM(y) = (s_g * gamma[b,:] + 1) * y + s_b * beta[b,:]
+//
+// Covers every LayerNorm site of the model: MHA tail (SubLayers.py:54-55 +
+// Layers.py:27-28), FFN tail + FiLM + mask (SubLayers.py:89-91, Layers.py:31-35),
+// variance-predictor ReLU->LN->Dropout (model/modules.py:216-245) and the
+// reference-encoder conv stack.  One wave per row, C/64 contiguous channels per
+// lane (C in {256, 512, 768, 1024}), fp32 statistics, bf16 I/O.  Dropout masks come
+// from a counter hash so the backward regenerates them (no mask tensor).
+// Grid: (ceil(L / 64), B) -> every block works on ONE batch item, which makes
+// the per-(b, c) FiLM gradient sums a block-local reduction.
+#include "common.h"
+
+namespace {
+
+constexpr int WAVES = 4;
+constexpr int ROWS_PER_WAVE = 16;
+constexpr int ROWS_PER_BLOCK = WAVES * ROWS_PER_WAVE;
+
+template <int EPL>
+__device__ __forceinline__ void load_row(const bf16_t* p, float* v) {
+  if constexpr (EPL == 4) {
+    short4v x = *reinterpret_cast<const short4v*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = bf2f((bf16_t)x[i]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < EPL / 8; ++j) {
+      short8 x = *reinterpret_cast<const short8*>(p + 8 * j);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[8 * j + i] = bf2f((bf16_t)x[i]);
+    }
+  }
+}
+
+template <int EPL>
+__device__ __forceinline__ void store_row(bf16_t* p, const float* v) {
+  if constexpr (EPL == 4) {
+    short4v x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = (short)f2bf(v[i]);
+    *reinterpret_cast<short4v*>(p) = x;
+  } else {
+#pragma unroll
+    for (int j = 0; j < EPL / 8; ++j) {
+      short8 x;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = (short)f2bf(v[8 * j + i]);
+      *reinterpret_cast<short8*>(p + 8 * j) = x;
+    }
+  }
+}
+
+template <int EPL>
+__global__ void __launch_bounds__(256) addln_fwd_kernel(
+    const bf16_t* __restrict__ a, const bf16_t* __restrict__ res, const float* __restrict__ w,
+    const float* __restrict__ bias, const float* __restrict__ fg, const float* __restrict__ fb,
+    const float* __restrict__ s_g, const float* __restrict__ s_b, const int64_t* __restrict__ lens,
+    bf16_t* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out, int L, int C,
+    float pre_p, float post_p, uint64_t seed, float eps) {
+  const int b = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c0 = lane * EPL;
+  const int len = lens ? (int)lens[b] : L;
+  float wv[EPL], bv[EPL], G[EPL], Bt[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    wv[i] = w[c0 + i];
+    bv[i] = bias[c0 + i];
+    G[i] = 1.f;
+    Bt[i] = 0.f;
+  }
+  if (fg) {
+    const float sg = *s_g, sb = *s_b;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      G[i] = sg * fg[(long)b * C + c0 + i] + 1.f;
+      Bt[i] = sb * fb[(long)b * C + c0 + i];
+    }
+  }
+  const float invC = 1.f / C;
+  for (int r = 0; r < ROWS_PER_WAVE; ++r) {
+    const int t = blockIdx.x * ROWS_PER_BLOCK + r * WAVES + wave;
+    if (t >= L) break;
+    const long row = (long)b * L + t;
+    float h[EPL];
+    load_row<EPL>(a + row * C + c0, h);
+    if (pre_p > 0.f) {
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) h[i] *= drop_scale(seed, (uint64_t)row * C + c0 + i, pre_p);
+    }
+    if (res) {
+      float rv[EPL];
+      load_row<EPL>(res + row * C + c0, rv);
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) h[i] += rv[i];
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) s += h[i];
+    const float mu = wave_sum(s) * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      const float d = h[i] - mu;
+      q += d * d;
+    }
+    const float rs = rsqrtf(wave_sum(q) * invC + eps);
+    float y[EPL];
+    const bool valid = t < len;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      float v = (h[i] - mu) * rs * wv[i] + bv[i];
+      if (post_p > 0.f) v *= drop_scale(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0 + i, post_p);
+      v = G[i] * v + Bt[i];
+      y[i] = valid ? v : 0.f;
+    }
+    store_row<EPL>(out + row * C + c0, y);
+    if (lane == 0 && mean_out) {
+      mean_out[row] = mu;
+      rstd_out[row] = rs;
+    }
+  }
+}
+
+// Backward.  dh = d(pre_drop(a) + res); da = dh * pre_mask; dres = dh.
+// Accumulates (fp32, atomics after an in-block LDS reduction):
+//   dw[c], db[c]                       LayerNorm affine
+//   S1[b,c] = sum_t dout*yd, S2[b,c] = sum_t dout   (FiLM: dgamma = s_g*S1 ...)
+template <int EPL>
+__global__ void __launch_bounds__(256) addln_bwd_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ a, const bf16_t* __restrict__ res,
+    const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ fg,
+    const float* __restrict__ s_g, const int64_t* __restrict__ lens, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ da_out,
+    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ S1, float* __restrict__ S2, int L, int C,
+    float pre_p, float post_p, uint64_t seed) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][C]
+  const int b = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c0 = lane * EPL;
+  const int len = lens ? (int)lens[b] : L;
+  float wv[EPL], bv[EPL], G[EPL];
+  float acc_w[EPL], acc_b[EPL], acc_s1[EPL], acc_s2[EPL];
+  const float sg = fg ? *s_g : 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    wv[i] = w[c0 + i];
+    bv[i] = bias[c0 + i];
+    G[i] = fg ? sg * fg[(long)b * C + c0 + i] + 1.f : 1.f;
+    acc_w[i] = acc_b[i] = acc_s1[i] = acc_s2[i] = 0.f;
+  }
+  const float invC = 1.f / C;
+  for (int r = 0; r < ROWS_PER_WAVE; ++r) {
+    const int t = blockIdx.x * ROWS_PER_BLOCK + r * WAVES + wave;
+    if (t >= L) break;
+    const long row = (long)b * L + t;
+    float dh[EPL];
+    if (t >= len) {  // masked row: zero gradient flows back
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) dh[i] = 0.f;
+      store_row<EPL>(dh_out + row * C + c0, dh);
+      if (da_out) store_row<EPL>(da_out + row * C + c0, dh);
+      continue;
+    }
+    float h[EPL], m1[EPL];
+    load_row<EPL>(a + row * C + c0, h);
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      m1[i] = drop_scale(seed, (uint64_t)row * C + c0 + i, pre_p);
+      h[i] *= m1[i];
+    }
+    if (res) {
+      float rv[EPL];
+      load_row<EPL>(res + row * C + c0, rv);
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) h[i] += rv[i];
+    }
+    float go[EPL];
+    load_row<EPL>(dout + row * C + c0, go);
+    const float mu = mean_in[row], rs = rstd_in[row];
+    float xh[EPL], dx[EPL];
+    float sum1 = 0.f, sum2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      xh[i] = (h[i] - mu) * rs;
+      const float m2 = drop_scale(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0 + i, post_p);
+      const float y = xh[i] * wv[i] + bv[i];
+      acc_s1[i] += go[i] * y * m2;
+      acc_s2[i] += go[i];
+      const float dy = go[i] * G[i] * m2;
+      acc_w[i] += dy * xh[i];
+      acc_b[i] += dy;
+      dx[i] = dy * wv[i];
+      sum1 += dx[i];
+      sum2 += dx[i] * xh[i];
+    }
+    sum1 = wave_sum(sum1) * invC;
+    sum2 = wave_sum(sum2) * invC;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) dh[i] = rs * (dx[i] - sum1 - xh[i] * sum2);
+    store_row<EPL>(dh_out + row * C + c0, dh);
+    if (da_out) {
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) dh[i] *= m1[i];
+      store_row<EPL>(da_out + row * C + c0, dh);
+    }
+  }
+  // block reduction of the four accumulators, then one atomic per channel
+  float* accs[4] = {acc_w, acc_b, acc_s1, acc_s2};
+  float* dsts[4] = {dw, db, S1 ? S1 + (long)b * C : nullptr, S2 ? S2 + (long)b * C : nullptr};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (dsts[k] == nullptr) continue;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) red[wave * C + c0 + i] = accs[k][i];
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float s = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
+      if (s != 0.f) atomicAdd(dsts[k] + c, s);
+    }
+  }
+}
+
+}  // namespace
+
+#define DISPATCH_EPL(C, ...)                                   \
+  switch ((C) / 64) {                                          \
+    case 4: { constexpr int EPL = 4; __VA_ARGS__; break; }     \
+    case 8: { constexpr int EPL = 8; __VA_ARGS__; break; }     \
+    case 16: { constexpr int EPL = 16; __VA_ARGS__; break; }   \
+    default: return -1;                                        \
+  }
+
+SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w, const float* bias, const float* fg,
+                              const float* fb, const float* s_g, const float* s_b, const int64_t* lens, bf16_t* out,
+                              float* mean, float* rstd, int B, int L, int C, float pre_p, float post_p,
+                              unsigned long long seed, float eps, hipStream_t stream) {
+  if (C % 256 != 0 && C != 256 && C != 512 && C != 1024) return -1;
+  if (B == 0 || L == 0) return 0;
+  dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
+  DISPATCH_EPL(C, hipLaunchKernelGGL(addln_fwd_kernel<EPL>, grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
+                                     s_b, lens, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t* res, const float* w,
+                              const float* bias, const float* fg, const float* s_g, const int64_t* lens,
+                              const float* mean, const float* rstd, bf16_t* dh, bf16_t* da, float* dw, float* db,
+                              float* S1, float* S2, int B, int L, int C, float pre_p, float post_p,
+                              unsigned long long seed, hipStream_t stream) {
+  if (B == 0 || L == 0) return 0;
+  dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
+  size_t lds = (size_t)WAVES * C * sizeof(float);
+  DISPATCH_EPL(C, hipLaunchKernelGGL(addln_bwd_kernel<EPL>, grid, dim3(256), lds, stream, dout, a, res, w, bias, fg,
+                                     s_g, lens, mean, rstd, dh, da, dw, db, S1, S2, L, C, pre_p, post_p,
+                                     (uint64_t)seed));
+  return (int)hipGetLastError();
+}

@@ -105,8 +105,7 @@ class PositionwiseFeedForward(nn.Module):
         self.k = tuple(kernel_size)
 
     def forward(self, x, lengths, film_params=None):
-        h = ops.conv1d(x, self.w_1.weight, self.w_1.bias, (self.k[0] - 1) // 2, 1, "relu")
-        z = ops.conv1d(h, self.w_2.weight, self.w_2.bias, (self.k[1] - 1) // 2, 1, None)
+        z = ops.ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias)
         return ops.add_layernorm(
             z, x, self.layer_norm.weight, self.layer_norm.bias,
             pre_drop=self.dropout, training=self.training, film_params=film_params, lengths=lengths,

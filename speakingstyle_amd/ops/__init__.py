@@ -58,6 +58,14 @@ def conv1d(x, w, b=None, pad=0, dil=1, act=None):
     return ref.conv1d(x, w, b, pad, dil, act)
 
 
+def ffn(x, w1, b1, w2, b2):
+    """Position-wise FFN core: conv(k0) -> ReLU -> conv(k1) (``SubLayers.py:84-87``)."""
+    if use_hip(x):
+        return _hip().ffn(x, w1, b1, w2, b2)
+    h = ref.conv1d(x, w1, b1, (w1.shape[2] - 1) // 2, 1, "relu")
+    return ref.conv1d(h, w2, b2, (w2.shape[2] - 1) // 2, 1, None)
+
+
 def attention(qkv, lengths, n_head):
     if use_hip(qkv):
         return _hip().attention(qkv, lengths, n_head)

@@ -1,0 +1,536 @@
+"""HIP/CDNA4 kernel bindings (``csrc/*.hip`` -> ``_lib/libssamd_kernels.so``).
+
+The library is a plain shared object loaded with ctypes (no torch C++ ABI
+coupling, seconds to rebuild).  Every entry point takes raw device pointers plus
+the current HIP stream, so the kernels order correctly with PyTorch's own work
+and are capturable in HIP graphs.  Shapes, dtypes and contiguity are validated
+on the host before every launch (a wrong shape must never reach a kernel).
+
+Autograd wiring: one ``torch.autograd.Function`` per fused op; master weights
+stay fp32 (flat arena), bf16 operand images in the kernels' layouts are produced
+once per optimizer step and cached on the parameter's version counter.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import threading
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libssamd_kernels.so")
+_lib = None
+_lock = threading.Lock()
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L_ = ctypes.c_long
+F = ctypes.c_float
+U64 = ctypes.c_ulonglong
+
+_SIGS = {
+    "ssamd_conv_gemm": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
+    "ssamd_conv_wgrad": [P, P, P, L_, P, I, I, I, I, I, I, I, I, P],
+    "ssamd_colsum": [P, P, L_, I, P],
+    "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
+    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],
+    "ssamd_lr_fwd": [P, P, P, P, I, I, I, I, P],
+    "ssamd_lr_bwd": [P, P, P, I, I, I, I, P],
+    "ssamd_embed_fwd": [I, P, P, P, I, P, P, I, P, P, L_, I, P],
+    "ssamd_embed_bwd": [P, P, P, L_, I, P],
+    "ssamd_l1pair_fwd": [P, P, P, P, I, I, I, I, P, P],
+    "ssamd_l1pair_bwd": [P, P, P, P, I, I, I, I, P, P, P, P, P],
+    "ssamd_clip_adam": [P, P, P, P, L_, P, F, F, F, F, F, F, I, P, P, P],
+    "ssamd_attn_fwd": [P, P, P, P, I, I, I, I, F, P],
+    "ssamd_attn_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, F, P],
+    "ssamd_relu_mask": [P, P, P, L_, P],
+}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(_LIB_PATH):
+                    raise RuntimeError(
+                        f"HIP kernel library not built: {_LIB_PATH}. Run `python csrc/build.py` "
+                        "(or __graft_entry__.build()). Refusing to fall back to eager PyTorch on a GPU.")
+                handle = ctypes.CDLL(_LIB_PATH)
+                for name, args in _SIGS.items():
+                    fn = getattr(handle, name, None)
+                    if fn is not None:
+                        fn.argtypes = args
+                        fn.restype = I
+                _lib = handle
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (RuntimeError, OSError):
+        return False
+
+
+def has(name: str) -> bool:
+    return getattr(lib(), name, None) is not None
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def _need(t, dtype, name):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: tensor must be on the GPU")
+
+
+# ------------------------------------------------------------------------ weight images
+_wcache = {}
+
+
+def _cached(param: torch.Tensor, kind: str, make):
+    key = (id(param), kind)
+    ver = param._version
+    hit = _wcache.get(key)
+    if hit is not None and hit[0] == ver and hit[1].data_ptr() == param.data_ptr():
+        return hit[2]
+    img = make(param.detach())
+    _wcache[key] = (ver, param, img)
+    return img
+
+
+def weight_fwd(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, ks] (or Linear [out, in]) fp32 -> bf16 [Cout][ks][Cin]."""
+    if w.dim() == 2:
+        return _cached(w, "fwd", lambda x: x.to(torch.bfloat16).contiguous())
+    return _cached(w, "fwd", lambda x: x.permute(0, 2, 1).to(torch.bfloat16).contiguous())
+
+
+def weight_dgrad(w: torch.Tensor) -> torch.Tensor:
+    """-> bf16 [Cin][ks][Cout] with taps flipped (data gradient = conv with W^T)."""
+    if w.dim() == 2:
+        return _cached(w, "dgrad", lambda x: x.t().to(torch.bfloat16).contiguous())
+    return _cached(w, "dgrad", lambda x: x.flip(2).permute(1, 2, 0).to(torch.bfloat16).contiguous())
+
+
+_ACT = {None: 0, "relu": 1, "lrelu": 2, "tanh": 3}
+
+_ws = {}
+
+
+def _workspace(device, nfloats: int) -> torch.Tensor:
+    cur = _ws.get(device)
+    if cur is None or cur.numel() < nfloats:
+        cur = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        _ws[device] = cur
+    return cur
+
+
+# ------------------------------------------------------------------------ raw launchers
+def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, resid=None, lens=None, out_f32=False):
+    _need(x, torch.bfloat16, "conv_gemm.x")
+    _need(wimg, torch.bfloat16, "conv_gemm.w")
+    assert x.numel() == B * L * Cin, "conv_gemm: x shape mismatch"
+    assert wimg.numel() == N * ks * Cin, "conv_gemm: w shape mismatch"
+    if Cin % 8:
+        raise ValueError("conv_gemm: Cin must be a multiple of 8")
+    y = torch.empty(B, L, N, device=x.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    if bias is not None:
+        _need(bias, torch.float32, "conv_gemm.bias")
+        assert bias.numel() == N
+    for t, nm in ((aux, "aux"), (resid, "resid")):
+        if t is not None:
+            _need(t, torch.bfloat16, "conv_gemm." + nm)
+            assert t.numel() == B * L * N
+    if lens is not None:
+        _need(lens, torch.int64, "conv_gemm.lens")
+        assert lens.numel() == B
+    rc = lib().ssamd_conv_gemm(_ptr(x), _ptr(wimg), _ptr(bias), _ptr(aux), _ptr(resid), _ptr(lens), _ptr(y),
+                               int(out_f32), B, L, Cin, ks, dil, pad, N, act, N, _stream())
+    _check(rc, "ssamd_conv_gemm")
+    return y
+
+
+def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N):
+    _need(x, torch.bfloat16, "wgrad.x")
+    _need(dy, torch.bfloat16, "wgrad.dy")
+    assert x.numel() == B * L * Cin and dy.numel() == B * L * N
+    if N % 8:
+        raise ValueError("wgrad: N must be a multiple of 8")
+    K = ks * Cin
+    tiles = ((N + 127) // 128) * ((K + 127) // 128)
+    max_splits = max(1, min(64, (1536 + tiles - 1) // tiles))
+    ws = _workspace(x.device, max_splits * N * K)
+    dW = torch.empty(N, Cin, ks, device=x.device, dtype=torch.float32)
+    rc = lib().ssamd_conv_wgrad(_ptr(x), _ptr(dy), _ptr(ws), ws.numel(), _ptr(dW), B, L, Cin, ks, dil, pad, N,
+                                max_splits, _stream())
+    _check(rc, "ssamd_conv_wgrad")
+    return dW
+
+
+def colsum_raw(dy, N):
+    _need(dy, torch.bfloat16, "colsum.dy")
+    db = torch.empty(N, device=dy.device, dtype=torch.float32)
+    rc = lib().ssamd_colsum(_ptr(dy), _ptr(db), dy.numel() // N, N, _stream())
+    _check(rc, "ssamd_colsum")
+    return db
+
+
+def relu_mask_(dy, y):
+    """dy *= (y > 0) in place (bf16)."""
+    _need(dy, torch.bfloat16, "relu_mask.dy")
+    _need(y, torch.bfloat16, "relu_mask.y")
+    rc = lib().ssamd_relu_mask(_ptr(dy), _ptr(y), _ptr(dy), dy.numel(), _stream())
+    _check(rc, "ssamd_relu_mask")
+    return dy
+
+
+# ------------------------------------------------------------------------ conv / linear
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, pad, dil, act, out_f32):
+        B, L, Cin = x.shape
+        ks = 1 if w.dim() == 2 else w.shape[2]
+        N = w.shape[0]
+        xc = x.contiguous()
+        y = conv_gemm_raw(xc, weight_fwd(w), None if b is None else b.detach().float().contiguous(), B, L, Cin, ks,
+                          dil, pad, N, _ACT[act], out_f32=out_f32)
+        ctx.geom = (B, L, Cin, ks, dil, pad, N)
+        ctx.act = act
+        ctx.has_b = b is not None
+        ctx.save_for_backward(xc, w, y if act == "relu" else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w, y = ctx.saved_tensors
+        B, L, Cin, ks, dil, pad, N = ctx.geom
+        dy = dy.to(torch.bfloat16).contiguous()
+        if ctx.act == "relu":
+            dy = relu_mask_(dy.clone(), y)
+        elif ctx.act is not None:
+            raise NotImplementedError("backward for activation " + str(ctx.act))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin)
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N)
+            if w.dim() == 2:
+                dw = dw.view(N, Cin)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = colsum_raw(dy, N)
+        return dx, dw, db, None, None, None, None
+
+
+def conv1d(x, w, b=None, pad=0, dil=1, act=None, out_f32=False):
+    return _ConvFn.apply(x, w, b, pad, dil, act, out_f32)
+
+
+def linear(x, w, b=None, act=None, out_f32=False):
+    shp = x.shape
+    x3 = x.reshape(1, -1, shp[-1]) if x.dim() != 3 else x
+    if x3.shape[-1] % 8 or w.shape[0] % 8:
+        # tiny heads (e.g. the variance-predictor Linear(256 -> 1)): not MFMA-shaped
+        return ref.linear(x, w, b, act)
+    y = _ConvFn.apply(x3, w, b, 0, 1, act, out_f32)
+    return y.reshape(*shp[:-1], w.shape[0])
+
+
+class _FFNFn(torch.autograd.Function):
+    """conv(k0) -> ReLU -> conv(k1): the ReLU derivative is fused into the
+    data-gradient epilogue of the second conv (aux = h), so no extra pass."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        B, L, C = x.shape
+        k1, k2 = w1.shape[2], w2.shape[2]
+        H = w1.shape[0]
+        xc = x.contiguous()
+        h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1)
+        z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0)
+        ctx.save_for_backward(xc, h, w1, w2)
+        ctx.dims = (B, L, C, H, k1, k2)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        xc, h, w1, w2 = ctx.saved_tensors
+        B, L, C, H, k1, k2 = ctx.dims
+        dz = dz.to(torch.bfloat16).contiguous()
+        p1, p2 = (k1 - 1) // 2, (k2 - 1) // 2
+        dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h)
+        dw2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C)
+        db2 = colsum_raw(dz, C)
+        dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0)
+        dw1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H)
+        db1 = colsum_raw(dh, H)
+        return dx, dw1, db1, dw2, db2
+
+
+def ffn(x, w1, b1, w2, b2):
+    return _FFNFn.apply(x, w1, b1, w2, b2)
+
+
+# ------------------------------------------------------------------------ add + LayerNorm
+_seed_counter = [0x1234]
+
+
+def _next_seed():
+    _seed_counter[0] = (_seed_counter[0] * 6364136223846793005 + 1442695040888963407) & ((1 << 64) - 1)
+    return _seed_counter[0]
+
+
+def set_seed(s: int):
+    _seed_counter[0] = int(s) & ((1 << 64) - 1)
+
+
+class _AddLNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps):
+        B, L, C = a.shape
+        ac = a.contiguous()
+        rc_ = None if res is None else res.contiguous()
+        out = torch.empty_like(ac)
+        mean = torch.empty(B * L, device=a.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        gf = None if g is None else g.detach().float().contiguous()
+        bf = None if bt is None else bt.detach().float().contiguous()
+        rc = lib().ssamd_addln_fwd(_ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb),
+                                   _ptr(lens), _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, pre_p, post_p, seed, eps,
+                                   _stream())
+        _check(rc, "ssamd_addln_fwd")
+        ctx.save_for_backward(ac, rc_, w, b, gf, bf, sg, sb, lens, mean, rstd)
+        ctx.cfg = (B, L, C, pre_p, post_p, seed, res is not None, g is not None)
+        ctx.gdtype = None if g is None else (g.dtype, bt.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ac, rc_, w, b, gf, bf, sg, sb, lens, mean, rstd = ctx.saved_tensors
+        B, L, C, pre_p, post_p, seed, has_res, has_film = ctx.cfg
+        dout = dout.to(torch.bfloat16).contiguous()
+        dh = torch.empty_like(ac)
+        da = torch.empty_like(ac) if pre_p > 0 else None
+        dw = torch.zeros(C, device=ac.device, dtype=torch.float32)
+        db = torch.zeros_like(dw)
+        S1 = torch.zeros(B, C, device=ac.device, dtype=torch.float32) if has_film else None
+        S2 = torch.zeros_like(S1) if has_film else None
+        rc = lib().ssamd_addln_bwd(_ptr(dout), _ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(sg), _ptr(lens),
+                                   _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da), _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
+                                   B, L, C, pre_p, post_p, seed, _stream())
+        _check(rc, "ssamd_addln_bwd")
+        d_a = da if da is not None else dh
+        d_res = dh if has_res else None
+        dg = dbt = dsg = dsb = None
+        if has_film:
+            dg = (S1 * sg).to(ctx.gdtype[0])
+            dbt = (S2 * sb).to(ctx.gdtype[1])
+            dsg = (S1 * gf).sum().reshape(1)
+            dsb = (S2 * bf).sum().reshape(1)
+        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None
+
+
+def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None,
+                  lengths=None, eps=1e-5):
+    C = a.shape[-1]
+    if C not in (256, 512, 1024) or a.dtype != torch.bfloat16:
+        return ref.add_layernorm(a, residual, ln_w, ln_b, pre_drop=pre_drop, post_drop=post_drop, training=training,
+                                 film_params=film_params, lengths=lengths, eps=eps)
+    if not training:
+        pre_drop = post_drop = 0.0
+    g = bt = sg = sb = None
+    if film_params is not None:
+        g, bt, sg, sb = film_params
+    lens = None if lengths is None else lengths.to(torch.int64).contiguous()
+    if residual is not None:
+        residual = residual.to(a.dtype)
+    out = _AddLNFn.apply(a, residual, ln_w, ln_b, g, bt, sg, sb, lens, float(pre_drop), float(post_drop),
+                         _next_seed(), float(eps))
+    return out
+
+
+# ------------------------------------------------------------------------ length regulator
+class _LRFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dur, M, pe):
+        B, T, C = x.shape
+        xc = x.contiguous()
+        out = torch.empty(B, M, C, device=x.device, dtype=x.dtype)
+        pe_c = None if pe is None else pe.to(x.dtype).contiguous()
+        if pe_c is not None:
+            assert pe_c.shape[0] >= M and pe_c.shape[1] == C
+        rc = lib().ssamd_lr_fwd(_ptr(xc), _ptr(dur), _ptr(pe_c), _ptr(out), B, T, M, C, _stream())
+        _check(rc, "ssamd_lr_fwd")
+        ctx.save_for_backward(dur)
+        ctx.dims = (B, T, M, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (dur,) = ctx.saved_tensors
+        B, T, M, C = ctx.dims
+        dout = dout.to(torch.bfloat16).contiguous()
+        dx = torch.empty(B, T, C, device=dout.device, dtype=torch.bfloat16)
+        rc = lib().ssamd_lr_bwd(_ptr(dout), _ptr(dur), _ptr(dx), B, T, M, C, _stream())
+        _check(rc, "ssamd_lr_bwd")
+        return dx, None, None, None
+
+
+def length_regulate(x, durations, max_len, pe=None):
+    if x.dtype != torch.bfloat16 or x.shape[-1] % 8:
+        out, ml = ref.length_regulate(x, durations, max_len)
+        return (out + pe[: out.shape[1]].to(out.dtype) if pe is not None else out), ml
+    dur = durations.to(torch.int64).contiguous()
+    mel_len = dur.clamp(min=0).sum(1)
+    if max_len is None:
+        max_len = int(mel_len.max().item()) if dur.shape[0] else 0  # inference: one D2H for allocation
+    return _LRFn.apply(x, dur, int(max_len), pe), mel_len
+
+
+# ------------------------------------------------------------------------ embeddings
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mode, ids, vals, bins, table, addend, L):
+        C = table.shape[1]
+        rows = (ids if mode == 0 else vals).numel()
+        out_shape = (*((ids if mode == 0 else vals).shape), C)
+        out = torch.empty(out_shape, device=table.device, dtype=torch.bfloat16)
+        idx = torch.empty(rows, device=table.device, dtype=torch.int32)
+        tb = table.to(torch.bfloat16).contiguous()
+        ad = addend.to(torch.bfloat16).contiguous()
+        rc = lib().ssamd_embed_fwd(mode, _ptr(ids), _ptr(vals), _ptr(bins), 0 if bins is None else bins.numel(),
+                                   _ptr(tb), _ptr(ad), L, _ptr(out), _ptr(idx), rows, C, _stream())
+        _check(rc, "ssamd_embed_fwd")
+        ctx.save_for_backward(idx)
+        ctx.tshape = (table.shape, table.dtype)
+        ctx.mode = mode
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (idx,) = ctx.saved_tensors
+        shape, dtype = ctx.tshape
+        dout = dout.to(torch.bfloat16).contiguous()
+        dt = torch.zeros(shape, device=dout.device, dtype=torch.float32)
+        rc = lib().ssamd_embed_bwd(_ptr(idx), _ptr(dout), _ptr(dt), idx.numel(), shape[1], _stream())
+        _check(rc, "ssamd_embed_bwd")
+        d_add = dout if ctx.mode == 1 else None
+        return None, None, None, None, dt.to(dtype), d_add, None
+
+
+def embed_add_pe(ids, table, pe, extra=None):
+    B, L = ids.shape
+    out = _EmbedFn.apply(0, ids.contiguous(), None, None, table, pe[:L].contiguous(), L)
+    if extra is not None:
+        out = out + extra.unsqueeze(1).to(out.dtype)
+    return out
+
+
+def bucketize_embed_add(x, values, bins, table):
+    return _EmbedFn.apply(1, None, values.float().contiguous(), bins.float().contiguous(), table, x, 0)
+
+
+# ------------------------------------------------------------------------ attention
+def attention(qkv, lengths, n_head):
+    if not has("ssamd_attn_fwd"):
+        return ref.attention(qkv, lengths, n_head)
+    return _AttnFn.apply(qkv, lengths.to(torch.int64).contiguous(), n_head)
+
+
+class _AttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, lens, n_head):
+        B, L, C3 = qkv.shape
+        D = C3 // (3 * n_head)
+        if D not in (32, 64, 128):
+            raise ValueError("attention head dim must be 32/64/128")
+        q = qkv.contiguous()
+        o = torch.empty(B, L, n_head * D, device=q.device, dtype=torch.bfloat16)
+        lse = torch.empty(B, n_head, L, device=q.device, dtype=torch.float32)
+        rc = lib().ssamd_attn_fwd(_ptr(q), _ptr(lens), _ptr(o), _ptr(lse), B, L, n_head, D, 1.0 / math.sqrt(D),
+                                  _stream())
+        _check(rc, "ssamd_attn_fwd")
+        ctx.save_for_backward(q, lens, o, lse)
+        ctx.dims = (B, L, n_head, D)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, lens, o, lse = ctx.saved_tensors
+        B, L, H, D = ctx.dims
+        do = do.to(torch.bfloat16).contiguous()
+        dqkv = torch.empty_like(q)
+        delta = torch.empty(B, H, L, device=q.device, dtype=torch.float32)
+        rc = lib().ssamd_attn_bwd(_ptr(q), _ptr(lens), _ptr(o), _ptr(lse), _ptr(do), _ptr(dqkv), _ptr(delta), None, B,
+                                  L, H, D, 1.0 / math.sqrt(D), _stream())
+        _check(rc, "ssamd_attn_bwd")
+        return dqkv, None, None
+
+
+# ------------------------------------------------------------------------ loss / optimizer
+class _L1PairFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p1, p2, tgt, lens, count):
+        B, M, C = p1.shape
+        Mt = tgt.shape[1]
+        p1c, p2c, tc = p1.float().contiguous(), p2.float().contiguous(), tgt.float().contiguous()
+        sums = torch.zeros(2, device=p1.device, dtype=torch.float32)
+        rc = lib().ssamd_l1pair_fwd(_ptr(p1c), _ptr(p2c), _ptr(tc), _ptr(lens), B, M, Mt, C, _ptr(sums), _stream())
+        _check(rc, "ssamd_l1pair_fwd")
+        cnt = count.float().reshape(1).contiguous()
+        ctx.save_for_backward(p1c, p2c, tc, lens, cnt)
+        res = sums / cnt.clamp(min=1)
+        return res[0], res[1]
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        p1c, p2c, tc, lens, cnt = ctx.saved_tensors
+        B, M, C = p1c.shape
+        gs = torch.stack([g1.reshape(()), g2.reshape(())]).float().contiguous()
+        d1 = torch.empty_like(p1c)
+        d2 = torch.empty_like(p2c)
+        rc = lib().ssamd_l1pair_bwd(_ptr(p1c), _ptr(p2c), _ptr(tc), _ptr(lens), B, M, tc.shape[1], C, _ptr(gs),
+                                    _ptr(cnt), _ptr(d1), _ptr(d2), _stream())
+        _check(rc, "ssamd_l1pair_bwd")
+        return d1, d2, None, None, None
+
+
+def masked_l1_pair(mel_p, post_p, mel_t, mel_valid, count):
+    lens = mel_valid.sum(1).to(torch.int64).contiguous()
+    return _L1PairFn.apply(mel_p, post_p, mel_t, lens, count)
+
+
+_adam_ws = {}
+
+
+def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped):
+    for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
+        _need(t, torch.float32, "adam." + nm)
+    assert p.numel() == g.numel() == m.numel() == v.numel()
+    ws = _adam_ws.get(p.device)
+    if ws is None:
+        ws = _adam_ws[p.device] = torch.zeros(4, device=p.device, dtype=torch.float32)
+    rc = lib().ssamd_clip_adam(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(ws), float(clip), float(lr),
+                               float(betas[0]), float(betas[1]), float(eps), float(wd), int(step), _ptr(norm_out),
+                               _ptr(skipped), _stream())
+    _check(rc, "ssamd_clip_adam")

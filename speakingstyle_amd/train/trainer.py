@@ -1,0 +1,79 @@
+"""Training step / loop shared by ``train.py`` and ``bench.py``.
+
+Per step (reference ``train.py:79-101``): forward -> loss -> (loss / grad_acc)
+backward -> every ``grad_acc_step``: clip + Adam + LR schedule + zero_grad.
+MI355X-specific structure:
+
+* multi-process DP (``parallel/ddp.py``): the global valid-element counts are
+  all-reduced asynchronously at the start of the step (overlapping the forward)
+  and the loss divides by them; gradient buckets are all-reduced during
+  backward; the fused clip+Adam kernel runs once ``finish()`` has ordered the
+  compute stream after the last bucket.
+* no host synchronisation inside the step: lengths needed for allocation come
+  with the batch (``max_src_len``, ``max_mel_len``), loss values stay on the
+  device until a ``log_step``.
+* non-finite guard without sync: a non-finite global gradient norm makes the
+  Adam kernel skip the update (``optimizer.skipped_steps`` counts them).
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import torch
+
+from ..models.loss import FastSpeech2Loss
+from ..parallel import ddp
+from .optim import ScheduledOptim
+
+
+class Trainer:
+    def __init__(self, model, configs, restore_step: int = 0, bucket_mb: Optional[float] = None):
+        preprocess_config, model_config, train_config = configs
+        self.model = model
+        self.configs = configs
+        self.loss_fn = FastSpeech2Loss(preprocess_config, train_config)
+        self.opt = ScheduledOptim(model, train_config, model_config, restore_step)
+        self.grad_acc = int(train_config["optimizer"]["grad_acc_step"])
+        self.world = ddp.world_size()
+        bm = bucket_mb if bucket_mb is not None else train_config.get("mi355x", {}).get("bucket_mb", 32)
+        self.buckets = ddp.GradBuckets(self.opt.arena, bm)
+        self.n_mel = preprocess_config["preprocessing"]["mel"]["n_mel_channels"]
+        self.max_seq_len = model_config["max_seq_len"]
+        self.micro = 0
+        self.last_lr = self.opt._get_lr()
+
+    def _global_counts(self, batch):
+        """[mel elements, phonemes, mel frames] valid in this rank's batch (device, fp32)."""
+        src_lens, mel_lens = batch[4], batch[7]
+        frames = mel_lens.clamp(max=self.max_seq_len).sum()
+        c = torch.stack([frames * self.n_mel, src_lens.sum(), frames]).float()
+        work = ddp.all_reduce_async(c)
+        return c, work
+
+    def train_step(self, batch):
+        self.model.train()
+        counts, work = self._global_counts(batch) if self.world > 1 else (None, None)
+        last_micro = (self.micro + 1) % self.grad_acc == 0
+        output = self.model(*batch[2:])
+        if work is not None:
+            work.wait()
+        named = self.model.film_scalars()
+        losses = self.loss_fn(batch, output, named, global_counts=counts)
+        total = losses[0]
+        if self.world > 1 and named is not None and self.loss_fn.lambda_f > 0:
+            # the FiLM L2 term is identical on every rank: scale so the SUM all-reduce counts it once
+            total = total - (1.0 - 1.0 / self.world) * self.loss_fn.lambda_f * torch.sum(torch.square(named))
+        if last_micro or self.world == 1:
+            (total / self.grad_acc).backward()
+        else:
+            with self.buckets.no_sync():
+                (total / self.grad_acc).backward()
+        self.micro += 1
+        lr = None
+        if last_micro:
+            self.buckets.finish()
+            lr = self.opt.step_and_update_lr()
+            self.opt.zero_grad()
+            self.last_lr = lr
+        return losses, output, lr
