@@ -52,3 +52,9 @@ static __device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, 
 }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Allow > 64 KiB of dynamic LDS for a kernel (gfx950: 160 KiB per CU).  Once per kernel.
+template <typename Kern>
+static inline void allow_lds(Kern k, size_t bytes) {
+  if (bytes > 65536) hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}

@@ -1,0 +1,478 @@
+// Fused multi-head self-attention with key-padding mask (flash-style, O(L) memory).
+//
+// Reference math: transformer/Modules.py:14-23 + SubLayers.py:39-57 -- softmax over
+// keys of QK^T / sqrt(d_k), keys >= len[b] masked to -inf, times V.  Heads are read
+// straight out of the fused QKV projection output qkv[B, L, 3*H*D] (channel h*D+d of
+// each third), the output is written head-interleaved o[B, L, H*D]; no permute copies.
+//
+// Forward (per block: 64 queries of one (b, h), 4 waves x 16 queries):
+//   S^T = K Q^T is computed "swapped" (A = K tile from LDS, B = Q fragments kept in
+//   registers) so that the 16x16 accumulator puts ONE query per lane column; the
+//   online softmax is then lane-local plus two cross-group shuffles, and the bf16
+//   P^T accumulator is *directly* the B operand of O^T += V^T P^T (key order
+//   permuted consistently on both operands).  V^T fragments come from LDS through
+//   ds_read_b64_tr_b16.  Scores live in the log2 domain (exp2); lse is stored as
+//   log2-domain m + log2(l) per (b, h, q).
+// Backward (FA2 split, no atomics, deterministic):
+//   delta = rowsum(dO * O);  kernel dKdV: per 64-key block, key on the MFMA lane,
+//   stream query tiles: S, dP -> P, dS are already the B operands of dV^T += dO^T P and
+//   dK^T += Q^T dS;  kernel dQ: per 64-query block, swapped again (query on the lane),
+//   dQ^T += K^T dS^T.  Every LDS image is XOR-swizzled for its read instruction
+//   (ds_read_b128 row reads / ds_read_b64_tr_b16 transposed reads).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int TQ = 64;   // queries per block
+constexpr int TK = 64;   // keys per tile
+
+__device__ __forceinline__ short4v tr_read(const char* p) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+// [rows][D] bf16 image read by 16-B rows (MFMA A/B "row" fragments)
+template <int D>
+__device__ __forceinline__ int row_off(int row, int c16) {
+  constexpr int RPB = 256 / (2 * D);  // rows per 256-B bank row
+  constexpr int CPR = D / 8;          // 16-B chunks per row
+  return row * (2 * D) + ((c16 ^ ((row / RPB) % CPR)) << 4);
+}
+// [rows][D] bf16 image read by ds_read_b64_tr_b16 (8-B chunks)
+template <int D>
+__device__ __forceinline__ int tr_off(int row, int c8) {
+  constexpr int RPB = 256 / (2 * D);
+  constexpr int CPR4 = D / 16;  // (8-B chunks per row) / 4
+  return row * (2 * D) + ((c8 ^ (((row / RPB) % CPR4) << 2)) << 3);
+}
+
+// stage a [64][D] tile (rows r0.., channel offset coff) of the [B*L, RS] matrix into registers
+template <int D>
+__device__ __forceinline__ void load_tile(const bf16_t* base, long row0, int nvalid, int RS, short8* regs) {
+  constexpr int CPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+    const int e = threadIdx.x + NT * i;
+    const int r = e / CPR, c = e % CPR;
+    short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < nvalid) v = *reinterpret_cast<const short8*>(base + (row0 + r) * (long)RS + c * 8);
+    regs[i] = v;
+  }
+}
+template <int D>
+__device__ __forceinline__ void store_row_img(char* img, const short8* regs) {
+  constexpr int CPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+    const int e = threadIdx.x + NT * i;
+    *reinterpret_cast<short8*>(img + row_off<D>(e / CPR, e % CPR)) = regs[i];
+  }
+}
+template <int D>
+__device__ __forceinline__ void store_tr_img(char* img, const short8* regs) {
+  constexpr int CPR = D / 8;
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+    const int e = threadIdx.x + NT * i;
+    *reinterpret_cast<short8*>(img + tr_off<D>(e / CPR, 2 * (e % CPR))) = regs[i];
+  }
+}
+
+__device__ __forceinline__ short8 pack8(const float4v& a, const float4v& b) {
+  short8 r;
+  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
+  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
+  return r;
+}
+
+// A fragment (16 rows x 32) of a transposed image: rows = reduction keys/queries in the
+// permuted order {base + 4g + q} u {base + 16 + 4g + q}, columns col0 .. col0+15.
+template <int D>
+__device__ __forceinline__ short8 tr_frag(const char* img, int base, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int c8 = col0 / 4 + p;
+  short4v a = tr_read(img + tr_off<D>(base + 4 * g + q, c8));
+  short4v b = tr_read(img + tr_off<D>(base + 16 + 4 * g + q, c8));
+  return (short8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// ------------------------------------------------------------------------------ forward
+template <int D>
+__global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
+                                                      bf16_t* __restrict__ out, float* __restrict__ lse, int L, int H,
+                                                      float scale_log2) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * TK * D * 2];
+  char* Ks = smem;
+  char* Vs = smem + TK * D * 2;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int RS = 3 * H * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int len = (int)lens[b];
+  const long rowb = (long)b * L;
+  const int q = blockIdx.x * TQ + wave * 16 + (lane & 15);
+  const bf16_t* Qp = qkv + h * D;
+  const bf16_t* Kp = qkv + H * D + h * D;
+  const bf16_t* Vp = qkv + 2 * H * D + h * D;
+
+  short8 qf[D / 32];
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q < L) v = *reinterpret_cast<const short8*>(Qp + (rowb + q) * RS + s * 32 + 8 * g);
+    qf[s] = v;
+  }
+  float4v oacc[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) oacc[i] = (float4v){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  const int nkt = (len + TK - 1) / TK;
+  short8 rk[D / 32], rv[D / 32];
+  if (nkt > 0) {
+    load_tile<D>(Kp, rowb, min(TK, len), RS, rk);
+    load_tile<D>(Vp, rowb, min(TK, len), RS, rv);
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    store_row_img<D>(Ks, rk);
+    store_tr_img<D>(Vs, rv);
+    __syncthreads();
+    if (kt + 1 < nkt) {
+      const int k1 = (kt + 1) * TK;
+      load_tile<D>(Kp, rowb + k1, min(TK, len - k1), RS, rk);
+      load_tile<D>(Vp, rowb + k1, min(TK, len - k1), RS, rv);
+    }
+    float4v st[4];
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf) {
+      st[kf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) {
+        short8 a = *reinterpret_cast<const short8*>(Ks + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
+        st[kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[s], st[kf], 0, 0, 0);
+      }
+    }
+    const int key0 = kt * TK;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = key0 + kf * 16 + 4 * g + r;
+        const float x = key < len ? st[kf][r] * scale_log2 : -INFINITY;
+        st[kf][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(st[kf][r] - mn);
+        st[kf][r] = p;
+        ls += p;
+      }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) oacc[i] *= alpha;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const short8 pb = pack8(st[2 * hh], st[2 * hh + 1]);
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) {
+        const short8 a = tr_frag<D>(Vs, hh * 32, df * 16, lane);
+        oacc[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, oacc[df], 0, 0, 0);
+      }
+    }
+  }
+  if (q < L) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16_t* op = out + (rowb + q) * (long)(H * D) + h * D;
+#pragma unroll
+    for (int df = 0; df < D / 16; ++df) {
+      short4v v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(oacc[df][r] * inv);
+      *reinterpret_cast<short4v*>(op + df * 16 + 4 * g) = v;
+    }
+    if (g == 0) lse[(long)bh * L + q] = l > 0.f ? m + log2f(l) : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+__global__ void __launch_bounds__(NT) attn_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dO,
+                                                        float* __restrict__ delta, long rows, int H, int D) {
+  // one wave per (row, head): delta[b, h, t] = sum_d dO * O
+  const long wid = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wid >= rows * H) return;
+  const long row = wid / H;
+  const int h = (int)(wid % H);
+  const long L_dummy = 0;
+  (void)L_dummy;
+  float s = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const long idx = row * (long)H * D + h * D + d;
+    s += bf2f(o[idx]) * bf2f(dO[idx]);
+  }
+  s = wave_sum(s);
+  if (lane == 0) delta[wid] = s;  // laid out [row][h]; transposed by the consumers' indexing
+}
+
+template <int D>
+__global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
+                                                           const int64_t* __restrict__ lens,
+                                                           const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                           int L, int H, float scale_log2, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Qr = smem;
+  char* Qt = Qr + TQ * D * 2;
+  char* Dr = Qt + TQ * D * 2;
+  char* Dt = Dr + TQ * D * 2;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int RS = 3 * H * D, OS = H * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int len = (int)lens[b];
+  const long rowb = (long)b * L;
+  const int key = blockIdx.x * TK + wave * 16 + (lane & 15);
+  const bf16_t* Qp = qkv + h * D;
+  const bf16_t* Kp = qkv + H * D + h * D;
+  const bf16_t* Vp = qkv + 2 * H * D + h * D;
+  const bf16_t* dOp = dO + h * D;
+
+  short8 kb[D / 32], vb[D / 32];
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    short8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (key < L) {
+      kv = *reinterpret_cast<const short8*>(Kp + (rowb + key) * RS + s * 32 + 8 * g);
+      vv = *reinterpret_cast<const short8*>(Vp + (rowb + key) * RS + s * 32 + 8 * g);
+    }
+    kb[s] = kv;
+    vb[s] = vv;
+  }
+  float4v dk[D / 16], dv[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) dk[i] = dv[i] = (float4v){0.f, 0.f, 0.f, 0.f};
+  const bool key_valid = key < len;
+
+  const int nqt = (blockIdx.x * TK < len) ? (L + TQ - 1) / TQ : 0;  // key block fully masked -> zero grads
+  short8 rq[D / 32], rd[D / 32];
+  if (nqt > 0) {
+    load_tile<D>(Qp, rowb, min(TQ, L), RS, rq);
+    load_tile<D>(dOp, rowb, min(TQ, L), OS, rd);
+  }
+  for (int qt = 0; qt < nqt; ++qt) {
+    __syncthreads();
+    store_row_img<D>(Qr, rq);
+    store_tr_img<D>(Qt, rq);
+    store_row_img<D>(Dr, rd);
+    store_tr_img<D>(Dt, rd);
+    __syncthreads();
+    if (qt + 1 < nqt) {
+      const int q1 = (qt + 1) * TQ;
+      load_tile<D>(Qp, rowb + q1, min(TQ, L - q1), RS, rq);
+      load_tile<D>(dOp, rowb + q1, min(TQ, L - q1), OS, rd);
+    }
+    float4v sp[4], dp[4];
+#pragma unroll
+    for (int qf = 0; qf < 4; ++qf) {
+      sp[qf] = dp[qf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) {
+        const short8 aq = *reinterpret_cast<const short8*>(Qr + row_off<D>(qf * 16 + (lane & 15), s * 4 + g));
+        const short8 ad = *reinterpret_cast<const short8*>(Dr + row_off<D>(qf * 16 + (lane & 15), s * 4 + g));
+        sp[qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kb[s], sp[qf], 0, 0, 0);
+        dp[qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vb[s], dp[qf], 0, 0, 0);
+      }
+    }
+    // P = exp2(S*c - lse2[q]); dS = P * (dP - delta[q]); rows = queries qt*64 + qf*16 + 4g + r
+#pragma unroll
+    for (int qf = 0; qf < 4; ++qf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qt * TQ + qf * 16 + 4 * g + r;
+        float p = 0.f, ds = 0.f;
+        if (qq < L && key_valid) {
+          p = exp2f(sp[qf][r] * scale_log2 - lse[(long)bh * L + qq]);
+          ds = p * (dp[qf][r] - delta[(rowb + qq) * H + h]);
+        }
+        sp[qf][r] = p;
+        dp[qf][r] = ds;
+      }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const short8 pb = pack8(sp[2 * hh], sp[2 * hh + 1]);
+      const short8 sb = pack8(dp[2 * hh], dp[2 * hh + 1]);
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) {
+        const short8 ado = tr_frag<D>(Dt, hh * 32, df * 16, lane);
+        dv[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pb, dv[df], 0, 0, 0);
+        const short8 aq = tr_frag<D>(Qt, hh * 32, df * 16, lane);
+        dk[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, sb, dk[df], 0, 0, 0);
+      }
+    }
+  }
+  if (key < L) {
+    bf16_t* dkp = dqkv + (rowb + key) * RS + H * D + h * D;
+    bf16_t* dvp = dqkv + (rowb + key) * RS + 2 * H * D + h * D;
+#pragma unroll
+    for (int df = 0; df < D / 16; ++df) {
+      short4v a, c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = (short)f2bf(dk[df][r] * scale);
+        c[r] = (short)f2bf(dv[df][r]);
+      }
+      *reinterpret_cast<short4v*>(dkp + df * 16 + 4 * g) = a;
+      *reinterpret_cast<short4v*>(dvp + df * 16 + 4 * g) = c;
+    }
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
+                                                         const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                                                         const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                         int L, int H, float scale_log2, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kr = smem;
+  char* Kt = Kr + TK * D * 2;
+  char* Vr = Kt + TK * D * 2;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int RS = 3 * H * D, OS = H * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int len = (int)lens[b];
+  const long rowb = (long)b * L;
+  const int q = blockIdx.x * TQ + wave * 16 + (lane & 15);
+  const bf16_t* Qp = qkv + h * D;
+  const bf16_t* Kp = qkv + H * D + h * D;
+  const bf16_t* Vp = qkv + 2 * H * D + h * D;
+
+  short8 qf[D / 32], df_[D / 32];
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    short8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q < L) {
+      a = *reinterpret_cast<const short8*>(Qp + (rowb + q) * RS + s * 32 + 8 * g);
+      c = *reinterpret_cast<const short8*>(dO + (rowb + q) * OS + h * D + s * 32 + 8 * g);
+    }
+    qf[s] = a;
+    df_[s] = c;
+  }
+  const float lq = q < L ? lse[(long)bh * L + q] : 0.f;
+  const float dq_delta = q < L ? delta[(rowb + q) * H + h] : 0.f;
+  float4v dq[D / 16];
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) dq[i] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (len + TK - 1) / TK;
+  short8 rk[D / 32], rv[D / 32];
+  if (nkt > 0) {
+    load_tile<D>(Kp, rowb, min(TK, len), RS, rk);
+    load_tile<D>(Vp, rowb, min(TK, len), RS, rv);
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    store_row_img<D>(Kr, rk);
+    store_tr_img<D>(Kt, rk);
+    store_row_img<D>(Vr, rv);
+    __syncthreads();
+    if (kt + 1 < nkt) {
+      const int k1 = (kt + 1) * TK;
+      load_tile<D>(Kp, rowb + k1, min(TK, len - k1), RS, rk);
+      load_tile<D>(Vp, rowb + k1, min(TK, len - k1), RS, rv);
+    }
+    float4v st[4], dpt[4];
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf) {
+      st[kf] = dpt[kf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) {
+        const short8 ak = *reinterpret_cast<const short8*>(Kr + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
+        const short8 av = *reinterpret_cast<const short8*>(Vr + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
+        st[kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[s], st[kf], 0, 0, 0);
+        dpt[kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df_[s], dpt[kf], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * TK + kf * 16 + 4 * g + r;
+        float ds = 0.f;
+        if (key < len && q < L) {
+          const float p = exp2f(st[kf][r] * scale_log2 - lq);
+          ds = p * (dpt[kf][r] - dq_delta);
+        }
+        st[kf][r] = ds;
+      }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const short8 sb = pack8(st[2 * hh], st[2 * hh + 1]);
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) {
+        const short8 ak = tr_frag<D>(Kt, hh * 32, df * 16, lane);
+        dq[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, sb, dq[df], 0, 0, 0);
+      }
+    }
+  }
+  if (q < L) {
+    bf16_t* dqp = dqkv + (rowb + q) * RS + h * D;
+#pragma unroll
+    for (int df = 0; df < D / 16; ++df) {
+      short4v a;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = (short)f2bf(dq[df][r] * scale);
+      *reinterpret_cast<short4v*>(dqp + df * 16 + 4 * g) = a;
+    }
+  }
+}
+
+}  // namespace
+
+#define ATTN_DISPATCH(D, ...)                                  \
+  switch (D) {                                                 \
+    case 32: { constexpr int DD = 32; __VA_ARGS__; break; }    \
+    case 64: { constexpr int DD = 64; __VA_ARGS__; break; }    \
+    case 128: { constexpr int DD = 128; __VA_ARGS__; break; }  \
+    default: return -1;                                        \
+  }
+
+static const float kLog2e = 1.4426950408889634f;
+
+SSAMD_API int ssamd_attn_fwd(const bf16_t* qkv, const int64_t* lens, bf16_t* out, float* lse, int B, int L, int H,
+                             int D, float scale, hipStream_t s) {
+  if ((long)B * L == 0) return 0;
+  dim3 grid(cdiv(L, TQ), B * H);
+  ATTN_DISPATCH(D, hipLaunchKernelGGL(attn_fwd_kernel<DD>, grid, dim3(NT), 0, s, qkv, lens, out, lse, L, H,
+                                      scale * kLog2e));
+  return (int)hipGetLastError();
+}
+
+// lse: [B, H, L] log2-domain; delta workspace: [B*L*H] fp32
+SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const bf16_t* o, const float* lse,
+                             const bf16_t* dO, bf16_t* dqkv, float* delta, void* unused, int B, int L, int H, int D,
+                             float scale, hipStream_t s) {
+  (void)unused;
+  if ((long)B * L == 0) return 0;
+  const long rows = (long)B * L;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
+  dim3 grid(cdiv(L, TK), B * H);
+  ATTN_DISPATCH(D, {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<DD>, grid, dim3(NT), 4 * TQ * DD * 2, s, qkv, lens, dO, lse, delta, dqkv, L,
+                       H, scale * kLog2e, scale);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<DD>, grid, dim3(NT), 3 * TK * DD * 2, s, qkv, lens, dO, lse, delta, dqkv, L,
+                       H, scale * kLog2e, scale);
+  });
+  return (int)hipGetLastError();
+}

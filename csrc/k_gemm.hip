@@ -393,6 +393,12 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
   const int nwg = ((g.M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = (size_t)BM * CSTRIDE * 4;  // >= 2 stages x (A+B) = 64 KiB
+  static bool lds_set = false;
+  if (!lds_set) {
+    allow_lds(conv_gemm_kernel<true>, lds);
+    allow_lds(conv_gemm_kernel<false>, lds);
+    lds_set = true;
+  }
   if (out_f32)
     hipLaunchKernelGGL(conv_gemm_kernel<true>, dim3(nwg), dim3(NT), lds, s, X, W, bias, aux, resid, lens, Y, g, act, ldy);
   else

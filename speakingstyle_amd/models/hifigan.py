@@ -1,0 +1,322 @@
+"""HiFi-GAN V1 vocoder (generator + multi-period / multi-scale discriminators + losses).
+
+Reference: ``hifigan/models.py`` (generator ``:112-174``, ResBlock1 ``:20-110``,
+MSD ``:176-232``, losses ``:234-264``) and ``hifigan/config.json``.  The
+reference's discriminator side cannot run (``MultiPeriodDiscriminator`` is
+imported by ``hifigan/train.py:17`` but never defined, ``spectral_norm`` /
+``AvgPool1d`` are not imported -- SURVEY D16); here both discriminators are
+implemented (MPD follows the HiFi-GAN paper: periods 2, 3, 5, 7, 11).
+
+State-dict keys of the generator match the reference (``conv_pre``, ``ups.i``,
+``resblocks.j.convs{1,2}.k``, ``conv_post`` with weight-norm ``weight_g`` /
+``weight_v``), so ``generator_*.pth.tar`` files load.  ``fold_weight_norm()``
+replaces every weight-normed conv by its folded weight (reference
+``remove_weight_norm``) for inference.
+
+Inference runs channel-last through ``ops.conv1d`` (HIP implicit-GEMM conv with
+fused LeakyReLU / tanh epilogues on the GPU); the transposed convolutions use a
+polyphase decomposition into ``stride`` ordinary convolutions whose outputs
+interleave, so they run on the same MFMA kernel.  Training runs in PyTorch NCL
+layout with autograd (vocoder training is not a headline config).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.nn.utils import spectral_norm, weight_norm
+
+from .. import ops
+
+LRELU_SLOPE = 0.1
+
+
+class AttrDict(dict):
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.__dict__ = self
+
+
+def default_config() -> AttrDict:
+    """HiFi-GAN V1 (the reference's ``hifigan/config.json``)."""
+    return AttrDict({
+        "resblock": "1", "num_gpus": 0, "batch_size": 16, "learning_rate": 0.0002, "adam_b1": 0.8,
+        "adam_b2": 0.99, "lr_decay": 0.999, "seed": 1234, "upsample_rates": [8, 8, 2, 2],
+        "upsample_kernel_sizes": [16, 16, 4, 4], "upsample_initial_channel": 512,
+        "resblock_kernel_sizes": [3, 7, 11], "resblock_dilation_sizes": [[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+        "segment_size": 8192, "num_mels": 80, "num_freq": 1025, "n_fft": 1024, "hop_size": 256, "win_size": 1024,
+        "sampling_rate": 22050, "fmin": 0, "fmax": 8000, "fmax_for_loss": None, "num_workers": 4,
+        "dist_config": {"dist_backend": "nccl", "dist_url": "tcp://127.0.0.1:54321", "world_size": 1},
+    })
+
+
+def get_padding(k, d=1):
+    return (k * d - d) // 2
+
+
+def _init(m, std=0.01):
+    if isinstance(m, (nn.Conv1d, nn.ConvTranspose1d)):
+        m.weight.data.normal_(0.0, std)
+
+
+def _w(conv):
+    """Effective weight of a (possibly weight-normed) conv."""
+    return conv.weight
+
+
+class ResBlock1(nn.Module):
+    def __init__(self, channels, kernel_size=3, dilation=(1, 3, 5)):
+        super().__init__()
+        self.convs1 = nn.ModuleList(
+            weight_norm(nn.Conv1d(channels, channels, kernel_size, 1, dilation=d, padding=get_padding(kernel_size, d)))
+            for d in dilation)
+        self.convs2 = nn.ModuleList(
+            weight_norm(nn.Conv1d(channels, channels, kernel_size, 1, dilation=1, padding=get_padding(kernel_size, 1)))
+            for _ in dilation)
+        self.convs1.apply(_init)
+        self.convs2.apply(_init)
+        self.kernel_size = kernel_size
+        self.dilation = tuple(dilation)
+
+    def forward(self, x):  # NCL, autograd (training path)
+        for c1, c2 in zip(self.convs1, self.convs2):
+            xt = c2(F.leaky_relu(c1(F.leaky_relu(x, LRELU_SLOPE)), LRELU_SLOPE))
+            x = xt + x
+        return x
+
+    def forward_cl(self, x):
+        """Channel-last inference path [B, T, C] through the HIP conv kernel."""
+        k = self.kernel_size
+        for c1, c2, d in zip(self.convs1, self.convs2, self.dilation):
+            xt = ops.conv1d(_lrelu(x), _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
+            xt = ops.conv1d(xt, _w(c2), c2.bias, get_padding(k, 1), 1, None)
+            x = xt + x
+        return x
+
+
+def _lrelu(x, slope=LRELU_SLOPE):
+    return F.leaky_relu(x, slope)
+
+
+class Generator(nn.Module):
+    def __init__(self, h):
+        super().__init__()
+        self.h = h
+        self.num_kernels = len(h.resblock_kernel_sizes)
+        self.num_upsamples = len(h.upsample_rates)
+        c0 = h.upsample_initial_channel
+        self.conv_pre = weight_norm(nn.Conv1d(h.get("num_mels", 80), c0, 7, 1, padding=3))
+        self.ups = nn.ModuleList()
+        for i, (u, k) in enumerate(zip(h.upsample_rates, h.upsample_kernel_sizes)):
+            self.ups.append(weight_norm(nn.ConvTranspose1d(c0 // 2 ** i, c0 // 2 ** (i + 1), k, u, padding=(k - u) // 2)))
+        self.resblocks = nn.ModuleList()
+        ch = c0
+        for i in range(len(self.ups)):
+            ch = c0 // 2 ** (i + 1)
+            for k, d in zip(h.resblock_kernel_sizes, h.resblock_dilation_sizes):
+                self.resblocks.append(ResBlock1(ch, k, d))
+        self.conv_post = weight_norm(nn.Conv1d(ch, 1, 7, 1, padding=3))
+        self.ups.apply(_init)
+        self.conv_post.apply(_init)
+
+    # ------------------------------------------------------------------ training (NCL)
+    def forward(self, x):
+        x = self.conv_pre(x)
+        for i in range(self.num_upsamples):
+            x = self.ups[i](F.leaky_relu(x, LRELU_SLOPE))
+            xs = None
+            for j in range(self.num_kernels):
+                y = self.resblocks[i * self.num_kernels + j](x)
+                xs = y if xs is None else xs + y
+            x = xs / self.num_kernels
+        x = self.conv_post(F.leaky_relu(x))  # default slope 0.01 (reference quirk, D16 preserved)
+        return torch.tanh(x)
+
+    # ------------------------------------------------------------------ inference (channel-last, HIP)
+    @torch.no_grad()
+    def infer(self, mel_cl: torch.Tensor) -> torch.Tensor:
+        """mel [B, T, n_mel] (channel-last) -> wav [B, T*hop] in [-1, 1]."""
+        x = ops.conv1d(mel_cl, _w(self.conv_pre), self.conv_pre.bias, 3, 1, None)
+        for i in range(self.num_upsamples):
+            up = self.ups[i]
+            x = conv_transpose_polyphase(_lrelu(x), _w(up), up.bias, up.stride[0], up.padding[0])
+            xs = None
+            for j in range(self.num_kernels):
+                y = self.resblocks[i * self.num_kernels + j].forward_cl(x)
+                xs = y if xs is None else xs + y
+            x = xs * (1.0 / self.num_kernels)
+        x = _lrelu(x, 0.01)
+        w = _w(self.conv_post)  # [1, C, 7]: N=1 output -> VALU path (not MFMA-shaped)
+        y = ref_conv_post(x, w, self.conv_post.bias)
+        return torch.tanh(y).squeeze(-1)
+
+    def fold_weight_norm(self):
+        for m in self.modules():
+            if isinstance(m, (nn.Conv1d, nn.ConvTranspose1d)) and hasattr(m, "weight_g"):
+                torch.nn.utils.remove_weight_norm(m)
+        return self
+
+    remove_weight_norm = fold_weight_norm
+
+
+def ref_conv_post(x, w, b):
+    return ops.ref.conv1d(x.float(), w.float(), None if b is None else b.float(), 3, 1, None)
+
+
+def conv_transpose_polyphase(x, w, b, stride: int, pad: int):
+    """ConvTranspose1d as ``stride`` phase convolutions (channel-last).
+
+    y[s*q + r] = sum_j x[q - j + c_r] * w[:, :, r + pad ... ] -- for output phase r, the taps
+    k = (r + pad) mod s + s*j hit input index (s*q + r + pad - k)/s.  Each phase is a normal
+    (correlation) conv over x with the tap-reversed sub-kernel, evaluated on the MFMA
+    implicit-GEMM kernel; phases are interleaved into the output.
+    x [B, T, Cin], w [Cin, Cout, K] (PyTorch ConvTranspose layout).
+    """
+    B, T, Cin = x.shape
+    Cout, K = w.shape[1], w.shape[2]
+    T_out = (T - 1) * stride - 2 * pad + K
+    outs = []
+    for r in range(stride):
+        k0 = (r + pad) % stride
+        ks = list(range(k0, K, stride))
+        if not ks:
+            outs.append(torch.zeros(B, (T_out - r + stride - 1) // stride, Cout, device=x.device, dtype=x.dtype))
+            continue
+        off = (r + pad - k0) // stride  # input index of tap j=0 for q=0
+        sub = w[:, :, ks].permute(1, 0, 2).flip(2).contiguous()  # [Cout, Cin, J] correlation taps
+        J = len(ks)
+        n_q = (T_out - r + stride - 1) // stride
+        # y_r[q] = sum_j x[q + off - j] * w[..., k0 + s*j]  ==  corr(x_padded, sub)[q + off - (J-1)]
+        left = (J - 1) - off
+        right = max(0, n_q + off - T)
+        xp = x
+        if left > 0 or right > 0:
+            xp = F.pad(x, (0, 0, max(left, 0), right))
+        start = 0 if left >= 0 else -left
+        y = ops.conv1d(xp.contiguous(), sub, None, 0, 1, None)
+        y = y[:, start:start + n_q]
+        outs.append(y)
+    y = torch.stack([o[:, : (T_out + stride - 1) // stride] if o.shape[1] >= (T_out + stride - 1) // stride
+                     else F.pad(o, (0, 0, 0, (T_out + stride - 1) // stride - o.shape[1])) for o in outs], dim=2)
+    y = y.reshape(B, -1, Cout)[:, :T_out]
+    if b is not None:
+        y = y + b.to(y.dtype)
+    return y
+
+
+# ------------------------------------------------------------------ discriminators (training)
+class DiscriminatorP(nn.Module):
+    def __init__(self, period, kernel_size=5, stride=3, use_spectral_norm=False):
+        super().__init__()
+        self.period = period
+        norm_f = spectral_norm if use_spectral_norm else weight_norm
+        chans = [1, 32, 128, 512, 1024]
+        self.convs = nn.ModuleList(
+            [norm_f(nn.Conv2d(chans[i], chans[i + 1], (kernel_size, 1), (stride, 1), padding=(get_padding(5, 1), 0)))
+             for i in range(4)]
+            + [norm_f(nn.Conv2d(1024, 1024, (kernel_size, 1), 1, padding=(2, 0)))])
+        self.conv_post = norm_f(nn.Conv2d(1024, 1, (3, 1), 1, padding=(1, 0)))
+
+    def forward(self, x):
+        fmap = []
+        b, c, t = x.shape
+        if t % self.period:
+            n_pad = self.period - (t % self.period)
+            x = F.pad(x, (0, n_pad), "reflect")
+            t = t + n_pad
+        x = x.view(b, c, t // self.period, self.period)
+        for layer in self.convs:
+            x = F.leaky_relu(layer(x), LRELU_SLOPE)
+            fmap.append(x)
+        x = self.conv_post(x)
+        fmap.append(x)
+        return torch.flatten(x, 1, -1), fmap
+
+
+class MultiPeriodDiscriminator(nn.Module):
+    def __init__(self, periods=(2, 3, 5, 7, 11)):
+        super().__init__()
+        self.discriminators = nn.ModuleList(DiscriminatorP(p) for p in periods)
+
+    def forward(self, y, y_hat):
+        rs, gs, frs, fgs = [], [], [], []
+        for d in self.discriminators:
+            a, fa = d(y)
+            b, fb = d(y_hat)
+            rs.append(a); frs.append(fa); gs.append(b); fgs.append(fb)
+        return rs, gs, frs, fgs
+
+
+class DiscriminatorS(nn.Module):
+    def __init__(self, use_spectral_norm=False):
+        super().__init__()
+        norm_f = spectral_norm if use_spectral_norm else weight_norm
+        self.convs = nn.ModuleList([
+            norm_f(nn.Conv1d(1, 128, 15, 1, padding=7)),
+            norm_f(nn.Conv1d(128, 128, 41, 2, groups=4, padding=20)),
+            norm_f(nn.Conv1d(128, 256, 41, 2, groups=16, padding=20)),
+            norm_f(nn.Conv1d(256, 512, 41, 4, groups=16, padding=20)),
+            norm_f(nn.Conv1d(512, 1024, 41, 4, groups=16, padding=20)),
+            norm_f(nn.Conv1d(1024, 1024, 41, 1, groups=16, padding=20)),
+            norm_f(nn.Conv1d(1024, 1024, 5, 1, padding=2)),
+        ])
+        self.conv_post = norm_f(nn.Conv1d(1024, 1, 3, 1, padding=1))
+
+    def forward(self, x):
+        fmap = []
+        for layer in self.convs:
+            x = F.leaky_relu(layer(x), LRELU_SLOPE)
+            fmap.append(x)
+        x = self.conv_post(x)
+        fmap.append(x)
+        return torch.flatten(x, 1, -1), fmap
+
+
+class MultiScaleDiscriminator(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.discriminators = nn.ModuleList([DiscriminatorS(use_spectral_norm=True), DiscriminatorS(), DiscriminatorS()])
+        self.meanpools = nn.ModuleList([nn.AvgPool1d(4, 2, padding=2), nn.AvgPool1d(4, 2, padding=2)])
+
+    def forward(self, y, y_hat):
+        rs, gs, frs, fgs = [], [], [], []
+        for i, d in enumerate(self.discriminators):
+            if i:
+                y = self.meanpools[i - 1](y)
+                y_hat = self.meanpools[i - 1](y_hat)
+            a, fa = d(y)
+            b, fb = d(y_hat)
+            rs.append(a); frs.append(fa); gs.append(b); fgs.append(fb)
+        return rs, gs, frs, fgs
+
+
+def feature_loss(fmap_r, fmap_g):
+    loss = 0.0
+    for dr, dg in zip(fmap_r, fmap_g):
+        for rl, gl in zip(dr, dg):
+            loss = loss + torch.mean(torch.abs(rl - gl))
+    return loss * 2
+
+
+def discriminator_loss(real_outs, gen_outs):
+    loss = 0.0
+    r_losses, g_losses = [], []
+    for dr, dg in zip(real_outs, gen_outs):
+        r = torch.mean((1 - dr) ** 2)
+        g = torch.mean(dg ** 2)
+        loss = loss + r + g
+        r_losses.append(r.detach())
+        g_losses.append(g.detach())
+    return loss, r_losses, g_losses
+
+
+def generator_loss(gen_outs):
+    loss = 0.0
+    losses: List[torch.Tensor] = []
+    for dg in gen_outs:
+        l_ = torch.mean((1 - dg) ** 2)
+        losses.append(l_)
+        loss = loss + l_
+    return loss, losses
