@@ -139,6 +139,7 @@ class PostNet(nn.Module):
         self.convolutions = nn.ModuleList(
             nn.Sequential(ConvHolder(chans[i], chans[i + 1], k), nn.BatchNorm1d(chans[i + 1])) for i in range(n)
         )
+        self.dropout = 0.5  # hard-coded in the reference (Layers.py:140-148)
 
     def forward(self, x):
         h = x
@@ -151,5 +152,5 @@ class PostNet(nn.Module):
                               self.training, bn.momentum, bn.eps).reshape(B, L, C)
             if i < last:
                 h2 = torch.tanh(h2)
-            h = F.dropout(h2, 0.5, self.training)
+            h = F.dropout(h2, self.dropout, self.training) if self.dropout > 0 else h2
         return h

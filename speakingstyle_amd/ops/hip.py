@@ -109,6 +109,8 @@ _wcache = {}
 
 
 def _cached(param: torch.Tensor, kind: str, make):
+    if not isinstance(param, torch.nn.Parameter):  # transient tensors: ids / addresses get reused
+        return make(param.detach())
     key = (id(param), kind)
     ver = param._version
     hit = _wcache.get(key)

