@@ -1,0 +1,311 @@
+// BatchNorm1d (channel-last, training batch statistics over all B*L rows incl. padding,
+// the reference PostNet semantics -- transformer/Layers.py:78-148) fused with tanh and
+// dropout, forward and backward.
+//
+//   stats:    per-block partial (sum, sum of squares) per channel  -> [nblk][C] fp32
+//   finalize: combine partials (fp64), mean / biased var -> rstd, scale = g*rstd,
+//             shift = b - mean*scale, running stats update (momentum, unbiased var);
+//             eval mode: scale/shift from the running stats
+//   apply:    y = drop( act( h*scale + shift ) )        bf16 or fp32 out
+//   bwd:      dz = dy * keep * act'(z);  partial sums of dz and dz*xhat;
+//             finalize dgamma / dbeta;  dh = g*rstd*(dz - dbeta/R - xhat*dgamma/R)
+// Row-major [R, C] with C % 8 == 0; one 16-B (8-channel) chunk per lane.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+struct RowMap {
+  int chunks;      // C / 8
+  int rows_iter;   // rows covered by one pass of the block
+};
+
+__device__ __forceinline__ RowMap rowmap(int C) {
+  RowMap m;
+  m.chunks = C / 8;
+  m.rows_iter = NT / m.chunks;
+  if (m.rows_iter < 1) m.rows_iter = 1;
+  return m;
+}
+
+__device__ __forceinline__ void load8(const bf16_t* p, float* v) {
+  short8 x = *reinterpret_cast<const short8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = bf2f((bf16_t)x[i]);
+}
+
+// grid: nblk blocks, each a contiguous slice of rows; requires C/8 <= 256 (C <= 2048)
+__global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__ h, long R, int C, long rows_per_blk,
+                                                      float* __restrict__ psum, float* __restrict__ psq) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][rows_iter][C]
+  const RowMap m = rowmap(C);
+  const int tid = threadIdx.x;
+  const int c8 = tid % m.chunks, ro = tid / m.chunks;
+  const bool active = ro < m.rows_iter;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+  if (active) {
+    for (long r = r0 + ro; r < r1; r += m.rows_iter) {
+      float v[8];
+      load8(h + r * C + c8 * 8, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[ro * C + c8 * 8 + i] = s[i];
+      red[(m.rows_iter + ro) * C + c8 * 8 + i] = q[i];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f;
+    for (int j = 0; j < m.rows_iter; ++j) { a += red[j * C + c]; b += red[(m.rows_iter + j) * C + c]; }
+    psum[(long)blockIdx.x * C + c] = a;
+    psq[(long)blockIdx.x * C + c] = b;
+  }
+}
+
+__global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq,
+                                                         int nblk, long R, int C, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ rmean,
+                                                         float* __restrict__ rvar, float momentum, float eps, int training,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                         float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int b = 0; b < nblk; ++b) { s += psum[(long)b * C + c]; q += psq[(long)b * C + c]; }
+    const double mu = s / (double)R;
+    double vb = q / (double)R - mu * mu;
+    if (vb < 0.0) vb = 0.0;
+    mean = (float)mu;
+    var = (float)vb;
+    if (rmean) {
+      const double unb = R > 1 ? vb * (double)R / (double)(R - 1) : vb;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  const float rs = rsqrtf(var + eps);
+  const float sc = gamma[c] * rs;
+  mean_out[c] = mean;
+  rstd_out[c] = rs;
+  scale[c] = sc;
+  shift[c] = beta[c] - mean * sc;
+}
+
+template <bool OUT_F32>
+__global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__ h, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, void* __restrict__ out, long R,
+                                                      int C, int act_tanh, float p, uint64_t seed) {
+  const int chunks = C / 8;
+  const long total = R * chunks;
+  for (long e = blockIdx.x * (long)NT + threadIdx.x; e < total; e += (long)gridDim.x * NT) {
+    const long r = e / chunks;
+    const int c0 = (int)(e - r * chunks) * 8;
+    float v[8];
+    load8(h + r * C + c0, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float z = v[i] * scale[c0 + i] + shift[c0 + i];
+      if (act_tanh) z = tanhf(z);
+      v[i] = z * drop_scale(seed, (uint64_t)(r * C + c0 + i), p);
+    }
+    if constexpr (OUT_F32) {
+      float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + r * C + c0);
+      o[0] = make_float4(v[0], v[1], v[2], v[3]);
+      o[1] = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      short8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(v[i]);
+      *reinterpret_cast<short8*>(reinterpret_cast<bf16_t*>(out) + r * C + c0) = o;
+    }
+  }
+}
+
+template <bool DY_F32>
+__device__ __forceinline__ void load_dy(const void* dy, long off, float* v) {
+  if constexpr (DY_F32) {
+    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dy) + off);
+    float4 a = p[0], b = p[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    load8(reinterpret_cast<const bf16_t*>(dy) + off, v);
+  }
+}
+
+// dz = dy * keep * act'(z); partial sums of dz and dz*xhat
+template <bool DY_F32>
+__global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restrict__ dy, const bf16_t* __restrict__ h,
+                                                           const float* __restrict__ scale, const float* __restrict__ shift,
+                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                           long R, int C, long rows_per_blk, int act_tanh, float p,
+                                                           uint64_t seed, float* __restrict__ pdb, float* __restrict__ pdg) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const RowMap m = rowmap(C);
+  const int tid = threadIdx.x;
+  const int c8 = tid % m.chunks, ro = tid / m.chunks;
+  const bool active = ro < m.rows_iter;
+  float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+  if (active) {
+    float sc[8], sh[8], mu[8], rs[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = scale[c8 * 8 + i]; sh[i] = shift[c8 * 8 + i]; mu[i] = mean[c8 * 8 + i]; rs[i] = rstd[c8 * 8 + i];
+    }
+    for (long r = r0 + ro; r < r1; r += m.rows_iter) {
+      const long off = r * C + c8 * 8;
+      float hv[8], g[8];
+      load8(h + off, hv);
+      load_dy<DY_F32>(dy, off, g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
+        if (act_tanh) {
+          const float t = tanhf(hv[i] * sc[i] + sh[i]);
+          dz *= 1.f - t * t;
+        }
+        a[i] += dz;
+        b[i] += dz * (hv[i] - mu[i]) * rs[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[ro * C + c8 * 8 + i] = a[i];
+      red[(m.rows_iter + ro) * C + c8 * 8 + i] = b[i];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float x = 0.f, y = 0.f;
+    for (int j = 0; j < m.rows_iter; ++j) { x += red[j * C + c]; y += red[(m.rows_iter + j) * C + c]; }
+    pdb[(long)blockIdx.x * C + c] = x;
+    pdg[(long)blockIdx.x * C + c] = y;
+  }
+}
+
+__global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ pdb, const float* __restrict__ pdg,
+                                                             int nblk, int C, float* __restrict__ dbeta,
+                                                             float* __restrict__ dgamma) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  double x = 0.0, y = 0.0;
+  for (int b = 0; b < nblk; ++b) { x += pdb[(long)b * C + c]; y += pdg[(long)b * C + c]; }
+  dbeta[c] = (float)x;
+  dgamma[c] = (float)y;
+}
+
+template <bool DY_F32>
+__global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict__ dy, const bf16_t* __restrict__ h,
+                                                          const float* __restrict__ gamma, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, const float* __restrict__ dbeta,
+                                                          const float* __restrict__ dgamma, bf16_t* __restrict__ dh, long R,
+                                                          int C, int act_tanh, float p, uint64_t seed, int training) {
+  const int chunks = C / 8;
+  const long total = R * chunks;
+  const float invR = 1.f / (float)R;
+  for (long e = blockIdx.x * (long)NT + threadIdx.x; e < total; e += (long)gridDim.x * NT) {
+    const long r = e / chunks;
+    const int c0 = (int)(e - r * chunks) * 8;
+    const long off = r * C + c0;
+    float hv[8], g[8];
+    load8(h + off, hv);
+    load_dy<DY_F32>(dy, off, g);
+    short8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
+      if (act_tanh) {
+        const float t = tanhf(hv[i] * scale[c] + shift[c]);
+        dz *= 1.f - t * t;
+      }
+      float d;
+      if (training) {
+        const float xh = (hv[i] - mean[c]) * rstd[c];
+        d = gamma[c] * rstd[c] * (dz - dbeta[c] * invR - xh * dgamma[c] * invR);
+      } else {
+        d = dz * scale[c];
+      }
+      o[i] = (short)f2bf(d);
+    }
+    *reinterpret_cast<short8*>(dh + off) = o;
+  }
+}
+
+}  // namespace
+
+static int blocks_for(long R) {
+  long b = (R + 255) / 256;
+  if (b > 1024) b = 1024;
+  return (int)(b < 1 ? 1 : b);
+}
+
+// ws: 2 * nblk * C floats (nblk = blocks_for(R) <= 1024)
+SSAMD_API int ssamd_bn_fwd(const bf16_t* h, const float* gamma, const float* beta, float* rmean, float* rvar,
+                           float* mean, float* rstd, float* scale, float* shift, void* out, int out_f32, long R, int C,
+                           int training, float momentum, float eps, int act_tanh, float p, unsigned long long seed,
+                           float* ws, hipStream_t s) {
+  if (C % 8 || C / 8 > NT) return -2;
+  const int nblk = blocks_for(R);
+  const long rpb = (R + nblk - 1) / nblk;
+  const RowMap m = {C / 8, NT / (C / 8)};
+  if (training && R > 0) {
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(NT), (size_t)2 * m.rows_iter * C * 4, s, h, R, C, rpb, ws,
+                       ws + (long)nblk * C);
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, ws, ws + (long)nblk * C, nblk, R, C,
+                     gamma, beta, rmean, rvar, momentum, eps, training, mean, rstd, scale, shift);
+  if (R > 0) {
+    const int g = (int)min((R * (C / 8) + NT - 1) / NT, 4096L);
+    if (out_f32)
+      hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(g), dim3(NT), 0, s, h, scale, shift, out, R, C, act_tanh, p,
+                         (uint64_t)seed);
+    else
+      hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(g), dim3(NT), 0, s, h, scale, shift, out, R, C, act_tanh, p,
+                         (uint64_t)seed);
+  }
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_bn_bwd(const void* dy, int dy_f32, const bf16_t* h, const float* gamma, const float* scale,
+                           const float* shift, const float* mean, const float* rstd, bf16_t* dh, float* dgamma,
+                           float* dbeta, long R, int C, int training, int act_tanh, float p, unsigned long long seed,
+                           float* ws, hipStream_t s) {
+  if (C % 8 || C / 8 > NT) return -2;
+  if (R == 0) {
+    hipMemsetAsync(dgamma, 0, C * 4, s);
+    hipMemsetAsync(dbeta, 0, C * 4, s);
+    return (int)hipGetLastError();
+  }
+  const int nblk = blocks_for(R);
+  const long rpb = (R + nblk - 1) / nblk;
+  const RowMap m = {C / 8, NT / (C / 8)};
+  const size_t lds = (size_t)2 * m.rows_iter * C * 4;
+  if (dy_f32)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nblk), dim3(NT), lds, s, dy, h, scale, shift, mean, rstd, R, C,
+                       rpb, act_tanh, p, (uint64_t)seed, ws, ws + (long)nblk * C);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(nblk), dim3(NT), lds, s, dy, h, scale, shift, mean, rstd, R, C,
+                       rpb, act_tanh, p, (uint64_t)seed, ws, ws + (long)nblk * C);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, ws, ws + (long)nblk * C, nblk, C,
+                     dbeta, dgamma);
+  const int g = (int)min((R * (C / 8) + NT - 1) / NT, 4096L);
+  if (dy_f32)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(NT), 0, s, dy, h, gamma, scale, shift, mean, rstd, dbeta,
+                       dgamma, dh, R, C, act_tanh, p, (uint64_t)seed, training);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(g), dim3(NT), 0, s, dy, h, gamma, scale, shift, mean, rstd,
+                       dbeta, dgamma, dh, R, C, act_tanh, p, (uint64_t)seed, training);
+  return (int)hipGetLastError();
+}

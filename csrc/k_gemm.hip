@@ -240,7 +240,8 @@ __device__ __forceinline__ short4v ds_read_tr(const char* p) {
 }
 
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
-                                                           float* __restrict__ slabs, ConvGeom g, int rows_per_split) {
+                                                           float* __restrict__ slabs, float* __restrict__ bias_slabs,
+                                                           ConvGeom g, int rows_per_split) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + 127) / 128;  // cout tiles
   const int nK = (g.K + 127) / 128;  // k tiles
@@ -289,6 +290,16 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
       ry[i] = vy;
     }
   };
+  // bias gradient (column sums of dY) rides on the staging registers of the k-tile-0 blocks
+  const bool do_bias = bias_slabs != nullptr && tk == 0;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto bias_acc = [&]() {
+    if (!do_bias) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bsum[q] += bf2f((bf16_t)ry[i][q]);
+  };
   auto lstore = [&](int buf) {
     char* Ys = smem + buf * (2 * RB * 256);
     char* Xs = Ys + RB * 256;
@@ -303,13 +314,17 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
   const int nsteps = (r_end - r_begin + RB - 1) / RB;
   if (nsteps > 0) {
     gload(r_begin);
+    bias_acc();
     lstore(0);
   }
   __syncthreads();
   const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
-    if (s + 1 < nsteps) gload(r_begin + (s + 1) * RB);
+    if (s + 1 < nsteps) {
+      gload(r_begin + (s + 1) * RB);
+      bias_acc();
+    }
     const char* Ys = smem + buf * (2 * RB * 256);
     const char* Xs = Ys + RB * 256;
 #pragma unroll
@@ -335,6 +350,18 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
     if (s + 1 < nsteps) lstore(buf ^ 1);
     __syncthreads();
   }
+  if (do_bias) {  // reduce the 16 row-groups that share a column chunk, one partial per split
+    float* red = reinterpret_cast<float*>(smem);  // [16][128]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[(tid >> 4) * 128 + c16 * 8 + q] = bsum[q];
+    __syncthreads();
+    if (tid < 128 && n0 + tid < g.N) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t += red[j * 128 + tid];
+      bias_slabs[(long)split * g.N + n0 + tid] = t;
+    }
+  }
   // partial slab [split][N][K] fp32
   float* S = slabs + (long)split * g.N * g.K;
 #pragma unroll
@@ -351,9 +378,17 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
 
 // dW[n][cin][tap] = sum_s slab[s][n][tap*Cin + cin]   (PyTorch Conv1d / Linear layout)
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ dW,
+                                                           const float* __restrict__ bslabs, float* __restrict__ db,
                                                            int splits, int N, int Cin, int ks) {
   const long K = (long)Cin * ks;
   const long total = (long)N * K;
+  if (bslabs) {
+    for (long n = blockIdx.x * (long)blockDim.x + threadIdx.x; n < N; n += (long)gridDim.x * blockDim.x) {
+      float s = 0.f;
+      for (int sp = 0; sp < splits; ++sp) s += bslabs[(long)sp * N + n];
+      db[n] = s;
+    }
+  }
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     float s = 0.f;
     for (int sp = 0; sp < splits; ++sp) s += slabs[(long)sp * total + e];
@@ -408,13 +443,15 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
 }
 
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.
-SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, int B, int L,
-                               int Cin, int ks, int dil, int pad, int N, int max_splits, hipStream_t s) {
+// ws: splits*N*ks*Cin (+ splits*N when db != null) floats.  db (optional): fused bias gradient.
+SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, float* db,
+                               int B, int L, int Cin, int ks, int dil, int pad, int N, int max_splits, hipStream_t s) {
   if (Cin % 8 != 0 || N % 8 != 0) return -2;
   ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
   const long slab = (long)N * g.K;
   if (g.M == 0) {
     hipMemsetAsync(dW, 0, slab * sizeof(float), s);
+    if (db) hipMemsetAsync(db, 0, N * sizeof(float), s);
     return (int)hipGetLastError();
   }
   const int tiles = ((N + 127) / 128) * ((g.K + 127) / 128);
@@ -422,16 +459,17 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   const int max_by_rows = (g.M + 511) / 512;
   if (splits > max_by_rows) splits = max_by_rows;
   if (splits > max_splits) splits = max_splits;
-  if ((long)splits * slab > ws_floats) splits = (int)(ws_floats / slab);
+  if ((long)splits * (slab + N) > ws_floats) splits = (int)(ws_floats / (slab + N));
   if (splits < 1) return -3;
   int rows_per_split = (g.M + splits - 1) / splits;
   rows_per_split = (rows_per_split + RB - 1) / RB * RB;
   splits = (g.M + rows_per_split - 1) / rows_per_split;
-  hipLaunchKernelGGL(conv_wgrad_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, g,
+  float* bws = db ? ws + (long)splits * slab : nullptr;
+  hipLaunchKernelGGL(conv_wgrad_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
                      rows_per_split);
   const long total = slab;
   int blocks = (int)min((total + 255) / 256, 8192L);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, splits, N, Cin, ks);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
   return (int)hipGetLastError();
 }
 

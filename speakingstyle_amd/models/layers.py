@@ -146,11 +146,5 @@ class PostNet(nn.Module):
         last = len(self.convolutions) - 1
         for i, seq in enumerate(self.convolutions):
             conv, bn = seq[0], seq[1]
-            h = conv(h)
-            B, L, C = h.shape
-            h2 = F.batch_norm(h.reshape(B * L, C), bn.running_mean, bn.running_var, bn.weight, bn.bias,
-                              self.training, bn.momentum, bn.eps).reshape(B, L, C)
-            if i < last:
-                h2 = torch.tanh(h2)
-            h = F.dropout(h2, self.dropout, self.training) if self.dropout > 0 else h2
+            h = ops.bn_act(conv(h), bn, self.training, act_tanh=i < last, p=self.dropout, out_f32=i == last)
         return h

@@ -99,3 +99,20 @@ def bucketize_embed_add(x, values, bins, table):
     if use_hip(x):
         return _hip().bucketize_embed_add(x, values, bins, table)
     return x + ref.bucketize_embed(values, bins, table).to(x.dtype)
+
+
+def bn_act(h, bn, training, act_tanh, p, out_f32=False):
+    """PostNet stage: BatchNorm1d (batch stats over all B*L rows) -> [tanh] -> dropout."""
+    if use_hip(h):
+        return _hip().bn_act(h, bn, training, act_tanh, p, out_f32)
+    import torch.nn.functional as F
+
+    B, L, C = h.shape
+    y = F.batch_norm(h.reshape(B * L, C), bn.running_mean, bn.running_var, bn.weight, bn.bias, training,
+                     bn.momentum, bn.eps).reshape(B, L, C)
+    if training and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    if act_tanh:
+        y = torch.tanh(y)
+    y = F.dropout(y, p, training) if p > 0 else y
+    return y.float() if out_f32 else y

@@ -34,7 +34,7 @@ U64 = ctypes.c_ulonglong
 
 _SIGS = {
     "ssamd_conv_gemm": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
-    "ssamd_conv_wgrad": [P, P, P, L_, P, I, I, I, I, I, I, I, I, P],
+    "ssamd_conv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, P],
     "ssamd_colsum": [P, P, L_, I, P],
     "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
     "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],
@@ -173,7 +173,8 @@ def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, re
     return y
 
 
-def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N):
+def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False):
+    """-> dW [N, Cin, ks] fp32 (and db [N] when ``with_bias``: fused column sums of dY)."""
     _need(x, torch.bfloat16, "wgrad.x")
     _need(dy, torch.bfloat16, "wgrad.dy")
     assert x.numel() == B * L * Cin and dy.numel() == B * L * N
@@ -182,12 +183,13 @@ def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N):
     K = ks * Cin
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
     max_splits = max(1, min(64, (1536 + tiles - 1) // tiles))
-    ws = _workspace(x.device, max_splits * N * K)
+    ws = _workspace(x.device, max_splits * (N * K + N))
     dW = torch.empty(N, Cin, ks, device=x.device, dtype=torch.float32)
-    rc = lib().ssamd_conv_wgrad(_ptr(x), _ptr(dy), _ptr(ws), ws.numel(), _ptr(dW), B, L, Cin, ks, dil, pad, N,
-                                max_splits, _stream())
+    db = torch.empty(N, device=x.device, dtype=torch.float32) if with_bias else None
+    rc = lib().ssamd_conv_wgrad(_ptr(x), _ptr(dy), _ptr(ws), ws.numel(), _ptr(dW), _ptr(db), B, L, Cin, ks, dil, pad,
+                                N, max_splits, _stream())
     _check(rc, "ssamd_conv_wgrad")
-    return dW
+    return (dW, db) if with_bias else dW
 
 
 def colsum_raw(dy, N):
@@ -235,11 +237,13 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin)
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            dw = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N)
+            res = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b)
+            dw, db = res if want_b else (res, None)
             if w.dim() == 2:
                 dw = dw.view(N, Cin)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+        elif want_b:
             db = colsum_raw(dy, N)
         return dx, dw, db, None, None, None, None
 
@@ -281,11 +285,9 @@ class _FFNFn(torch.autograd.Function):
         dz = dz.to(torch.bfloat16).contiguous()
         p1, p2 = (k1 - 1) // 2, (k2 - 1) // 2
         dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h)
-        dw2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C)
-        db2 = colsum_raw(dz, C)
+        dw2, db2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True)
         dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0)
-        dw1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H)
-        db1 = colsum_raw(dh, H)
+        dw1, db1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True)
         return dx, dw1, db1, dw2, db2
 
 
@@ -536,3 +538,60 @@ def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped
                                float(betas[0]), float(betas[1]), float(eps), float(wd), int(step), _ptr(norm_out),
                                _ptr(skipped), _stream())
     _check(rc, "ssamd_clip_adam")
+
+
+# ------------------------------------------------------------------------ BatchNorm (+tanh, dropout)
+_SIGS.update({
+    "ssamd_bn_fwd": [P, P, P, P, P, P, P, P, P, P, I, L_, I, I, F, F, I, F, U64, P, P],
+    "ssamd_bn_bwd": [P, I, P, P, P, P, P, P, P, P, P, L_, I, I, I, F, U64, P, P],
+})
+
+
+def _bn_ws(device, R, C):
+    return _workspace(device, 2 * 1024 * C + 16)
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, gamma, beta, rmean, rvar, training, momentum, eps, act_tanh, p, out_f32, seed):
+        B, L, C = h.shape
+        R = B * L
+        hc = h.contiguous()
+        _need(hc, torch.bfloat16, "bn.h")
+        dev = h.device
+        stats = torch.empty(4, C, device=dev, dtype=torch.float32)  # mean, rstd, scale, shift
+        out = torch.empty(B, L, C, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        ws = _bn_ws(dev, R, C)
+        rc = lib().ssamd_bn_fwd(_ptr(hc), _ptr(gamma), _ptr(beta), _ptr(rmean), _ptr(rvar), _ptr(stats[0]),
+                                _ptr(stats[1]), _ptr(stats[2]), _ptr(stats[3]), _ptr(out), int(out_f32), R, C,
+                                int(training), float(momentum), float(eps), int(act_tanh), float(p), seed, _ptr(ws),
+                                _stream())
+        _check(rc, "ssamd_bn_fwd")
+        ctx.save_for_backward(hc, gamma, stats)
+        ctx.cfg = (R, C, int(training), int(act_tanh), float(p), seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        hc, gamma, stats = ctx.saved_tensors
+        R, C, training, act_tanh, p, seed = ctx.cfg
+        dyf32 = dy.dtype == torch.float32
+        dy = dy.contiguous() if dyf32 else dy.to(torch.bfloat16).contiguous()
+        dh = torch.empty_like(hc)
+        dg = torch.empty(C, device=hc.device, dtype=torch.float32)
+        db = torch.empty_like(dg)
+        ws = _bn_ws(hc.device, R, C)
+        rc = lib().ssamd_bn_bwd(_ptr(dy), int(dyf32), _ptr(hc), _ptr(gamma), _ptr(stats[2]), _ptr(stats[3]),
+                                _ptr(stats[0]), _ptr(stats[1]), _ptr(dh), _ptr(dg), _ptr(db), R, C, training, act_tanh,
+                                p, seed, _ptr(ws), _stream())
+        _check(rc, "ssamd_bn_bwd")
+        return dh, dg, db, None, None, None, None, None, None, None, None, None
+
+
+def bn_act(h, bn, training, act_tanh, p, out_f32=False):
+    """BatchNorm1d over all rows of channel-last h (+tanh) + dropout, one fused op."""
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    if training and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return _BNActFn.apply(h.to(torch.bfloat16), bn.weight, bn.bias, bn.running_mean, bn.running_var, bool(training),
+                          momentum, bn.eps, bool(act_tanh), float(p if training else 0.0), bool(out_f32), _next_seed())

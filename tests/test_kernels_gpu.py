@@ -272,3 +272,40 @@ def test_model_step_hip_vs_reference():
         if gr[n].grad.norm() > 1e-6 and _rel(p.grad, gr[n].grad) > 0.15:
             bad.append((n, _rel(p.grad, gr[n].grad)))
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("C,act,training,out_f32", [(512, True, True, False), (80, False, True, True), (512, True, False, False)])
+def test_bn_act(C, act, training, out_f32):
+    torch.manual_seed(10)
+    B, L = 5, 93
+    bn = torch.nn.BatchNorm1d(C).to(DEV)
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-0.3, 0.3)
+    bn.running_mean.uniform_(-0.2, 0.2)
+    bn.running_var.uniform_(0.5, 2.0)
+    bnr = copy_bn = torch.nn.BatchNorm1d(C).to(DEV)
+    bnr.load_state_dict(bn.state_dict())
+    h = (torch.randn(B, L, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    hh = h.clone().requires_grad_(True)
+    hr = h.float().requires_grad_(True)
+    y = hip.bn_act(hh, bn, training, act, 0.0, out_f32)
+    yr = F.batch_norm(hr.reshape(-1, C), bnr.running_mean, bnr.running_var, bnr.weight, bnr.bias, training, 0.1,
+                      1e-5).reshape(B, L, C)
+    if act:
+        yr = torch.tanh(yr)
+    assert _rel(y, yr) < 1e-2
+    torch.testing.assert_close(bn.running_mean, bnr.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, bnr.running_var, rtol=1e-4, atol=1e-5)
+    g = torch.randn_like(yr)
+    y.backward(g.to(y.dtype))
+    yr.backward(g.to(y.dtype).float())
+    assert _rel(hh.grad, hr.grad) < 2e-2
+    assert _rel(bn.weight.grad, bnr.weight.grad) < 1e-2 and _rel(bn.bias.grad, bnr.bias.grad) < 1e-2
+
+
+def test_bn_dropout_rate():
+    bn = torch.nn.BatchNorm1d(512).to(DEV)
+    h = torch.randn(4, 200, 512, device=DEV).to(torch.bfloat16)
+    y = hip.bn_act(h, bn, True, True, 0.5)
+    frac = (y == 0).float().mean().item()
+    assert 0.47 < frac < 0.53
