@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--backend", default=None, choices=[None, "hip", "reference"])
     ap.add_argument("--profile-steps", type=int, default=0)
     args = ap.parse_args()
+    # variable-shape batches: let the caching allocator grow segments instead of re-mallocing
+    os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
+    os.environ.setdefault("PYTORCH_CUDA_ALLOC_CONF", "expandable_segments:True")
 
     import torch
 
@@ -74,6 +77,8 @@ def main():
     for _ in range(args.pool):
         b = gen.make_batch()
         pool.append((b, gen.last_valid_frames))
+    # largest padded batch first: the first warm-up step sizes the allocator for all others
+    pool.sort(key=lambda e: -(e[0][0].__len__() * e[0][8]))
 
     def step(i):
         b, frames = pool[i % len(pool)]

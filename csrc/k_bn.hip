@@ -16,6 +16,12 @@ namespace {
 
 constexpr int NT = 256;
 
+__device__ __forceinline__ float fast_tanh(float z) {
+  // 1 - 2/(exp(2z)+1): one exp + one rcp; saturates correctly for |z| large
+  const float e = __expf(2.f * z);
+  return 1.f - 2.f / (e + 1.f);
+}
+
 struct RowMap {
   int chunks;      // C / 8
   int rows_iter;   // rows covered by one pass of the block
@@ -73,18 +79,22 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict
                                                          float* __restrict__ rvar, float momentum, float eps, int training,
                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                          float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * NT + threadIdx.x;
+  // one wave per channel: lanes stride over the per-block partials, shuffle reduction
+  const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
   float mean, var;
   if (training) {
     double s = 0.0, q = 0.0;
-    for (int b = 0; b < nblk; ++b) { s += psum[(long)b * C + c]; q += psq[(long)b * C + c]; }
+    for (int b = lane; b < nblk; b += 64) { s += psum[(long)b * C + c]; q += psq[(long)b * C + c]; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
     const double mu = s / (double)R;
     double vb = q / (double)R - mu * mu;
     if (vb < 0.0) vb = 0.0;
     mean = (float)mu;
     var = (float)vb;
-    if (rmean) {
+    if (rmean && lane == 0) {
       const double unb = R > 1 ? vb * (double)R / (double)(R - 1) : vb;
       rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
       rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
@@ -93,6 +103,7 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict
     mean = rmean[c];
     var = rvar[c];
   }
+  if (lane != 0) return;
   const float rs = rsqrtf(var + eps);
   const float sc = gamma[c] * rs;
   mean_out[c] = mean;
@@ -105,17 +116,20 @@ template <bool OUT_F32>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__ h, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, void* __restrict__ out, long R,
                                                       int C, int act_tanh, float p, uint64_t seed) {
-  const int chunks = C / 8;
-  const long total = R * chunks;
-  for (long e = blockIdx.x * (long)NT + threadIdx.x; e < total; e += (long)gridDim.x * NT) {
-    const long r = e / chunks;
-    const int c0 = (int)(e - r * chunks) * 8;
+  const RowMap m = rowmap(C);
+  const int c8 = threadIdx.x % m.chunks, ro = threadIdx.x / m.chunks;
+  if (ro >= m.rows_iter) return;
+  const int c0 = c8 * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sc[i] = scale[c0 + i]; sh[i] = shift[c0 + i]; }
+  for (long r = (long)blockIdx.x * m.rows_iter + ro; r < R; r += (long)gridDim.x * m.rows_iter) {
     float v[8];
     load8(h + r * C + c0, v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float z = v[i] * scale[c0 + i] + shift[c0 + i];
-      if (act_tanh) z = tanhf(z);
+      float z = v[i] * sc[i] + sh[i];
+      if (act_tanh) z = fast_tanh(z);
       v[i] = z * drop_scale(seed, (uint64_t)(r * C + c0 + i), p);
     }
     if constexpr (OUT_F32) {
@@ -171,7 +185,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restric
       for (int i = 0; i < 8; ++i) {
         float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
         if (act_tanh) {
-          const float t = tanhf(hv[i] * sc[i] + sh[i]);
+          const float t = fast_tanh(hv[i] * sc[i] + sh[i]);
           dz *= 1.f - t * t;
         }
         a[i] += dz;
@@ -196,12 +210,17 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restric
 __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ pdb, const float* __restrict__ pdg,
                                                              int nblk, int C, float* __restrict__ dbeta,
                                                              float* __restrict__ dgamma) {
-  const int c = blockIdx.x * NT + threadIdx.x;
+  const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
   double x = 0.0, y = 0.0;
-  for (int b = 0; b < nblk; ++b) { x += pdb[(long)b * C + c]; y += pdg[(long)b * C + c]; }
-  dbeta[c] = (float)x;
-  dgamma[c] = (float)y;
+  for (int b = lane; b < nblk; b += 64) { x += pdb[(long)b * C + c]; y += pdg[(long)b * C + c]; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { x += __shfl_xor(x, o, 64); y += __shfl_xor(y, o, 64); }
+  if (lane == 0) {
+    dbeta[c] = (float)x;
+    dgamma[c] = (float)y;
+  }
 }
 
 template <bool DY_F32>
@@ -211,12 +230,30 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
                                                           const float* __restrict__ rstd, const float* __restrict__ dbeta,
                                                           const float* __restrict__ dgamma, bf16_t* __restrict__ dh, long R,
                                                           int C, int act_tanh, float p, uint64_t seed, int training) {
-  const int chunks = C / 8;
-  const long total = R * chunks;
+  const RowMap m = rowmap(C);
+  const int c8 = threadIdx.x % m.chunks, ro = threadIdx.x / m.chunks;
+  if (ro >= m.rows_iter) return;
+  const int c0 = c8 * 8;
   const float invR = 1.f / (float)R;
-  for (long e = blockIdx.x * (long)NT + threadIdx.x; e < total; e += (long)gridDim.x * NT) {
-    const long r = e / chunks;
-    const int c0 = (int)(e - r * chunks) * 8;
+  // dh = k1 * dz + k2 * h + k3   (training);   dh = scale * dz (eval)
+  float sc[8], sh[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    sc[i] = scale[c];
+    sh[i] = shift[c];
+    if (training) {
+      const float gr = gamma[c] * rstd[c];
+      k1[i] = gr;
+      k2[i] = -gr * rstd[c] * dgamma[c] * invR;
+      k3[i] = -gr * dbeta[c] * invR - k2[i] * mean[c];
+    } else {
+      k1[i] = sc[i];
+      k2[i] = 0.f;
+      k3[i] = 0.f;
+    }
+  }
+  for (long r = (long)blockIdx.x * m.rows_iter + ro; r < R; r += (long)gridDim.x * m.rows_iter) {
     const long off = r * C + c0;
     float hv[8], g[8];
     load8(h + off, hv);
@@ -224,20 +261,12 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
     short8 o;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
       float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
       if (act_tanh) {
-        const float t = tanhf(hv[i] * scale[c] + shift[c]);
+        const float t = fast_tanh(hv[i] * sc[i] + sh[i]);
         dz *= 1.f - t * t;
       }
-      float d;
-      if (training) {
-        const float xh = (hv[i] - mean[c]) * rstd[c];
-        d = gamma[c] * rstd[c] * (dz - dbeta[c] * invR - xh * dgamma[c] * invR);
-      } else {
-        d = dz * scale[c];
-      }
-      o[i] = (short)f2bf(d);
+      o[i] = (short)f2bf(k1[i] * dz + k2[i] * hv[i] + k3[i]);
     }
     *reinterpret_cast<short8*>(dh + off) = o;
   }
@@ -247,7 +276,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
 
 static int blocks_for(long R) {
   long b = (R + 255) / 256;
-  if (b > 1024) b = 1024;
+  if (b > 512) b = 512;
   return (int)(b < 1 ? 1 : b);
 }
 
@@ -264,10 +293,10 @@ SSAMD_API int ssamd_bn_fwd(const bf16_t* h, const float* gamma, const float* bet
     hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(NT), (size_t)2 * m.rows_iter * C * 4, s, h, R, C, rpb, ws,
                        ws + (long)nblk * C);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, ws, ws + (long)nblk * C, nblk, R, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, s, ws, ws + (long)nblk * C, nblk, R, C,
                      gamma, beta, rmean, rvar, momentum, eps, training, mean, rstd, scale, shift);
   if (R > 0) {
-    const int g = (int)min((R * (C / 8) + NT - 1) / NT, 4096L);
+    const int g = (int)min((R + m.rows_iter - 1) / m.rows_iter, 4096L);
     if (out_f32)
       hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(g), dim3(NT), 0, s, h, scale, shift, out, R, C, act_tanh, p,
                          (uint64_t)seed);
@@ -298,9 +327,9 @@ SSAMD_API int ssamd_bn_bwd(const void* dy, int dy_f32, const bf16_t* h, const fl
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(nblk), dim3(NT), lds, s, dy, h, scale, shift, mean, rstd, R, C,
                        rpb, act_tanh, p, (uint64_t)seed, ws, ws + (long)nblk * C);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, ws, ws + (long)nblk * C, nblk, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, s, ws, ws + (long)nblk * C, nblk, C,
                      dbeta, dgamma);
-  const int g = (int)min((R * (C / 8) + NT - 1) / NT, 4096L);
+  const int g = (int)min((R + m.rows_iter - 1) / m.rows_iter, 4096L);
   if (dy_f32)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(g), dim3(NT), 0, s, dy, h, gamma, scale, shift, mean, rstd, dbeta,
                        dgamma, dh, R, C, act_tanh, p, (uint64_t)seed, training);

@@ -57,7 +57,7 @@ __device__ __forceinline__ short8 load_a_chunk(const bf16_t* __restrict__ X, con
   return v;
 }
 
-template <bool OUT_F32>
+template <bool OUT_F32, bool REG_EPI>
 __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                           const float* __restrict__ bias, const bf16_t* __restrict__ aux,
                                                           const bf16_t* __restrict__ resid,
@@ -136,10 +136,67 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restri
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (REG_EPI)  // transposed accumulator: lane holds 4 consecutive columns of one row
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
     }
     if (kt + 1 < nk) lstore(buf ^ 1);
     __syncthreads();
+  }
+
+  if constexpr (REG_EPI) {
+    // ---- register epilogue (no LDS round trip): fragment (i, j) -> row m, columns n..n+3
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (m >= g.M) continue;
+      const int bb = m / g.L, tt = m - bb * g.L;
+      const bool valid = lens == nullptr || tt < (int)lens[bb];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+        if (n >= g.N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (bias) {
+          const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+          v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+        }
+        if (act == ACT_RELU) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        } else if (act == ACT_LRELU) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+        } else if (act == ACT_TANH) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+        }
+        const long off = (long)m * ldy + n;
+        if (aux) {
+          const short4v x = *reinterpret_cast<const short4v*>(aux + off);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
+        }
+        if (resid) {
+          const short4v x = *reinterpret_cast<const short4v*>(resid + off);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
+        }
+        if (!valid) v[0] = v[1] = v[2] = v[3] = 0.f;
+        if constexpr (OUT_F32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          short4v o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
+          *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
+        }
+      }
+    }
+    return;
   }
 
   // ---- epilogue: stage fp32 tile in LDS, then coalesced 8-wide row segments
@@ -413,6 +470,10 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
 
 }  // namespace
 
+static bool g_force_lds_epilogue = false;
+
+SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
+
 static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N) {
   ConvGeom g;
   g.B = B; g.L = L; g.Cin = Cin; g.ks = ks; g.dil = dil; g.pad = pad;
@@ -430,15 +491,27 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   const size_t lds = (size_t)BM * CSTRIDE * 4;  // >= 2 stages x (A+B) = 64 KiB
   static bool lds_set = false;
   if (!lds_set) {
-    allow_lds(conv_gemm_kernel<true>, lds);
-    allow_lds(conv_gemm_kernel<false>, lds);
+    allow_lds(conv_gemm_kernel<true, false>, lds);
+    allow_lds(conv_gemm_kernel<false, false>, lds);
     lds_set = true;
   }
-  if (out_f32)
-    hipLaunchKernelGGL(conv_gemm_kernel<true>, dim3(nwg), dim3(NT), lds, s, X, W, bias, aux, resid, lens, Y, g, act, ldy);
-  else
-    hipLaunchKernelGGL(conv_gemm_kernel<false>, dim3(nwg), dim3(NT), lds, s, X, W, bias, aux, resid, lens, Y, g, act,
-                       ldy);
+  // register epilogue needs N % 4 == 0 and an 8-B aligned ldy; LDS-staged epilogue otherwise
+  const bool reg = (N % 4 == 0) && (ldy % 4 == 0) && !g_force_lds_epilogue;
+  const size_t lds_reg = (size_t)2 * 2 * BM * BK * 2;
+  if (reg) {
+    if (out_f32)
+      hipLaunchKernelGGL((conv_gemm_kernel<true, true>), dim3(nwg), dim3(NT), lds_reg, s, X, W, bias, aux, resid, lens,
+                         Y, g, act, ldy);
+    else
+      hipLaunchKernelGGL((conv_gemm_kernel<false, true>), dim3(nwg), dim3(NT), lds_reg, s, X, W, bias, aux, resid, lens,
+                         Y, g, act, ldy);
+  } else if (out_f32) {
+    hipLaunchKernelGGL((conv_gemm_kernel<true, false>), dim3(nwg), dim3(NT), lds, s, X, W, bias, aux, resid, lens, Y, g,
+                       act, ldy);
+  } else {
+    hipLaunchKernelGGL((conv_gemm_kernel<false, false>), dim3(nwg), dim3(NT), lds, s, X, W, bias, aux, resid, lens, Y,
+                       g, act, ldy);
+  }
   return (int)hipGetLastError();
 }
 

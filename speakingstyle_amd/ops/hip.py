@@ -48,6 +48,7 @@ _SIGS = {
     "ssamd_attn_fwd": [P, P, P, P, I, I, I, I, F, P],
     "ssamd_attn_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, F, P],
     "ssamd_relu_mask": [P, P, P, L_, P],
+    "ssamd_gemm_set_epilogue": [I],
 }
 
 
