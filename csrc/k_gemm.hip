@@ -279,6 +279,149 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restri
 }
 
 // ----------------------------------------------------------------------------
+// Same GEMM with global_load_lds staging (gfx950 LDS-DMA): each lane DMAs one 16-B chunk
+// straight into LDS (no VGPR round trip, no ds_write); the XOR swizzle moves to the
+// per-lane SOURCE address (the LDS image is lane-linear per wave instruction).  Lanes
+// whose chunk is conv padding / out of range read a 16-B zero block instead.
+// ----------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) bf16_t g_zero_chunk[8];
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <bool OUT_F32>
+__global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                               const float* __restrict__ bias,
+                                                               const bf16_t* __restrict__ aux,
+                                                               const bf16_t* __restrict__ resid,
+                                                               const int64_t* __restrict__ lens, void* __restrict__ Yv,
+                                                               ConvGeom g, int act, int ldy) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + BN - 1) / BN;
+  const int nM = (g.M + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, nN * nM);
+  const int tn = wg % nN, tm = wg / nN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const float invCin = 1.f / (float)g.Cin;
+
+  // DMA assignment: wave instruction i (0..3) fills rows rb(i) .. rb(i)+7, lane -> (row, phys chunk)
+  int a_b[4], a_t[4], a_m[4], rowi[4], lchunk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 4 + wave) * 8 + (lane >> 3);
+    rowi[i] = row;
+    lchunk[i] = (lane & 7) ^ ((row >> 1) & 7);
+    a_m[i] = m0 + row;
+    const int mm = a_m[i] < g.M ? a_m[i] : 0;
+    a_b[i] = mm / g.L;
+    a_t[i] = mm - a_b[i] * g.L;
+  }
+  auto stage = [&](int kt, int buf) {
+    char* As = smem + buf * (2 * BM * BK * 2);
+    char* Bs = As + BM * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = kt * BK + lchunk[i] * 8;
+      const void* src = g_zero_chunk;
+      if (a_m[i] < g.M && k < g.K) {
+        const int tap = (int)(((float)k + 0.5f) * invCin);
+        const int cin = k - tap * g.Cin;
+        const int ts = a_t[i] + tap * g.dil - g.pad;
+        if (ts >= 0 && ts < g.L) src = X + ((long)a_b[i] * g.L + ts) * g.Cin + cin;
+      }
+      glds16(src, As + (i * 4 + wave) * 8 * 128);
+      const int n = n0 + rowi[i];
+      const void* srcb = (n < g.N && k < g.K) ? (const void*)(W + (long)n * g.K + k) : (const void*)g_zero_chunk;
+      glds16(srcb, Bs + (i * 4 + wave) * 8 * 128);
+    }
+  };
+
+  float4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + BK - 1) / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const char* As = smem + buf * (2 * BM * BK * 2);
+    const char* Bs = As + BM * BK * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      short8 fa[4], fb[4];
+      const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i] = *reinterpret_cast<const short8*>(As + swz128(wm * 64 + i * 16 + (lane & 15), c));
+        fb[i] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + i * 16 + (lane & 15), c));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    const int bb = m / g.L, tt = m - bb * g.L;
+    const bool valid = lens == nullptr || tt < (int)lens[bb];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+        const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+        v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+      }
+      if (act == ACT_RELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      } else if (act == ACT_LRELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+      } else if (act == ACT_TANH) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+      }
+      const long off = (long)m * ldy + n;
+      if (aux) {
+        const short4v x = *reinterpret_cast<const short4v*>(aux + off);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
+      }
+      if (resid) {
+        const short4v x = *reinterpret_cast<const short4v*>(resid + off);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
+      }
+      if (!valid) v[0] = v[1] = v[2] = v[3] = 0.f;
+      if constexpr (OUT_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        short4v o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
+        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
 // Weight gradient.  Tile: 128 (n = cout) x 128 (k = tap*Cin + cin), reduction over
 // rows m in steps of RB = 64.  LDS image per operand: [64 rows][128 cols] bf16,
 // 256-B rows, 8-B column chunks XOR-swizzled by f(row) = ((row&3) | ((row>>3)&1)<<2) << 2
@@ -297,6 +440,138 @@ __device__ __forceinline__ short4v ds_read_tr(const char* p) {
 }
 
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
+                                                           float* __restrict__ slabs, float* __restrict__ bias_slabs,
+                                                           ConvGeom g, int rows_per_split) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + 127) / 128;  // cout tiles
+  const int nK = (g.K + 127) / 128;  // k tiles
+  const int tile = blockIdx.x % (nN * nK);
+  const int split = blockIdx.x / (nN * nK);
+  const int tn = tile / nK, tk = tile % nK;
+  const int n0 = tn * 128, k0 = tk * 128;
+  const int r_begin = split * rows_per_split;
+  const int r_end = min(g.M, r_begin + rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const float invCin = 1.f / (float)g.Cin;
+
+  float4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  // LDS-DMA staging: a wave instruction fills 4 rows x 256 B; lane -> (row rr, physical 16-B chunk p16);
+  // the tr-read swizzle f(row) permutes 16-B chunks by f>>1, applied on the source side.
+  int rr[4], c_n[4], c_tap[4], c_cin[4];
+  bool c_kok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 4 + wave) * 4 + (lane >> 4);
+    rr[i] = row;
+    const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
+    const int c16 = (lane & 15) ^ (f >> 1);
+    c_n[i] = n0 + c16 * 8;
+    const int k = k0 + c16 * 8;
+    c_kok[i] = k < g.K;
+    c_tap[i] = c_kok[i] ? (int)(((float)k + 0.5f) * invCin) : 0;
+    c_cin[i] = k - c_tap[i] * g.Cin;
+  }
+  auto stage = [&](int r0, int buf) {
+    char* Ys = smem + buf * (2 * RB * 256);
+    char* Xs = Ys + RB * 256;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + rr[i];
+      const void* sy = g_zero_chunk;
+      const void* sx = g_zero_chunk;
+      if (m < r_end) {
+        if (c_n[i] < g.N) sy = dY + (long)m * g.N + c_n[i];
+        if (c_kok[i]) {
+          const int bb = m / g.L, tt = m - bb * g.L;
+          const int ts = tt + c_tap[i] * g.dil - g.pad;
+          if (ts >= 0 && ts < g.L) sx = X + ((long)bb * g.L + ts) * g.Cin + c_cin[i];
+        }
+      }
+      glds16(sy, Ys + (i * 4 + wave) * 4 * 256);
+      glds16(sx, Xs + (i * 4 + wave) * 4 * 256);
+    }
+  };
+  // bias gradient (column sums of dY) for the k-tile-0 blocks, read back from the LDS image
+  const bool do_bias = bias_slabs != nullptr && tk == 0;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int bc16 = tid & 15;
+
+  const int nsteps = (r_end - r_begin + RB - 1) / RB;
+  if (nsteps > 0) stage(r_begin, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) stage(r_begin + (s + 1) * RB, buf ^ 1);
+    const char* Ys = smem + buf * (2 * RB * 256);
+    const char* Xs = Ys + RB * 256;
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = (tid >> 4) + 16 * j;
+        const short8 v = *reinterpret_cast<const short8*>(Ys + swz_tr(row, bc16 * 2));
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bsum[t] += bf2f((bf16_t)v[t]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < RB / 32; ++kk) {
+      short8 fa[4], fb[4];
+      const int rbase = kk * 32 + grp * 8 + q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ca = (wn * 64 + i * 16) / 4 + p;
+        const int cb = (wk * 64 + i * 16) / 4 + p;
+        short4v a0 = ds_read_tr(Ys + swz_tr(rbase, ca));
+        short4v a1 = ds_read_tr(Ys + swz_tr(rbase + 4, ca));
+        short4v b0 = ds_read_tr(Xs + swz_tr(rbase, cb));
+        short4v b1 = ds_read_tr(Xs + swz_tr(rbase + 4, cb));
+        fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        fb[i] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (do_bias) {  // reduce the 16 row-groups that share a column chunk, one partial per split
+    float* red = reinterpret_cast<float*>(smem);  // [16][128]
+#pragma unroll
+    for (int t = 0; t < 8; ++t) red[(tid >> 4) * 128 + bc16 * 8 + t] = bsum[t];
+    __syncthreads();
+    if (tid < 128 && n0 + tid < g.N) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t += red[j * 128 + tid];
+      bias_slabs[(long)split * g.N + n0 + tid] = t;
+    }
+  }
+  // partial slab [split][N][K] fp32
+  float* S = slabs + (long)split * g.N * g.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
+        if (n < g.N && k < g.K) S[(long)n * g.K + k] = acc[i][j][r];
+      }
+}
+
+// Register-staged variant (faster at large K = ks*Cin; the LDS-DMA one wins at K <= 1024).
+__global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                                                            float* __restrict__ slabs, float* __restrict__ bias_slabs,
                                                            ConvGeom g, int rows_per_split) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -446,13 +721,23 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
       db[n] = s;
     }
   }
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += slabs[(long)sp * total + e];
+  // 4 consecutive k per thread (K % 4 == 0: Cin % 8 == 0), float4 slab reads
+  const long total4 = total / 4;
+  for (long e4 = blockIdx.x * (long)blockDim.x + threadIdx.x; e4 < total4; e4 += (long)gridDim.x * blockDim.x) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4 v = reinterpret_cast<const float4*>(slabs + (long)sp * total)[e4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    const long e = e4 * 4;
     const long n = e / K;
     const int k = (int)(e - n * K);
-    const int tap = k / Cin, cin = k - tap * Cin;
-    dW[(n * Cin + cin) * ks + tap] = s;
+    const int tap = k / Cin, cin = k - tap * Cin;  // the 4 k share a tap (Cin % 4 == 0)
+    float* dst = dW + (n * Cin + cin) * ks + tap;
+    dst[0] = acc.x;
+    dst[ks] = acc.y;
+    dst[2 * ks] = acc.z;
+    dst[3 * ks] = acc.w;
   }
 }
 
@@ -471,8 +756,10 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
 }  // namespace
 
 static bool g_force_lds_epilogue = false;
+static int g_gemm_variant = 1;  // 0: register staging, 1: global_load_lds staging
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
+SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N) {
   ConvGeom g;
@@ -498,7 +785,14 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   // register epilogue needs N % 4 == 0 and an 8-B aligned ldy; LDS-staged epilogue otherwise
   const bool reg = (N % 4 == 0) && (ldy % 4 == 0) && !g_force_lds_epilogue;
   const size_t lds_reg = (size_t)2 * 2 * BM * BK * 2;
-  if (reg) {
+  if (reg && g_gemm_variant == 1) {
+    if (out_f32)
+      hipLaunchKernelGGL((conv_gemm_glds_kernel<true>), dim3(nwg), dim3(NT), lds_reg, s, X, W, bias, aux, resid, lens,
+                         Y, g, act, ldy);
+    else
+      hipLaunchKernelGGL((conv_gemm_glds_kernel<false>), dim3(nwg), dim3(NT), lds_reg, s, X, W, bias, aux, resid, lens,
+                         Y, g, act, ldy);
+  } else if (reg) {
     if (out_f32)
       hipLaunchKernelGGL((conv_gemm_kernel<true, true>), dim3(nwg), dim3(NT), lds_reg, s, X, W, bias, aux, resid, lens,
                          Y, g, act, ldy);
@@ -538,8 +832,12 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   rows_per_split = (rows_per_split + RB - 1) / RB * RB;
   splits = (g.M + rows_per_split - 1) / rows_per_split;
   float* bws = db ? ws + (long)splits * slab : nullptr;
-  hipLaunchKernelGGL(conv_wgrad_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
-                     rows_per_split);
+  if (g.K > 1024)
+    hipLaunchKernelGGL(conv_wgrad_reg_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
+                       rows_per_split);
+  else
+    hipLaunchKernelGGL(conv_wgrad_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
+                       rows_per_split);
   const long total = slab;
   int blocks = (int)min((total + 255) / 256, 8192L);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);

@@ -49,6 +49,7 @@ _SIGS = {
     "ssamd_attn_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, F, P],
     "ssamd_relu_mask": [P, P, P, L_, P],
     "ssamd_gemm_set_epilogue": [I],
+    "ssamd_gemm_set_variant": [I],
 }
 
 
