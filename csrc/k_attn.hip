@@ -98,7 +98,8 @@ __device__ __forceinline__ short8 tr_frag(const char* img, int base, int col0, i
 }
 
 // ------------------------------------------------------------------------------ forward
-template <int D>
+// NF = query fragments (of 16) per wave: each LDS fragment read feeds NF MFMAs.
+template <int D, int NF>
 __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
                                                       bf16_t* __restrict__ out, float* __restrict__ lse, int L, int H,
                                                       float scale_log2) {
@@ -110,22 +111,30 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int len = (int)lens[b];
   const long rowb = (long)b * L;
-  const int q = blockIdx.x * TQ + wave * 16 + (lane & 15);
   const bf16_t* Qp = qkv + h * D;
   const bf16_t* Kp = qkv + H * D + h * D;
   const bf16_t* Vp = qkv + 2 * H * D + h * D;
-
-  short8 qf[D / 32];
+  int qv[NF];
+  short8 qf[NF][D / 32];
 #pragma unroll
-  for (int s = 0; s < D / 32; ++s) {
-    short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (q < L) v = *reinterpret_cast<const short8*>(Qp + (rowb + q) * RS + s * 32 + 8 * g);
-    qf[s] = v;
+  for (int f = 0; f < NF; ++f) {
+    qv[f] = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qv[f] < L) v = *reinterpret_cast<const short8*>(Qp + (rowb + qv[f]) * RS + s * 32 + 8 * g);
+      qf[f][s] = v;
+    }
   }
-  float4v oacc[D / 16];
+  float4v oacc[NF][D / 16];
+  float m[NF], l[NF];
 #pragma unroll
-  for (int i = 0; i < D / 16; ++i) oacc[i] = (float4v){0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int f = 0; f < NF; ++f) {
+    m[f] = -INFINITY;
+    l[f] = 0.f;
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) oacc[f][i] = (float4v){0.f, 0.f, 0.f, 0.f};
+  }
 
   const int nkt = (len + TK - 1) / TK;
   short8 rk[D / 32], rv[D / 32];
@@ -143,91 +152,100 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
       load_tile<D>(Kp, rowb + k1, min(TK, len - k1), RS, rk);
       load_tile<D>(Vp, rowb + k1, min(TK, len - k1), RS, rv);
     }
-    float4v st[4];
+    float4v st[NF][4];
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf) {
-      st[kf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f = 0; f < NF; ++f) st[f][kf] = (float4v){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < D / 32; ++s) {
-        short8 a = *reinterpret_cast<const short8*>(Ks + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
-        st[kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[s], st[kf], 0, 0, 0);
+        const short8 a = *reinterpret_cast<const short8*>(Ks + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
+#pragma unroll
+        for (int f = 0; f < NF; ++f) st[f][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[f][s], st[f][kf], 0, 0, 0);
       }
     }
     const int key0 = kt * TK;
-    float mx = -INFINITY;
 #pragma unroll
-    for (int kf = 0; kf < 4; ++kf)
+    for (int f = 0; f < NF; ++f) {
+      float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = key0 + kf * 16 + 4 * g + r;
-        const float x = key < len ? st[kf][r] * scale_log2 : -INFINITY;
-        st[kf][r] = x;
-        mx = fmaxf(mx, x);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
-    float ls = 0.f;
+      for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
-    for (int kf = 0; kf < 4; ++kf)
+        for (int r = 0; r < 4; ++r) {
+          const int key = key0 + kf * 16 + 4 * g + r;
+          const float x = key < len ? st[f][kf][r] * scale_log2 : -INFINITY;
+          st[f][kf][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[f], mx);
+      const float alpha = exp2f(m[f] - mn);
+      float ls = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(st[kf][r] - mn);
-        st[kf][r] = p;
-        ls += p;
-      }
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
-    l = l * alpha + ls;
-    m = mn;
+      for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
-    for (int i = 0; i < D / 16; ++i) oacc[i] *= alpha;
+        for (int r = 0; r < 4; ++r) {
+          const float pv = exp2f(st[f][kf][r] - mn);
+          st[f][kf][r] = pv;
+          ls += pv;
+        }
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      l[f] = l[f] * alpha + ls;
+      m[f] = mn;
+#pragma unroll
+      for (int i = 0; i < D / 16; ++i) oacc[f][i] *= alpha;
+    }
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const short8 pb = pack8(st[2 * hh], st[2 * hh + 1]);
+      short8 pb[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) pb[f] = pack8(st[f][2 * hh], st[f][2 * hh + 1]);
 #pragma unroll
       for (int df = 0; df < D / 16; ++df) {
         const short8 a = tr_frag<D>(Vs, hh * 32, df * 16, lane);
-        oacc[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, oacc[df], 0, 0, 0);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) oacc[f][df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[f], oacc[f][df], 0, 0, 0);
       }
     }
   }
-  if (q < L) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    bf16_t* op = out + (rowb + q) * (long)(H * D) + h * D;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    if (qv[f] >= L) continue;
+    const float inv = l[f] > 0.f ? 1.f / l[f] : 0.f;
+    bf16_t* op = out + (rowb + qv[f]) * (long)(H * D) + h * D;
 #pragma unroll
     for (int df = 0; df < D / 16; ++df) {
       short4v v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(oacc[df][r] * inv);
+      for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(oacc[f][df][r] * inv);
       *reinterpret_cast<short4v*>(op + df * 16 + 4 * g) = v;
     }
-    if (g == 0) lse[(long)bh * L + q] = l > 0.f ? m + log2f(l) : INFINITY;
+    if (g == 0) lse[(long)bh * L + qv[f]] = l[f] > 0.f ? m[f] + log2f(l[f]) : INFINITY;
   }
 }
 
 // ------------------------------------------------------------------------------ backward
 __global__ void __launch_bounds__(NT) attn_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dO,
                                                         float* __restrict__ delta, long rows, int H, int D) {
-  // one wave per (row, head): delta[b, h, t] = sum_d dO * O
+  // one wave per (row, head): delta[row * H + h] = sum_d dO * O
   const long wid = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (wid >= rows * H) return;
   const long row = wid / H;
   const int h = (int)(wid % H);
-  const long L_dummy = 0;
-  (void)L_dummy;
   float s = 0.f;
   for (int d = lane; d < D; d += 64) {
     const long idx = row * (long)H * D + h * D + d;
     s += bf2f(o[idx]) * bf2f(dO[idx]);
   }
   s = wave_sum(s);
-  if (lane == 0) delta[wid] = s;  // laid out [row][h]; transposed by the consumers' indexing
+  if (lane == 0) delta[wid] = s;
 }
 
-template <int D>
+// NF = key fragments (of 16) per wave; block = 4 waves x 16*NF keys
+template <int D, int NF>
 __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
                                                            const int64_t* __restrict__ lens,
                                                            const bf16_t* __restrict__ dO, const float* __restrict__ lse,
@@ -243,29 +261,37 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int len = (int)lens[b];
   const long rowb = (long)b * L;
-  const int key = blockIdx.x * TK + wave * 16 + (lane & 15);
+  const int kblk0 = blockIdx.x * (64 * NF);
   const bf16_t* Qp = qkv + h * D;
   const bf16_t* Kp = qkv + H * D + h * D;
   const bf16_t* Vp = qkv + 2 * H * D + h * D;
   const bf16_t* dOp = dO + h * D;
 
-  short8 kb[D / 32], vb[D / 32];
+  int keyv[NF];
+  bool kval[NF];
+  short8 kb[NF][D / 32], vb[NF][D / 32];
 #pragma unroll
-  for (int s = 0; s < D / 32; ++s) {
-    short8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (key < L) {
-      kv = *reinterpret_cast<const short8*>(Kp + (rowb + key) * RS + s * 32 + 8 * g);
-      vv = *reinterpret_cast<const short8*>(Vp + (rowb + key) * RS + s * 32 + 8 * g);
+  for (int f = 0; f < NF; ++f) {
+    keyv[f] = kblk0 + wave * (16 * NF) + f * 16 + (lane & 15);
+    kval[f] = keyv[f] < len;
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      short8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (keyv[f] < L) {
+        kv = *reinterpret_cast<const short8*>(Kp + (rowb + keyv[f]) * RS + s * 32 + 8 * g);
+        vv = *reinterpret_cast<const short8*>(Vp + (rowb + keyv[f]) * RS + s * 32 + 8 * g);
+      }
+      kb[f][s] = kv;
+      vb[f][s] = vv;
     }
-    kb[s] = kv;
-    vb[s] = vv;
   }
-  float4v dk[D / 16], dv[D / 16];
+  float4v dk[NF][D / 16], dv[NF][D / 16];
 #pragma unroll
-  for (int i = 0; i < D / 16; ++i) dk[i] = dv[i] = (float4v){0.f, 0.f, 0.f, 0.f};
-  const bool key_valid = key < len;
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dk[f][i] = dv[f][i] = (float4v){0.f, 0.f, 0.f, 0.f};
 
-  const int nqt = (blockIdx.x * TK < len) ? (L + TQ - 1) / TQ : 0;  // key block fully masked -> zero grads
+  const int nqt = (kblk0 < len) ? (L + TQ - 1) / TQ : 0;  // fully masked key block -> zero grads
   short8 rq[D / 32], rd[D / 32];
   if (nqt > 0) {
     load_tile<D>(Qp, rowb, min(TQ, L), RS, rq);
@@ -283,16 +309,20 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
       load_tile<D>(Qp, rowb + q1, min(TQ, L - q1), RS, rq);
       load_tile<D>(dOp, rowb + q1, min(TQ, L - q1), OS, rd);
     }
-    float4v sp[4], dp[4];
+    float4v sp[NF][4], dp[NF][4];
 #pragma unroll
     for (int qf = 0; qf < 4; ++qf) {
-      sp[qf] = dp[qf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f = 0; f < NF; ++f) sp[f][qf] = dp[f][qf] = (float4v){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < D / 32; ++s) {
         const short8 aq = *reinterpret_cast<const short8*>(Qr + row_off<D>(qf * 16 + (lane & 15), s * 4 + g));
         const short8 ad = *reinterpret_cast<const short8*>(Dr + row_off<D>(qf * 16 + (lane & 15), s * 4 + g));
-        sp[qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kb[s], sp[qf], 0, 0, 0);
-        dp[qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vb[s], dp[qf], 0, 0, 0);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          sp[f][qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kb[f][s], sp[f][qf], 0, 0, 0);
+          dp[f][qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vb[f][s], dp[f][qf], 0, 0, 0);
+        }
       }
     }
     // P = exp2(S*c - lse2[q]); dS = P * (dP - delta[q]); rows = queries qt*64 + qf*16 + 4g + r
@@ -301,37 +331,52 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qt * TQ + qf * 16 + 4 * g + r;
-        float p = 0.f, ds = 0.f;
-        if (qq < L && key_valid) {
-          p = exp2f(sp[qf][r] * scale_log2 - lse[(long)bh * L + qq]);
-          ds = p * (dp[qf][r] - delta[(rowb + qq) * H + h]);
+        const bool qok = qq < L;
+        const float lq = qok ? lse[(long)bh * L + qq] : 0.f;
+        const float dq = qok ? delta[(rowb + qq) * H + h] : 0.f;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          float pv = 0.f, ds = 0.f;
+          if (qok && kval[f]) {
+            pv = exp2f(sp[f][qf][r] * scale_log2 - lq);
+            ds = pv * (dp[f][qf][r] - dq);
+          }
+          sp[f][qf][r] = pv;
+          dp[f][qf][r] = ds;
         }
-        sp[qf][r] = p;
-        dp[qf][r] = ds;
       }
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const short8 pb = pack8(sp[2 * hh], sp[2 * hh + 1]);
-      const short8 sb = pack8(dp[2 * hh], dp[2 * hh + 1]);
+      short8 pb[NF], sb[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        pb[f] = pack8(sp[f][2 * hh], sp[f][2 * hh + 1]);
+        sb[f] = pack8(dp[f][2 * hh], dp[f][2 * hh + 1]);
+      }
 #pragma unroll
       for (int df = 0; df < D / 16; ++df) {
         const short8 ado = tr_frag<D>(Dt, hh * 32, df * 16, lane);
-        dv[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pb, dv[df], 0, 0, 0);
         const short8 aq = tr_frag<D>(Qt, hh * 32, df * 16, lane);
-        dk[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, sb, dk[df], 0, 0, 0);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          dv[f][df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pb[f], dv[f][df], 0, 0, 0);
+          dk[f][df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, sb[f], dk[f][df], 0, 0, 0);
+        }
       }
     }
   }
-  if (key < L) {
-    bf16_t* dkp = dqkv + (rowb + key) * RS + H * D + h * D;
-    bf16_t* dvp = dqkv + (rowb + key) * RS + 2 * H * D + h * D;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    if (keyv[f] >= L) continue;
+    bf16_t* dkp = dqkv + (rowb + keyv[f]) * RS + H * D + h * D;
+    bf16_t* dvp = dqkv + (rowb + keyv[f]) * RS + 2 * H * D + h * D;
 #pragma unroll
     for (int df = 0; df < D / 16; ++df) {
       short4v a, c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        a[r] = (short)f2bf(dk[df][r] * scale);
-        c[r] = (short)f2bf(dv[df][r]);
+        a[r] = (short)f2bf(dk[f][df][r] * scale);
+        c[r] = (short)f2bf(dv[f][df][r]);
       }
       *reinterpret_cast<short4v*>(dkp + df * 16 + 4 * g) = a;
       *reinterpret_cast<short4v*>(dvp + df * 16 + 4 * g) = c;
@@ -339,7 +384,8 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   }
 }
 
-template <int D>
+// NF = query fragments per wave; block = 4 waves x 16*NF queries
+template <int D, int NF>
 __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
                                                          const bf16_t* __restrict__ dO, const float* __restrict__ lse,
                                                          const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
@@ -353,27 +399,34 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int len = (int)lens[b];
   const long rowb = (long)b * L;
-  const int q = blockIdx.x * TQ + wave * 16 + (lane & 15);
   const bf16_t* Qp = qkv + h * D;
   const bf16_t* Kp = qkv + H * D + h * D;
   const bf16_t* Vp = qkv + 2 * H * D + h * D;
 
-  short8 qf[D / 32], df_[D / 32];
+  int qv[NF];
+  float lq[NF], dd[NF];
+  short8 qf[NF][D / 32], df_[NF][D / 32];
 #pragma unroll
-  for (int s = 0; s < D / 32; ++s) {
-    short8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (q < L) {
-      a = *reinterpret_cast<const short8*>(Qp + (rowb + q) * RS + s * 32 + 8 * g);
-      c = *reinterpret_cast<const short8*>(dO + (rowb + q) * OS + h * D + s * 32 + 8 * g);
+  for (int f = 0; f < NF; ++f) {
+    qv[f] = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      short8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qv[f] < L) {
+        a = *reinterpret_cast<const short8*>(Qp + (rowb + qv[f]) * RS + s * 32 + 8 * g);
+        c = *reinterpret_cast<const short8*>(dO + (rowb + qv[f]) * OS + h * D + s * 32 + 8 * g);
+      }
+      qf[f][s] = a;
+      df_[f][s] = c;
     }
-    qf[s] = a;
-    df_[s] = c;
+    lq[f] = qv[f] < L ? lse[(long)bh * L + qv[f]] : 0.f;
+    dd[f] = qv[f] < L ? delta[(rowb + qv[f]) * H + h] : 0.f;
   }
-  const float lq = q < L ? lse[(long)bh * L + q] : 0.f;
-  const float dq_delta = q < L ? delta[(rowb + q) * H + h] : 0.f;
-  float4v dq[D / 16];
+  float4v dq[NF][D / 16];
 #pragma unroll
-  for (int i = 0; i < D / 16; ++i) dq[i] = (float4v){0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dq[f][i] = (float4v){0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (len + TK - 1) / TK;
   short8 rk[D / 32], rv[D / 32];
@@ -392,16 +445,20 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
       load_tile<D>(Kp, rowb + k1, min(TK, len - k1), RS, rk);
       load_tile<D>(Vp, rowb + k1, min(TK, len - k1), RS, rv);
     }
-    float4v st[4], dpt[4];
+    float4v st[NF][4], dpt[NF][4];
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf) {
-      st[kf] = dpt[kf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f = 0; f < NF; ++f) st[f][kf] = dpt[f][kf] = (float4v){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < D / 32; ++s) {
         const short8 ak = *reinterpret_cast<const short8*>(Kr + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
         const short8 av = *reinterpret_cast<const short8*>(Vr + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
-        st[kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[s], st[kf], 0, 0, 0);
-        dpt[kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df_[s], dpt[kf], 0, 0, 0);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          st[f][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[f][s], st[f][kf], 0, 0, 0);
+          dpt[f][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df_[f][s], dpt[f][kf], 0, 0, 0);
+        }
       }
     }
 #pragma unroll
@@ -409,30 +466,38 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kt * TK + kf * 16 + 4 * g + r;
-        float ds = 0.f;
-        if (key < len && q < L) {
-          const float p = exp2f(st[kf][r] * scale_log2 - lq);
-          ds = p * (dpt[kf][r] - dq_delta);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          float ds = 0.f;
+          if (key < len && qv[f] < L) {
+            const float pv = exp2f(st[f][kf][r] * scale_log2 - lq[f]);
+            ds = pv * (dpt[f][kf][r] - dd[f]);
+          }
+          st[f][kf][r] = ds;
         }
-        st[kf][r] = ds;
       }
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const short8 sb = pack8(st[2 * hh], st[2 * hh + 1]);
+      short8 sb[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) sb[f] = pack8(st[f][2 * hh], st[f][2 * hh + 1]);
 #pragma unroll
       for (int df = 0; df < D / 16; ++df) {
         const short8 ak = tr_frag<D>(Kt, hh * 32, df * 16, lane);
-        dq[df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, sb, dq[df], 0, 0, 0);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) dq[f][df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, sb[f], dq[f][df], 0, 0, 0);
       }
     }
   }
-  if (q < L) {
-    bf16_t* dqp = dqkv + (rowb + q) * RS + h * D;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    if (qv[f] >= L) continue;
+    bf16_t* dqp = dqkv + (rowb + qv[f]) * RS + h * D;
 #pragma unroll
     for (int df = 0; df < D / 16; ++df) {
       short4v a;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] = (short)f2bf(dq[df][r] * scale);
+      for (int r = 0; r < 4; ++r) a[r] = (short)f2bf(dq[f][df][r] * scale);
       *reinterpret_cast<short4v*>(dqp + df * 16 + 4 * g) = a;
     }
   }
@@ -440,12 +505,14 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
 
 }  // namespace
 
-#define ATTN_DISPATCH(D, ...)                                  \
-  switch (D) {                                                 \
-    case 32: { constexpr int DD = 32; __VA_ARGS__; break; }    \
-    case 64: { constexpr int DD = 64; __VA_ARGS__; break; }    \
-    case 128: { constexpr int DD = 128; __VA_ARGS__; break; }  \
-    default: return -1;                                        \
+// NF (fragments per wave) chosen from measurement on MI355X: the forward keeps 2 waves/SIMD
+// with NF = 1; the D >= 64 backward is LDS-read bound and gains from NF = 2.
+#define ATTN_DISPATCH(D, FWD, ...)                                                                 \
+  switch (D) {                                                                                     \
+    case 32: { constexpr int DD = 32; constexpr int NF = 1; __VA_ARGS__; break; }                 \
+    case 64: { constexpr int DD = 64; constexpr int NF = FWD ? 1 : 2; __VA_ARGS__; break; }       \
+    case 128: { constexpr int DD = 128; constexpr int NF = FWD ? 1 : 2; __VA_ARGS__; break; }     \
+    default: return -1;                                                                            \
   }
 
 static const float kLog2e = 1.4426950408889634f;
@@ -453,9 +520,10 @@ static const float kLog2e = 1.4426950408889634f;
 SSAMD_API int ssamd_attn_fwd(const bf16_t* qkv, const int64_t* lens, bf16_t* out, float* lse, int B, int L, int H,
                              int D, float scale, hipStream_t s) {
   if ((long)B * L == 0) return 0;
-  dim3 grid(cdiv(L, TQ), B * H);
-  ATTN_DISPATCH(D, hipLaunchKernelGGL(attn_fwd_kernel<DD>, grid, dim3(NT), 0, s, qkv, lens, out, lse, L, H,
-                                      scale * kLog2e));
+  ATTN_DISPATCH(D, true, {
+    dim3 grid(cdiv(L, 64 * NF), B * H);
+    hipLaunchKernelGGL((attn_fwd_kernel<DD, NF>), grid, dim3(NT), 0, s, qkv, lens, out, lse, L, H, scale * kLog2e);
+  });
   return (int)hipGetLastError();
 }
 
@@ -467,12 +535,12 @@ SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const bf16_
   if ((long)B * L == 0) return 0;
   const long rows = (long)B * L;
   hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
-  dim3 grid(cdiv(L, TK), B * H);
-  ATTN_DISPATCH(D, {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<DD>, grid, dim3(NT), 4 * TQ * DD * 2, s, qkv, lens, dO, lse, delta, dqkv, L,
-                       H, scale * kLog2e, scale);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<DD>, grid, dim3(NT), 3 * TK * DD * 2, s, qkv, lens, dO, lse, delta, dqkv, L,
-                       H, scale * kLog2e, scale);
+  ATTN_DISPATCH(D, false, {
+    dim3 grid(cdiv(L, 64 * NF), B * H);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), 4 * TQ * DD * 2, s, qkv, lens, dO, lse, delta,
+                       dqkv, L, H, scale * kLog2e, scale);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), 3 * TK * DD * 2, s, qkv, lens, dO, lse, delta,
+                       dqkv, L, H, scale * kLog2e, scale);
   });
   return (int)hipGetLastError();
 }
