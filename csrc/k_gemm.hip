@@ -422,6 +422,187 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
 }
 
 // ----------------------------------------------------------------------------
+// 256x128 tile, 8 waves (4x2, 64x64 each), 3-stage LDS-DMA ring with a COUNTED vmcnt:
+// the DMA for stage k+2 is issued before computing stage k, and only stage k+1 is
+// waited for at the end of the iteration (raw s_barrier -- __syncthreads() would drain
+// every in-flight LDS-DMA).  144 KiB LDS, 1 block (2 waves/SIMD) per CU.
+// ----------------------------------------------------------------------------
+constexpr int BM3 = 256, NT3 = 512, NSTAGE = 3;
+constexpr int STAGE_BYTES = (BM3 + BN) * BK * 2;  // 48 KiB
+
+template <bool OUT_F32, bool FASTK>
+__global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                                const float* __restrict__ bias,
+                                                                const bf16_t* __restrict__ aux,
+                                                                const bf16_t* __restrict__ resid,
+                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
+                                                                ConvGeom g, int act, int ldy) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + BN - 1) / BN;
+  const int nM = (g.M + BM3 - 1) / BM3;
+  const int wg = xcd_remap(blockIdx.x, nN * nM);
+  const int tn = wg % nN, tm = wg / nN;
+  const int m0 = tm * BM3, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const float invCin = 1.f / (float)g.Cin;
+
+  // A: 256 rows = 32 wave-instructions (4 per wave); B: 128 rows = 16 (2 per wave)
+  int a_b[4], a_t[4], a_m[4], achunk[4];
+  const bf16_t* arow_ptr[4];
+  const bf16_t* brow_ptr[2];
+  bool a_ok[4], b_ok[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    achunk[i] = (lane & 7) ^ ((row >> 1) & 7);
+    a_m[i] = m0 + row;
+    a_ok[i] = a_m[i] < g.M;
+    const int mm = a_ok[i] ? a_m[i] : 0;
+    a_b[i] = mm / g.L;
+    a_t[i] = mm - a_b[i] * g.L;
+    arow_ptr[i] = X + ((long)a_b[i] * g.L + a_t[i]) * g.Cin + achunk[i] * 8;  // tap-0, cin-0 origin
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    const int bch = (lane & 7) ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    b_ok[i] = n < g.N;
+    brow_ptr[i] = W + (long)(b_ok[i] ? n : 0) * g.K + bch * 8;
+  }
+  auto stage = [&](int kt, int buf) {
+    char* As = smem + buf * STAGE_BYTES;
+    char* Bs = As + BM3 * BK * 2;
+    const int k0 = kt * BK;
+    if constexpr (FASTK) {
+      // Cin % 64 == 0: the whole 64-wide k slab sits in one tap -> wave-uniform shift / offset
+      const int tap = k0 / g.Cin;
+      const int cin0 = k0 - tap * g.Cin;
+      const int shift = tap * g.dil - g.pad;
+      const long off = (long)shift * g.Cin + cin0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ts = a_t[i] + shift;
+        const bool ok = a_ok[i] && ts >= 0 && ts < g.L;
+        glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 8 * 128);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        glds16(b_ok[i] ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk, Bs + (i * 8 + wave) * 8 * 128);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + achunk[i] * 8;
+        const void* src = g_zero_chunk;
+        if (a_ok[i] && k < g.K) {
+          const int tap = (int)(((float)k + 0.5f) * invCin);
+          const int cin = k - tap * g.Cin;
+          const int ts = a_t[i] + tap * g.dil - g.pad;
+          if (ts >= 0 && ts < g.L) src = X + ((long)a_b[i] * g.L + ts) * g.Cin + cin;
+        }
+        glds16(src, As + (i * 8 + wave) * 8 * 128);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (i * 8 + wave) * 8 + (lane >> 3);
+        const int k = k0 + ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+        glds16((b_ok[i] && k < g.K) ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk,
+               Bs + (i * 8 + wave) * 8 * 128);
+      }
+    }
+  };
+
+  float4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + BK - 1) / BK;
+  stage(0, 0);
+  if (nk > 1) {
+    stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 2 < nk) stage(kt + 2, (buf + 2) % NSTAGE);
+    const char* As = smem + buf * STAGE_BYTES;
+    const char* Bs = As + BM3 * BK * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      short8 fa[4], fb[4];
+      const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i] = *reinterpret_cast<const short8*>(As + swz128(wm * 64 + i * 16 + (lane & 15), c));
+        fb[i] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + i * 16 + (lane & 15), c));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    // retire stage kt+1 (leave kt+2 in flight), make it visible, and free buf for re-staging
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    buf = (buf + 1) % NSTAGE;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    const int bb = m / g.L, tt = m - bb * g.L;
+    const bool valid = lens == nullptr || tt < (int)lens[bb];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+        const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+        v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+      }
+      if (act == ACT_RELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      } else if (act == ACT_LRELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+      } else if (act == ACT_TANH) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+      }
+      const long off = (long)m * ldy + n;
+      if (aux) {
+        const short4v x = *reinterpret_cast<const short4v*>(aux + off);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
+      }
+      if (resid) {
+        const short4v x = *reinterpret_cast<const short4v*>(resid + off);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
+      }
+      if (!valid) v[0] = v[1] = v[2] = v[3] = 0.f;
+      if constexpr (OUT_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        short4v o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
+        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
 // Weight gradient.  Tile: 128 (n = cout) x 128 (k = tap*Cin + cin), reduction over
 // rows m in steps of RB = 64.  LDS image per operand: [64 rows][128 cols] bf16,
 // 256-B rows, 8-B column chunks XOR-swizzled by f(row) = ((row&3) | ((row>>3)&1)<<2) << 2
@@ -477,24 +658,29 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
     c_tap[i] = c_kok[i] ? (int)(((float)k + 0.5f) * invCin) : 0;
     c_cin[i] = k - c_tap[i] * g.Cin;
   }
+  // per-row time index t = m mod L, advanced incrementally (stage() is called for r0 = r_begin, +RB, ...)
+  int tcur[4], shift[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    tcur[i] = (r_begin + rr[i]) % g.L;
+    shift[i] = c_tap[i] * g.dil - g.pad;
+  }
   auto stage = [&](int r0, int buf) {
     char* Ys = smem + buf * (2 * RB * 256);
     char* Xs = Ys + RB * 256;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + rr[i];
-      const void* sy = g_zero_chunk;
-      const void* sx = g_zero_chunk;
-      if (m < r_end) {
-        if (c_n[i] < g.N) sy = dY + (long)m * g.N + c_n[i];
-        if (c_kok[i]) {
-          const int bb = m / g.L, tt = m - bb * g.L;
-          const int ts = tt + c_tap[i] * g.dil - g.pad;
-          if (ts >= 0 && ts < g.L) sx = X + ((long)bb * g.L + ts) * g.Cin + c_cin[i];
-        }
-      }
+      const bool mok = m < r_end;
+      const int ts = tcur[i] + shift[i];
+      const bool xok = mok && c_kok[i] && ts >= 0 && ts < g.L;
+      const void* sy = (mok && c_n[i] < g.N) ? (const void*)(dY + (long)m * g.N + c_n[i]) : (const void*)g_zero_chunk;
+      const void* sx = xok ? (const void*)(X + (long)(m + shift[i]) * g.Cin + c_cin[i]) : (const void*)g_zero_chunk;
       glds16(sy, Ys + (i * 4 + wave) * 4 * 256);
       glds16(sx, Xs + (i * 4 + wave) * 4 * 256);
+      int t = tcur[i] + RB;
+      while (t >= g.L) t -= g.L;
+      tcur[i] = t;
     }
   };
   // bias gradient (column sums of dY) for the k-tile-0 blocks, read back from the LDS image
@@ -605,6 +791,10 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
   }
   const int n_ld = n0 + c16 * 8;
   short8 rx[4], ry[4];
+  int tcur[4];
+  const int xshift = tap * g.dil - g.pad;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tcur[i] = (r_begin + (tid >> 4) + 16 * i) % g.L;
   auto gload = [&](int r0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -612,14 +802,14 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
       short8 vx = {0, 0, 0, 0, 0, 0, 0, 0}, vy = {0, 0, 0, 0, 0, 0, 0, 0};
       if (m < r_end) {
         if (n_ld < g.N) vy = *reinterpret_cast<const short8*>(dY + (long)m * g.N + n_ld);
-        if (k_ok) {
-          const int bb = m / g.L, tt = m - bb * g.L;
-          const int ts = tt + tap * g.dil - g.pad;
-          if (ts >= 0 && ts < g.L) vx = *reinterpret_cast<const short8*>(X + ((long)bb * g.L + ts) * g.Cin + cin);
-        }
+        const int ts = tcur[i] + xshift;
+        if (k_ok && ts >= 0 && ts < g.L) vx = *reinterpret_cast<const short8*>(X + (long)(m + xshift) * g.Cin + cin);
       }
       rx[i] = vx;
       ry[i] = vy;
+      int t = tcur[i] + RB;
+      while (t >= g.L) t -= g.L;
+      tcur[i] = t;
     }
   };
   // bias gradient (column sums of dY) rides on the staging registers of the k-tile-0 blocks
@@ -756,7 +946,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
 }  // namespace
 
 static bool g_force_lds_epilogue = false;
-static int g_gemm_variant = 1;  // 0: register staging, 1: global_load_lds staging
+static int g_gemm_variant = -1;  // -1 auto, 0: register staging, 1: LDS-DMA 128x128, 2: LDS-DMA 3-stage ring 256x128
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
 SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
@@ -785,7 +975,29 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   // register epilogue needs N % 4 == 0 and an 8-B aligned ldy; LDS-staged epilogue otherwise
   const bool reg = (N % 4 == 0) && (ldy % 4 == 0) && !g_force_lds_epilogue;
   const size_t lds_reg = (size_t)2 * 2 * BM * BK * 2;
-  if (reg && g_gemm_variant == 1) {
+  int variant = g_gemm_variant;
+  if (variant < 0) variant = (Cin % BK == 0) ? 2 : 1;  // measured on MI355X: ring wins whenever K-slabs are tap-aligned
+  if (reg && variant == 2) {
+    static bool ring_set = false;
+    if (!ring_set) {
+      allow_lds(conv_gemm_ring_kernel<true, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<true, false>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, false>, NSTAGE * STAGE_BYTES);
+      ring_set = true;
+    }
+    const int nwg3 = ((g.M + BM3 - 1) / BM3) * ((N + BN - 1) / BN);
+    const bool fastk = (Cin % BK) == 0;
+    const size_t L3 = NSTAGE * STAGE_BYTES;
+#define RING_LAUNCH(F32, FK) \
+    hipLaunchKernelGGL((conv_gemm_ring_kernel<F32, FK>), dim3(nwg3), dim3(NT3), L3, s, X, W, bias, aux, resid, lens, Y, g, act, ldy)
+    if (out_f32) {
+      if (fastk) RING_LAUNCH(true, true); else RING_LAUNCH(true, false);
+    } else {
+      if (fastk) RING_LAUNCH(false, true); else RING_LAUNCH(false, false);
+    }
+#undef RING_LAUNCH
+  } else if (reg && variant == 1) {
     if (out_f32)
       hipLaunchKernelGGL((conv_gemm_glds_kernel<true>), dim3(nwg), dim3(NT), lds_reg, s, X, W, bias, aux, resid, lens,
                          Y, g, act, ldy);

@@ -309,3 +309,20 @@ def test_bn_dropout_rate():
     y = hip.bn_act(h, bn, True, True, 0.5)
     frac = (y == 0).float().mean().item()
     assert 0.47 < frac < 0.53
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_conv_gemm_variants(variant):
+    """Every GEMM main-loop variant (register staging / LDS-DMA / 3-stage ring) vs fp32."""
+    torch.manual_seed(12)
+    B, L, Cin, N, ks = 3, 97, 256, 1024, 9
+    x = torch.randn(B, L, Cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, ks, Cin, device=DEV).to(torch.bfloat16) / 48
+    bias = torch.randn(N, device=DEV)
+    hip.lib().ssamd_gemm_set_variant(variant)
+    try:
+        y = hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, 4, N, 1)
+    finally:
+        hip.lib().ssamd_gemm_set_variant(-1)
+    yr = ref.conv1d(x.float(), w.float().permute(0, 2, 1), bias, 4, 1, "relu")
+    assert _rel(y, yr) < 1e-2

@@ -18,14 +18,7 @@ cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python "$R/bench.py" --steps 3 --warmup 2 ${BENCHARGS} > "$R/gpurun_out/prof.log" 2>&1 || { tail -30 "$R/gpurun_out/prof.log"; exit 1; }
 cd "$R"
 f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1)
+t=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
 echo "stats: $f"
-python - "$f" <<'PY'
-import csv, sys
-rows = list(csv.DictReader(open(sys.argv[1])))
-tot = sum(float(r["TotalDurationNs"]) for r in rows)
-rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
-print(f"total kernel time {tot/1e6:.1f} ms")
-for r in rows[:30]:
-    print(f'{float(r["TotalDurationNs"])/1e6:9.2f} ms {100*float(r["TotalDurationNs"])/tot:5.1f}% n={r["Calls"]:>5} {r["Name"][:110]}')
-PY
+python tools/prof_summary.py "$f" "$t"
 fi
