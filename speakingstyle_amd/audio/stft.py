@@ -40,7 +40,8 @@ class TacotronSTFT(torch.nn.Module):
 
     def mel_spectrogram(self, y: torch.Tensor):
         """y [B, N] in [-1, 1] -> (mel [B, n_mel, frames], energy [B, frames])."""
-        assert float(y.min()) >= -1 and float(y.max()) <= 1
+        if not y.requires_grad and not y.is_cuda:  # reference range check (audio/stft.py:169-170), host tensors only
+            assert float(y.min()) >= -1 and float(y.max()) <= 1
         mag = self.magnitudes(y)
         mel = dynamic_range_compression(torch.matmul(self.mel_basis.to(y.device), mag))
         energy = torch.norm(mag, dim=1)

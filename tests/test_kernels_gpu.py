@@ -326,3 +326,17 @@ def test_conv_gemm_variants(variant):
         hip.lib().ssamd_gemm_set_variant(-1)
     yr = ref.conv1d(x.float(), w.float().permute(0, 2, 1), bias, 4, 1, "relu")
     assert _rel(y, yr) < 1e-2
+
+
+def test_hifigan_infer_gpu():
+    """Channel-last HIP vocoder path (implicit-GEMM dilated convs + polyphase ConvT) vs fp32 NCL forward."""
+    from speakingstyle_amd.models import hifigan as H
+
+    torch.manual_seed(13)
+    g = H.Generator(H.default_config()).eval().fold_weight_norm().to(DEV)
+    mel = torch.randn(2, 80, 24, device=DEV) * 2 - 5
+    with torch.no_grad():
+        ref_w = g(mel).squeeze(1)
+        w = g.infer(mel.transpose(1, 2).contiguous().to(torch.bfloat16)).float()
+    assert w.shape == ref_w.shape
+    assert _rel(w, ref_w) < 5e-2
