@@ -61,8 +61,16 @@ def corpus(tmp_path_factory):
 
 def test_prepare_and_preprocess(corpus):
     root, pf, p = corpus
-    import prepare_align
-    import preprocess
+    import importlib.util
+
+    def _load(name):  # by path: the session-scoped reference fixture may shadow same-named top-level modules
+        spec = importlib.util.spec_from_file_location("ssamd_cli_" + name, os.path.join(ROOT, name + ".py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+
+    prepare_align = _load("prepare_align")
+    preprocess = _load("preprocess")
 
     assert prepare_align.main([str(pf)]) == 12
     assert (root / "raw" / "LJSpeech" / "LJ000.lab").read_text().startswith("hello world")
