@@ -335,3 +335,49 @@ SSAMD_API int ssamd_relu_mask(const bf16_t* dy, const bf16_t* y, bf16_t* out, lo
   hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(n, 8)), dim3(256), 0, s, dy, y, out, n);
   return (int)hipGetLastError();
 }
+
+// ----------------------------------------------------------------------------
+// Batched weight-image refresh: ONE launch re-derives every bf16 operand image of
+// every weight after an optimizer step (instead of one cast/permute kernel per weight).
+//   mode 0: conv fwd   [Cout][ks][Cin]  <- fp32 [Cout][Cin][ks]   (Linear: ks = 1, plain cast)
+//   mode 1: conv dgrad [Cin][ks][Cout]  <- fp32 [Cout][Cin][ks], taps flipped (Linear: transpose)
+// ----------------------------------------------------------------------------
+struct WDesc {
+  const float* src;
+  bf16_t* dst;
+  int cout, cin, ks, mode;
+};
+
+namespace {
+__global__ void __launch_bounds__(256) weight_prep_kernel(const WDesc* __restrict__ tab, const long* __restrict__ cum,
+                                                          int n, long total) {
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    int lo = 0, hi = n;  // last d with cum[d] <= e
+    while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cum[mid] <= e) lo = mid; else hi = mid; }
+    const WDesc d = tab[lo];
+    const long i = e - cum[lo];
+    long src;
+    if (d.mode == 0) {  // dst [co][tap][ci]
+      const int ci = (int)(i % d.cin);
+      const long r = i / d.cin;
+      const int tap = (int)(r % d.ks);
+      const int co = (int)(r / d.ks);
+      src = ((long)co * d.cin + ci) * d.ks + tap;
+    } else {  // dst [ci][tap'][co], tap = ks-1-tap'
+      const int co = (int)(i % d.cout);
+      const long r = i / d.cout;
+      const int tp = (int)(r % d.ks);
+      const int ci = (int)(r / d.ks);
+      src = ((long)co * d.cin + ci) * d.ks + (d.ks - 1 - tp);
+    }
+    d.dst[i] = f2bf(d.src[src]);
+  }
+}
+}  // namespace
+
+SSAMD_API int ssamd_weight_prep(const void* table, const long* cum, int n, long total, hipStream_t s) {
+  if (n == 0 || total == 0) return 0;
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_for(total, 4)), dim3(256), 0, s,
+                     reinterpret_cast<const WDesc*>(table), cum, n, total);
+  return (int)hipGetLastError();
+}

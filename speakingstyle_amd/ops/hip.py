@@ -16,6 +16,7 @@ import ctypes
 import math
 import os
 import threading
+import weakref
 from typing import Optional
 
 import torch
@@ -50,6 +51,7 @@ _SIGS = {
     "ssamd_relu_mask": [P, P, P, L_, P],
     "ssamd_gemm_set_epilogue": [I],
     "ssamd_gemm_set_variant": [I],
+    "ssamd_weight_prep": [P, P, I, L_, P],
 }
 
 
@@ -107,34 +109,85 @@ def _need(t, dtype, name):
 
 
 # ------------------------------------------------------------------------ weight images
-_wcache = {}
+# bf16 operand images of fp32 master weights, keyed by (parameter, layout).  An image is
+# valid for one (param._version, weight generation) pair: the fused Adam kernel writes the
+# arena through raw pointers (torch's version counters do not see it), so the optimizer
+# calls ``bump_weight_generation()``; the first stale lookup afterwards refreshes EVERY
+# registered image in one batched ``weight_prep`` launch instead of ~2 cast kernels per weight.
+_wcache = {}          # key -> [version, generation, weakref(param), image, mode, src_ptr]
+_wgen = 0
+_wtable = {"n": -1}   # device descriptor table for the batched refresh
 
 
-def _cached(param: torch.Tensor, kind: str, make):
+def bump_weight_generation():
+    """Mark every cached weight image stale (call after writing parameters through raw pointers)."""
+    global _wgen
+    _wgen += 1
+
+
+def _eligible(w: torch.Tensor) -> bool:
+    return w.is_cuda and w.dtype == torch.float32 and w.is_contiguous() and w.dim() in (2, 3)
+
+
+def _refresh_all(device):
+    live = []
+    for k in list(_wcache):
+        e = _wcache[k]
+        w = e[2]()
+        if w is None or w.data_ptr() != e[5]:
+            del _wcache[k]
+            _wtable["n"] = -1
+        elif w.device == device and _eligible(w):
+            live.append((e, w))
+    if _wtable.get("n") != len(live) or _wtable.get("dev") != device:
+        import numpy as np
+        desc = np.zeros(len(live), dtype=[("src", "<u8"), ("dst", "<u8"), ("cout", "<i4"), ("cin", "<i4"),
+                                          ("ks", "<i4"), ("mode", "<i4")])
+        cum = np.zeros(len(live) + 1, dtype=np.int64)
+        for i, (e, w) in enumerate(live):
+            ks = w.shape[2] if w.dim() == 3 else 1
+            desc[i] = (w.data_ptr(), e[3].data_ptr(), w.shape[0], w.shape[1], ks, e[4])
+            cum[i + 1] = cum[i] + w.numel()
+        _wtable.update(n=len(live), dev=device, total=int(cum[-1]),
+                       desc=torch.from_numpy(desc.view(np.uint8).copy()).to(device),
+                       cum=torch.from_numpy(cum).to(device))
+    if _wtable["n"]:
+        rc = lib().ssamd_weight_prep(_ptr(_wtable["desc"]), _ptr(_wtable["cum"]), _wtable["n"], _wtable["total"],
+                                     _stream())
+        _check(rc, "ssamd_weight_prep")
+    for e, w in live:
+        e[0], e[1] = w._version, _wgen
+
+
+def _cached(param: torch.Tensor, kind: str, mode: int, make):
     if not isinstance(param, torch.nn.Parameter):  # transient tensors: ids / addresses get reused
         return make(param.detach())
     key = (id(param), kind)
-    ver = param._version
     hit = _wcache.get(key)
-    if hit is not None and hit[0] == ver and hit[1].data_ptr() == param.data_ptr():
-        return hit[2]
+    if hit is not None and hit[2]() is param and hit[5] == param.data_ptr():
+        if hit[0] == param._version and hit[1] == _wgen:
+            return hit[3]
+        if _eligible(param) and has("ssamd_weight_prep"):
+            _refresh_all(param.device)
+            return hit[3]
     img = make(param.detach())
-    _wcache[key] = (ver, param, img)
+    _wcache[key] = [param._version, _wgen, weakref.ref(param), img, mode, param.data_ptr()]
+    _wtable["n"] = -1  # entry set changed: rebuild the descriptor table on the next refresh
     return img
 
 
 def weight_fwd(w: torch.Tensor) -> torch.Tensor:
     """[Cout, Cin, ks] (or Linear [out, in]) fp32 -> bf16 [Cout][ks][Cin]."""
     if w.dim() == 2:
-        return _cached(w, "fwd", lambda x: x.to(torch.bfloat16).contiguous())
-    return _cached(w, "fwd", lambda x: x.permute(0, 2, 1).to(torch.bfloat16).contiguous())
+        return _cached(w, "fwd", 0, lambda x: x.to(torch.bfloat16).contiguous())
+    return _cached(w, "fwd", 0, lambda x: x.permute(0, 2, 1).to(torch.bfloat16).contiguous())
 
 
 def weight_dgrad(w: torch.Tensor) -> torch.Tensor:
     """-> bf16 [Cin][ks][Cout] with taps flipped (data gradient = conv with W^T)."""
     if w.dim() == 2:
-        return _cached(w, "dgrad", lambda x: x.t().to(torch.bfloat16).contiguous())
-    return _cached(w, "dgrad", lambda x: x.flip(2).permute(1, 2, 0).to(torch.bfloat16).contiguous())
+        return _cached(w, "dgrad", 1, lambda x: x.t().to(torch.bfloat16).contiguous())
+    return _cached(w, "dgrad", 1, lambda x: x.flip(2).permute(1, 2, 0).to(torch.bfloat16).contiguous())
 
 
 _ACT = {None: 0, "relu": 1, "lrelu": 2, "tanh": 3}

@@ -146,6 +146,9 @@ def broadcast_module_state(module: torch.nn.Module, src: int = 0):
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src)
+    from ..ops import hip  # ``.data`` writes bypass version counters: cached bf16 images are stale
+
+    hip.bump_weight_generation()
 
 
 def all_reduce_async(t: torch.Tensor):

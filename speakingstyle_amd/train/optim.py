@@ -166,6 +166,7 @@ def fused_adam_step(opt: ScheduledOptim, lr: float):
 
         hip.clip_adam_step(a.data, a.grad, opt.exp_avg, opt.exp_avg_sq, lr, opt.betas, opt.eps, opt.weight_decay,
                            opt.step_count, opt.grad_clip, opt.last_grad_norm, opt.skipped_steps)
+        hip.bump_weight_generation()  # raw-pointer writes: torch version counters do not move
         return
     g = a.grad
     norm = torch.linalg.vector_norm(g)

@@ -340,3 +340,40 @@ def test_hifigan_infer_gpu():
         w = g.infer(mel.transpose(1, 2).contiguous().to(torch.bfloat16)).float()
     assert w.shape == ref_w.shape
     assert _rel(w, ref_w) < 5e-2
+
+
+def test_weight_images_follow_optimizer():
+    """bf16 weight images must be re-derived after the fused Adam step (raw-pointer writes)."""
+    import copy
+
+    from speakingstyle_amd import ops
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+    from speakingstyle_amd.models.loss import FastSpeech2Loss
+    from speakingstyle_amd.train.optim import ScheduledOptim, fused_adam_step
+
+    pp, mc, tc = load_named("LJSpeech")
+    mc["transformer"]["encoder_layer"] = mc["transformer"]["decoder_layer"] = 2
+    torch.manual_seed(3)
+    m = FastSpeech2(pp, mc).to(DEV).set_compute_dtype(torch.bfloat16)
+    opt = ScheduledOptim(m, tc, mc, 0)
+    b = SyntheticBatches(4, device=DEV, seed=5, phone_counts=[30, 41, 17, 25]).make_batch()
+    lossf = FastSpeech2Loss(pp, tc)
+    m.train()
+    for _ in range(2):
+        opt.zero_grad()
+        lo = lossf(b, m(*b[2:]), m.film_scalars())
+        lo[0].backward()
+        opt.step_count += 1
+        fused_adam_step(opt, 1e-2)  # large lr: weights move visibly
+    m.eval()
+    with torch.no_grad():
+        out = m(*b[2:])
+        mr = copy.deepcopy(m).set_compute_dtype(torch.float32)
+        ops.set_backend("reference")
+        try:
+            outr = mr(*b[2:])
+        finally:
+            ops.set_backend(None)
+    assert _rel(out[1], outr[1]) < 3e-2
