@@ -101,6 +101,7 @@ __device__ __forceinline__ short8 tr_frag(const char* img, int base, int col0, i
 // NF = query fragments (of 16) per wave: each LDS fragment read feeds NF MFMAs.
 template <int D, int NF>
 __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
+                                                      const int64_t* __restrict__ cu,
                                                       bf16_t* __restrict__ out, float* __restrict__ lse, int L, int H,
                                                       float scale_log2) {
   __shared__ __attribute__((aligned(16))) char smem[2 * TK * D * 2];
@@ -110,19 +111,35 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
   const int RS = 3 * H * D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int len = (int)lens[b];
-  const long rowb = (long)b * L;
+  // packed variable-length rows (cu = row offsets): only rows < len exist for sequence b
+  const long rowb = cu ? (long)cu[b] : (long)b * L;
+  const int Lq = cu ? len : L;
   const bf16_t* Qp = qkv + h * D;
   const bf16_t* Kp = qkv + H * D + h * D;
   const bf16_t* Vp = qkv + 2 * H * D + h * D;
   int qv[NF];
   short8 qf[NF][D / 32];
+  if (blockIdx.x * (64 * NF) >= len) {
+    // query rows past the sequence length are defined as zero output (they are masked
+    // downstream): a fully padded query block only writes zeros
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int q = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
+      if (q >= Lq) continue;
+      bf16_t* op = out + (rowb + q) * (long)(H * D) + h * D;
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) *reinterpret_cast<short4v*>(op + df * 16 + 4 * g) = (short4v){0, 0, 0, 0};
+      if (g == 0) lse[(long)bh * L + q] = INFINITY;
+    }
+    return;
+  }
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     qv[f] = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
 #pragma unroll
     for (int s = 0; s < D / 32; ++s) {
       short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (qv[f] < L) v = *reinterpret_cast<const short8*>(Qp + (rowb + qv[f]) * RS + s * 32 + 8 * g);
+      if (qv[f] < len) v = *reinterpret_cast<const short8*>(Qp + (rowb + qv[f]) * RS + s * 32 + 8 * g);
       qf[f][s] = v;
     }
   }
@@ -212,8 +229,8 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
   }
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    if (qv[f] >= L) continue;
-    const float inv = l[f] > 0.f ? 1.f / l[f] : 0.f;
+    if (qv[f] >= Lq) continue;
+    const float inv = (l[f] > 0.f && qv[f] < len) ? 1.f / l[f] : 0.f;
     bf16_t* op = out + (rowb + qv[f]) * (long)(H * D) + h * D;
 #pragma unroll
     for (int df = 0; df < D / 16; ++df) {
@@ -222,7 +239,7 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
       for (int r = 0; r < 4; ++r) v[r] = (short)f2bf(oacc[f][df][r] * inv);
       *reinterpret_cast<short4v*>(op + df * 16 + 4 * g) = v;
     }
-    if (g == 0) lse[(long)bh * L + qv[f]] = l[f] > 0.f ? m[f] + log2f(l[f]) : INFINITY;
+    if (g == 0) lse[(long)bh * L + qv[f]] = (l[f] > 0.f && qv[f] < len) ? m[f] + log2f(l[f]) : INFINITY;
   }
 }
 
@@ -248,6 +265,7 @@ __global__ void __launch_bounds__(NT) attn_delta_kernel(const bf16_t* __restrict
 template <int D, int NF>
 __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv,
                                                            const int64_t* __restrict__ lens,
+                                                           const int64_t* __restrict__ cu,
                                                            const bf16_t* __restrict__ dO, const float* __restrict__ lse,
                                                            const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                            int L, int H, float scale_log2, float scale) {
@@ -260,7 +278,9 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   const int RS = 3 * H * D, OS = H * D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int len = (int)lens[b];
-  const long rowb = (long)b * L;
+  // packed variable-length rows (cu = row offsets): only rows < len exist for sequence b
+  const long rowb = cu ? (long)cu[b] : (long)b * L;
+  const int Lq = cu ? len : L;
   const int kblk0 = blockIdx.x * (64 * NF);
   const bf16_t* Qp = qkv + h * D;
   const bf16_t* Kp = qkv + H * D + h * D;
@@ -277,7 +297,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
 #pragma unroll
     for (int s = 0; s < D / 32; ++s) {
       short8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (keyv[f] < L) {
+      if (keyv[f] < Lq) {
         kv = *reinterpret_cast<const short8*>(Kp + (rowb + keyv[f]) * RS + s * 32 + 8 * g);
         vv = *reinterpret_cast<const short8*>(Vp + (rowb + keyv[f]) * RS + s * 32 + 8 * g);
       }
@@ -291,11 +311,12 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
 #pragma unroll
     for (int i = 0; i < D / 16; ++i) dk[f][i] = dv[f][i] = (float4v){0.f, 0.f, 0.f, 0.f};
 
-  const int nqt = (kblk0 < len) ? (L + TQ - 1) / TQ : 0;  // fully masked key block -> zero grads
+  // fully masked key block -> zero grads; query rows >= len have zero output -> no contribution
+  const int nqt = (kblk0 < len) ? (len + TQ - 1) / TQ : 0;
   short8 rq[D / 32], rd[D / 32];
   if (nqt > 0) {
-    load_tile<D>(Qp, rowb, min(TQ, L), RS, rq);
-    load_tile<D>(dOp, rowb, min(TQ, L), OS, rd);
+    load_tile<D>(Qp, rowb, min(TQ, len), RS, rq);
+    load_tile<D>(dOp, rowb, min(TQ, len), OS, rd);
   }
   for (int qt = 0; qt < nqt; ++qt) {
     __syncthreads();
@@ -306,8 +327,8 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
     __syncthreads();
     if (qt + 1 < nqt) {
       const int q1 = (qt + 1) * TQ;
-      load_tile<D>(Qp, rowb + q1, min(TQ, L - q1), RS, rq);
-      load_tile<D>(dOp, rowb + q1, min(TQ, L - q1), OS, rd);
+      load_tile<D>(Qp, rowb + q1, min(TQ, len - q1), RS, rq);
+      load_tile<D>(dOp, rowb + q1, min(TQ, len - q1), OS, rd);
     }
     float4v sp[NF][4], dp[NF][4];
 #pragma unroll
@@ -331,7 +352,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qt * TQ + qf * 16 + 4 * g + r;
-        const bool qok = qq < L;
+        const bool qok = qq < len;
         const float lq = qok ? lse[(long)bh * L + qq] : 0.f;
         const float dq = qok ? delta[(rowb + qq) * H + h] : 0.f;
 #pragma unroll
@@ -367,7 +388,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   }
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    if (keyv[f] >= L) continue;
+    if (keyv[f] >= Lq) continue;
     bf16_t* dkp = dqkv + (rowb + keyv[f]) * RS + H * D + h * D;
     bf16_t* dvp = dqkv + (rowb + keyv[f]) * RS + 2 * H * D + h * D;
 #pragma unroll
@@ -387,6 +408,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
 // NF = query fragments per wave; block = 4 waves x 16*NF queries
 template <int D, int NF>
 __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
+                                                         const int64_t* __restrict__ cu,
                                                          const bf16_t* __restrict__ dO, const float* __restrict__ lse,
                                                          const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                          int L, int H, float scale_log2, float scale) {
@@ -398,7 +420,9 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
   const int RS = 3 * H * D, OS = H * D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int len = (int)lens[b];
-  const long rowb = (long)b * L;
+  // packed variable-length rows (cu = row offsets): only rows < len exist for sequence b
+  const long rowb = cu ? (long)cu[b] : (long)b * L;
+  const int Lq = cu ? len : L;
   const bf16_t* Qp = qkv + h * D;
   const bf16_t* Kp = qkv + H * D + h * D;
   const bf16_t* Vp = qkv + 2 * H * D + h * D;
@@ -406,21 +430,32 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
   int qv[NF];
   float lq[NF], dd[NF];
   short8 qf[NF][D / 32], df_[NF][D / 32];
+  if (blockIdx.x * (64 * NF) >= len) {  // padded query block: dQ = 0
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int q = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
+      if (q >= Lq) continue;
+      bf16_t* dqp = dqkv + (rowb + q) * RS + h * D;
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) *reinterpret_cast<short4v*>(dqp + df * 16 + 4 * g) = (short4v){0, 0, 0, 0};
+    }
+    return;
+  }
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     qv[f] = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
 #pragma unroll
     for (int s = 0; s < D / 32; ++s) {
       short8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (qv[f] < L) {
+      if (qv[f] < len) {
         a = *reinterpret_cast<const short8*>(Qp + (rowb + qv[f]) * RS + s * 32 + 8 * g);
         c = *reinterpret_cast<const short8*>(dO + (rowb + qv[f]) * OS + h * D + s * 32 + 8 * g);
       }
       qf[f][s] = a;
       df_[f][s] = c;
     }
-    lq[f] = qv[f] < L ? lse[(long)bh * L + qv[f]] : 0.f;
-    dd[f] = qv[f] < L ? delta[(rowb + qv[f]) * H + h] : 0.f;
+    lq[f] = qv[f] < len ? lse[(long)bh * L + qv[f]] : 0.f;
+    dd[f] = qv[f] < len ? delta[(rowb + qv[f]) * H + h] : 0.f;
   }
   float4v dq[NF][D / 16];
 #pragma unroll
@@ -469,7 +504,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
           float ds = 0.f;
-          if (key < len && qv[f] < L) {
+          if (key < len && qv[f] < len) {
             const float pv = exp2f(st[f][kf][r] * scale_log2 - lq[f]);
             ds = pv * (dpt[f][kf][r] - dd[f]);
           }
@@ -491,7 +526,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
   }
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    if (qv[f] >= L) continue;
+    if (qv[f] >= Lq) continue;
     bf16_t* dqp = dqkv + (rowb + qv[f]) * RS + h * D;
 #pragma unroll
     for (int df = 0; df < D / 16; ++df) {
@@ -517,29 +552,29 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
 
 static const float kLog2e = 1.4426950408889634f;
 
-SSAMD_API int ssamd_attn_fwd(const bf16_t* qkv, const int64_t* lens, bf16_t* out, float* lse, int B, int L, int H,
-                             int D, float scale, hipStream_t s) {
+// cu (optional): packed rows, sequence b = rows cu[b] .. cu[b]+lens[b]-1; L = longest sequence.
+SSAMD_API int ssamd_attn_fwd(const bf16_t* qkv, const int64_t* lens, const int64_t* cu, bf16_t* out, float* lse, int B,
+                             int L, int H, int D, float scale, hipStream_t s) {
   if ((long)B * L == 0) return 0;
   ATTN_DISPATCH(D, true, {
     dim3 grid(cdiv(L, 64 * NF), B * H);
-    hipLaunchKernelGGL((attn_fwd_kernel<DD, NF>), grid, dim3(NT), 0, s, qkv, lens, out, lse, L, H, scale * kLog2e);
+    hipLaunchKernelGGL((attn_fwd_kernel<DD, NF>), grid, dim3(NT), 0, s, qkv, lens, cu, out, lse, L, H,
+                       scale * kLog2e);
   });
   return (int)hipGetLastError();
 }
 
-// lse: [B, H, L] log2-domain; delta workspace: [B*L*H] fp32
-SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const bf16_t* o, const float* lse,
-                             const bf16_t* dO, bf16_t* dqkv, float* delta, void* unused, int B, int L, int H, int D,
-                             float scale, hipStream_t s) {
-  (void)unused;
-  if ((long)B * L == 0) return 0;
-  const long rows = (long)B * L;
+// lse: [B, H, L] log2-domain; delta workspace: [rows*H] fp32 (rows = B*L, or the packed row count)
+SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const int64_t* cu, const bf16_t* o,
+                             const float* lse, const bf16_t* dO, bf16_t* dqkv, float* delta, long rows, int B, int L,
+                             int H, int D, float scale, hipStream_t s) {
+  if ((long)B * L == 0 || rows == 0) return 0;
   hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
   ATTN_DISPATCH(D, false, {
     dim3 grid(cdiv(L, 64 * NF), B * H);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), 4 * TQ * DD * 2, s, qkv, lens, dO, lse, delta,
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), 4 * TQ * DD * 2, s, qkv, lens, cu, dO, lse, delta,
                        dqkv, L, H, scale * kLog2e, scale);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), 3 * TK * DD * 2, s, qkv, lens, dO, lse, delta,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), 3 * TK * DD * 2, s, qkv, lens, cu, dO, lse, delta,
                        dqkv, L, H, scale * kLog2e, scale);
   });
   return (int)hipGetLastError();

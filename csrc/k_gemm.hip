@@ -32,7 +32,17 @@ constexpr int CSTRIDE = 132;  // fp32 epilogue staging row stride (conflict-free
 struct ConvGeom {
   int B, L, Cin, ks, dil, pad;  // A operand geometry
   int M, N, K;                  // GEMM sizes (M = B*L, K = ks*Cin)
+  // packed variable-length rows (optional): rinfo[m] = {position in its sequence, sequence length};
+  // sequences are contiguous, so tap shifts stay row offsets.  nullptr: fixed L per sequence.
+  const int2* rinfo;
 };
+
+// (position, bound) of row m for the conv zero-padding test
+__device__ __forceinline__ int2 row_pos(const ConvGeom& g, int m) {
+  if (g.rinfo) return g.rinfo[m];
+  const int b = m / g.L;
+  return make_int2(m - b * g.L, g.L);
+}
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
 
@@ -45,14 +55,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // swizzled byte offset of 16-B chunk `c` (0..7) of row `row` in a [rows][64 bf16] image
 __device__ __forceinline__ int swz128(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
 
-__device__ __forceinline__ short8 load_a_chunk(const bf16_t* __restrict__ X, const ConvGeom& g, int m, int bb, int tt,
+__device__ __forceinline__ short8 load_a_chunk(const bf16_t* __restrict__ X, const ConvGeom& g, int m, int tt, int lim,
                                                int k, float invCin) {
   short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
   if (m < g.M && k < g.K) {
     const int tap = (int)(((float)k + 0.5f) * invCin);
     const int cin = k - tap * g.Cin;
-    const int ts = tt + tap * g.dil - g.pad;
-    if (ts >= 0 && ts < g.L) v = *reinterpret_cast<const short8*>(X + ((long)bb * g.L + ts) * g.Cin + cin);
+    const int sh = tap * g.dil - g.pad;
+    const int ts = tt + sh;
+    if (ts >= 0 && ts < lim) v = *reinterpret_cast<const short8*>(X + ((long)m + sh) * g.Cin + cin);
   }
   return v;
 }
@@ -74,14 +85,14 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restri
   const float invCin = 1.f / (float)g.Cin;
 
   // staging assignment: chunk e = tid + 256*i, row = e/8, c = e%8 (i = 0..3)
-  int a_b[4], a_t[4], a_m[4];
+  int a_lim[4], a_t[4], a_m[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (tid >> 3) + 32 * i;
     a_m[i] = m0 + row;
-    const int mm = a_m[i] < g.M ? a_m[i] : 0;
-    a_b[i] = mm / g.L;
-    a_t[i] = mm - a_b[i] * g.L;
+    const int2 rp = row_pos(g, a_m[i] < g.M ? a_m[i] : 0);
+    a_t[i] = rp.x;
+    a_lim[i] = rp.y;
   }
   const int cchunk = tid & 7;
 
@@ -95,7 +106,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restri
   auto gload = [&](int kt) {
     const int k = kt * BK + cchunk * 8;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = load_a_chunk(X, g, a_m[i], a_b[i], a_t[i], k, invCin);
+    for (int i = 0; i < 4; ++i) ra[i] = load_a_chunk(X, g, a_m[i], a_t[i], a_lim[i], k, invCin);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int n = n0 + (tid >> 3) + 32 * i;
@@ -309,16 +320,16 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
   const float invCin = 1.f / (float)g.Cin;
 
   // DMA assignment: wave instruction i (0..3) fills rows rb(i) .. rb(i)+7, lane -> (row, phys chunk)
-  int a_b[4], a_t[4], a_m[4], rowi[4], lchunk[4];
+  int a_lim[4], a_t[4], a_m[4], rowi[4], lchunk[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = (i * 4 + wave) * 8 + (lane >> 3);
     rowi[i] = row;
     lchunk[i] = (lane & 7) ^ ((row >> 1) & 7);
     a_m[i] = m0 + row;
-    const int mm = a_m[i] < g.M ? a_m[i] : 0;
-    a_b[i] = mm / g.L;
-    a_t[i] = mm - a_b[i] * g.L;
+    const int2 rp = row_pos(g, a_m[i] < g.M ? a_m[i] : 0);
+    a_t[i] = rp.x;
+    a_lim[i] = rp.y;
   }
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * (2 * BM * BK * 2);
@@ -330,8 +341,9 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
       if (a_m[i] < g.M && k < g.K) {
         const int tap = (int)(((float)k + 0.5f) * invCin);
         const int cin = k - tap * g.Cin;
-        const int ts = a_t[i] + tap * g.dil - g.pad;
-        if (ts >= 0 && ts < g.L) src = X + ((long)a_b[i] * g.L + ts) * g.Cin + cin;
+        const int sh = tap * g.dil - g.pad;
+        const int ts = a_t[i] + sh;
+        if (ts >= 0 && ts < a_lim[i]) src = X + ((long)a_m[i] + sh) * g.Cin + cin;
       }
       glds16(src, As + (i * 4 + wave) * 8 * 128);
       const int n = n0 + rowi[i];
@@ -430,7 +442,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
 constexpr int BM3 = 256, NT3 = 512, NSTAGE = 3;
 constexpr int STAGE_BYTES = (BM3 + BN) * BK * 2;  // 48 KiB
 
-template <bool OUT_F32, bool FASTK>
+template <bool OUT_F32, bool FASTK, bool PACKED>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                 const float* __restrict__ bias,
                                                                 const bf16_t* __restrict__ aux,
@@ -448,7 +460,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
   const float invCin = 1.f / (float)g.Cin;
 
   // A: 256 rows = 32 wave-instructions (4 per wave); B: 128 rows = 16 (2 per wave)
-  int a_b[4], a_t[4], a_m[4], achunk[4];
+  int a_lim[4], a_t[4], a_m[4], achunk[4];
   const bf16_t* arow_ptr[4];
   const bf16_t* brow_ptr[2];
   bool a_ok[4], b_ok[2];
@@ -459,9 +471,16 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
     a_m[i] = m0 + row;
     a_ok[i] = a_m[i] < g.M;
     const int mm = a_ok[i] ? a_m[i] : 0;
-    a_b[i] = mm / g.L;
-    a_t[i] = mm - a_b[i] * g.L;
-    arow_ptr[i] = X + ((long)a_b[i] * g.L + a_t[i]) * g.Cin + achunk[i] * 8;  // tap-0, cin-0 origin
+    if constexpr (PACKED) {
+      const int2 rp = g.rinfo[mm];  // unconditional: the four loads issue back to back
+      a_t[i] = rp.x;
+      a_lim[i] = rp.y;
+    } else {
+      const int bb = mm / g.L;
+      a_t[i] = mm - bb * g.L;
+      a_lim[i] = g.L;
+    }
+    arow_ptr[i] = X + (long)mm * g.Cin + achunk[i] * 8;  // tap-0, cin-0 origin
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -484,7 +503,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ts = a_t[i] + shift;
-        const bool ok = a_ok[i] && ts >= 0 && ts < g.L;
+        const bool ok = a_ok[i] && ts >= 0 && ts < a_lim[i];
         glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 8 * 128);
       }
 #pragma unroll
@@ -498,8 +517,9 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
         if (a_ok[i] && k < g.K) {
           const int tap = (int)(((float)k + 0.5f) * invCin);
           const int cin = k - tap * g.Cin;
-          const int ts = a_t[i] + tap * g.dil - g.pad;
-          if (ts >= 0 && ts < g.L) src = X + ((long)a_b[i] * g.L + ts) * g.Cin + cin;
+          const int sh = tap * g.dil - g.pad;
+          const int ts = a_t[i] + sh;
+          if (ts >= 0 && ts < a_lim[i]) src = arow_ptr[i] - achunk[i] * 8 + (long)sh * g.Cin + cin;
         }
         glds16(src, As + (i * 8 + wave) * 8 * 128);
       }
@@ -620,6 +640,7 @@ __device__ __forceinline__ short4v ds_read_tr(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
+template <bool PACKED>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                                                            float* __restrict__ slabs, float* __restrict__ bias_slabs,
                                                            ConvGeom g, int rows_per_split) {
@@ -660,10 +681,14 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
   }
   // per-row time index t = m mod L, advanced incrementally (stage() is called for r0 = r_begin, +RB, ...)
   int tcur[4], shift[4];
+  // PACKED: (position, length) of the next stage's rows, loaded one stage ahead with a clamped
+  // (branch-free) index so the read never sits in front of the operand DMA
+  int2 rnext[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    tcur[i] = (r_begin + rr[i]) % g.L;
     shift[i] = c_tap[i] * g.dil - g.pad;
+    if constexpr (PACKED) rnext[i] = g.rinfo[min(r_begin + rr[i], g.M - 1)];
+    else tcur[i] = (r_begin + rr[i]) % g.L;
   }
   auto stage = [&](int r0, int buf) {
     char* Ys = smem + buf * (2 * RB * 256);
@@ -672,15 +697,25 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + rr[i];
       const bool mok = m < r_end;
-      const int ts = tcur[i] + shift[i];
-      const bool xok = mok && c_kok[i] && ts >= 0 && ts < g.L;
+      int ts, lim;
+      if constexpr (PACKED) {
+        ts = rnext[i].x + shift[i];
+        lim = rnext[i].y;
+        rnext[i] = g.rinfo[min(m + RB, g.M - 1)];
+      } else {
+        ts = tcur[i] + shift[i];
+        lim = g.L;
+      }
+      const bool xok = mok && c_kok[i] && ts >= 0 && ts < lim;
       const void* sy = (mok && c_n[i] < g.N) ? (const void*)(dY + (long)m * g.N + c_n[i]) : (const void*)g_zero_chunk;
       const void* sx = xok ? (const void*)(X + (long)(m + shift[i]) * g.Cin + c_cin[i]) : (const void*)g_zero_chunk;
       glds16(sy, Ys + (i * 4 + wave) * 4 * 256);
       glds16(sx, Xs + (i * 4 + wave) * 4 * 256);
-      int t = tcur[i] + RB;
-      while (t >= g.L) t -= g.L;
-      tcur[i] = t;
+      if constexpr (!PACKED) {
+        int t = tcur[i] + RB;
+        while (t >= g.L) t -= g.L;
+        tcur[i] = t;
+      }
     }
   };
   // bias gradient (column sums of dY) for the k-tile-0 blocks, read back from the LDS image
@@ -757,6 +792,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
 }
 
 // Register-staged variant (faster at large K = ks*Cin; the LDS-DMA one wins at K <= 1024).
+template <bool PACKED>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                                                            float* __restrict__ slabs, float* __restrict__ bias_slabs,
                                                            ConvGeom g, int rows_per_split) {
@@ -793,23 +829,40 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
   short8 rx[4], ry[4];
   int tcur[4];
   const int xshift = tap * g.dil - g.pad;
+  // packed rows: (position, length) of the rows of the NEXT gload, prefetched one step ahead so
+  // the table read never sits in front of the operand loads
+  int2 rnext[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) tcur[i] = (r_begin + (tid >> 4) + 16 * i) % g.L;
+  for (int i = 0; i < 4; ++i) {
+    const int m = r_begin + (tid >> 4) + 16 * i;
+    if constexpr (PACKED) rnext[i] = g.rinfo[min(m, g.M - 1)];
+    else tcur[i] = m % g.L;
+  }
   auto gload = [&](int r0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + (tid >> 4) + 16 * i;
       short8 vx = {0, 0, 0, 0, 0, 0, 0, 0}, vy = {0, 0, 0, 0, 0, 0, 0, 0};
+      int ts, lim;
+      if constexpr (PACKED) {  // clamped, branch-free prefetch of the next step's row table
+        ts = rnext[i].x + xshift;
+        lim = rnext[i].y;
+        rnext[i] = g.rinfo[min(m + RB, g.M - 1)];
+      } else {
+        ts = tcur[i] + xshift;
+        lim = g.L;
+      }
       if (m < r_end) {
         if (n_ld < g.N) vy = *reinterpret_cast<const short8*>(dY + (long)m * g.N + n_ld);
-        const int ts = tcur[i] + xshift;
-        if (k_ok && ts >= 0 && ts < g.L) vx = *reinterpret_cast<const short8*>(X + (long)(m + xshift) * g.Cin + cin);
+        if (k_ok && ts >= 0 && ts < lim) vx = *reinterpret_cast<const short8*>(X + (long)(m + xshift) * g.Cin + cin);
       }
       rx[i] = vx;
       ry[i] = vy;
-      int t = tcur[i] + RB;
-      while (t >= g.L) t -= g.L;
-      tcur[i] = t;
+      if constexpr (!PACKED) {
+        int t = tcur[i] + RB;
+        while (t >= g.L) t -= g.L;
+        tcur[i] = t;
+      }
     }
   };
   // bias gradient (column sums of dY) rides on the staging registers of the k-tile-0 blocks
@@ -955,15 +1008,17 @@ static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N
   ConvGeom g;
   g.B = B; g.L = L; g.Cin = Cin; g.ks = ks; g.dil = dil; g.pad = pad;
   g.M = B * L; g.N = N; g.K = ks * Cin;
+  g.rinfo = nullptr;
   return g;
 }
 
 SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
                               const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
-                              int ks, int dil, int pad, int N, int act, int ldy, hipStream_t s) {
+                              int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, hipStream_t s) {
   if (Cin % 8 != 0) return -2;
   if ((long)B * L == 0 || N == 0) return 0;
   ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
+  g.rinfo = reinterpret_cast<const int2*>(rinfo);
   const int nwg = ((g.M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = (size_t)BM * CSTRIDE * 4;  // >= 2 stages x (A+B) = 64 KiB
   static bool lds_set = false;
@@ -980,17 +1035,24 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   if (reg && variant == 2) {
     static bool ring_set = false;
     if (!ring_set) {
-      allow_lds(conv_gemm_ring_kernel<true, true>, NSTAGE * STAGE_BYTES);
-      allow_lds(conv_gemm_ring_kernel<false, true>, NSTAGE * STAGE_BYTES);
-      allow_lds(conv_gemm_ring_kernel<true, false>, NSTAGE * STAGE_BYTES);
-      allow_lds(conv_gemm_ring_kernel<false, false>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<true, true, false>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, true, false>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<true, false, false>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, false, false>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<true, true, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, true, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<true, false, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, false, true>, NSTAGE * STAGE_BYTES);
       ring_set = true;
     }
     const int nwg3 = ((g.M + BM3 - 1) / BM3) * ((N + BN - 1) / BN);
     const bool fastk = (Cin % BK) == 0;
     const size_t L3 = NSTAGE * STAGE_BYTES;
-#define RING_LAUNCH(F32, FK) \
-    hipLaunchKernelGGL((conv_gemm_ring_kernel<F32, FK>), dim3(nwg3), dim3(NT3), L3, s, X, W, bias, aux, resid, lens, Y, g, act, ldy)
+#define RING_LAUNCH(F32, FK)                                                                        \
+    do {                                                                                            \
+      auto kfn = g.rinfo ? conv_gemm_ring_kernel<F32, FK, true> : conv_gemm_ring_kernel<F32, FK, false>; \
+      hipLaunchKernelGGL(kfn, dim3(nwg3), dim3(NT3), L3, s, X, W, bias, aux, resid, lens, Y, g, act, ldy); \
+    } while (0)
     if (out_f32) {
       if (fastk) RING_LAUNCH(true, true); else RING_LAUNCH(true, false);
     } else {
@@ -1024,9 +1086,11 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.
 // ws: splits*N*ks*Cin (+ splits*N when db != null) floats.  db (optional): fused bias gradient.
 SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, float* db,
-                               int B, int L, int Cin, int ks, int dil, int pad, int N, int max_splits, hipStream_t s) {
+                               int B, int L, int Cin, int ks, int dil, int pad, int N, int max_splits, const int* rinfo,
+                               hipStream_t s) {
   if (Cin % 8 != 0 || N % 8 != 0) return -2;
   ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
+  g.rinfo = reinterpret_cast<const int2*>(rinfo);
   const long slab = (long)N * g.K;
   if (g.M == 0) {
     hipMemsetAsync(dW, 0, slab * sizeof(float), s);
@@ -1044,11 +1108,13 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   rows_per_split = (rows_per_split + RB - 1) / RB * RB;
   splits = (g.M + rows_per_split - 1) / rows_per_split;
   float* bws = db ? ws + (long)splits * slab : nullptr;
+  auto wreg = g.rinfo ? conv_wgrad_reg_kernel<true> : conv_wgrad_reg_kernel<false>;
+  auto wdma = g.rinfo ? conv_wgrad_kernel<true> : conv_wgrad_kernel<false>;
   if (g.K > 1024)
-    hipLaunchKernelGGL(conv_wgrad_reg_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
+    hipLaunchKernelGGL(wreg, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
                        rows_per_split);
   else
-    hipLaunchKernelGGL(conv_wgrad_kernel, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
+    hipLaunchKernelGGL(wdma, dim3(tiles * splits), dim3(NT), 2 * 2 * RB * 256, s, X, dY, ws, bws, g,
                        rows_per_split);
   const long total = slab;
   int blocks = (int)min((total + 255) / 256, 8192L);

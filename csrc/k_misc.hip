@@ -25,17 +25,22 @@ __device__ int block_prefix_durations(const int64_t* d, int T, int* cum) {
   return T > 0 ? cum[T - 1] : 0;
 }
 
+// packed mode (cu != nullptr): frame f of sequence b is row cu[b] + f, frames f >= plen[b] do not exist
 __global__ void __launch_bounds__(256) lr_fwd_kernel(const bf16_t* __restrict__ x, const int64_t* __restrict__ dur,
                                                      const bf16_t* __restrict__ pe, bf16_t* __restrict__ out,
+                                                     const int64_t* __restrict__ cu, const int64_t* __restrict__ plen,
                                                      int T, int M, int C) {
   extern __shared__ int cum[];
   const int b = blockIdx.y;
+  const int Mb = cu ? min(M, (int)plen[b]) : M;
+  if (blockIdx.x * LR_ROWS >= Mb) return;  // block-uniform
+  const long obase = cu ? (long)cu[b] : (long)b * M;
   const int total = block_prefix_durations(dur + (long)b * T, T, cum);
   const int vec = C / 8;  // 16-B chunks per row
   for (int e = threadIdx.x; e < LR_ROWS * vec; e += blockDim.x) {
     const int r = e / vec, c8 = e % vec;
     const int f = blockIdx.x * LR_ROWS + r;
-    if (f >= M) break;
+    if (f >= Mb) break;
     short8 v = {0, 0, 0, 0, 0, 0, 0, 0};
     if (f < total) {
       int lo = 0, hi = T;  // first i with cum[i] > f
@@ -47,15 +52,18 @@ __global__ void __launch_bounds__(256) lr_fwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = (short)f2bf(bf2f((bf16_t)v[i]) + bf2f((bf16_t)p[i]));
     }
-    *reinterpret_cast<short8*>(out + ((long)b * M + f) * C + c8 * 8) = v;
+    *reinterpret_cast<short8*>(out + (obase + f) * C + c8 * 8) = v;
   }
 }
 
 // dx[b, p] = sum over the frames f in [cum[p-1], cum[p]) with f < M of dout[b, f]
 __global__ void __launch_bounds__(256) lr_bwd_kernel(const bf16_t* __restrict__ dout, const int64_t* __restrict__ dur,
-                                                     bf16_t* __restrict__ dx, int T, int M, int C) {
+                                                     bf16_t* __restrict__ dx, const int64_t* __restrict__ cu,
+                                                     const int64_t* __restrict__ plen, int T, int M, int C) {
   extern __shared__ int cum[];
   const int b = blockIdx.y;
+  const int Mb = cu ? min(M, (int)plen[b]) : M;
+  const long obase = cu ? (long)cu[b] : (long)b * M;
   block_prefix_durations(dur + (long)b * T, T, cum);
   const int vec = C / 8;
   for (int e = threadIdx.x; e < LR_ROWS * vec; e += blockDim.x) {
@@ -63,10 +71,10 @@ __global__ void __launch_bounds__(256) lr_bwd_kernel(const bf16_t* __restrict__ 
     const int p = blockIdx.x * LR_ROWS + r;
     if (p >= T) break;
     const int f0 = p ? cum[p - 1] : 0;
-    const int f1 = min(cum[p], M);
+    const int f1 = min(cum[p], Mb);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int f = f0; f < f1; ++f) {
-      short8 v = *reinterpret_cast<const short8*>(dout + ((long)b * M + f) * C + c8 * 8);
+      short8 v = *reinterpret_cast<const short8*>(dout + (obase + f) * C + c8 * 8);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += bf2f((bf16_t)v[i]);
     }
@@ -249,21 +257,58 @@ static int grid_for(long work, int per_thread = 1) {
   return (int)(blocks > 4096 ? 4096 : blocks);
 }
 
-SSAMD_API int ssamd_lr_fwd(const bf16_t* x, const int64_t* dur, const bf16_t* pe, bf16_t* out, int B, int T, int M,
-                           int C, hipStream_t s) {
+SSAMD_API int ssamd_lr_fwd(const bf16_t* x, const int64_t* dur, const bf16_t* pe, bf16_t* out, const int64_t* cu,
+                           const int64_t* plen, int B, int T, int M, int C, hipStream_t s) {
   if (C % 8) return -1;
   if (B == 0 || M == 0) return 0;
-  hipLaunchKernelGGL(lr_fwd_kernel, dim3(cdiv(M, LR_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, x, dur, pe, out, T,
-                     M, C);
+  hipLaunchKernelGGL(lr_fwd_kernel, dim3(cdiv(M, LR_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, x, dur, pe, out, cu,
+                     plen, T, M, C);
   return (int)hipGetLastError();
 }
 
-SSAMD_API int ssamd_lr_bwd(const bf16_t* dout, const int64_t* dur, bf16_t* dx, int B, int T, int M, int C,
-                           hipStream_t s) {
+SSAMD_API int ssamd_lr_bwd(const bf16_t* dout, const int64_t* dur, bf16_t* dx, const int64_t* cu, const int64_t* plen,
+                           int B, int T, int M, int C, hipStream_t s) {
   if (C % 8) return -1;
   if (B == 0 || T == 0) return 0;
-  hipLaunchKernelGGL(lr_bwd_kernel, dim3(cdiv(T, LR_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, dout, dur, dx, T,
-                     M, C);
+  hipLaunchKernelGGL(lr_bwd_kernel, dim3(cdiv(T, LR_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, dout, dur, dx, cu,
+                     plen, T, M, C);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// Packed-sequence bookkeeping, one launch: grid = B blocks.
+//   cu[b] = sum_{i<b} len[i] (cu[B] = total), rinfo[cu[b]+t] = {t, len[b]}, dst[cu[b]+t] = b*M + t
+// ----------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) pack_info_kernel(const int64_t* __restrict__ lens, int B, int M,
+                                                        int64_t* __restrict__ cu, int2* __restrict__ rinfo,
+                                                        int64_t* __restrict__ dst) {
+  __shared__ long part[256];
+  const int b = blockIdx.x;
+  long sacc = 0;
+  for (int i = threadIdx.x; i < b; i += 256) sacc += min((long)lens[i], (long)M);
+  part[threadIdx.x] = sacc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  const long base = part[0];
+  const int len = (int)min((long)lens[b], (long)M);
+  if (threadIdx.x == 0) {
+    cu[b] = base;
+    if (b == B - 1) cu[B] = base + len;
+  }
+  for (int t = threadIdx.x; t < len; t += 256) {
+    rinfo[base + t] = make_int2(t, len);
+    dst[base + t] = (long)b * M + t;
+  }
+}
+}  // namespace
+
+SSAMD_API int ssamd_pack_info(const int64_t* lens, int B, int M, int64_t* cu, int* rinfo, int64_t* dst, hipStream_t s) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(pack_info_kernel, dim3(B), dim3(256), 0, s, lens, B, M, cu, reinterpret_cast<int2*>(rinfo), dst);
   return (int)hipGetLastError();
 }
 

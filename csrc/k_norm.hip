@@ -58,12 +58,16 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
     const bf16_t* __restrict__ a, const bf16_t* __restrict__ res, const float* __restrict__ w,
     const float* __restrict__ bias, const float* __restrict__ fg, const float* __restrict__ fb,
     const float* __restrict__ s_g, const float* __restrict__ s_b, const int64_t* __restrict__ lens,
-    bf16_t* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out, int L, int C,
+    const int64_t* __restrict__ cu, bf16_t* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out, int L, int C,
     float pre_p, float post_p, uint64_t seed, float eps) {
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c0 = lane * EPL;
   const int len = lens ? (int)lens[b] : L;
+  // packed variable-length rows (cu = row offsets): sequence b owns rows cu[b] .. cu[b]+len-1
+  const long rowb = cu ? (long)cu[b] : (long)b * L;
+  const int Lb = cu ? len : L;
+  if (blockIdx.x * ROWS_PER_BLOCK >= Lb) return;
   float wv[EPL], bv[EPL], G[EPL], Bt[EPL];
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
@@ -83,8 +87,8 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
   const float invC = 1.f / C;
   for (int r = 0; r < ROWS_PER_WAVE; ++r) {
     const int t = blockIdx.x * ROWS_PER_BLOCK + r * WAVES + wave;
-    if (t >= L) break;
-    const long row = (long)b * L + t;
+    if (t >= Lb) break;
+    const long row = rowb + t;
     float h[EPL];
     load_row<EPL>(a + row * C + c0, h);
     if (pre_p > 0.f) {
@@ -133,7 +137,8 @@ template <int EPL>
 __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ a, const bf16_t* __restrict__ res,
     const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ fg,
-    const float* __restrict__ s_g, const int64_t* __restrict__ lens, const float* __restrict__ mean_in,
+    const float* __restrict__ s_g, const int64_t* __restrict__ lens, const int64_t* __restrict__ cu,
+    const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ da_out,
     float* __restrict__ dw, float* __restrict__ db, float* __restrict__ S1, float* __restrict__ S2, int L, int C,
     float pre_p, float post_p, uint64_t seed) {
@@ -142,6 +147,9 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c0 = lane * EPL;
   const int len = lens ? (int)lens[b] : L;
+  const long rowb = cu ? (long)cu[b] : (long)b * L;
+  const int Lb = cu ? len : L;
+  if (blockIdx.x * ROWS_PER_BLOCK >= Lb) return;  // block-uniform: before any barrier
   float wv[EPL], bv[EPL], G[EPL];
   float acc_w[EPL], acc_b[EPL], acc_s1[EPL], acc_s2[EPL];
   const float sg = fg ? *s_g : 0.f;
@@ -155,8 +163,8 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
   const float invC = 1.f / C;
   for (int r = 0; r < ROWS_PER_WAVE; ++r) {
     const int t = blockIdx.x * ROWS_PER_BLOCK + r * WAVES + wave;
-    if (t >= L) break;
-    const long row = (long)b * L + t;
+    if (t >= Lb) break;
+    const long row = rowb + t;
     float dh[EPL];
     if (t >= len) {  // masked row: zero gradient flows back
 #pragma unroll
@@ -236,27 +244,28 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
   }
 
 SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w, const float* bias, const float* fg,
-                              const float* fb, const float* s_g, const float* s_b, const int64_t* lens, bf16_t* out,
+                              const float* fb, const float* s_g, const float* s_b, const int64_t* lens,
+                              const int64_t* cu, bf16_t* out,
                               float* mean, float* rstd, int B, int L, int C, float pre_p, float post_p,
                               unsigned long long seed, float eps, hipStream_t stream) {
   if (C % 256 != 0 && C != 256 && C != 512 && C != 1024) return -1;
   if (B == 0 || L == 0) return 0;
   dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
   DISPATCH_EPL(C, hipLaunchKernelGGL(addln_fwd_kernel<EPL>, grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
-                                     s_b, lens, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
+                                     s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
   return (int)hipGetLastError();
 }
 
 SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t* res, const float* w,
                               const float* bias, const float* fg, const float* s_g, const int64_t* lens,
-                              const float* mean, const float* rstd, bf16_t* dh, bf16_t* da, float* dw, float* db,
+                              const int64_t* cu, const float* mean, const float* rstd, bf16_t* dh, bf16_t* da, float* dw, float* db,
                               float* S1, float* S2, int B, int L, int C, float pre_p, float post_p,
                               unsigned long long seed, hipStream_t stream) {
   if (B == 0 || L == 0) return 0;
   dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
   size_t lds = (size_t)WAVES * C * sizeof(float);
   DISPATCH_EPL(C, hipLaunchKernelGGL(addln_bwd_kernel<EPL>, grid, dim3(256), lds, stream, dout, a, res, w, bias, fg,
-                                     s_g, lens, mean, rstd, dh, da, dw, db, S1, S2, L, C, pre_p, post_p,
+                                     s_g, lens, cu, mean, rstd, dh, da, dw, db, S1, S2, L, C, pre_p, post_p,
                                      (uint64_t)seed));
   return (int)hipGetLastError();
 }

@@ -156,8 +156,12 @@ def to_device(batch, device):
 
     if len(batch) == 12:
         ids, raw, spk, texts, src_lens, max_src, mels, mel_lens, max_mel, p, e, d = batch
+        ml = t(mel_lens, torch.long)
+        # host copy of the lengths: sizes the packed decoder (models/fastspeech2.py) without a sync
+        if not (isinstance(mel_lens, torch.Tensor) and mel_lens.is_cuda):
+            ml.host_lengths = np.asarray(mel_lens.numpy() if isinstance(mel_lens, torch.Tensor) else mel_lens)
         return (ids, raw, t(spk, torch.long), t(texts, torch.long), t(src_lens, torch.long), max_src,
-                t(mels, torch.float32), t(mel_lens, torch.long), max_mel, t(p, torch.float32), t(e, torch.float32),
+                t(mels, torch.float32), ml, max_mel, t(p, torch.float32), t(e, torch.float32),
                 t(d, torch.long))
     if len(batch) == 9:
         ids, raw, spk, texts, src_lens, max_src, mels, mel_lens, max_mel = batch

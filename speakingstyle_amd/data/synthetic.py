@@ -117,8 +117,10 @@ class SyntheticBatches:
         nb = dev.type == "cuda"
         tt = lambda x: x.to(dev, non_blocking=nb)  # noqa: E731
         ids = [f"synth_{i}" for i in range(B)]
+        ml = tt(torch.from_numpy(mel_lens))
+        ml.host_lengths = mel_lens  # host copy: sizes the packed decoder without a device sync
         return (ids, ["" for _ in range(B)], tt(speakers), tt(texts), tt(torch.from_numpy(Ts)), T, tt(mels),
-                tt(torch.from_numpy(mel_lens)), M, tt(pitch), tt(energy), tt(torch.from_numpy(dur)))
+                ml, M, tt(pitch), tt(energy), tt(torch.from_numpy(dur)))
 
     def __iter__(self):
         while True:

@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..config import style_mode
 from ..text.symbols import symbols
-from .layers import FFTBlock, FiLM, LinearNorm, PostNet
+from .layers import FFTBlock, FiLM, LinearNorm, PostNet, fused_param_groups
 from .style import GlobalStyleTokens, ReferenceEncoder
 
 
@@ -95,6 +95,21 @@ class Decoder(nn.Module):
         for layer in self.layer_stack:
             x = layer(x, mel_lens, style)
         return x, mel_lens
+
+    def forward_packed(self, x_phone, durations, mel_lens, M, R, style=None):
+        """Length regulation + decoder over the valid frames only (``ops/packing.py``).
+
+        Same result as ``forward(LR(x_phone))`` on every valid frame; returns the packed
+        ``[1, R, C]`` output, the (truncated) lengths and the PackInfo."""
+        if self.training and M > self.max_seq_len:
+            M = self.max_seq_len
+        dec_lens = mel_lens.clamp(max=M)
+        pk = ops.PackInfo.build(dec_lens, M, R)
+        pe = positional_rows(self.position_enc, M, self.d_model, x_phone.device).to(x_phone.dtype)
+        x = ops.length_regulate_packed(x_phone, durations, pk, pe)
+        for layer in self.layer_stack:
+            x = layer(x, dec_lens, style, pack=pk)
+        return x, dec_lens, pk
 
 
 class VariancePredictor(nn.Module):
@@ -184,8 +199,12 @@ class VarianceAdaptor(nn.Module):
         x = ops.bucketize_embed_add(x, values, bins, table.weight.to(x.dtype))
         return pred, x
 
+    def packable(self):
+        """Frame-level variance features act on the padded frame domain: no packed decoder then."""
+        return self.pitch_feature_level == "phoneme_level" and self.energy_feature_level == "phoneme_level"
+
     def forward(self, x, src_lens, mel_lens=None, max_len=None, pitch_target=None, energy_target=None,
-                duration_target=None, p_control=1.0, e_control=1.0, d_control=1.0, style=None):
+                duration_target=None, p_control=1.0, e_control=1.0, d_control=1.0, style=None, regulate=True):
         log_d = self.duration_predictor(x, src_lens, style)
         p_pred = e_pred = None
         if self.pitch_feature_level == "phoneme_level":
@@ -193,6 +212,8 @@ class VarianceAdaptor(nn.Module):
         if self.energy_feature_level == "phoneme_level":
             e_pred, x = self._variance(self.energy_predictor, self.energy_bins, self.energy_embedding, x, energy_target, src_lens, e_control)
 
+        if not regulate:  # the packed decoder regulates itself (Decoder.forward_packed)
+            return x, p_pred, e_pred, log_d, duration_target, mel_lens
         if duration_target is not None:
             d_rounded = duration_target
             x, mel_len = ops.length_regulate(x, duration_target, max_len)
@@ -260,6 +281,9 @@ class FastSpeech2(nn.Module):
         self.compute_dtype = dtype
         return self
 
+    def fused_param_groups(self):
+        return fused_param_groups(self)
+
     def style_encoder(self):
         return getattr(self, "reference_encoder", None) or getattr(self, "gst", None)
 
@@ -285,9 +309,13 @@ class FastSpeech2(nn.Module):
     # ------------------------------------------------------------------ forward
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None, max_mel_len=None,
                 p_targets=None, e_targets=None, d_targets=None, p_control=1.0, e_control=1.0, d_control=1.0,
-                style_weights=None):
+                style_weights=None, mel_lens_host=None):
+        """Reference ``model/fastspeech2.py:45-113``.  ``mel_lens_host`` (host int array of the
+        batch's mel lengths, provided by the data pipeline) enables the packed decoder in training."""
         dev = texts.device
         cd = self.compute_dtype
+        if mel_lens_host is None and mel_lens is not None:
+            mel_lens_host = getattr(mel_lens, "host_lengths", None)
         if mels is not None and max_mel_len is None:
             max_mel_len = mels.shape[1]
         style = self.compute_style(mels, mel_lens, max_mel_len, texts.shape[0], dev, style_weights)
@@ -295,12 +323,22 @@ class FastSpeech2(nn.Module):
         if self.speaker_emb is not None:
             x = x + self.speaker_emb(speakers).to(cd).unsqueeze(1)
         training_lr = d_targets is not None
+        packed = (self.training and training_lr and mel_lens is not None and mel_lens_host is not None
+                  and max_mel_len is not None and self.variance_adaptor.packable())
         x, p_pred, e_pred, log_d, d_rounded, mel_lens_out = self.variance_adaptor(
             x, src_lens, mel_lens, max_mel_len if training_lr else None, p_targets, e_targets, d_targets,
-            p_control, e_control, d_control, style,
+            p_control, e_control, d_control, style, regulate=not packed,
         )
-        x, dec_lens = self.decoder(x, mel_lens_out, style)
-        mel = ops.linear(x, self.mel_linear.weight, self.mel_linear.bias).float()
+        if packed:
+            M = min(int(max_mel_len), self.decoder.max_seq_len)
+            R = int(sum(min(int(v), M) for v in mel_lens_host))
+            x, dec_lens, pk = self.decoder.forward_packed(x, d_targets, mel_lens, int(max_mel_len), R, style)
+            mel = ops.linear(x, self.mel_linear.weight, self.mel_linear.bias).float()
+            # padded frames: decoder output 0 -> mel_linear gives the bias there (reference semantics)
+            mel = ops.unpack_rows(mel, pk, fill=self.mel_linear.bias)
+        else:
+            x, dec_lens = self.decoder(x, mel_lens_out, style)
+            mel = ops.linear(x, self.mel_linear.weight, self.mel_linear.bias).float()
         post = self.postnet(mel.to(cd)).float() + mel
         src_masks = ops.lengths_to_mask(src_lens, texts.shape[1])
         mel_masks = ops.lengths_to_mask(dec_lens, mel.shape[1])

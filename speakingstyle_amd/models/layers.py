@@ -62,6 +62,15 @@ class ConvHolder(nn.Module):
         return ops.conv1d(x, self.conv.weight, self.conv.bias, self.pad, self.dil, act)
 
 
+def fused_param_groups(module: nn.Module):
+    """All contiguous-parameter groups of the attention layers in ``module`` (``train/optim.py::FlatArena``)."""
+    groups = []
+    for m in module.modules():
+        if isinstance(m, MultiHeadAttention):
+            groups.extend(m.fused_param_groups())
+    return groups
+
+
 class MultiHeadAttention(nn.Module):
     """Self-attention + output projection + residual + post-LN.
 
@@ -80,16 +89,19 @@ class MultiHeadAttention(nn.Module):
         self.fc = nn.Linear(n_head * d_v, d_model)
         self.dropout = dropout
 
-    def forward(self, x, lengths):
-        w = torch.cat([self.w_qs.weight, self.w_ks.weight, self.w_vs.weight], 0)
-        b = torch.cat([self.w_qs.bias, self.w_ks.bias, self.w_vs.bias], 0)
-        qkv = ops.linear(x, w, b)
-        o = ops.attention(qkv, lengths, self.n_head)
+    def fused_param_groups(self):
+        """Q/K/V weights (and biases) adjacent in the flat arena -> the fused projection is a view."""
+        return [[self.w_qs.weight, self.w_ks.weight, self.w_vs.weight], [self.w_qs.bias, self.w_ks.bias, self.w_vs.bias]]
+
+    def forward(self, x, lengths, pack=None):
+        qkv = ops.linear_group(x, (self.w_qs.weight, self.w_ks.weight, self.w_vs.weight),
+                               (self.w_qs.bias, self.w_ks.bias, self.w_vs.bias))
+        o = ops.attention(qkv, lengths, self.n_head, pack)
         a = ops.linear(o, self.fc.weight, self.fc.bias)
         # LN(dropout(fc(o)) + x), then the FFT block's pad mask-fill (Layers.py:27-28)
         return ops.add_layernorm(
             a, x, self.layer_norm.weight, self.layer_norm.bias,
-            pre_drop=self.dropout, training=self.training, lengths=lengths,
+            pre_drop=self.dropout, training=self.training, lengths=lengths, pack=pack,
         )
 
 
@@ -104,11 +116,11 @@ class PositionwiseFeedForward(nn.Module):
         self.dropout = dropout
         self.k = tuple(kernel_size)
 
-    def forward(self, x, lengths, film_params=None):
-        z = ops.ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias)
+    def forward(self, x, lengths, film_params=None, pack=None):
+        z = ops.ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias, pack)
         return ops.add_layernorm(
             z, x, self.layer_norm.weight, self.layer_norm.bias,
-            pre_drop=self.dropout, training=self.training, film_params=film_params, lengths=lengths,
+            pre_drop=self.dropout, training=self.training, film_params=film_params, lengths=lengths, pack=pack,
         )
 
 
@@ -122,10 +134,11 @@ class FFTBlock(nn.Module):
         if film:
             self.film = FiLM()
 
-    def forward(self, x, lengths, style: FiLMParams = None):
-        x = self.slf_attn(x, lengths)
+    def forward(self, x, lengths, style: FiLMParams = None, pack=None):
+        """``pack``: x is the packed ``[1, R, C]`` decoder input (``ops/packing.py``)."""
+        x = self.slf_attn(x, lengths, pack)
         fp = self.film.pack(style) if (style is not None and hasattr(self, "film")) else None
-        return self.pos_ffn(x, lengths, fp)
+        return self.pos_ffn(x, lengths, fp, pack)
 
 
 class PostNet(nn.Module):

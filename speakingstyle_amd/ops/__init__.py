@@ -16,6 +16,7 @@ from typing import Optional
 import torch
 
 from . import reference as ref
+from .packing import PackInfo, pack as pack_rows, unpack as unpack_rows  # noqa: F401
 
 _FORCED = os.environ.get("SSAMD_BACKEND")  # "reference" | "hip" | None
 
@@ -52,29 +53,50 @@ def linear(x, w, b=None, act=None):
     return ref.linear(x, w, b, act)
 
 
+def linear_group(x, weights, biases):
+    """y = x @ cat(weights)^T + cat(biases): one GEMM for several projections (Q/K/V).
+
+    On the HIP path, when the group is contiguous in the flat arena, the fused
+    weight is a view (no concatenation) and its gradient is written in place.
+    """
+    if use_hip(x):
+        return _hip().linear_group(x, weights, biases)
+    return ref.linear(x, torch.cat(list(weights), 0), torch.cat(list(biases), 0))
+
+
 def conv1d(x, w, b=None, pad=0, dil=1, act=None):
     if use_hip(x):
         return _hip().conv1d(x, w, b, pad, dil, act)
     return ref.conv1d(x, w, b, pad, dil, act)
 
 
-def ffn(x, w1, b1, w2, b2):
-    """Position-wise FFN core: conv(k0) -> ReLU -> conv(k1) (``SubLayers.py:84-87``)."""
+def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None):
+    """Position-wise FFN core: conv(k0) -> ReLU -> conv(k1) (``SubLayers.py:84-87``).
+
+    ``pack``: x is packed ``[1, R, C]``; the convs zero-pad at every sequence end."""
     if use_hip(x):
-        return _hip().ffn(x, w1, b1, w2, b2)
+        return _hip().ffn(x, w1, b1, w2, b2, pack)
+    if pack is not None:
+        return pack_rows(ffn(unpack_rows(x, pack), w1, b1, w2, b2), pack)
     h = ref.conv1d(x, w1, b1, (w1.shape[2] - 1) // 2, 1, "relu")
     return ref.conv1d(h, w2, b2, (w2.shape[2] - 1) // 2, 1, None)
 
 
-def attention(qkv, lengths, n_head):
+def attention(qkv, lengths, n_head, pack: Optional[PackInfo] = None):
     if use_hip(qkv):
-        return _hip().attention(qkv, lengths, n_head)
+        return _hip().attention(qkv, lengths, n_head, pack)
+    if pack is not None:
+        return pack_rows(ref.attention(unpack_rows(qkv, pack), pack.lens, n_head), pack)
     return ref.attention(qkv, lengths, n_head)
 
 
-def add_layernorm(a, residual, ln_w, ln_b, **kw):
+def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, **kw):
     if use_hip(a):
-        return _hip().add_layernorm(a, residual, ln_w, ln_b, **kw)
+        return _hip().add_layernorm(a, residual, ln_w, ln_b, pack=pack, **kw)
+    if pack is not None:
+        kw["lengths"] = pack.lens
+        res = None if residual is None else unpack_rows(residual, pack)
+        return pack_rows(ref.add_layernorm(unpack_rows(a, pack), res, ln_w, ln_b, **kw), pack)
     return ref.add_layernorm(a, residual, ln_w, ln_b, **kw)
 
 
@@ -82,6 +104,14 @@ def length_regulate(x, durations, max_len):
     if use_hip(x):
         return _hip().length_regulate(x, durations, max_len)
     return ref.length_regulate(x, durations, max_len)
+
+
+def length_regulate_packed(x, durations, pack: PackInfo, pe):
+    """LengthRegulator writing packed decoder rows (+ positional encoding)."""
+    if use_hip(x):
+        return _hip().length_regulate_packed(x, durations, pack, pe)
+    out, _ = ref.length_regulate(x, durations, pack.M)
+    return pack_rows(out + pe[: pack.M].to(out.dtype).unsqueeze(0), pack)
 
 
 def embed_add_pe(ids, table, pe, extra=None):

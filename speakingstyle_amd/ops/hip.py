@@ -21,6 +21,7 @@ from typing import Optional
 
 import torch
 
+from . import gradslots
 from . import reference as ref
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libssamd_kernels.so")
@@ -34,20 +35,21 @@ F = ctypes.c_float
 U64 = ctypes.c_ulonglong
 
 _SIGS = {
-    "ssamd_conv_gemm": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
-    "ssamd_conv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, P],
+    "ssamd_conv_gemm": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
+    "ssamd_conv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, P, P],
     "ssamd_colsum": [P, P, L_, I, P],
-    "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
-    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],
-    "ssamd_lr_fwd": [P, P, P, P, I, I, I, I, P],
-    "ssamd_lr_bwd": [P, P, P, I, I, I, I, P],
+    "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
+    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],
+    "ssamd_lr_fwd": [P, P, P, P, P, P, I, I, I, I, P],
+    "ssamd_lr_bwd": [P, P, P, P, P, I, I, I, I, P],
+    "ssamd_pack_info": [P, I, I, P, P, P, P],
     "ssamd_embed_fwd": [I, P, P, P, I, P, P, I, P, P, L_, I, P],
     "ssamd_embed_bwd": [P, P, P, L_, I, P],
     "ssamd_l1pair_fwd": [P, P, P, P, I, I, I, I, P, P],
     "ssamd_l1pair_bwd": [P, P, P, P, I, I, I, I, P, P, P, P, P],
     "ssamd_clip_adam": [P, P, P, P, L_, P, F, F, F, F, F, F, I, P, P, P],
-    "ssamd_attn_fwd": [P, P, P, P, I, I, I, I, F, P],
-    "ssamd_attn_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, F, P],
+    "ssamd_attn_fwd": [P, P, P, P, P, I, I, I, I, F, P],
+    "ssamd_attn_bwd": [P, P, P, P, P, P, P, P, L_, I, I, I, I, F, P],
     "ssamd_relu_mask": [P, P, P, L_, P],
     "ssamd_gemm_set_epilogue": [I],
     "ssamd_gemm_set_variant": [I],
@@ -133,8 +135,8 @@ def _refresh_all(device):
     live = []
     for k in list(_wcache):
         e = _wcache[k]
-        w = e[2]()
-        if w is None or w.data_ptr() != e[5]:
+        owner, w = e[2](), e[7]
+        if owner is None or w.data_ptr() != e[5]:
             del _wcache[k]
             _wtable["n"] = -1
         elif w.device == device and _eligible(w):
@@ -156,38 +158,44 @@ def _refresh_all(device):
                                      _stream())
         _check(rc, "ssamd_weight_prep")
     for e, w in live:
-        e[0], e[1] = w._version, _wgen
+        owner = e[2]()
+        e[0], e[1] = owner._version, _wgen
 
 
-def _cached(param: torch.Tensor, kind: str, mode: int, make):
+def _cached(param: torch.Tensor, kind: str, mode: int, make, src: Optional[torch.Tensor] = None):
+    """Image of ``src`` (default: ``param`` itself), cached under the parameter ``param``."""
+    src = param if src is None else src
     if not isinstance(param, torch.nn.Parameter):  # transient tensors: ids / addresses get reused
-        return make(param.detach())
-    key = (id(param), kind)
+        return make(src.detach())
+    key = (id(param), kind, tuple(src.shape))
     hit = _wcache.get(key)
-    if hit is not None and hit[2]() is param and hit[5] == param.data_ptr():
+    if hit is not None and hit[2]() is param and hit[5] == src.data_ptr() and hit[6] == tuple(src.shape):
         if hit[0] == param._version and hit[1] == _wgen:
             return hit[3]
-        if _eligible(param) and has("ssamd_weight_prep"):
-            _refresh_all(param.device)
+        if _eligible(src) and has("ssamd_weight_prep"):
+            _refresh_all(src.device)
             return hit[3]
-    img = make(param.detach())
-    _wcache[key] = [param._version, _wgen, weakref.ref(param), img, mode, param.data_ptr()]
+    img = make(src.detach())
+    _wcache[key] = [param._version, _wgen, weakref.ref(param), img, mode, src.data_ptr(), tuple(src.shape),
+                    src.detach()]
     _wtable["n"] = -1  # entry set changed: rebuild the descriptor table on the next refresh
     return img
 
 
-def weight_fwd(w: torch.Tensor) -> torch.Tensor:
+def weight_fwd(w: torch.Tensor, owner: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[Cout, Cin, ks] (or Linear [out, in]) fp32 -> bf16 [Cout][ks][Cin]."""
+    o = w if owner is None else owner
     if w.dim() == 2:
-        return _cached(w, "fwd", 0, lambda x: x.to(torch.bfloat16).contiguous())
-    return _cached(w, "fwd", 0, lambda x: x.permute(0, 2, 1).to(torch.bfloat16).contiguous())
+        return _cached(o, "fwd", 0, lambda x: x.to(torch.bfloat16).contiguous(), w)
+    return _cached(o, "fwd", 0, lambda x: x.permute(0, 2, 1).to(torch.bfloat16).contiguous(), w)
 
 
-def weight_dgrad(w: torch.Tensor) -> torch.Tensor:
+def weight_dgrad(w: torch.Tensor, owner: Optional[torch.Tensor] = None) -> torch.Tensor:
     """-> bf16 [Cin][ks][Cout] with taps flipped (data gradient = conv with W^T)."""
+    o = w if owner is None else owner
     if w.dim() == 2:
-        return _cached(w, "dgrad", 1, lambda x: x.t().to(torch.bfloat16).contiguous())
-    return _cached(w, "dgrad", 1, lambda x: x.flip(2).permute(1, 2, 0).to(torch.bfloat16).contiguous())
+        return _cached(o, "dgrad", 1, lambda x: x.t().to(torch.bfloat16).contiguous(), w)
+    return _cached(o, "dgrad", 1, lambda x: x.flip(2).permute(1, 2, 0).to(torch.bfloat16).contiguous(), w)
 
 
 _ACT = {None: 0, "relu": 1, "lrelu": 2, "tanh": 3}
@@ -204,7 +212,16 @@ def _workspace(device, nfloats: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------ raw launchers
-def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, resid=None, lens=None, out_f32=False):
+def _rinfo_ptr(rinfo, rows):
+    """Packed-sequence row table: int32 [rows, 2] = (position in sequence, sequence length)."""
+    if rinfo is None:
+        return None
+    _need(rinfo, torch.int32, "rinfo")
+    assert rinfo.numel() == 2 * rows, "rinfo must hold (t, len) for every row"
+    return _ptr(rinfo)
+
+def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, resid=None, lens=None, out_f32=False,
+                  rinfo=None):
     _need(x, torch.bfloat16, "conv_gemm.x")
     _need(wimg, torch.bfloat16, "conv_gemm.w")
     assert x.numel() == B * L * Cin, "conv_gemm: x shape mismatch"
@@ -223,13 +240,15 @@ def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, re
         _need(lens, torch.int64, "conv_gemm.lens")
         assert lens.numel() == B
     rc = lib().ssamd_conv_gemm(_ptr(x), _ptr(wimg), _ptr(bias), _ptr(aux), _ptr(resid), _ptr(lens), _ptr(y),
-                               int(out_f32), B, L, Cin, ks, dil, pad, N, act, N, _stream())
+                               int(out_f32), B, L, Cin, ks, dil, pad, N, act, N, _rinfo_ptr(rinfo, B * L), _stream())
     _check(rc, "ssamd_conv_gemm")
     return y
 
 
-def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False):
-    """-> dW [N, Cin, ks] fp32 (and db [N] when ``with_bias``: fused column sums of dY)."""
+def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, db=None, rinfo=None):
+    """-> dW [N, Cin, ks] fp32 (and db [N] when ``with_bias``: fused column sums of dY).
+
+    ``dW`` / ``db``: optional destinations (arena gradient slots), fully overwritten."""
     _need(x, torch.bfloat16, "wgrad.x")
     _need(dy, torch.bfloat16, "wgrad.dy")
     assert x.numel() == B * L * Cin and dy.numel() == B * L * N
@@ -239,17 +258,26 @@ def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False):
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
     max_splits = max(1, min(64, (1536 + tiles - 1) // tiles))
     ws = _workspace(x.device, max_splits * (N * K + N))
-    dW = torch.empty(N, Cin, ks, device=x.device, dtype=torch.float32)
-    db = torch.empty(N, device=x.device, dtype=torch.float32) if with_bias else None
+    if dW is None:
+        dW = torch.empty(N, Cin, ks, device=x.device, dtype=torch.float32)
+    else:
+        assert dW.dtype == torch.float32 and dW.is_contiguous() and dW.numel() == N * Cin * ks
+    if not with_bias:
+        db = None
+    elif db is None:
+        db = torch.empty(N, device=x.device, dtype=torch.float32)
+    else:
+        assert db.dtype == torch.float32 and db.is_contiguous() and db.numel() == N
     rc = lib().ssamd_conv_wgrad(_ptr(x), _ptr(dy), _ptr(ws), ws.numel(), _ptr(dW), _ptr(db), B, L, Cin, ks, dil, pad,
-                                N, max_splits, _stream())
+                                N, max_splits, _rinfo_ptr(rinfo, B * L), _stream())
     _check(rc, "ssamd_conv_wgrad")
     return (dW, db) if with_bias else dW
 
 
-def colsum_raw(dy, N):
+def colsum_raw(dy, N, db=None):
     _need(dy, torch.bfloat16, "colsum.dy")
-    db = torch.empty(N, device=dy.device, dtype=torch.float32)
+    if db is None:
+        db = torch.empty(N, device=dy.device, dtype=torch.float32)
     rc = lib().ssamd_colsum(_ptr(dy), _ptr(db), dy.numel() // N, N, _stream())
     _check(rc, "ssamd_colsum")
     return db
@@ -277,6 +305,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.geom = (B, L, Cin, ks, dil, pad, N)
         ctx.act = act
         ctx.has_b = b is not None
+        ctx.b = b if isinstance(b, torch.nn.Parameter) else None  # gradient-slot owner only
         ctx.save_for_backward(xc, w, y if act == "relu" else None)
         return y
 
@@ -293,13 +322,15 @@ class _ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin)
         want_b = ctx.has_b and ctx.needs_input_grad[2]
+        sb = gradslots.claim(ctx.b) if want_b else None
         if ctx.needs_input_grad[1]:
-            res = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b)
+            sw = gradslots.claim(w)
+            res = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b, dW=sw, db=sb)
             dw, db = res if want_b else (res, None)
             if w.dim() == 2:
                 dw = dw.view(N, Cin)
         elif want_b:
-            db = colsum_raw(dy, N)
+            db = colsum_raw(dy, N, sb)
         return dx, dw, db, None, None, None, None
 
 
@@ -317,19 +348,66 @@ def linear(x, w, b=None, act=None, out_f32=False):
     return y.reshape(*shp[:-1], w.shape[0])
 
 
+class _GroupLinearFn(torch.autograd.Function):
+    """One GEMM for several Linear layers whose weights / biases are contiguous in the
+    arena: ``wf`` / ``bf`` are the fused data views; the member parameters are inputs
+    only so autograd routes each one its slice of the (in-place written) gradient."""
+
+    @staticmethod
+    def forward(ctx, x, wf, bf, n, *params):
+        ws, bs = params[:n], params[n:]
+        B, L, Cin = x.shape
+        N = wf.shape[0]
+        xc = x.contiguous()
+        y = conv_gemm_raw(xc, weight_fwd(wf, owner=ws[0]), bf, B, L, Cin, 1, 1, 0, N, 0)
+        ctx.save_for_backward(xc, wf)
+        ctx.members = (ws, bs)
+        ctx.dims = (B, L, Cin, N)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wf = ctx.saved_tensors
+        ws, bs = ctx.members
+        B, L, Cin, N = ctx.dims
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin)
+        sw, sb = gradslots.claim_fused(ws), gradslots.claim_fused(bs)
+        dw, db = conv_wgrad_raw(xc, dy, B, L, Cin, 1, 1, 0, N, with_bias=True,
+                                dW=None if sw is None else sw.view(N, Cin, 1), db=sb)
+        dw = dw.view(N, Cin)
+        return (dx, None, None, None, *gradslots.split_rows(dw, ws), *gradslots.split_rows(db, bs))
+
+
+def linear_group(x, weights, biases):
+    weights, biases = list(weights), list(biases)
+    wf, bf = gradslots.fused_data(weights), gradslots.fused_data(biases)
+    if wf is None or bf is None:
+        w, b = torch.cat(weights, 0), torch.cat(biases, 0)
+        return linear(x, w, b)
+    shp = x.shape
+    x3 = x.reshape(1, -1, shp[-1]) if x.dim() != 3 else x
+    y = _GroupLinearFn.apply(x3, wf, bf, len(weights), *weights, *biases)
+    return y.reshape(*shp[:-1], wf.shape[0])
+
+
 class _FFNFn(torch.autograd.Function):
     """conv(k0) -> ReLU -> conv(k1): the ReLU derivative is fused into the
     data-gradient epilogue of the second conv (aux = h), so no extra pass."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, rinfo):
         B, L, C = x.shape
         k1, k2 = w1.shape[2], w2.shape[2]
         H = w1.shape[0]
         xc = x.contiguous()
-        h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1)
-        z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0)
+        r1 = rinfo if k1 > 1 else None
+        r2 = rinfo if k2 > 1 else None
+        h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1, rinfo=r1)
+        z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0, rinfo=r2)
+        ctx.rinfo = (r1, r2)
         ctx.save_for_backward(xc, h, w1, w2)
+        ctx.biases = (b1, b2)
         ctx.dims = (B, L, C, H, k1, k2)
         return z
 
@@ -339,15 +417,21 @@ class _FFNFn(torch.autograd.Function):
         B, L, C, H, k1, k2 = ctx.dims
         dz = dz.to(torch.bfloat16).contiguous()
         p1, p2 = (k1 - 1) // 2, (k2 - 1) // 2
-        dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h)
-        dw2, db2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True)
-        dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0)
-        dw1, db1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True)
-        return dx, dw1, db1, dw2, db2
+        b1, b2 = ctx.biases
+        r1, r2 = ctx.rinfo
+        dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
+        dw2, db2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=gradslots.claim(w2),
+                                  db=gradslots.claim(b2), rinfo=r2)
+        dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1)
+        dw1, db1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=gradslots.claim(w1),
+                                  db=gradslots.claim(b1), rinfo=r1)
+        return dx, dw1, db1, dw2, db2, None
 
 
-def ffn(x, w1, b1, w2, b2):
-    return _FFNFn.apply(x, w1, b1, w2, b2)
+def ffn(x, w1, b1, w2, b2, pack=None):
+    if pack is not None:
+        assert x.shape[0] == 1 and x.shape[1] == pack.R, "packed FFN expects [1, R, C]"
+    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else pack.rinfo)
 
 
 # ------------------------------------------------------------------------ add + LayerNorm
@@ -365,19 +449,20 @@ def set_seed(s: int):
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps):
-        B, L, C = a.shape
+    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom):
+        B, L, C = a.shape if geom is None else geom  # packed: (sequences, longest, C) over [1, R, C] rows
         ac = a.contiguous()
         rc_ = None if res is None else res.contiguous()
         out = torch.empty_like(ac)
-        mean = torch.empty(B * L, device=a.device, dtype=torch.float32)
+        mean = torch.empty(a.numel() // C, device=a.device, dtype=torch.float32)
         rstd = torch.empty_like(mean)
         gf = None if g is None else g.detach().float().contiguous()
         bf = None if bt is None else bt.detach().float().contiguous()
         rc = lib().ssamd_addln_fwd(_ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb),
-                                   _ptr(lens), _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, pre_p, post_p, seed, eps,
-                                   _stream())
+                                   _ptr(lens), _ptr(cu), _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, pre_p, post_p,
+                                   seed, eps, _stream())
         _check(rc, "ssamd_addln_fwd")
+        ctx.cu = cu
         ctx.save_for_backward(ac, rc_, w, b, gf, bf, sg, sb, lens, mean, rstd)
         ctx.cfg = (B, L, C, pre_p, post_p, seed, res is not None, g is not None)
         ctx.gdtype = None if g is None else (g.dtype, bt.dtype)
@@ -390,12 +475,15 @@ class _AddLNFn(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous()
         dh = torch.empty_like(ac)
         da = torch.empty_like(ac) if pre_p > 0 else None
-        dw = torch.zeros(C, device=ac.device, dtype=torch.float32)
-        db = torch.zeros_like(dw)
+        dw, db = gradslots.claim(w), gradslots.claim(b)  # zeroed slots double as the atomic accumulators
+        if dw is None:
+            dw = torch.zeros(C, device=ac.device, dtype=torch.float32)
+        if db is None:
+            db = torch.zeros(C, device=ac.device, dtype=torch.float32)
         S1 = torch.zeros(B, C, device=ac.device, dtype=torch.float32) if has_film else None
         S2 = torch.zeros_like(S1) if has_film else None
         rc = lib().ssamd_addln_bwd(_ptr(dout), _ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(sg), _ptr(lens),
-                                   _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da), _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
+                                   _ptr(ctx.cu), _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da), _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
                                    B, L, C, pre_p, post_p, seed, _stream())
         _check(rc, "ssamd_addln_bwd")
         d_a = da if da is not None else dh
@@ -406,13 +494,15 @@ class _AddLNFn(torch.autograd.Function):
             dbt = (S2 * sb).to(ctx.gdtype[1])
             dsg = (S1 * gf).sum().reshape(1)
             dsb = (S2 * bf).sum().reshape(1)
-        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None
+        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None
 
 
 def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None,
-                  lengths=None, eps=1e-5):
+                  lengths=None, eps=1e-5, pack=None):
     C = a.shape[-1]
     if C not in (256, 512, 1024) or a.dtype != torch.bfloat16:
+        if pack is not None:
+            raise ValueError("packed add_layernorm needs C in (256, 512, 1024) and bf16")
         return ref.add_layernorm(a, residual, ln_w, ln_b, pre_drop=pre_drop, post_drop=post_drop, training=training,
                                  film_params=film_params, lengths=lengths, eps=eps)
     if not training:
@@ -420,11 +510,16 @@ def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, train
     g = bt = sg = sb = None
     if film_params is not None:
         g, bt, sg, sb = film_params
-    lens = None if lengths is None else lengths.to(torch.int64).contiguous()
+    cu = geom = None
+    if pack is not None:
+        assert a.shape[0] == 1 and a.shape[1] == pack.R, "packed add_layernorm expects [1, R, C]"
+        lens, cu, geom = pack.lens, pack.cu, (pack.B, pack.M, C)
+    else:
+        lens = None if lengths is None else lengths.to(torch.int64).contiguous()
     if residual is not None:
         residual = residual.to(a.dtype)
     out = _AddLNFn.apply(a, residual, ln_w, ln_b, g, bt, sg, sb, lens, float(pre_drop), float(post_drop),
-                         _next_seed(), float(eps))
+                         _next_seed(), float(eps), cu, geom)
     return out
 
 
@@ -438,7 +533,7 @@ class _LRFn(torch.autograd.Function):
         pe_c = None if pe is None else pe.to(x.dtype).contiguous()
         if pe_c is not None:
             assert pe_c.shape[0] >= M and pe_c.shape[1] == C
-        rc = lib().ssamd_lr_fwd(_ptr(xc), _ptr(dur), _ptr(pe_c), _ptr(out), B, T, M, C, _stream())
+        rc = lib().ssamd_lr_fwd(_ptr(xc), _ptr(dur), _ptr(pe_c), _ptr(out), None, None, B, T, M, C, _stream())
         _check(rc, "ssamd_lr_fwd")
         ctx.save_for_backward(dur)
         ctx.dims = (B, T, M, C)
@@ -450,7 +545,7 @@ class _LRFn(torch.autograd.Function):
         B, T, M, C = ctx.dims
         dout = dout.to(torch.bfloat16).contiguous()
         dx = torch.empty(B, T, C, device=dout.device, dtype=torch.bfloat16)
-        rc = lib().ssamd_lr_bwd(_ptr(dout), _ptr(dur), _ptr(dx), B, T, M, C, _stream())
+        rc = lib().ssamd_lr_bwd(_ptr(dout), _ptr(dur), _ptr(dx), None, None, B, T, M, C, _stream())
         _check(rc, "ssamd_lr_bwd")
         return dx, None, None, None
 
@@ -464,6 +559,45 @@ def length_regulate(x, durations, max_len, pe=None):
     if max_len is None:
         max_len = int(mel_len.max().item()) if dur.shape[0] else 0  # inference: one D2H for allocation
     return _LRFn.apply(x, dur, int(max_len), pe), mel_len
+
+
+class _LRPackedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dur, pe, cu, plen, R, M):
+        B, T, C = x.shape
+        xc = x.contiguous()
+        out = torch.empty(1, R, C, device=x.device, dtype=x.dtype)
+        pe_c = pe.to(x.dtype).contiguous()
+        assert pe_c.shape[0] >= M and pe_c.shape[1] == C
+        rc = lib().ssamd_lr_fwd(_ptr(xc), _ptr(dur), _ptr(pe_c), _ptr(out), _ptr(cu), _ptr(plen), B, T, M, C,
+                                _stream())
+        _check(rc, "ssamd_lr_fwd(packed)")
+        ctx.save_for_backward(dur, cu, plen)
+        ctx.dims = (B, T, M, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dur, cu, plen = ctx.saved_tensors
+        B, T, M, C = ctx.dims
+        dout = dout.to(torch.bfloat16).contiguous()
+        dx = torch.empty(B, T, C, device=dout.device, dtype=torch.bfloat16)
+        rc = lib().ssamd_lr_bwd(_ptr(dout), _ptr(dur), _ptr(dx), _ptr(cu), _ptr(plen), B, T, M, C, _stream())
+        _check(rc, "ssamd_lr_bwd(packed)")
+        return dx, None, None, None, None, None, None
+
+
+def length_regulate_packed(x, durations, pack, pe):
+    if x.dtype != torch.bfloat16 or x.shape[-1] % 8:
+        raise ValueError("packed length regulator needs bf16 and C % 8 == 0")
+    dur = durations.to(torch.int64).contiguous()
+    return _LRPackedFn.apply(x, dur, pe, pack.cu, pack.lens, pack.R, pack.M)
+
+
+def pack_info(lens, M, cu, rinfo, dst):
+    _need(lens, torch.int64, "pack.lens")
+    rc = lib().ssamd_pack_info(_ptr(lens), lens.numel(), int(M), _ptr(cu), _ptr(rinfo), _ptr(dst), _stream())
+    _check(rc, "ssamd_pack_info")
 
 
 # ------------------------------------------------------------------------ embeddings
@@ -481,6 +615,7 @@ class _EmbedFn(torch.autograd.Function):
                                    _ptr(tb), _ptr(ad), L, _ptr(out), _ptr(idx), rows, C, _stream())
         _check(rc, "ssamd_embed_fwd")
         ctx.save_for_backward(idx)
+        ctx.table = table if isinstance(table, torch.nn.Parameter) else None
         ctx.tshape = (table.shape, table.dtype)
         ctx.mode = mode
         return out
@@ -490,11 +625,13 @@ class _EmbedFn(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         shape, dtype = ctx.tshape
         dout = dout.to(torch.bfloat16).contiguous()
-        dt = torch.zeros(shape, device=dout.device, dtype=torch.float32)
+        dt = gradslots.claim(ctx.table) if ctx.needs_input_grad[4] else None
+        if dt is None:
+            dt = torch.zeros(shape, device=dout.device, dtype=torch.float32)
         rc = lib().ssamd_embed_bwd(_ptr(idx), _ptr(dout), _ptr(dt), idx.numel(), shape[1], _stream())
         _check(rc, "ssamd_embed_bwd")
         d_add = dout if ctx.mode == 1 else None
-        return None, None, None, None, dt.to(dtype), d_add, None
+        return None, None, None, None, dt if dtype == torch.float32 else dt.to(dtype), d_add, None
 
 
 def embed_add_pe(ids, table, pe, extra=None):
@@ -510,40 +647,44 @@ def bucketize_embed_add(x, values, bins, table):
 
 
 # ------------------------------------------------------------------------ attention
-def attention(qkv, lengths, n_head):
-    if not has("ssamd_attn_fwd"):
-        return ref.attention(qkv, lengths, n_head)
-    return _AttnFn.apply(qkv, lengths.to(torch.int64).contiguous(), n_head)
+def attention(qkv, lengths, n_head, pack=None):
+    if pack is not None:
+        assert qkv.shape[0] == 1 and qkv.shape[1] == pack.R, "packed attention expects [1, R, 3C]"
+        return _AttnFn.apply(qkv, pack.lens, n_head, pack.cu, (pack.B, pack.M))
+    return _AttnFn.apply(qkv, lengths.to(torch.int64).contiguous(), n_head, None, None)
 
 
 class _AttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, lens, n_head):
-        B, L, C3 = qkv.shape
+    def forward(ctx, qkv, lens, n_head, cu, geom):
+        rows = qkv.shape[0] * qkv.shape[1]
+        C3 = qkv.shape[2]
+        B, L = (qkv.shape[0], qkv.shape[1]) if geom is None else geom
         D = C3 // (3 * n_head)
         if D not in (32, 64, 128):
             raise ValueError("attention head dim must be 32/64/128")
         q = qkv.contiguous()
-        o = torch.empty(B, L, n_head * D, device=q.device, dtype=torch.bfloat16)
+        o = torch.empty(*qkv.shape[:2], n_head * D, device=q.device, dtype=torch.bfloat16)
         lse = torch.empty(B, n_head, L, device=q.device, dtype=torch.float32)
-        rc = lib().ssamd_attn_fwd(_ptr(q), _ptr(lens), _ptr(o), _ptr(lse), B, L, n_head, D, 1.0 / math.sqrt(D),
-                                  _stream())
+        rc = lib().ssamd_attn_fwd(_ptr(q), _ptr(lens), _ptr(cu), _ptr(o), _ptr(lse), B, L, n_head, D,
+                                  1.0 / math.sqrt(D), _stream())
         _check(rc, "ssamd_attn_fwd")
         ctx.save_for_backward(q, lens, o, lse)
-        ctx.dims = (B, L, n_head, D)
+        ctx.cu = cu
+        ctx.dims = (B, L, n_head, D, rows)
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, lens, o, lse = ctx.saved_tensors
-        B, L, H, D = ctx.dims
+        B, L, H, D, rows = ctx.dims
         do = do.to(torch.bfloat16).contiguous()
         dqkv = torch.empty_like(q)
-        delta = torch.empty(B, H, L, device=q.device, dtype=torch.float32)
-        rc = lib().ssamd_attn_bwd(_ptr(q), _ptr(lens), _ptr(o), _ptr(lse), _ptr(do), _ptr(dqkv), _ptr(delta), None, B,
-                                  L, H, D, 1.0 / math.sqrt(D), _stream())
+        delta = torch.empty(rows * H, device=q.device, dtype=torch.float32)
+        rc = lib().ssamd_attn_bwd(_ptr(q), _ptr(lens), _ptr(ctx.cu), _ptr(o), _ptr(lse), _ptr(do), _ptr(dqkv),
+                                  _ptr(delta), rows, B, L, H, D, 1.0 / math.sqrt(D), _stream())
         _check(rc, "ssamd_attn_bwd")
-        return dqkv, None, None
+        return dqkv, None, None, None, None
 
 
 # ------------------------------------------------------------------------ loss / optimizer
@@ -623,6 +764,7 @@ class _BNActFn(torch.autograd.Function):
                                 _stream())
         _check(rc, "ssamd_bn_fwd")
         ctx.save_for_backward(hc, gamma, stats)
+        ctx.beta = beta
         ctx.cfg = (R, C, int(training), int(act_tanh), float(p), seed)
         return out
 
@@ -633,8 +775,11 @@ class _BNActFn(torch.autograd.Function):
         dyf32 = dy.dtype == torch.float32
         dy = dy.contiguous() if dyf32 else dy.to(torch.bfloat16).contiguous()
         dh = torch.empty_like(hc)
-        dg = torch.empty(C, device=hc.device, dtype=torch.float32)
-        db = torch.empty_like(dg)
+        dg, db = gradslots.claim(gamma), gradslots.claim(ctx.beta)
+        if dg is None:
+            dg = torch.empty(C, device=hc.device, dtype=torch.float32)
+        if db is None:
+            db = torch.empty(C, device=hc.device, dtype=torch.float32)
         ws = _bn_ws(hc.device, R, C)
         rc = lib().ssamd_bn_bwd(_ptr(dy), int(dyf32), _ptr(hc), _ptr(gamma), _ptr(stats[2]), _ptr(stats[3]),
                                 _ptr(stats[0]), _ptr(stats[1]), _ptr(dh), _ptr(dg), _ptr(db), R, C, training, act_tanh,

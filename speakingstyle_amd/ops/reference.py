@@ -69,7 +69,9 @@ def attention(qkv: torch.Tensor, lengths: torch.Tensor, n_head: int) -> torch.Te
     qkv: [B, L, 3*H*dk] = [q | k | v] with head-major channels (h*dk + d), exactly
     the reference's ``view(sz_b, len, n_head, d_k)`` split (``transformer/SubLayers.py:39-44``).
     Softmax over keys with keys >= length masked to -inf (``transformer/Modules.py:14-21``).
-    Returns [B, L, H*dk].
+    Returns [B, L, H*dk].  Query rows >= length are zero: the reference computes them and
+    masks them after the block (``transformer/Layers.py:27``); every consumer here masks
+    them too, so defining them as 0 lets the kernels skip padded query tiles entirely.
     """
     B, L, C3 = qkv.shape
     D = C3 // (3 * n_head)
@@ -78,7 +80,7 @@ def attention(qkv: torch.Tensor, lengths: torch.Tensor, n_head: int) -> torch.Te
     key_pad = lengths_to_mask(lengths, L)[:, None, None, :]
     s = s.masked_fill(key_pad, float("-inf"))
     p = torch.softmax(s, dim=-1)
-    o = torch.matmul(p, v.float()).to(qkv.dtype)
+    o = torch.matmul(p, v.float()).masked_fill(lengths_to_mask(lengths, L)[:, None, :, None], 0.0).to(qkv.dtype)
     return o.permute(0, 2, 1, 3).reshape(B, L, n_head * D)
 
 

@@ -78,6 +78,7 @@ class GradBuckets:
         cap = max(1, int(bucket_mb * 1024 * 1024 // 4))
         self.buckets: List[tuple] = []  # (start, end, n_params)
         self.param_bucket = {}
+        self.param_index = {id(p): i for i, p in enumerate(arena.params)}
         start = 0
         members = 0
         cur_end = 0
@@ -107,6 +108,7 @@ class GradBuckets:
     def _hook(self, p):
         if not self.enabled:
             return
+        self.arena.ensure_slot(p, self.param_index[id(p)])  # gradients from plain-torch ops: into the bucket
         bi = self.param_bucket[id(p)]
         self.pending[bi] -= 1
         if self.pending[bi] == 0 and self.works[bi] is None:

@@ -32,10 +32,35 @@ import torch.nn as nn
 
 
 class FlatArena:
-    """Packs the given parameters into contiguous fp32 data / grad buffers."""
+    """Packs the given parameters into contiguous fp32 data / grad buffers.
 
-    def __init__(self, params: List[nn.Parameter], device=None, align: int = 64):
-        self.params = list(params)
+    ``groups``: lists of parameters to place back to back in the given order (e.g.
+    the Q/K/V projections of an attention layer, so the fused QKV weight and its
+    gradient are views).  Each group takes the position of its first member.
+    Gradients are written in place by the backward kernels (``ops/gradslots.py``);
+    between steps ``p.grad`` is None.
+    """
+
+    def __init__(self, params: List[nn.Parameter], device=None, align: int = 64, groups=None):
+        from ..ops import gradslots
+
+        params = list(params)
+        if groups:
+            member = {}
+            for gi, g in enumerate(groups):
+                if all(any(q is p for p in params) for q in g):
+                    for q in g:
+                        member[id(q)] = gi
+            ordered, done = [], set()
+            for p in params:
+                gi = member.get(id(p))
+                if gi is None:
+                    ordered.append(p)
+                elif gi not in done:
+                    done.add(gi)
+                    ordered.extend(groups[gi])
+            params = ordered
+        self.params = params
         device = device or (self.params[0].device if self.params else "cpu")
         offs, n = [], 0
         for p in self.params:
@@ -45,25 +70,59 @@ class FlatArena:
         self.numel = n
         self.data = torch.zeros(n, dtype=torch.float32, device=device)
         self.grad = torch.zeros(n, dtype=torch.float32, device=device)
+        self._slot_ptr = {}
+        self.copied = 0  # gradients that did not arrive in their slot (diagnostics)
         for p, o in zip(self.params, offs):
             k = p.numel()
             self.data[o:o + k].copy_(p.detach().reshape(-1).float())
             p.data = self.data[o:o + k].view_as(p)
-            p.grad = self.grad[o:o + k].view_as(p)
+            p.grad = None
+            gradslots.register(p, self, o)
+            self._slot_ptr[id(p)] = self.grad[o:o + k].data_ptr()
+        gradslots.reset()
 
     def slice(self, i):
         o = self.offsets[i]
         return o, o + self.params[i].numel()
 
+    def grad_view(self, i):
+        o = self.offsets[i]
+        p = self.params[i]
+        return self.grad[o:o + p.numel()].view_as(p)
+
     def zero_grad(self):
+        from ..ops import gradslots
+
         self.grad.zero_()
+        for p in self.params:
+            p.grad = None
+        gradslots.reset()
+
+    def ensure_slot(self, p, i=None):
+        """Make ``p.grad`` the arena slot (copying a gradient produced outside it)."""
+        g = p.grad
+        if g is None or g.data_ptr() == self._slot_ptr[id(p)]:
+            return
+        if i is None:
+            i = next(j for j, q in enumerate(self.params) if q is p)
+        slot = self.grad_view(i)
+        slot.copy_(g)
+        p.grad = slot
+        self.copied += 1
+
+    def finalize_grads(self):
+        """After backward: every produced gradient lives in the arena."""
+        for i, p in enumerate(self.params):
+            g = p.grad
+            if g is not None and g.data_ptr() != self._slot_ptr[id(p)]:
+                self.ensure_slot(p, i)
 
     def rebind_grads(self):
-        """Re-point p.grad at the arena (after something replaced it)."""
-        for p, o in zip(self.params, self.offsets):
-            g = self.grad[o:o + p.numel()].view_as(p)
-            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
-                p.grad = g
+        """Re-point p.grad at the arena (e.g. before reading gradients of every parameter)."""
+        self.finalize_grads()
+        for i, p in enumerate(self.params):
+            if p.grad is None:
+                p.grad = self.grad_view(i)
 
 
 class ScheduledOptim:
@@ -85,7 +144,8 @@ class ScheduledOptim:
 
         self.all_params = list(model.parameters())  # torch.optim index space
         trainable = [p for p in self.all_params if p.requires_grad]
-        self.arena = FlatArena(list(reversed(trainable)))
+        groups = model.fused_param_groups() if hasattr(model, "fused_param_groups") else None
+        self.arena = FlatArena(list(reversed(trainable)), groups=groups)
         self._index = {id(p): i for i, p in enumerate(self.all_params)}
         self.exp_avg = torch.zeros_like(self.arena.data)
         self.exp_avg_sq = torch.zeros_like(self.arena.data)

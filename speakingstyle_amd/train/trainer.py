@@ -69,6 +69,7 @@ class Trainer:
         else:
             with self.buckets.no_sync():
                 (total / self.grad_acc).backward()
+        self.opt.arena.finalize_grads()
         self.micro += 1
         lr = None
         if last_micro:

@@ -103,7 +103,8 @@ def test_dp2_matches_single_process():
     cfg = _setup()
     model = _model(cfg)
     model.train()
-    arena = FlatArena(list(reversed([p for p in model.parameters() if p.requires_grad])))
+    arena = FlatArena(list(reversed([p for p in model.parameters() if p.requires_grad])),
+                      groups=model.fused_param_groups())
     shards = _shards()
     n_mel = 80
     counts = torch.zeros(3)
@@ -117,4 +118,5 @@ def test_dp2_matches_single_process():
         loss = lf(s, out, named, global_counts=counts)[0]
         loss = loss - 0.5 * lf.lambda_f * torch.sum(named ** 2)
         loss.backward()
+        arena.finalize_grads()
     torch.testing.assert_close(res[0][0], arena.grad, rtol=1e-4, atol=1e-6)

@@ -249,11 +249,18 @@ def test_model_step_hip_vs_reference():
     m = FastSpeech2(pp, mc).to(DEV).eval()
     mr = copy.deepcopy(m)
     m.set_compute_dtype(torch.bfloat16)
+    # flat arena with fused QKV groups: the kernels write weight gradients into their slots
+    from speakingstyle_amd.train.optim import FlatArena
+
+    arena = FlatArena(list(reversed(list(m.parameters()))), groups=m.fused_param_groups())
     b = SyntheticBatches(4, device=DEV, seed=11, phone_counts=[40, 55, 61, 20]).make_batch()
     lossf = FastSpeech2Loss(pp, tc)
     out = m(*b[2:])
     lo = lossf(b, out, m.film_scalars())
     lo[0].backward()
+    arena.finalize_grads()
+    assert all(p.grad is None or p.grad.data_ptr() == arena.grad_view(i).data_ptr()
+               for i, p in enumerate(arena.params))
     ops.set_backend("reference")
     try:
         outr = mr(*b[2:])
@@ -377,3 +384,140 @@ def test_weight_images_follow_optimizer():
         finally:
             ops.set_backend(None)
     assert _rel(out[1], outr[1]) < 3e-2
+
+
+def _pack_case():
+    from speakingstyle_amd.ops.packing import PackInfo
+
+    lens = torch.tensor([150, 77, 5, 129], device=DEV)
+    M = 150
+    return PackInfo.build(lens, M, int(lens.sum())), lens, M
+
+
+def test_pack_info_gpu():
+    from speakingstyle_amd.ops.packing import PackInfo
+
+    pk, lens, M = _pack_case()
+    ref_pk = PackInfo.build(lens.cpu(), M, pk.R)
+    assert pk.cu.cpu().tolist() == ref_pk.cu.tolist()
+    assert torch.equal(pk.rinfo.cpu(), ref_pk.rinfo)
+    assert torch.equal(pk.dst.cpu(), ref_pk.dst)
+
+
+@pytest.mark.parametrize("D,H", [(128, 2), (32, 8)])
+def test_attention_packed(D, H):
+    from speakingstyle_amd.ops.packing import pack, unpack
+
+    torch.manual_seed(12)
+    pk, lens, M = _pack_case()
+    qkv = torch.randn(pk.B, M, 3 * H * D, device=DEV).to(torch.bfloat16)
+    qp = pack(qkv, pk).detach().requires_grad_(True)
+    qd = qkv.clone().requires_grad_(True)
+    op = hip.attention(qp, None, H, pk)
+    od = hip.attention(qd, lens, H)
+    assert _rel(unpack(op, pk), od) < 1e-2
+    g = torch.randn_like(od)
+    od.backward(g)
+    op.backward(pack(g, pk))
+    assert _rel(unpack(qp.grad, pk), qd.grad) < 1e-2
+
+
+def test_ffn_packed():
+    from speakingstyle_amd.ops.packing import pack, unpack
+
+    torch.manual_seed(13)
+    pk, lens, M = _pack_case()
+    C, Hd = 256, 1024
+    mask = (torch.arange(M, device=DEV)[None] < lens[:, None]).unsqueeze(-1)
+    x = (torch.randn(pk.B, M, C, device=DEV) * mask).to(torch.bfloat16)
+    w1 = torch.nn.Parameter(torch.randn(Hd, C, 9, device=DEV) * 0.03)
+    b1 = torch.nn.Parameter(torch.randn(Hd, device=DEV) * 0.1)
+    w2 = torch.nn.Parameter(torch.randn(C, Hd, 1, device=DEV) * 0.03)
+    b2 = torch.nn.Parameter(torch.randn(C, device=DEV) * 0.1)
+    xp = pack(x, pk).detach().requires_grad_(True)
+    yp = hip.ffn(xp, w1, b1, w2, b2, pk)
+    g = torch.randn(pk.B, M, C, device=DEV).to(torch.bfloat16) * mask
+    yp.backward(pack(g, pk))
+    gp = [t.grad.clone() for t in (w1, b1, w2, b2)]
+    for t in (w1, b1, w2, b2):
+        t.grad = None
+    xd = x.clone().requires_grad_(True)
+    yd = hip.ffn(xd, w1, b1, w2, b2)
+    yd.backward(g)
+    assert _rel(unpack(yp, pk) * mask, yd * mask) < 1e-2
+    assert _rel(unpack(xp.grad, pk) * mask, xd.grad * mask) < 2e-2
+    for a, t in zip(gp, (w1, b1, w2, b2)):
+        assert _rel(a, t.grad) < 2e-2
+
+
+def test_add_layernorm_packed_film():
+    from speakingstyle_amd.ops.packing import pack, unpack
+
+    torch.manual_seed(14)
+    pk, lens, M = _pack_case()
+    C = 256
+    a = torch.randn(pk.B, M, C, device=DEV).to(torch.bfloat16)
+    r = torch.randn(pk.B, M, C, device=DEV).to(torch.bfloat16)
+    w = torch.randn(C, device=DEV).requires_grad_(True)
+    bb = torch.randn(C, device=DEV).requires_grad_(True)
+    fg = torch.randn(pk.B, C, device=DEV).requires_grad_(True)
+    fb = torch.randn(pk.B, C, device=DEV).requires_grad_(True)
+    sg = torch.ones(1, device=DEV).requires_grad_(True)
+    sb = torch.ones(1, device=DEV).requires_grad_(True)
+    mask = (torch.arange(M, device=DEV)[None] < lens[:, None]).unsqueeze(-1)
+    outs, grads = [], []
+    for packed in (True, False):
+        for t in (w, bb, fg, fb, sg, sb):
+            t.grad = None
+        ai = (pack(a, pk) if packed else a).detach().requires_grad_(True)
+        ri = (pack(r, pk) if packed else r).detach().requires_grad_(True)
+        o = hip.add_layernorm(ai, ri, w, bb, film_params=(fg, fb, sg, sb), lengths=lens,
+                              pack=pk if packed else None)
+        gout = torch.randn(pk.B, M, C, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).to(torch.bfloat16)
+        o.backward(pack(gout, pk) if packed else gout)
+        o = unpack(o, pk) if packed else o
+        da = unpack(ai.grad, pk) if packed else ai.grad
+        outs.append(o * mask)
+        grads.append([da * mask] + [t.grad.clone() for t in (w, bb, fg, fb, sg, sb)])
+    assert _rel(outs[0], outs[1]) < 1e-2
+    for x, y in zip(grads[0], grads[1]):
+        assert _rel(x, y) < 2e-2
+
+
+def test_model_packed_vs_padded_gpu():
+    """Packed decoder (HIP) vs padded decoder (HIP): same mel / loss / grads up to bf16."""
+    import copy
+
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+    from speakingstyle_amd.models.loss import FastSpeech2Loss
+
+    pp, mc, tc = load_named("BC2013")
+    mc["transformer"].update(encoder_dropout=0.0, decoder_dropout=0.0)
+    mc["variance_predictor"]["dropout"] = 0.0
+    if mc.get("reference_encoder"):
+        mc["reference_encoder"]["dropout"] = 0.0
+    torch.manual_seed(15)
+    m1 = FastSpeech2(pp, mc).to(DEV).set_compute_dtype(torch.bfloat16)
+    m1.postnet.dropout = 0.0
+    m2 = copy.deepcopy(m1)
+    m1.train()
+    m2.train()
+    b = SyntheticBatches(6, device=DEV, seed=16, phone_counts=[40, 55, 61, 20, 33, 47]).make_batch()
+    lossf = FastSpeech2Loss(pp, tc)
+    out_p = m1(*b[2:])
+    b2 = list(b)
+    b2[7] = b[7].clone()  # drops host_lengths -> padded decoder
+    out_d = m2(*b2[2:])
+    assert _rel(out_p[1], out_d[1]) < 3e-2
+    lp, ld = lossf(b, out_p, m1.film_scalars()), lossf(b, out_d, m2.film_scalars())
+    for x, y in zip(lp[:6], ld[:6]):
+        assert abs(x.item() - y.item()) <= 3e-2 * abs(y.item()) + 1e-3
+    lp[0].backward()
+    ld[0].backward()
+    g2 = dict(m2.named_parameters())
+    bad = [(n, _rel(p.grad, g2[n].grad)) for n, p in m1.named_parameters()
+           if p.grad is not None and g2[n].grad is not None and g2[n].grad.norm() > 1e-6
+           and _rel(p.grad, g2[n].grad) > 0.1]
+    assert not bad, bad[:10]

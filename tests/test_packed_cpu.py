@@ -1,0 +1,75 @@
+"""Packed decoder (valid frames only, ``ops/packing.py``) == padded decoder.
+
+Training forward + backward with and without the host lengths that enable packing
+must give the same outputs (every element of mel / postnet, incl. padded frames) and
+the same parameter gradients (fp32 CPU reference ops; dropout off)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+
+def _cfg(name):
+    from speakingstyle_amd.config import load_named
+
+    pp, mc, tc = load_named(name)
+    mc["transformer"].update(encoder_layer=1, decoder_layer=2, encoder_dropout=0.0, decoder_dropout=0.0)
+    mc["variance_predictor"]["dropout"] = 0.0
+    if mc.get("reference_encoder"):
+        mc["reference_encoder"].update(encoder_layer=1, conv_layer=1, dropout=0.0)
+    return pp, mc, tc
+
+
+@pytest.mark.parametrize("name", ["LJSpeech", "BC2013"])
+def test_packed_decoder_matches_padded(name):
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+    from speakingstyle_amd.models.loss import FastSpeech2Loss
+
+    pp, mc, tc = _cfg(name)
+    torch.manual_seed(0)
+    m1 = FastSpeech2(pp, mc)
+    m1.postnet.dropout = 0.0
+    m2 = copy.deepcopy(m1)
+    m1.train()
+    m2.train()
+    b = SyntheticBatches(3, seed=4, phone_counts=[12, 30, 7]).make_batch()
+    assert getattr(b[7], "host_lengths", None) is not None
+    lossf = FastSpeech2Loss(pp, tc)
+    calls = []
+    orig = m1.decoder.forward_packed
+    m1.decoder.forward_packed = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    out_p = m1(*b[2:])  # host lengths attached -> packed decoder
+    assert calls, "packed decoder path not taken"
+    b_nohost = list(b)
+    b_nohost[7] = b[7].clone()  # no host_lengths attribute -> padded decoder
+    out_d = m2(*b_nohost[2:])
+    for i in (0, 1, 9):
+        torch.testing.assert_close(out_p[i], out_d[i], rtol=1e-5, atol=1e-5)
+    lp = lossf(b, out_p, m1.film_scalars())[0]
+    ld = lossf(b, out_d, m2.film_scalars())[0]
+    torch.testing.assert_close(lp, ld, rtol=1e-5, atol=1e-6)
+    lp.backward()
+    ld.backward()
+    g2 = dict(m2.named_parameters())
+    for n, p in m1.named_parameters():
+        if p.grad is None:
+            assert g2[n].grad is None or g2[n].grad.abs().max() == 0, n
+            continue
+        torch.testing.assert_close(p.grad, g2[n].grad, rtol=1e-4, atol=1e-6, msg=n)
+
+
+def test_pack_info_cpu():
+    from speakingstyle_amd.ops.packing import PackInfo, pack, unpack
+
+    lens = torch.tensor([3, 5, 1])
+    pk = PackInfo.build(lens, 4, 3 + 4 + 1)
+    assert pk.cu.tolist() == [0, 3, 7, 8]
+    assert pk.rinfo[:, 0].tolist() == [0, 1, 2, 0, 1, 2, 3, 0]
+    assert pk.rinfo[:, 1].tolist() == [3, 3, 3, 4, 4, 4, 4, 1]
+    x = torch.randn(3, 4, 2)
+    y = unpack(pack(x, pk), pk, fill=torch.tensor([7.0, 8.0]))
+    mask = torch.arange(4)[None] < lens.clamp(max=4)[:, None]
+    torch.testing.assert_close(y[mask], x[mask])
+    assert (y[~mask] == torch.tensor([7.0, 8.0])).all()

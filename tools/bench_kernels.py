@@ -69,6 +69,15 @@ def main():
         row = {"op": name, "fwd_ms": round(t, 3), "fwd_TF": round(flops / t / 1e9, 1),
                "fwd_regstage_TF": round(flops / t_lds / 1e9, 1), "fwd_ring256_TF": round(flops / t_ring / 1e9, 1), "wgrad_ms": round(tw, 3),
                "wgrad_TF": round(flops / tw / 1e9, 1)}
+        if ks > 1:  # packed-sequence geometry (rinfo table), same data
+            from speakingstyle_amd.ops.packing import PackInfo
+
+            ri = PackInfo.build(torch.full((B,), L, device=dev), L, R).rinfo
+            tpf = timeit(lambda: hip.conv_gemm_raw(x, w, bias, 1, R, Cin, ks, 1, pad, N, 1, rinfo=ri), args.iters)
+            tpw = timeit(lambda: hip.conv_wgrad_raw(x, dy, 1, R, Cin, ks, 1, pad, N, with_bias=True, rinfo=ri),
+                         args.iters)
+            row["fwd_packed_TF"] = round(flops / tpf / 1e9, 1)
+            row["wgrad_packed_TF"] = round(flops / tpw / 1e9, 1)
         if ks == 1:
             a2 = x.view(R, Cin)
             w2 = w.view(N, Cin)
