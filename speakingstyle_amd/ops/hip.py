@@ -36,7 +36,8 @@ U64 = ctypes.c_ulonglong
 
 _SIGS = {
     "ssamd_conv_gemm": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, P],
-    "ssamd_conv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, P, P],
+    "ssamd_conv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, P, P, I, P],
+    "ssamd_wgrad_set_variant": [I],
     "ssamd_colsum": [P, P, L_, I, P],
     "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
     "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],
@@ -245,7 +246,7 @@ def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, re
     return y
 
 
-def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, db=None, rinfo=None):
+def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, db=None, rinfo=None, cu=None):
     """-> dW [N, Cin, ks] fp32 (and db [N] when ``with_bias``: fused column sums of dY).
 
     ``dW`` / ``db``: optional destinations (arena gradient slots), fully overwritten."""
@@ -269,7 +270,8 @@ def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, 
     else:
         assert db.dtype == torch.float32 and db.is_contiguous() and db.numel() == N
     rc = lib().ssamd_conv_wgrad(_ptr(x), _ptr(dy), _ptr(ws), ws.numel(), _ptr(dW), _ptr(db), B, L, Cin, ks, dil, pad,
-                                N, max_splits, _rinfo_ptr(rinfo, B * L), _stream())
+                                N, max_splits, _rinfo_ptr(rinfo, B * L), _ptr(cu),
+                                0 if cu is None else cu.numel() - 1, _stream())
     _check(rc, "ssamd_conv_wgrad")
     return (dW, db) if with_bias else dW
 
@@ -401,8 +403,10 @@ class _FFNFn(torch.autograd.Function):
         k1, k2 = w1.shape[2], w2.shape[2]
         H = w1.shape[0]
         xc = x.contiguous()
+        rinfo, cu = (None, None) if rinfo is None else rinfo
         r1 = rinfo if k1 > 1 else None
         r2 = rinfo if k2 > 1 else None
+        ctx.cu = (cu if k1 > 1 else None, cu if k2 > 1 else None)
         h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1, rinfo=r1)
         z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0, rinfo=r2)
         ctx.rinfo = (r1, r2)
@@ -421,17 +425,17 @@ class _FFNFn(torch.autograd.Function):
         r1, r2 = ctx.rinfo
         dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
         dw2, db2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=gradslots.claim(w2),
-                                  db=gradslots.claim(b2), rinfo=r2)
+                                  db=gradslots.claim(b2), rinfo=r2, cu=ctx.cu[1])
         dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1)
         dw1, db1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=gradslots.claim(w1),
-                                  db=gradslots.claim(b1), rinfo=r1)
+                                  db=gradslots.claim(b1), rinfo=r1, cu=ctx.cu[0])
         return dx, dw1, db1, dw2, db2, None
 
 
 def ffn(x, w1, b1, w2, b2, pack=None):
     if pack is not None:
         assert x.shape[0] == 1 and x.shape[1] == pack.R, "packed FFN expects [1, R, C]"
-    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else pack.rinfo)
+    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu))
 
 
 # ------------------------------------------------------------------------ add + LayerNorm

@@ -318,20 +318,21 @@ def test_bn_dropout_rate():
     assert 0.47 < frac < 0.53
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_conv_gemm_variants(variant):
-    """Every GEMM main-loop variant (register staging / LDS-DMA / 3-stage ring) vs fp32."""
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("Cin,N,ks", [(256, 1024, 9), (80, 512, 5), (1024, 256, 1), (256, 768, 1)])
+def test_conv_gemm_variants(variant, Cin, N, ks):
+    """Every GEMM main-loop variant (register staging / LDS-DMA / 256x128 ring / 256x256 ring) vs fp32."""
     torch.manual_seed(12)
-    B, L, Cin, N, ks = 3, 97, 256, 1024, 9
+    B, L = 3, 197
     x = torch.randn(B, L, Cin, device=DEV).to(torch.bfloat16)
-    w = torch.randn(N, ks, Cin, device=DEV).to(torch.bfloat16) / 48
+    w = (torch.randn(N, ks, Cin, device=DEV) / math.sqrt(ks * Cin)).to(torch.bfloat16)
     bias = torch.randn(N, device=DEV)
     hip.lib().ssamd_gemm_set_variant(variant)
     try:
-        y = hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, 4, N, 1)
+        y = hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, (ks - 1) // 2, N, 1)
     finally:
         hip.lib().ssamd_gemm_set_variant(-1)
-    yr = ref.conv1d(x.float(), w.float().permute(0, 2, 1), bias, 4, 1, "relu")
+    yr = ref.conv1d(x.float(), w.float().permute(0, 2, 1), bias, (ks - 1) // 2, 1, "relu")
     assert _rel(y, yr) < 1e-2
 
 
@@ -521,3 +522,25 @@ def test_model_packed_vs_padded_gpu():
            if p.grad is not None and g2[n].grad is not None and g2[n].grad.norm() > 1e-6
            and _rel(p.grad, g2[n].grad) > 0.1]
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("Cin,N,ks", [(256, 1024, 9), (1024, 256, 1), (512, 512, 5), (80, 512, 5)])
+def test_wgrad_ring_vs_reference(Cin, N, ks):
+    """256x128 ring weight-gradient kernel (auto for N >= 256) vs fp32 torch, incl. row tails."""
+    torch.manual_seed(17)
+    B, L = 5, 301
+    pad = (ks - 1) // 2
+    x = torch.randn(B, L, Cin, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(B, L, N, device=DEV).to(torch.bfloat16)
+    w = torch.zeros(N, Cin, ks, device=DEV, requires_grad=True)
+    y = F.conv1d(x.float().transpose(1, 2), w, None, padding=pad)
+    y.backward(dy.float().transpose(1, 2))
+    dW_ref, db_ref = w.grad, dy.float().sum((0, 1))
+    for variant in (-1, 0, 1):
+        hip.lib().ssamd_wgrad_set_variant(variant)
+        try:
+            dW, db = hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, pad, N, with_bias=True)
+        finally:
+            hip.lib().ssamd_wgrad_set_variant(-1)
+        assert _rel(dW, dW_ref) < 1e-2, variant
+        assert _rel(db, db_ref) < 1e-2, variant

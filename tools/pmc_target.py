@@ -16,6 +16,9 @@ for Cin, N, ks in ((256, 1024, 9), (256, 256, 1)):
     for _ in range(3):
         hip.conv_gemm_raw(x, w, None, B, L, Cin, ks, 1, (ks - 1) // 2, N, 1)
         hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, (ks - 1) // 2, N, with_bias=True)
+        hip.lib().ssamd_wgrad_set_variant(0)  # 128x128 kernels for comparison
+        hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, (ks - 1) // 2, N, with_bias=True)
+        hip.lib().ssamd_wgrad_set_variant(-1)
 qkv = torch.randn(B, L, 768, device=dev).to(torch.bfloat16).requires_grad_(True)
 lens = torch.full((B,), L, device=dev)
 o = hip.attention(qkv, lens, 2)
