@@ -274,6 +274,10 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   char* Qt = Qr + TQ * D * 2;
   char* Dr = Qt + TQ * D * 2;
   char* Dt = Dr + TQ * D * 2;
+  // per-query lse / delta of the current tile, staged with the Q / dO images (the global
+  // loads ride with the tile prefetch instead of stalling the softmax every iteration)
+  float* Ls = reinterpret_cast<float*>(Dt + TQ * D * 2);
+  float* Ds = Ls + TQ;
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int RS = 3 * H * D, OS = H * D;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
@@ -282,6 +286,11 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   const long rowb = cu ? (long)cu[b] : (long)b * L;
   const int Lq = cu ? len : L;
   const int kblk0 = blockIdx.x * (64 * NF);
+  auto load_ld = [&](int q0) -> float {  // thread t < 64: lse of query q0+t; 64 <= t < 128: delta
+    const int qq = q0 + (tid & 63);
+    if (tid >= 128 || qq >= len) return 0.f;
+    return tid < 64 ? lse[(long)bh * L + qq] : delta[(rowb + qq) * H + h];
+  };
   const bf16_t* Qp = qkv + h * D;
   const bf16_t* Kp = qkv + H * D + h * D;
   const bf16_t* Vp = qkv + 2 * H * D + h * D;
@@ -314,9 +323,11 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   // fully masked key block -> zero grads; query rows >= len have zero output -> no contribution
   const int nqt = (kblk0 < len) ? (len + TQ - 1) / TQ : 0;
   short8 rq[D / 32], rd[D / 32];
+  float rld = 0.f;
   if (nqt > 0) {
     load_tile<D>(Qp, rowb, min(TQ, len), RS, rq);
     load_tile<D>(dOp, rowb, min(TQ, len), OS, rd);
+    rld = load_ld(0);
   }
   for (int qt = 0; qt < nqt; ++qt) {
     __syncthreads();
@@ -324,11 +335,13 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
     store_tr_img<D>(Qt, rq);
     store_row_img<D>(Dr, rd);
     store_tr_img<D>(Dt, rd);
+    if (tid < 128) Ls[tid] = rld;  // Ls[0..63] = lse, Ds = Ls + 64 = delta
     __syncthreads();
     if (qt + 1 < nqt) {
       const int q1 = (qt + 1) * TQ;
       load_tile<D>(Qp, rowb + q1, min(TQ, len - q1), RS, rq);
       load_tile<D>(dOp, rowb + q1, min(TQ, len - q1), OS, rd);
+      rld = load_ld(q1);
     }
     float4v sp[NF][4], dp[NF][4];
 #pragma unroll
@@ -351,10 +364,10 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
     for (int qf = 0; qf < 4; ++qf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int qq = qt * TQ + qf * 16 + 4 * g + r;
-        const bool qok = qq < len;
-        const float lq = qok ? lse[(long)bh * L + qq] : 0.f;
-        const float dq = qok ? delta[(rowb + qq) * H + h] : 0.f;
+        const int ql = qf * 16 + 4 * g + r;
+        const bool qok = qt * TQ + ql < len;
+        const float lq = Ls[ql];
+        const float dq = Ds[ql];
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
           float pv = 0.f, ds = 0.f;
@@ -572,7 +585,9 @@ SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const int64
   hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
   ATTN_DISPATCH(D, false, {
     dim3 grid(cdiv(L, 64 * NF), B * H);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), 4 * TQ * DD * 2, s, qkv, lens, cu, dO, lse, delta,
+    static const bool lds_once = (allow_lds(attn_bwd_dkdv_kernel<DD, NF>, 4 * TQ * DD * 2 + 2 * TQ * 4), true);
+    (void)lds_once;
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), 4 * TQ * DD * 2 + 2 * TQ * 4, s, qkv, lens, cu, dO, lse, delta,
                        dqkv, L, H, scale * kLog2e, scale);
     hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), 3 * TK * DD * 2, s, qkv, lens, cu, dO, lse, delta,
                        dqkv, L, H, scale * kLog2e, scale);
