@@ -32,9 +32,22 @@ __device__ __forceinline__ short4v tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
+// D = 128 (256-B rows): ONE swizzle serves both read kinds, so a tensor needs a single LDS
+// image.  16-B chunk c of row r sits at c ^ h(r), h = {0,2,..,14, 9,11,13,15, 1,3,5,7}[r % 16]:
+// the ds_read_b128 lane groups (rows {0-3,12-15} at chunk c, rows 4-11 at c+1, and the
+// mirrored groups) hit 16 distinct slots because h(rows 0-3,12-15) and h(rows 4-11)^1 are
+// disjoint, and the ds_read_b64_tr_b16 half-waves (8 consecutive rows x 4 chunks) because
+// h(r) >> 1 is a permutation of 0..7 on rows 0-7 and on rows 8-15.
+template <int D>
+constexpr bool kUnified = (D == 128);
+__device__ __forceinline__ int uni_h(int row) {
+  const int r = row & 15;
+  return r < 8 ? 2 * r : (2 * r + 9) & 15;
+}
 // [rows][D] bf16 image read by 16-B rows (MFMA A/B "row" fragments)
 template <int D>
 __device__ __forceinline__ int row_off(int row, int c16) {
+  if constexpr (kUnified<D>) return row * 256 + ((c16 ^ uni_h(row)) << 4);
   constexpr int RPB = 256 / (2 * D);  // rows per 256-B bank row
   constexpr int CPR = D / 8;          // 16-B chunks per row
   return row * (2 * D) + ((c16 ^ ((row / RPB) % CPR)) << 4);
@@ -42,6 +55,7 @@ __device__ __forceinline__ int row_off(int row, int c16) {
 // [rows][D] bf16 image read by ds_read_b64_tr_b16 (8-B chunks)
 template <int D>
 __device__ __forceinline__ int tr_off(int row, int c8) {
+  if constexpr (kUnified<D>) return row * 256 + ((c8 ^ (2 * uni_h(row))) << 3);
   constexpr int RPB = 256 / (2 * D);
   constexpr int CPR4 = D / 16;  // (8-B chunks per row) / 4
   return row * (2 * D) + ((c8 ^ (((row / RPB) % CPR4) << 2)) << 3);
@@ -71,6 +85,10 @@ __device__ __forceinline__ void store_row_img(char* img, const short8* regs) {
 }
 template <int D>
 __device__ __forceinline__ void store_tr_img(char* img, const short8* regs) {
+  if constexpr (kUnified<D>) {
+    store_row_img<D>(img, regs);
+    return;
+  }
   constexpr int CPR = D / 8;
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) {
@@ -270,13 +288,14 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
                                                            const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                            int L, int H, float scale_log2, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NIMG = kUnified<D> ? 2 : 4;  // unified swizzle: row and transposed reads share an image
   char* Qr = smem;
-  char* Qt = Qr + TQ * D * 2;
-  char* Dr = Qt + TQ * D * 2;
-  char* Dt = Dr + TQ * D * 2;
+  char* Qt = kUnified<D> ? Qr : Qr + TQ * D * 2;
+  char* Dr = kUnified<D> ? Qr + TQ * D * 2 : Qt + TQ * D * 2;
+  char* Dt = kUnified<D> ? Dr : Dr + TQ * D * 2;
   // per-query lse / delta of the current tile, staged with the Q / dO images (the global
   // loads ride with the tile prefetch instead of stalling the softmax every iteration)
-  float* Ls = reinterpret_cast<float*>(Dt + TQ * D * 2);
+  float* Ls = reinterpret_cast<float*>(smem + NIMG * TQ * D * 2);
   float* Ds = Ls + TQ;
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int RS = 3 * H * D, OS = H * D;
@@ -332,9 +351,9 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   for (int qt = 0; qt < nqt; ++qt) {
     __syncthreads();
     store_row_img<D>(Qr, rq);
-    store_tr_img<D>(Qt, rq);
+    if constexpr (!kUnified<D>) store_tr_img<D>(Qt, rq);
     store_row_img<D>(Dr, rd);
-    store_tr_img<D>(Dt, rd);
+    if constexpr (!kUnified<D>) store_tr_img<D>(Dt, rd);
     if (tid < 128) Ls[tid] = rld;  // Ls[0..63] = lse, Ds = Ls + 64 = delta
     __syncthreads();
     if (qt + 1 < nqt) {
@@ -427,7 +446,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
                                                          int L, int H, float scale_log2, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kr = smem;
-  char* Kt = Kr + TK * D * 2;
+  char* Kt = kUnified<D> ? Kr : Kr + TK * D * 2;
   char* Vr = Kt + TK * D * 2;
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const int RS = 3 * H * D, OS = H * D;
@@ -485,7 +504,7 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
   for (int kt = 0; kt < nkt; ++kt) {
     __syncthreads();
     store_row_img<D>(Kr, rk);
-    store_tr_img<D>(Kt, rk);
+    if constexpr (!kUnified<D>) store_tr_img<D>(Kt, rk);
     store_row_img<D>(Vr, rv);
     __syncthreads();
     if (kt + 1 < nkt) {
@@ -585,11 +604,12 @@ SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const int64
   hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
   ATTN_DISPATCH(D, false, {
     dim3 grid(cdiv(L, 64 * NF), B * H);
-    static const bool lds_once = (allow_lds(attn_bwd_dkdv_kernel<DD, NF>, 4 * TQ * DD * 2 + 2 * TQ * 4), true);
+    constexpr size_t lds_kv = (kUnified<DD> ? 2 : 4) * TQ * DD * 2 + 2 * TQ * 4;
+    static const bool lds_once = (allow_lds(attn_bwd_dkdv_kernel<DD, NF>, lds_kv), true);
     (void)lds_once;
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), 4 * TQ * DD * 2 + 2 * TQ * 4, s, qkv, lens, cu, dO, lse, delta,
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), lds_kv, s, qkv, lens, cu, dO, lse, delta,
                        dqkv, L, H, scale * kLog2e, scale);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), 3 * TK * DD * 2, s, qkv, lens, cu, dO, lse, delta,
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), (kUnified<DD> ? 2 : 3) * TK * DD * 2, s, qkv, lens, cu, dO, lse, delta,
                        dqkv, L, H, scale * kLog2e, scale);
   });
   return (int)hipGetLastError();
