@@ -583,6 +583,30 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
   }
 
 static const float kLog2e = 1.4426950408889634f;
+static int g_nf_kv = 2, g_nf_q = 1;  // measured on MI355X (D=128): dK/dV NF=2, dQ NF=1 -> -14 %
+SSAMD_API void ssamd_attn_set_nf(int nf_kv, int nf_q) {
+  g_nf_kv = nf_kv;
+  g_nf_q = nf_q;
+}
+
+template <int DD, int NF>
+static void launch_dkdv(const bf16_t* qkv, const int64_t* lens, const int64_t* cu, const bf16_t* dO, const float* lse,
+                        const float* delta, bf16_t* dqkv, int B, int L, int H, float scale, hipStream_t s) {
+  dim3 grid(cdiv(L, 64 * NF), B * H);
+  constexpr size_t lds_kv = (kUnified<DD> ? 2 : 4) * TQ * DD * 2 + 2 * TQ * 4;
+  static const bool lds_once = (allow_lds(attn_bwd_dkdv_kernel<DD, NF>, lds_kv), true);
+  (void)lds_once;
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), lds_kv, s, qkv, lens, cu, dO, lse, delta, dqkv, L,
+                     H, scale * kLog2e, scale);
+}
+
+template <int DD, int NF>
+static void launch_dq(const bf16_t* qkv, const int64_t* lens, const int64_t* cu, const bf16_t* dO, const float* lse,
+                      const float* delta, bf16_t* dqkv, int B, int L, int H, float scale, hipStream_t s) {
+  dim3 grid(cdiv(L, 64 * NF), B * H);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), (kUnified<DD> ? 2 : 3) * TK * DD * 2, s, qkv, lens,
+                     cu, dO, lse, delta, dqkv, L, H, scale * kLog2e, scale);
+}
 
 // cu (optional): packed rows, sequence b = rows cu[b] .. cu[b]+lens[b]-1; L = longest sequence.
 SSAMD_API int ssamd_attn_fwd(const bf16_t* qkv, const int64_t* lens, const int64_t* cu, bf16_t* out, float* lse, int B,
@@ -602,15 +626,16 @@ SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const int64
                              int H, int D, float scale, hipStream_t s) {
   if ((long)B * L == 0 || rows == 0) return 0;
   hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
-  ATTN_DISPATCH(D, false, {
-    dim3 grid(cdiv(L, 64 * NF), B * H);
-    constexpr size_t lds_kv = (kUnified<DD> ? 2 : 4) * TQ * DD * 2 + 2 * TQ * 4;
-    static const bool lds_once = (allow_lds(attn_bwd_dkdv_kernel<DD, NF>, lds_kv), true);
-    (void)lds_once;
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DD, NF>), grid, dim3(NT), lds_kv, s, qkv, lens, cu, dO, lse, delta,
-                       dqkv, L, H, scale * kLog2e, scale);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<DD, NF>), grid, dim3(NT), (kUnified<DD> ? 2 : 3) * TK * DD * 2, s, qkv, lens, cu, dO, lse, delta,
-                       dqkv, L, H, scale * kLog2e, scale);
-  });
+  if (D == 128) {  // fragments per wave of the two kernels: runtime-tunable (measured defaults)
+    if (g_nf_kv == 1) launch_dkdv<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+    else launch_dkdv<128, 2>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+    if (g_nf_q == 1) launch_dq<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+    else launch_dq<128, 2>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+  } else {
+    ATTN_DISPATCH(D, false, {
+      launch_dkdv<DD, NF>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+      launch_dq<DD, NF>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+    });
+  }
   return (int)hipGetLastError();
 }

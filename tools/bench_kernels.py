@@ -35,6 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=160000)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only-attn", action="store_true")
     args = ap.parse_args()
     dev = "cuda"
     B = 200
@@ -51,7 +52,7 @@ def main():
         ("postnet (k5 512->512)", 512, 512, 5),
         ("postnet in (k5 80->512)", 80, 512, 5),
     ]
-    for name, Cin, N, ks in shapes:
+    for name, Cin, N, ks in ([] if args.only_attn else shapes):
         x = torch.randn(B, L, Cin, device=dev).to(torch.bfloat16)
         w = torch.randn(N, ks, Cin, device=dev).to(torch.bfloat16)
         bias = torch.randn(N, device=dev)
@@ -109,6 +110,12 @@ def main():
         tb = timeit(lambda: torch.autograd.grad(o, qh, g, retain_graph=True), args.iters)
         row = {"op": f"attention H{H} D{D} L{Lq}", "fwd_ms": round(tf, 3), "fwd_TF": round(fl / tf / 1e9, 1),
                "bwd_ms": round(tb, 3), "bwd_TF": round(2.5 * fl / tb / 1e9, 1)}
+        if D == 128:  # fragments-per-wave of the dK/dV and dQ kernels
+            for nkv, nq in ((1, 1), (1, 2), (2, 2)):
+                hip.lib().ssamd_attn_set_nf(nkv, nq)
+                t2 = timeit(lambda: torch.autograd.grad(o, qh, g, retain_graph=True), args.iters)
+                row[f"bwd_ms_nf{nkv}{nq}"] = round(t2, 3)
+            hip.lib().ssamd_attn_set_nf(2, 1)
         print(json.dumps(row), flush=True)
 
 
