@@ -83,7 +83,8 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restri
   const int wg = xcd_remap(blockIdx.x, nN * nM);
   const int tn = wg % nN, tm = wg / nN;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const float invCin = 1.f / (float)g.Cin;
 
@@ -318,7 +319,8 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
   const int wg = xcd_remap(blockIdx.x, nN * nM);
   const int tn = wg % nN, tm = wg / nN;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const float invCin = 1.f / (float)g.Cin;
 
@@ -458,7 +460,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
   const int wg = xcd_remap(blockIdx.x, nN * nM);
   const int tn = wg % nN, tm = wg / nN;
   const int m0 = tm * BM3, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const float invCin = 1.f / (float)g.Cin;
 
@@ -506,7 +509,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ts = a_t[i] + shift;
-        const bool ok = a_ok[i] && ts >= 0 && ts < a_lim[i];
+        const bool ok = a_ok[i] && (unsigned)ts < (unsigned)a_lim[i];
         glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 8 * 128);
       }
 #pragma unroll
@@ -692,7 +695,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
   const int wg = xcd_remap(blockIdx.x, nN * nM);
   const int tn = wg % nN, tm = wg / nN;
   const int m0 = tm * BG, n0 = tn * BG;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 128 (m) x 64 (n)
   const float invCin = 1.f / (float)g.Cin;
 
@@ -739,7 +743,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int ts = a_t[i] + shift;
-        const bool ok = a_ok[i] && ts >= 0 && ts < a_lim[i];
+        const bool ok = a_ok[i] && (unsigned)ts < (unsigned)a_lim[i];
         glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 1024);
       }
 #pragma unroll
@@ -823,6 +827,150 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
   }
 }
 
+constexpr int STG64_BYTES = 2 * BG * 64 * 2;  // 64 KiB
+
+template <bool OUT_F32, bool FASTK, bool PACKED>
+__global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                               const float* __restrict__ bias,
+                                                               const bf16_t* __restrict__ aux,
+                                                               const bf16_t* __restrict__ resid,
+                                                               const int64_t* __restrict__ lens, void* __restrict__ Yv,
+                                                               ConvGeom g, int act, int ldy) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + BG - 1) / BG;
+  const int nM = (g.M + BG - 1) / BG;
+  const int wg = xcd_remap(blockIdx.x, nN * nM);
+  const int tn = wg % nN, tm = wg / nN;
+  const int m0 = tm * BG, n0 = tn * BG;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 128 (m) x 64 (n)
+  const float invCin = 1.f / (float)g.Cin;
+
+  // DMA: a wave instruction fills 8 rows x 128 B; A and B: 256 rows = 32 instructions = 4 per wave
+  int a_lim[4], a_t[4], a_m[4], achunk[4];
+  const bf16_t* arow_ptr[4];
+  const bf16_t* brow_ptr[4];
+  bool a_ok[4], b_ok[4];
+  int2 rp[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    achunk[i] = (lane & 7) ^ ((row >> 1) & 7);
+    a_m[i] = m0 + row;
+    a_ok[i] = a_m[i] < g.M;
+    if constexpr (PACKED) rp[i] = g.rinfo[a_ok[i] ? a_m[i] : 0];  // both loads issue back to back
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int mm = a_ok[i] ? a_m[i] : 0;
+    if constexpr (PACKED) {
+      a_t[i] = rp[i].x;
+      a_lim[i] = rp[i].y;
+    } else {
+      const int bb = mm / g.L;
+      a_t[i] = mm - bb * g.L;
+      a_lim[i] = g.L;
+    }
+    arow_ptr[i] = X + (long)mm * g.Cin + achunk[i] * 8;
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    const int n = n0 + row;
+    b_ok[i] = n < g.N;
+    brow_ptr[i] = W + (long)(b_ok[i] ? n : 0) * g.K + achunk[i] * 8;  // same row -> same chunk swizzle
+  }
+  auto stage = [&](int kt, int buf) {
+    char* As = smem + buf * STG64_BYTES;
+    char* Bs = As + BG * 64 * 2;
+    const int k0 = kt * 64;
+    if constexpr (FASTK) {  // Cin % 64 == 0: the 64-wide k slab sits in one tap
+      const int tap = k0 / g.Cin;
+      const int cin0 = k0 - tap * g.Cin;
+      const int shift = tap * g.dil - g.pad;
+      const long off = (long)shift * g.Cin + cin0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ts = a_t[i] + shift;
+        const bool ok = a_ok[i] && (unsigned)ts < (unsigned)a_lim[i];
+        glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        glds16(b_ok[i] ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk, Bs + (i * 8 + wave) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + achunk[i] * 8;
+        const void* src = g_zero_chunk;
+        if (a_ok[i] && k < g.K) {
+          const int tap = (int)(((float)k + 0.5f) * invCin);
+          const int cin = k - tap * g.Cin;
+          const int sh = tap * g.dil - g.pad;
+          const int ts = a_t[i] + sh;
+          if (ts >= 0 && ts < a_lim[i]) src = arow_ptr[i] - achunk[i] * 8 + (long)sh * g.Cin + cin;
+        }
+        glds16(src, As + (i * 8 + wave) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + achunk[i] * 8;
+        glds16((b_ok[i] && k < g.K) ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk,
+               Bs + (i * 8 + wave) * 1024);
+      }
+    }
+  };
+
+  float4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + 63) / 64;
+  // double buffer: stage kt+1 is DMA'd while stage kt is computed (one stage = 1024 MFMA cycles
+  // per wave, far longer than an L2-warm LDS-DMA), one barrier per 64-wide k slab
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const char* As = smem + buf * STG64_BYTES;
+    const char* Bs = As + BG * 64 * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      short8 fa[8], fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + j * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    bool valid = true;
+    if (lens) {
+      const int bb = m / g.L, tt = m - bb * g.L;
+      valid = tt < (int)lens[bb];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      epi_store4<OUT_F32>(v, m, n, bias, aux, resid, valid, act, ldy, Yv);
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------
 // Weight gradient.  Tile: 128 (n = cout) x 128 (k = tap*Cin + cin), reduction over
 // rows m in steps of RB = 64.  LDS image per operand: [64 rows][128 cols] bf16,
@@ -854,7 +1002,8 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
   const int n0 = tn * 128, k0 = tk * 128;
   const int r_begin = split * rows_per_split;
   const int r_end = min(g.M, r_begin + rows_per_split);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 1, wk = wave & 1;
   const float invCin = 1.f / (float)g.Cin;
 
@@ -1045,7 +1194,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_ring_kernel(const bf16_t* _
   const int n0 = tn * 256, k0 = tk * 128;
   const int r_begin = split * rows_per_split;
   const int r_end = min(g.M, r_begin + rows_per_split);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 1, wk = wave & 1;
   const float invCin = 1.f / (float)g.Cin;
   int* cu_s = reinterpret_cast<int*>(smem + NSTAGE * WR_STAGE);
@@ -1236,7 +1386,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big_kernel(const bf16_t* __
   const int n0 = tn * 256, k0 = tk * 256;
   const int r_begin = split * rows_per_split;
   const int r_end = min(g.M, r_begin + rows_per_split);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wk = wave & 3;
   const float invCin = 1.f / (float)g.Cin;
   int* cu_s = reinterpret_cast<int*>(smem + NSTG * WB_STAGE);
@@ -1411,7 +1562,8 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
   const int n0 = tn * 128, k0 = tk * 128;
   const int r_begin = split * rows_per_split;
   const int r_end = min(g.M, r_begin + rows_per_split);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 1, wk = wave & 1;
   const float invCin = 1.f / (float)g.Cin;
 
@@ -1639,9 +1791,10 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   const bool reg = (N % 4 == 0) && (ldy % 4 == 0) && !g_force_lds_epilogue;
   const size_t lds_reg = (size_t)2 * 2 * BM * BK * 2;
   int variant = g_gemm_variant;
-  // measured on MI355X (tools/bench_kernels.py): the 256x256 ring wins for N >= 512 (+11..23 %), the
-  // 256x128 ring for N = 256 and whenever K-slabs are tap-aligned, LDS-DMA 128x128 otherwise
-  if (variant < 0) variant = N >= 512 ? 3 : (Cin % BK == 0) ? 2 : 1;
+  // measured on MI355X (tools/bench_kernels.py): the 256x256 tile with a BK=64 double buffer wins for
+  // every N >= 256 shape (+3..15 % over the 256x128 ring, +4..8 % over 256x256 with a BK=32 4-stage ring);
+  // the 256x128 ring for narrower N when K-slabs are tap-aligned, LDS-DMA 128x128 otherwise
+  if (variant < 0) variant = N >= 256 ? 4 : (Cin % BK == 0) ? 2 : 1;
   if (reg && variant == 3 && N >= 256) {
     static bool big_set = false;
     if (!big_set) {
@@ -1669,6 +1822,33 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
       if (fastk) BIG_LAUNCH(false, true); else BIG_LAUNCH(false, false);
     }
 #undef BIG_LAUNCH
+  } else if (reg && variant == 4 && N >= 256) {
+    static bool b64_set = false;
+    if (!b64_set) {
+      allow_lds(conv_gemm_big64_kernel<true, true, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<false, true, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<true, false, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<false, false, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<true, true, true>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<false, true, true>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<true, false, true>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<false, false, true>, 2 * STG64_BYTES);
+      b64_set = true;
+    }
+    const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
+    const bool fastk = (Cin % 64) == 0;
+    const size_t LB = 2 * STG64_BYTES;
+#define B64_LAUNCH(F32, FK)                                                                              \
+    do {                                                                                                 \
+      auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true> : conv_gemm_big64_kernel<F32, FK, false>; \
+      hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy);     \
+    } while (0)
+    if (out_f32) {
+      if (fastk) B64_LAUNCH(true, true); else B64_LAUNCH(true, false);
+    } else {
+      if (fastk) B64_LAUNCH(false, true); else B64_LAUNCH(false, false);
+    }
+#undef B64_LAUNCH
   } else if (reg && variant >= 2) {
     static bool ring_set = false;
     if (!ring_set) {

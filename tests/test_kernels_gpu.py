@@ -318,7 +318,7 @@ def test_bn_dropout_rate():
     assert 0.47 < frac < 0.53
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("Cin,N,ks", [(256, 1024, 9), (80, 512, 5), (1024, 256, 1), (256, 768, 1)])
 def test_conv_gemm_variants(variant, Cin, N, ks):
     """Every GEMM main-loop variant (register staging / LDS-DMA / 256x128 ring / 256x256 ring) vs fp32."""
