@@ -1548,6 +1548,183 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big_kernel(const bf16_t* __
       }
 }
 
+constexpr int WB64_STAGE = 2 * 64 * 512;  // 64 KiB: dY [64][256] + X [64][256]
+
+template <bool PACKED>
+__global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* __restrict__ X,
+                                                                const bf16_t* __restrict__ dY,
+                                                                float* __restrict__ slabs,
+                                                                float* __restrict__ bias_slabs, ConvGeom g,
+                                                                int rows_per_split) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + 255) / 256;
+  const int nK = (g.K + 255) / 256;
+  const int tiles = nN * nK;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % tiles, split = wg / tiles;
+  const int tn = tile / nK, tk = tile % nK;
+  const int n0 = tn * 256, k0 = tk * 256;
+  const int r_begin = split * rows_per_split;
+  const int r_end = min(g.M, r_begin + rows_per_split);
+  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave >> 2, wk = wave & 3;
+  const float invCin = 1.f / (float)g.Cin;
+  int* cu_s = reinterpret_cast<int*>(smem + 2 * WB64_STAGE);
+  if constexpr (PACKED) {
+    for (int i = tid; i <= g.nseq; i += NT3) cu_s[i] = (int)g.cu[i];
+    __syncthreads();
+  }
+
+  float4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  // DMA: a wave instruction = 2 rows of 512 B; each image 32 rows = 16 instructions = 2 per wave
+  int drow[4];
+  const bf16_t* ysrc[4];
+  bool yok[4];
+  int xshift[4], xcin[4];
+  bool xkok[4];
+  int t_cur[4], s0[4], s1[4], sb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 2 * (i * 8 + wave) + (lane >> 5);
+    drow[i] = row;
+    const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
+    const int c16 = (lane & 31) ^ (f >> 1);
+    const int n = n0 + c16 * 8;
+    yok[i] = n < g.N;
+    ysrc[i] = dY + (yok[i] ? n : 0);
+    const int k = k0 + c16 * 8;
+    xkok[i] = k < g.K;
+    const int tap = xkok[i] ? (int)(((float)k + 0.5f) * invCin) : 0;
+    xcin[i] = k - tap * g.Cin;
+    xshift[i] = tap * g.dil - g.pad;
+    const int m = r_begin + row;
+    if constexpr (PACKED) {
+      int lo = 0, hi = g.nseq;
+      while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cu_s[mid] <= m) lo = mid; else hi = mid; }
+      sb[i] = lo;
+      s0[i] = cu_s[lo];
+      s1[i] = cu_s[lo + 1];
+    } else {
+      t_cur[i] = m % g.L;
+    }
+  }
+  auto stage = [&](int r0, int buf) {
+    char* Ys = smem + buf * WB64_STAGE;
+    char* Xs = Ys + 64 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + drow[i];
+      glds16((yok[i] && m < r_end) ? (const void*)(ysrc[i] + (long)m * g.N) : (const void*)g_zero_chunk,
+             Ys + (i * 8 + wave) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + drow[i];
+      int ts, lim;
+      if constexpr (PACKED) {
+        while (m >= s1[i] && sb[i] + 1 < g.nseq) {
+          ++sb[i];
+          s0[i] = s1[i];
+          s1[i] = cu_s[sb[i] + 1];
+        }
+        ts = m - s0[i] + xshift[i];
+        lim = s1[i] - s0[i];
+      } else {
+        ts = t_cur[i] + xshift[i];
+        lim = g.L;
+        int t = t_cur[i] + 64;
+        while (t >= g.L) t -= g.L;
+        t_cur[i] = t;
+      }
+      const bool ok = xkok[i] && m < r_end && ts >= 0 && ts < lim;
+      glds16(ok ? (const void*)(X + (long)(m + xshift[i]) * g.Cin + xcin[i]) : (const void*)g_zero_chunk,
+             Xs + (i * 8 + wave) * 1024);
+    }
+  };
+  const bool do_bias = bias_slabs != nullptr && tk == 0;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int bc16 = tid & 31;
+
+  const int nsteps = (r_end - r_begin + 64 - 1) / 64;
+  if (nsteps > 0) stage(r_begin, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) stage(r_begin + (s + 1) * 64, buf ^ 1);
+    const char* Ys = smem + buf * WB64_STAGE;
+    const char* Xs = Ys + 64 * 512;
+    if (do_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = (tid >> 5) + 16 * j;
+        const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
+        const short8 v = *reinterpret_cast<const short8*>(Ys + row * 512 + ((bc16 ^ (f >> 1)) << 4));
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bsum[t] += bf2f((bf16_t)v[t]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int rbase = kk * 32 + grp * 8 + q;
+      short8 fa[8], fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cb = (wk * 64 + j * 16) / 4 + p;
+        short4v b0 = ds_read_tr_asm(Xs + swz_tr512(rbase, cb));
+        short4v b1 = ds_read_tr_asm(Xs + swz_tr512(rbase + 4, cb));
+        fb[j] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ca = (wn * 128 + i * 16) / 4 + p;
+        short4v a0 = ds_read_tr_asm(Ys + swz_tr512(rbase, ca));
+        short4v a1 = ds_read_tr_asm(Ys + swz_tr512(rbase + 4, ca));
+        fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
+                     "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(smem);  // [16][256]
+#pragma unroll
+    for (int t = 0; t < 8; ++t) red[(tid >> 5) * 256 + bc16 * 8 + t] = bsum[t];
+    __syncthreads();
+    if (tid < 256 && n0 + tid < g.N) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t += red[j * 256 + tid];
+      bias_slabs[(long)split * g.N + n0 + tid] = t;
+    }
+  }
+  float* S = slabs + (long)split * g.N * g.K;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
+        if (n < g.N && k < g.K) S[(long)n * g.K + k] = acc[i][j][r];
+      }
+}
+
 // Register-staged variant (faster at large K = ks*Cin; the LDS-DMA one wins at K <= 1024).
 template <bool PACKED>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
@@ -1902,7 +2079,9 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
 
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.
 // ws: splits*N*ks*Cin (+ splits*N when db != null) floats.  db (optional): fused bias gradient.
-static int g_wgrad_variant = -1;  // -1 auto, 0: 128x128 kernels, 1: 256x128 ring, 2: 256x256 ring
+static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64), 0: 128x128, 1: 256x128 ring, 2: 256x256 BK=32 ring
+static int g_wgrad_blocks = 512;  // split-M target: blocks per launch
+SSAMD_API void ssamd_wgrad_set_blocks(int b) { g_wgrad_blocks = b > 0 ? b : 512; }
 SSAMD_API void ssamd_wgrad_set_variant(int v) { g_wgrad_variant = v; }
 
 SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, float* db,
@@ -1927,6 +2106,31 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   const bool big = ring && g_wgrad_variant != 1 && N >= 256 && g.K >= 256 && (long)N * g.K >= 2L * 256 * 256 &&
                    (!packed || nseq < 8192);
   if (g_wgrad_variant < 0 && !big) ring = false;
+  if (big && g_wgrad_variant != 2) {
+    static bool b64_set = false;
+    if (!b64_set) {
+      allow_lds(conv_wgrad_big64_kernel<false>, 2 * WB64_STAGE + 32768);
+      allow_lds(conv_wgrad_big64_kernel<true>, 2 * WB64_STAGE + 32768);
+      b64_set = true;
+    }
+    const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
+    int splits = (g_wgrad_blocks + tiles - 1) / tiles;
+    const int max_by_rows = (g.M + 8 * 64 - 1) / (8 * 64);  // >= 8 steps per split
+    if (splits > max_by_rows) splits = max_by_rows;
+    if (splits > max_splits) splits = max_splits;
+    if ((long)splits * (slab + N) > ws_floats) splits = (int)(ws_floats / (slab + N));
+    if (splits < 1) return -3;
+    int rows_per_split = (g.M + splits - 1) / splits;
+    rows_per_split = (rows_per_split + 63) / 64 * 64;
+    splits = (g.M + rows_per_split - 1) / rows_per_split;
+    float* bws = db ? ws + (long)splits * slab : nullptr;
+    const size_t lds = 2 * WB64_STAGE + (packed ? (size_t)(nseq + 1) * 4 : 0);
+    auto wb = packed ? conv_wgrad_big64_kernel<true> : conv_wgrad_big64_kernel<false>;
+    hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
+    const int blocks = (int)min((slab + 255) / 256, 8192L);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+    return (int)hipGetLastError();
+  }
   if (big) {
     static bool big_set = false;
     if (!big_set) {

@@ -39,6 +39,7 @@ _SIGS = {
     "ssamd_conv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, P, P, I, P],
     "ssamd_wgrad_set_variant": [I],
     "ssamd_attn_set_nf": [I, I],
+    "ssamd_wgrad_set_blocks": [I],
     "ssamd_colsum": [P, P, L_, I, P],
     "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
     "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],

@@ -536,7 +536,7 @@ def test_wgrad_ring_vs_reference(Cin, N, ks):
     y = F.conv1d(x.float().transpose(1, 2), w, None, padding=pad)
     y.backward(dy.float().transpose(1, 2))
     dW_ref, db_ref = w.grad, dy.float().sum((0, 1))
-    for variant in (-1, 0, 1):
+    for variant in (-1, 0, 1, 2):
         hip.lib().ssamd_wgrad_set_variant(variant)
         try:
             dW, db = hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, pad, N, with_bias=True)

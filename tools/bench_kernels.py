@@ -75,13 +75,19 @@ def main():
         tw_old = timeit(lambda: hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, pad, N, with_bias=True), args.iters)
         hip.lib().ssamd_wgrad_set_variant(1)
         tw_r = timeit(lambda: hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, pad, N, with_bias=True), args.iters)
+        hip.lib().ssamd_wgrad_set_variant(2)
+        tw_32 = timeit(lambda: hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, pad, N, with_bias=True), args.iters)
         hip.lib().ssamd_wgrad_set_variant(-1)
+        hip.lib().ssamd_wgrad_set_blocks(256)
+        tw_256 = timeit(lambda: hip.conv_wgrad_raw(x, dy, B, L, Cin, ks, 1, pad, N, with_bias=True), args.iters)
+        hip.lib().ssamd_wgrad_set_blocks(0)
         row = {"op": name, "fwd_ms": round(t, 3), "fwd_TF": round(flops / t / 1e9, 1),
                "fwd_regstage_TF": round(flops / t_lds / 1e9, 1), "fwd_ring256_TF": round(flops / t_ring / 1e9, 1),
                "fwd_big256x256_TF": round(flops / t_big / 1e9, 1),
                "fwd_big_bk64_TF": round(flops / t_b64 / 1e9, 1), "wgrad_ms": round(tw, 3),
                "wgrad_TF": round(flops / tw / 1e9, 1), "wgrad_128x128_TF": round(flops / tw_old / 1e9, 1),
-               "wgrad_256x128_TF": round(flops / tw_r / 1e9, 1)}
+               "wgrad_256x128_TF": round(flops / tw_r / 1e9, 1), "wgrad_bk32_TF": round(flops / tw_32 / 1e9, 1),
+               "wgrad_256blocks_TF": round(flops / tw_256 / 1e9, 1)}
         if ks > 1:  # packed-sequence geometry (rinfo table), same data
             from speakingstyle_amd.ops.packing import PackInfo
 
