@@ -646,6 +646,7 @@ template <bool OUT_F32>
 __device__ __forceinline__ void epi_store4(float (&v)[4], int m, int n, const float* __restrict__ bias,
                                            const bf16_t* __restrict__ aux, const bf16_t* __restrict__ resid,
                                            bool valid, int act, int ldy, void* __restrict__ Yv) {
+  if (act < 0) return;  // timing experiments only (ssamd_gemm_debug_nostore)
   if (bias) {
     const float4 bv = *reinterpret_cast<const float4*>(bias + n);
     v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
@@ -968,6 +969,183 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       epi_store4<OUT_F32>(v, m, n, bias, aux, resid, valid, act, ldy, Yv);
     }
+  }
+}
+
+
+// ----------------------------------------------------------------------------
+// Persistent 256x256 / BK=64 GEMM: one block per CU walks its tiles (t = blockIdx + i*grid)
+// as ONE flat sequence of k-steps, so the first stage of the next tile is DMA'd while the
+// current tile's last stage is computed and its epilogue stored -- no exposed prologue or
+// epilogue per tile (that was ~40 % of a K = 256 tile's time).  Same LDS layout and
+// per-stage schedule as conv_gemm_big64_kernel.
+// ----------------------------------------------------------------------------
+template <bool OUT_F32, bool FASTK, bool PACKED>
+__global__ void __launch_bounds__(NT3, 1) conv_gemm_pers_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                                const float* __restrict__ bias,
+                                                                const bf16_t* __restrict__ aux,
+                                                                const bf16_t* __restrict__ resid,
+                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
+                                                                ConvGeom g, int act, int ldy) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nN = (g.N + BG - 1) / BG;
+  const int nM = (g.M + BG - 1) / BG;
+  const int ntile = nN * nM;
+  const int G = gridDim.x;
+  const int my_tiles = ((int)blockIdx.x < ntile) ? (ntile - (int)blockIdx.x + G - 1) / G : 0;
+  const int nk = (g.K + 63) / 64;
+  const long total = (long)my_tiles * nk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const float invCin = 1.f / (float)g.Cin;
+
+  // ---- stage-side per-lane state (the tile being DMA'd)
+  int a_lim[4], a_t[4], achunk[4];
+  const bf16_t* arow_ptr[4];
+  const bf16_t* brow_ptr[4];
+  bool a_ok[4], b_ok[4];
+  auto tile_coords = [&](int local, int& m0, int& n0) {
+    const int wg = xcd_remap((int)blockIdx.x + local * G, ntile);
+    m0 = (wg / nN) * BG;
+    n0 = (wg % nN) * BG;
+  };
+  auto setup = [&](int local) {
+    int m0, n0;
+    tile_coords(local, m0, n0);
+    int2 rp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (i * 8 + wave) * 8 + (lane >> 3);
+      achunk[i] = (lane & 7) ^ ((row >> 1) & 7);
+      const int m = m0 + row;
+      a_ok[i] = m < g.M;
+      if constexpr (PACKED) rp[i] = g.rinfo[a_ok[i] ? m : 0];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (i * 8 + wave) * 8 + (lane >> 3);
+      const int mm = a_ok[i] ? m0 + row : 0;
+      if constexpr (PACKED) {
+        a_t[i] = rp[i].x;
+        a_lim[i] = rp[i].y;
+      } else {
+        const int bb = mm / g.L;
+        a_t[i] = mm - bb * g.L;
+        a_lim[i] = g.L;
+      }
+      arow_ptr[i] = X + (long)mm * g.Cin + achunk[i] * 8;
+      const int n = n0 + row;
+      b_ok[i] = n < g.N;
+      brow_ptr[i] = W + (long)(b_ok[i] ? n : 0) * g.K + achunk[i] * 8;
+    }
+  };
+  auto stage = [&](int kt, int buf) {
+    char* As = smem + buf * STG64_BYTES;
+    char* Bs = As + BG * 64 * 2;
+    const int k0 = kt * 64;
+    if constexpr (FASTK) {
+      const int tap = k0 / g.Cin;
+      const int cin0 = k0 - tap * g.Cin;
+      const int shift = tap * g.dil - g.pad;
+      const long off = (long)shift * g.Cin + cin0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ts = a_t[i] + shift;
+        const bool ok = a_ok[i] && (unsigned)ts < (unsigned)a_lim[i];
+        glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        glds16(b_ok[i] ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk, Bs + (i * 8 + wave) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + achunk[i] * 8;
+        const void* src = g_zero_chunk;
+        if (a_ok[i] && k < g.K) {
+          const int tap = (int)(((float)k + 0.5f) * invCin);
+          const int cin = k - tap * g.Cin;
+          const int sh = tap * g.dil - g.pad;
+          const int ts = a_t[i] + sh;
+          if (ts >= 0 && ts < a_lim[i]) src = arow_ptr[i] - achunk[i] * 8 + (long)sh * g.Cin + cin;
+        }
+        glds16(src, As + (i * 8 + wave) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + achunk[i] * 8;
+        glds16((b_ok[i] && k < g.K) ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk,
+               Bs + (i * 8 + wave) * 1024);
+      }
+    }
+  };
+
+  float4v acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  if (total == 0) return;
+  setup(0);
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int kt = 0, local = 0;  // compute-side position
+  for (long gs = 0; gs < total; ++gs) {
+    const int buf = (int)(gs & 1);
+    const bool last_k = kt + 1 == nk;
+    if (gs + 1 < total) {
+      if (last_k) {  // next tile: set up its pointers and start its first stage now
+        setup(local + 1);
+        stage(0, buf ^ 1);
+      } else {
+        stage(kt + 1, buf ^ 1);
+      }
+    }
+    const char* As = smem + buf * STG64_BYTES;
+    const char* Bs = As + BG * 64 * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + (lane >> 4);
+      short8 fa[8], fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + j * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (last_k) {  // epilogue of this tile overlaps the next tile's first DMA
+      int m0, n0;
+      tile_coords(local, m0, n0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+        bool valid = m < g.M;
+        if (valid && lens) {
+          const int bb = m / g.L, tt = m - bb * g.L;
+          valid = tt < (int)lens[bb];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+          if (m < g.M && n < g.N) {
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            epi_store4<OUT_F32>(v, m, n, bias, aux, resid, valid, act, ldy, Yv);
+          }
+          acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      kt = 0;
+      ++local;
+    } else {
+      ++kt;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 }
 
@@ -1934,6 +2112,9 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
 }  // namespace
 
 static bool g_force_lds_epilogue = false;
+static int g_debug_nostore = 0;
+SSAMD_API void ssamd_gemm_debug_nostore(int v) { g_debug_nostore = v; }
+static int g_num_cus = 256;  // persistent grid size (MI355X: 256 CUs); set from the device at first use
 static int g_gemm_variant = -1;  // -1 auto, 0: register staging, 1: LDS-DMA 128x128, 2: LDS-DMA 3-stage ring 256x128
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
@@ -1972,6 +2153,7 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   // every N >= 256 shape (+3..15 % over the 256x128 ring, +4..8 % over 256x256 with a BK=32 4-stage ring);
   // the 256x128 ring for narrower N when K-slabs are tap-aligned, LDS-DMA 128x128 otherwise
   if (variant < 0) variant = N >= 256 ? 4 : (Cin % BK == 0) ? 2 : 1;
+  if (g_debug_nostore && variant >= 3) act = -1;
   if (reg && variant == 3 && N >= 256) {
     static bool big_set = false;
     if (!big_set) {
@@ -1999,6 +2181,41 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
       if (fastk) BIG_LAUNCH(false, true); else BIG_LAUNCH(false, false);
     }
 #undef BIG_LAUNCH
+  } else if (reg && variant == 5 && N >= 256) {
+    static bool pers_set = false;
+    if (!pers_set) {
+      allow_lds(conv_gemm_pers_kernel<true, true, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_pers_kernel<false, true, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_pers_kernel<true, false, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_pers_kernel<false, false, false>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_pers_kernel<true, true, true>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_pers_kernel<false, true, true>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_pers_kernel<true, false, true>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_pers_kernel<false, false, true>, 2 * STG64_BYTES);
+      pers_set = true;
+    }
+    const int ntile = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
+    static const bool cus_once = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+        g_num_cus = n;
+      return true;
+    }();
+    (void)cus_once;
+    const int grid = ntile < g_num_cus ? ntile : g_num_cus;
+    const bool fastk = (Cin % 64) == 0;
+    const size_t LB = 2 * STG64_BYTES;
+#define PERS_LAUNCH(F32, FK)                                                                             \
+    do {                                                                                                 \
+      auto kfn = g.rinfo ? conv_gemm_pers_kernel<F32, FK, true> : conv_gemm_pers_kernel<F32, FK, false>;   \
+      hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy);     \
+    } while (0)
+    if (out_f32) {
+      if (fastk) PERS_LAUNCH(true, true); else PERS_LAUNCH(true, false);
+    } else {
+      if (fastk) PERS_LAUNCH(false, true); else PERS_LAUNCH(false, false);
+    }
+#undef PERS_LAUNCH
   } else if (reg && variant == 4 && N >= 256) {
     static bool b64_set = false;
     if (!b64_set) {

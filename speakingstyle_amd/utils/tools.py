@@ -6,6 +6,12 @@ import torch
 
 
 def pad_1d(inputs, pad_value=0):
+    if pad_value == 0:
+        from .native import pad_rows
+
+        out = pad_rows(inputs)  # native host library (csrc/host_collate.cpp)
+        if out is not None:
+            return out
     max_len = max(len(x) for x in inputs)
     out = np.full((len(inputs), max_len), pad_value, dtype=np.asarray(inputs[0]).dtype)
     for i, x in enumerate(inputs):
@@ -14,6 +20,11 @@ def pad_1d(inputs, pad_value=0):
 
 
 def pad_2d(inputs, max_len=None):
+    from .native import pad_rows
+
+    out = pad_rows(inputs, max_len)  # native host library (csrc/host_collate.cpp)
+    if out is not None:
+        return out
     max_len = max_len or max(x.shape[0] for x in inputs)
     C = inputs[0].shape[1]
     out = np.zeros((len(inputs), max_len, C), dtype=inputs[0].dtype)

@@ -318,7 +318,7 @@ def test_bn_dropout_rate():
     assert 0.47 < frac < 0.53
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("Cin,N,ks", [(256, 1024, 9), (80, 512, 5), (1024, 256, 1), (256, 768, 1)])
 def test_conv_gemm_variants(variant, Cin, N, ks):
     """Every GEMM main-loop variant (register staging / LDS-DMA / 256x128 ring / 256x256 ring) vs fp32."""
@@ -544,3 +544,38 @@ def test_wgrad_ring_vs_reference(Cin, N, ks):
             hip.lib().ssamd_wgrad_set_variant(-1)
         assert _rel(dW, dW_ref) < 1e-2, variant
         assert _rel(db, db_ref) < 1e-2, variant
+
+
+@pytest.mark.parametrize("Cin,N,ks,packed", [(256, 768, 1, False), (256, 1024, 9, True), (1024, 256, 9, False)])
+def test_gemm_persistent_many_tiles(Cin, N, ks, packed):
+    """Persistent GEMM (variant 5) with several tiles per block (M >> 256 * CUs) vs the
+    non-persistent kernel and fp32; packed geometry included."""
+    from speakingstyle_amd.ops.packing import PackInfo, pack
+
+    torch.manual_seed(18)
+    B, L = 40, 2000
+    lens = torch.randint(L // 2, L + 1, (B,), device=DEV)
+    lens[0] = L
+    x = torch.randn(B, L, Cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, ks, Cin, device=DEV) / math.sqrt(ks * Cin)).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    pad = (ks - 1) // 2
+    if packed:
+        pk = PackInfo.build(lens, L, int(lens.sum()))
+        xp = pack(x, pk).contiguous()
+        args = (xp, w, bias, 1, pk.R, Cin, ks, 1, pad, N, 1)
+        kw = {"rinfo": pk.rinfo}
+    else:
+        args = (x, w, bias, B, L, Cin, ks, 1, pad, N, 1)
+        kw = {}
+    outs = []
+    for variant in (5, 4):
+        hip.lib().ssamd_gemm_set_variant(variant)
+        try:
+            outs.append(hip.conv_gemm_raw(*args, **kw))
+        finally:
+            hip.lib().ssamd_gemm_set_variant(-1)
+    torch.testing.assert_close(outs[0].float(), outs[1].float(), rtol=0, atol=0)  # same math, same order
+    if not packed:
+        yr = ref.conv1d(x[:4].float(), w.float().permute(0, 2, 1), bias, pad, 1, "relu")
+        assert _rel(outs[0][:4], yr) < 1e-2

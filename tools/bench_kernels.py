@@ -66,6 +66,8 @@ def main():
         t_big = timeit(lambda: hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, pad, N, 1), args.iters)
         hip.lib().ssamd_gemm_set_variant(4)
         t_b64 = timeit(lambda: hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, pad, N, 1), args.iters)
+        hip.lib().ssamd_gemm_set_variant(5)
+        t_pers = timeit(lambda: hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, pad, N, 1), args.iters)
         hip.lib().ssamd_gemm_set_variant(-1)
         t = timeit(lambda: hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, pad, N, 1), args.iters)
         t_lds = min(t_lds, timeit(lambda: hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, pad, N, 1), 1) * 0 + t_lds)
@@ -84,7 +86,8 @@ def main():
         row = {"op": name, "fwd_ms": round(t, 3), "fwd_TF": round(flops / t / 1e9, 1),
                "fwd_regstage_TF": round(flops / t_lds / 1e9, 1), "fwd_ring256_TF": round(flops / t_ring / 1e9, 1),
                "fwd_big256x256_TF": round(flops / t_big / 1e9, 1),
-               "fwd_big_bk64_TF": round(flops / t_b64 / 1e9, 1), "wgrad_ms": round(tw, 3),
+               "fwd_big_bk64_TF": round(flops / t_b64 / 1e9, 1),
+               "fwd_persistent_TF": round(flops / t_pers / 1e9, 1), "wgrad_ms": round(tw, 3),
                "wgrad_TF": round(flops / tw / 1e9, 1), "wgrad_128x128_TF": round(flops / tw_old / 1e9, 1),
                "wgrad_256x128_TF": round(flops / tw_r / 1e9, 1), "wgrad_bk32_TF": round(flops / tw_32 / 1e9, 1),
                "wgrad_256blocks_TF": round(flops / tw_256 / 1e9, 1)}
