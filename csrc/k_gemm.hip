@@ -829,6 +829,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
 }
 
 constexpr int STG64_BYTES = 2 * BG * 64 * 2;  // 64 KiB
+constexpr int B64_LDS = 256 * 528;          // 2 stages (128 KiB) or the padded bf16 epilogue tile (132 KiB)
 
 template <bool OUT_F32, bool FASTK, bool PACKED>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
@@ -952,6 +953,78 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  }
+  if constexpr (!OUT_F32) {
+    if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
+      // LDS-staged epilogue: the accumulator layout gives each lane 4 columns of one row, i.e.
+      // 32-B row pieces per store instruction (16 rows each); staging the bf16 tile through LDS
+      // (528-B padded rows: conflict-free both ways) turns that into 16-B-per-lane stores of whole
+      // 512-B rows, and the aux / residual operands are read the same coalesced way.
+      // (Measured: the direct register stores cost up to 55 % of a K = 256 GEMM.)
+      constexpr int RSB = 528;
+      char* Ct = smem;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int ml = wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int nl = wn * 64 + j * 16 + 4 * (lane >> 4);
+          const int n = n0 + nl;
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          if (bias && n < g.N) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+          }
+          if (act == ACT_RELU) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+          } else if (act == ACT_LRELU) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+          } else if (act == ACT_TANH) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+          }
+          short4v o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
+          *reinterpret_cast<short4v*>(Ct + ml * RSB + nl * 2) = o;
+        }
+      }
+      __syncthreads();
+      bf16_t* Y = reinterpret_cast<bf16_t*>(Yv);
+      for (int e = tid; e < BG * 32; e += NT3) {
+        const int r = e >> 5, c = e & 31;
+        const int m = m0 + r, n = n0 + c * 8;
+        if (m >= g.M || n >= g.N) continue;
+        short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
+        bool valid = true;
+        if (lens) {
+          const int bb = m / g.L, tt = m - bb * g.L;
+          valid = tt < (int)lens[bb];
+        }
+        const long off = (long)m * ldy + n;
+        if (aux || resid || !valid) {
+          float f[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)v[q]);
+          if (aux) {
+            const short8 a = *reinterpret_cast<const short8*>(aux + off);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)a[q]) > 0.f ? f[q] : 0.f;
+          }
+          if (resid) {
+            const short8 rr = *reinterpret_cast<const short8*>(resid + off);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)rr[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = valid ? (short)f2bf(f[q]) : (short)0;
+        }
+        *reinterpret_cast<short8*>(Y + off) = v;
+      }
+      return;
+    }
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -1891,6 +1964,37 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
     }
   }
   float* S = slabs + (long)split * g.N * g.K;
+  if ((g.K & 3) == 0) {
+    // slab tile through LDS in two 128-row halves (rows padded to 1088 B: the 2 rows x 16 k of a
+    // ds_write_b32 half-wave land on distinct banks): float4 stores of whole 1-KiB rows instead of
+    // 64-B pieces.  The stage buffers and the cu table are dead after the main loop.
+    constexpr int RSF = 1088;
+    char* Ct = smem;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      __syncthreads();
+      if (wn == half) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int nl = i * 16 + (lane >> 4) * 4 + r;
+              const int kl = wk * 64 + j * 16 + (lane & 15);
+              *reinterpret_cast<float*>(Ct + nl * RSF + kl * 4) = acc[i][j][r];
+            }
+      }
+      __syncthreads();
+      for (int e = tid; e < 128 * 64; e += NT3) {
+        const int nl = e >> 6, c4 = e & 63;
+        const int n = n0 + half * 128 + nl, k = k0 + c4 * 4;
+        if (n < g.N && k < g.K)
+          *reinterpret_cast<float4*>(S + (long)n * g.K + k) = *reinterpret_cast<const float4*>(Ct + nl * RSF + c4 * 16);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -2219,19 +2323,19 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   } else if (reg && variant == 4 && N >= 256) {
     static bool b64_set = false;
     if (!b64_set) {
-      allow_lds(conv_gemm_big64_kernel<true, true, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_big64_kernel<false, true, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_big64_kernel<true, false, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_big64_kernel<false, false, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_big64_kernel<true, true, true>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_big64_kernel<false, true, true>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_big64_kernel<true, false, true>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_big64_kernel<false, false, true>, 2 * STG64_BYTES);
+      allow_lds(conv_gemm_big64_kernel<true, true, false>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, false, false>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, false, false>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, false, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
     const bool fastk = (Cin % 64) == 0;
-    const size_t LB = 2 * STG64_BYTES;
+    const size_t LB = B64_LDS;
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true> : conv_gemm_big64_kernel<F32, FK, false>; \
@@ -2326,8 +2430,8 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   if (big && g_wgrad_variant != 2) {
     static bool b64_set = false;
     if (!b64_set) {
-      allow_lds(conv_wgrad_big64_kernel<false>, 2 * WB64_STAGE + 32768);
-      allow_lds(conv_wgrad_big64_kernel<true>, 2 * WB64_STAGE + 32768);
+      allow_lds(conv_wgrad_big64_kernel<false>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true>, 160 * 1024);
       b64_set = true;
     }
     const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
@@ -2341,7 +2445,8 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     rows_per_split = (rows_per_split + 63) / 64 * 64;
     splits = (g.M + rows_per_split - 1) / rows_per_split;
     float* bws = db ? ws + (long)splits * slab : nullptr;
-    const size_t lds = 2 * WB64_STAGE + (packed ? (size_t)(nseq + 1) * 4 : 0);
+    size_t lds = 2 * WB64_STAGE + (packed ? (size_t)(nseq + 1) * 4 : 0);
+    if (lds < 128 * 1088) lds = 128 * 1088;  // the LDS-staged slab epilogue tile
     auto wb = packed ? conv_wgrad_big64_kernel<true> : conv_wgrad_big64_kernel<false>;
     hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);

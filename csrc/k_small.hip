@@ -1,0 +1,177 @@
+// Small-N kernels that are not MFMA-shaped (N = 1 output channel):
+//
+//  * variance-predictor head (reference model/modules.py:247,253-257):
+//    out[r] = (h[r,:] . w + b) masked to 0 at padded rows; one wave per row, fused mask.
+//    Backward: dh = g (x) w (masked), dw = sum_r g h, db = sum_r g -- block-reduced, then
+//    one fp32 atomic per channel per block.
+//  * HiFi-GAN conv_post (K V4/V6, reference hifigan/models.py:145,161-163 +
+//    utils/model.py:105-113): LeakyReLU(0.01) -> Conv1d(C -> 1, k=7, pad 3) -> tanh, and
+//    optionally * max_wav_value -> clamp -> int16, channel-last input read once through an
+//    LDS tile (each input row feeds 7 outputs).
+#include "common.h"
+
+namespace {
+
+constexpr int HEAD_ROWS = 64;  // rows per 256-thread block (16 per wave)
+
+template <int EPL>  // elements per lane: C = 64 * EPL
+__global__ void __launch_bounds__(256) head_fwd_kernel(const bf16_t* __restrict__ h, const float* __restrict__ w,
+                                                       const float* __restrict__ b, const int64_t* __restrict__ lens,
+                                                       long R, int L, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float wv[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) wv[i] = w[lane * EPL + i];
+  const float bias = b ? *b : 0.f;
+  for (int rr = 0; rr < HEAD_ROWS / 4; ++rr) {
+    const long r = (long)blockIdx.x * HEAD_ROWS + rr * 4 + wave;
+    if (r >= R) break;
+    float s = 0.f;
+    const bf16_t* hp = h + r * (64 * EPL) + lane * EPL;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) s += bf2f(hp[i]) * wv[i];
+    s = wave_sum(s);
+    if (lane == 0) {
+      bool valid = true;
+      if (lens) {
+        const long bb = r / L;
+        valid = (r - bb * L) < lens[bb];
+      }
+      out[r] = valid ? s + bias : 0.f;
+    }
+  }
+}
+
+template <int EPL>
+__global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__ g, const bf16_t* __restrict__ h,
+                                                       const float* __restrict__ w, const int64_t* __restrict__ lens,
+                                                       long R, int L, bf16_t* __restrict__ dh, float* __restrict__ dw,
+                                                       float* __restrict__ db) {
+  __shared__ float red[4][64 * EPL + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float wv[EPL], acc[EPL];
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    wv[i] = w[lane * EPL + i];
+    acc[i] = 0.f;
+  }
+  float gsum = 0.f;
+  for (int rr = 0; rr < HEAD_ROWS / 4; ++rr) {
+    const long r = (long)blockIdx.x * HEAD_ROWS + rr * 4 + wave;
+    if (r >= R) break;
+    float gv = g[r];
+    if (lens) {
+      const long bb = r / L;
+      if ((r - bb * L) >= lens[bb]) gv = 0.f;
+    }
+    const bf16_t* hp = h + r * (64 * EPL) + lane * EPL;
+    bf16_t* dp = dh + r * (64 * EPL) + lane * EPL;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) {
+      acc[i] += gv * bf2f(hp[i]);
+      dp[i] = f2bf(gv * wv[i]);
+    }
+    gsum += gv;
+  }
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) red[wave][lane * EPL + i] = acc[i];
+  if (lane == 0) red[wave][64 * EPL] = gsum;
+  __syncthreads();
+  for (int c = threadIdx.x; c <= 64 * EPL; c += 256) {
+    const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    if (c < 64 * EPL) {
+      if (v != 0.f) atomicAdd(dw + c, v);
+    } else if (db && v != 0.f) {
+      atomicAdd(db, v);
+    }
+  }
+}
+
+// conv_post: block = 256 output samples of one utterance; LDS tile of (256 + 6) input rows x C
+constexpr int CP_T = 256;
+
+template <int C>
+__global__ void __launch_bounds__(CP_T) conv_post_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, int T, float slope,
+                                                         float scale, float* __restrict__ outf,
+                                                         int16_t* __restrict__ outi) {
+  __shared__ float xs[(CP_T + 6) * (C + 1)];
+  __shared__ float ws[7 * C];
+  const int bb = blockIdx.y;
+  const int t0 = blockIdx.x * CP_T;
+  const bf16_t* xb = x + (long)bb * T * C;
+  for (int e = threadIdx.x; e < 7 * C; e += CP_T) {  // w[0][c][tap] -> ws[tap][c]
+    const int c = e / 7, tap = e % 7;
+    ws[tap * C + c] = w[e];
+  }
+  for (int e = threadIdx.x; e < (CP_T + 6) * C; e += CP_T) {
+    const int rr = e / C, c = e % C;
+    const int t = t0 - 3 + rr;
+    float v = 0.f;
+    if (t >= 0 && t < T) {
+      v = bf2f(xb[(long)t * C + c]);
+      v = v > 0.f ? v : slope * v;  // fused pre-activation
+    }
+    xs[rr * (C + 1) + c] = v;
+  }
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= T) return;
+  float s = b ? *b : 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 7; ++tap) {
+    const float* xr = xs + (threadIdx.x + tap) * (C + 1);
+    const float* wr = ws + tap * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) s += xr[c] * wr[c];
+  }
+  const float y = tanhf(s);
+  const long o = (long)bb * T + t;
+  if (outi) {
+    float v = y * scale;
+    v = fminf(fmaxf(v, -32768.f), 32767.f);
+    outi[o] = (int16_t)v;
+  } else {
+    outf[o] = y;
+  }
+}
+
+}  // namespace
+
+#define HEAD_DISPATCH(C, ...)                                                     \
+  switch (C) {                                                                    \
+    case 64: { constexpr int EPL = 1; __VA_ARGS__; break; }                      \
+    case 128: { constexpr int EPL = 2; __VA_ARGS__; break; }                     \
+    case 256: { constexpr int EPL = 4; __VA_ARGS__; break; }                     \
+    case 512: { constexpr int EPL = 8; __VA_ARGS__; break; }                     \
+    default: return -1;                                                           \
+  }
+
+SSAMD_API int ssamd_head_fwd(const bf16_t* h, const float* w, const float* b, const int64_t* lens, long R, int L,
+                             int C, float* out, hipStream_t s) {
+  if (R == 0) return 0;
+  HEAD_DISPATCH(C, hipLaunchKernelGGL(head_fwd_kernel<EPL>, dim3(cdiv(R, HEAD_ROWS)), dim3(256), 0, s, h, w, b, lens,
+                                      R, L, out));
+  return (int)hipGetLastError();
+}
+
+// dw / db must be zeroed by the caller (they accumulate)
+SSAMD_API int ssamd_head_bwd(const float* g, const bf16_t* h, const float* w, const int64_t* lens, long R, int L,
+                             int C, bf16_t* dh, float* dw, float* db, hipStream_t s) {
+  if (R == 0) return 0;
+  HEAD_DISPATCH(C, hipLaunchKernelGGL(head_bwd_kernel<EPL>, dim3(cdiv(R, HEAD_ROWS)), dim3(256), 0, s, g, h, w, lens,
+                                      R, L, dh, dw, db));
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_conv_post(const bf16_t* x, const float* w, const float* b, int B, int T, int C, float slope,
+                              float scale, float* outf, int16_t* outi, hipStream_t s) {
+  if ((long)B * T == 0) return 0;
+  dim3 grid(cdiv(T, CP_T), B);
+  switch (C) {
+    case 32: hipLaunchKernelGGL(conv_post_kernel<32>, grid, dim3(CP_T), 0, s, x, w, b, T, slope, scale, outf, outi); break;
+    case 8: hipLaunchKernelGGL(conv_post_kernel<8>, grid, dim3(CP_T), 0, s, x, w, b, T, slope, scale, outf, outi); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}

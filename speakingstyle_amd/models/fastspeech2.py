@@ -148,10 +148,7 @@ class VariancePredictor(nn.Module):
         fp = self.film.pack(style) if (style is not None and hasattr(self, "film")) else None
         h = ops.add_layernorm(h, None, cl.layer_norm_2.weight, cl.layer_norm_2.bias,
                               post_drop=self.dropout, training=self.training, film_params=fp)
-        out = ops.linear(h, self.linear_layer.weight, self.linear_layer.bias).float().squeeze(-1)
-        if lengths is not None:
-            out = out.masked_fill(ops.lengths_to_mask(lengths, out.shape[1]), 0.0)
-        return out
+        return ops.predictor_head(h, self.linear_layer.weight, self.linear_layer.bias, lengths)
 
 
 def _apply_control(pred, control):

@@ -136,8 +136,9 @@ class Generator(nn.Module):
 
     # ------------------------------------------------------------------ inference (channel-last, HIP)
     @torch.no_grad()
-    def infer(self, mel_cl: torch.Tensor) -> torch.Tensor:
-        """mel [B, T, n_mel] (channel-last) -> wav [B, T*hop] in [-1, 1]."""
+    def infer(self, mel_cl: torch.Tensor, int16_scale=None) -> torch.Tensor:
+        """mel [B, T, n_mel] (channel-last) -> wav [B, T*hop] in [-1, 1] (or int16 samples
+        scaled by ``int16_scale``, fused into the conv_post kernel)."""
         x = ops.conv1d(mel_cl, _w(self.conv_pre), self.conv_pre.bias, 3, 1, None)
         for i in range(self.num_upsamples):
             up = self.ups[i]
@@ -147,10 +148,13 @@ class Generator(nn.Module):
                 y = self.resblocks[i * self.num_kernels + j].forward_cl(x)
                 xs = y if xs is None else xs + y
             x = xs * (1.0 / self.num_kernels)
-        x = _lrelu(x, 0.01)
-        w = _w(self.conv_post)  # [1, C, 7]: N=1 output -> VALU path (not MFMA-shaped)
-        y = ref_conv_post(x, w, self.conv_post.bias)
-        return torch.tanh(y).squeeze(-1)
+        w = _w(self.conv_post)  # [1, C, 7]: N = 1 output -> VALU kernel (lrelu + conv + tanh [+ int16] fused)
+        if x.is_cuda and ops.use_hip(x) and x.shape[-1] in (8, 32):
+            return ops._hip().conv_post(x, w, self.conv_post.bias, 0.01, int16_scale)
+        y = torch.tanh(ref_conv_post(_lrelu(x, 0.01), w, self.conv_post.bias)).squeeze(-1)
+        if int16_scale is not None:
+            y = (y * int16_scale).clamp(-32768, 32767).to(torch.int16)
+        return y
 
     def fold_weight_norm(self):
         for m in self.modules():

@@ -131,6 +131,14 @@ def bucketize_embed_add(x, values, bins, table):
     return x + ref.bucketize_embed(values, bins, table).to(x.dtype)
 
 
+def predictor_head(h, w, b, lengths=None):
+    """Variance-predictor head: Linear(C -> 1) -> squeeze -> pad mask-fill (``modules.py:253-257``)."""
+    if use_hip(h):
+        return _hip().predictor_head(h, w, b, lengths)
+    out = ref.linear(h, w, b).float().squeeze(-1)
+    return out if lengths is None else out.masked_fill(ref.lengths_to_mask(lengths, out.shape[1]), 0.0)
+
+
 def bn_act(h, bn, training, act_tanh, p, out_f32=False):
     """PostNet stage: BatchNorm1d (batch stats over all B*L rows) -> [tanh] -> dropout."""
     if use_hip(h):

@@ -40,6 +40,9 @@ _SIGS = {
     "ssamd_wgrad_set_variant": [I],
     "ssamd_attn_set_nf": [I, I],
     "ssamd_wgrad_set_blocks": [I],
+    "ssamd_head_fwd": [P, P, P, P, L_, I, I, P, P],
+    "ssamd_head_bwd": [P, P, P, P, L_, I, I, P, P, P, P],
+    "ssamd_conv_post": [P, P, P, I, I, I, F, F, P, P, P],
     "ssamd_colsum": [P, P, L_, I, P],
     "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
     "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],
@@ -801,3 +804,71 @@ def bn_act(h, bn, training, act_tanh, p, out_f32=False):
         bn.num_batches_tracked.add_(1)
     return _BNActFn.apply(h.to(torch.bfloat16), bn.weight, bn.bias, bn.running_mean, bn.running_var, bool(training),
                           momentum, bn.eps, bool(act_tanh), float(p if training else 0.0), bool(out_f32), _next_seed())
+
+
+# ------------------------------------------------------------------------ N = 1 heads
+class _HeadFn(torch.autograd.Function):
+    """Variance-predictor head Linear(C -> 1) + pad mask (one wave per row)."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, lens):
+        B, L, C = h.shape
+        hc = h.to(torch.bfloat16).contiguous()
+        wf = w.detach().reshape(-1).float().contiguous()
+        bf = None if b is None else b.detach().reshape(-1).float().contiguous()
+        out = torch.empty(B, L, device=h.device, dtype=torch.float32)
+        rc = lib().ssamd_head_fwd(_ptr(hc), _ptr(wf), _ptr(bf), _ptr(lens), B * L, L, C, _ptr(out), _stream())
+        _check(rc, "ssamd_head_fwd")
+        ctx.save_for_backward(hc, wf, lens)
+        ctx.params = (w, b)
+        ctx.hdtype = h.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        hc, wf, lens = ctx.saved_tensors
+        w, b = ctx.params
+        B, L, C = hc.shape
+        g = g.float().contiguous()
+        dh = torch.empty_like(hc)
+        dw = gradslots.claim(w)  # zeroed arena slot, or a fresh zeroed accumulator
+        if dw is None:
+            dw = torch.zeros_like(w, dtype=torch.float32)
+        db = None
+        if b is not None:
+            db = gradslots.claim(b)
+            if db is None:
+                db = torch.zeros_like(b, dtype=torch.float32)
+        rc = lib().ssamd_head_bwd(_ptr(g), _ptr(hc), _ptr(wf), _ptr(lens), B * L, L, C, _ptr(dh), _ptr(dw), _ptr(db),
+                                  _stream())
+        _check(rc, "ssamd_head_bwd")
+        return dh.to(ctx.hdtype), dw, db, None
+
+
+def predictor_head(h, w, b, lengths):
+    """[B, L, C] -> [B, L] fp32 = h @ w^T + b, 0 at padded rows (lengths may be None)."""
+    C = h.shape[-1]
+    if C not in (64, 128, 256, 512) or w.shape[0] != 1:
+        out = ref.linear(h, w, b).float().squeeze(-1)
+        return out if lengths is None else out.masked_fill(ref.lengths_to_mask(lengths, out.shape[1]), 0.0)
+    lens = None if lengths is None else lengths.to(torch.int64).contiguous()
+    return _HeadFn.apply(h, w, b, lens)
+
+
+def conv_post(x, w, b, slope=0.01, int16_scale=None):
+    """HiFi-GAN conv_post (inference): lrelu(slope) -> Conv1d(C->1, k7, pad 3) -> tanh, channel-last
+    x [B, T, C] bf16 -> [B, T] fp32, or int16 (x int16_scale, clamped) when ``int16_scale`` is given."""
+    B, T, C = x.shape
+    xc = x.to(torch.bfloat16).contiguous()
+    wf = w.detach().reshape(-1).float().contiguous()
+    assert wf.numel() == C * 7, "conv_post expects a [1, C, 7] weight"
+    bf = None if b is None else b.detach().reshape(-1).float().contiguous()
+    if int16_scale is None:
+        out = torch.empty(B, T, device=x.device, dtype=torch.float32)
+        rc = lib().ssamd_conv_post(_ptr(xc), _ptr(wf), _ptr(bf), B, T, C, float(slope), 1.0, _ptr(out), None, _stream())
+    else:
+        out = torch.empty(B, T, device=x.device, dtype=torch.int16)
+        rc = lib().ssamd_conv_post(_ptr(xc), _ptr(wf), _ptr(bf), B, T, C, float(slope), float(int16_scale), None,
+                                   _ptr(out), _stream())
+    _check(rc, "ssamd_conv_post")
+    return out

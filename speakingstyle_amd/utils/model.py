@@ -139,13 +139,13 @@ def vocoder_infer(mels, vocoder, model_config, preprocess_config, lengths=None, 
     """mels [B, n_mel, T] (reference layout) or [B, T, n_mel] with ``channel_last``
     -> list of int16 numpy wavs trimmed to ``lengths`` samples (``utils/model.py:97-115``)."""
     x = mels if channel_last else mels.transpose(1, 2)
+    mx = preprocess_config["preprocessing"]["audio"]["max_wav_value"]
     if x.is_cuda:
         x = x.to(torch.bfloat16).contiguous()
-        wavs = vocoder.infer(x).float()
+        wavs = vocoder.infer(x, int16_scale=mx).cpu().numpy()  # int16 written by the conv_post kernel
     else:
         wavs = vocoder(x.transpose(1, 2).float()).squeeze(1)
-    mx = preprocess_config["preprocessing"]["audio"]["max_wav_value"]
-    wavs = (wavs * mx).clamp(-32768, 32767).cpu().numpy().astype(np.int16)
+        wavs = (wavs * mx).clamp(-32768, 32767).cpu().numpy().astype(np.int16)
     out = [w for w in wavs]
     if lengths is not None:
         out = [w[: int(n)] for w, n in zip(out, lengths)]

@@ -579,3 +579,43 @@ def test_gemm_persistent_many_tiles(Cin, N, ks, packed):
     if not packed:
         yr = ref.conv1d(x[:4].float(), w.float().permute(0, 2, 1), bias, pad, 1, "relu")
         assert _rel(outs[0][:4], yr) < 1e-2
+
+
+def test_predictor_head():
+    """Variance-predictor head kernel (Linear C->1 + pad mask) fwd/bwd vs fp32 torch."""
+    torch.manual_seed(19)
+    B, L, C = 5, 77, 256
+    h = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
+    lens = torch.tensor([77, 10, 50, 1, 64], device=DEV)
+    w = torch.nn.Parameter(torch.randn(1, C, device=DEV) * 0.1)
+    b = torch.nn.Parameter(torch.randn(1, device=DEV))
+    hh = h.clone().requires_grad_(True)
+    out = hip.predictor_head(hh, w, b, lens)
+    g = torch.randn(B, L, device=DEV)
+    out.backward(g)
+    gw, gb, gh = w.grad.clone(), b.grad.clone(), hh.grad.clone()
+    w.grad = b.grad = None
+    hr = h.float().requires_grad_(True)
+    mask = ref.lengths_to_mask(lens, L)
+    outr = ref.linear(hr, w, b).squeeze(-1).masked_fill(mask, 0.0)
+    outr.backward(g)
+    assert _rel(out, outr) < 1e-2
+    assert _rel(gh, hr.grad) < 1e-2
+    assert _rel(gw, w.grad) < 1e-2 and _rel(gb, b.grad) < 1e-2
+
+
+@pytest.mark.parametrize("C", [32, 8])
+def test_conv_post(C):
+    """HiFi-GAN conv_post kernel (lrelu -> conv k7 -> tanh [-> int16]) vs fp32 torch."""
+    torch.manual_seed(20)
+    B, T = 3, 1000
+    x = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    w = torch.randn(1, C, 7, device=DEV) * 0.2
+    b = torch.randn(1, device=DEV)
+    y = hip.conv_post(x, w, b, 0.01)
+    xr = F.leaky_relu(x.float(), 0.01).transpose(1, 2)
+    yr = torch.tanh(F.conv1d(xr, w, b, padding=3)).squeeze(1)
+    assert (y - yr).abs().max().item() < 2e-3
+    yi = hip.conv_post(x, w, b, 0.01, int16_scale=32768.0)
+    yri = (yr * 32768.0).clamp(-32768, 32767)
+    assert yi.dtype == torch.int16 and (yi.float() - yri).abs().max().item() <= 70
