@@ -94,14 +94,15 @@ class MultiHeadAttention(nn.Module):
         return [[self.w_qs.weight, self.w_ks.weight, self.w_vs.weight], [self.w_qs.bias, self.w_ks.bias, self.w_vs.bias]]
 
     def forward(self, x, lengths, pack=None):
-        qkv = ops.linear_group(x, (self.w_qs.weight, self.w_ks.weight, self.w_vs.weight),
-                               (self.w_qs.bias, self.w_ks.bias, self.w_vs.bias))
+        ws = (self.w_qs.weight, self.w_ks.weight, self.w_vs.weight)
+        mb = ops.residual_mailbox(x, ws)  # d(residual x) joins the QKV data gradient in its epilogue
+        qkv = ops.linear_group(x, ws, (self.w_qs.bias, self.w_ks.bias, self.w_vs.bias), mailbox=mb)
         o = ops.attention(qkv, lengths, self.n_head, pack)
         a = ops.linear(o, self.fc.weight, self.fc.bias)
         # LN(dropout(fc(o)) + x), then the FFT block's pad mask-fill (Layers.py:27-28)
         return ops.add_layernorm(
             a, x, self.layer_norm.weight, self.layer_norm.bias,
-            pre_drop=self.dropout, training=self.training, lengths=lengths, pack=pack,
+            pre_drop=self.dropout, training=self.training, lengths=lengths, pack=pack, mailbox=mb,
         )
 
 
@@ -117,10 +118,12 @@ class PositionwiseFeedForward(nn.Module):
         self.k = tuple(kernel_size)
 
     def forward(self, x, lengths, film_params=None, pack=None):
-        z = ops.ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias, pack)
+        mb = ops.residual_mailbox(x)  # d(residual x) joins the first conv's data gradient
+        z = ops.ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias, pack, mailbox=mb)
         return ops.add_layernorm(
             z, x, self.layer_norm.weight, self.layer_norm.bias,
             pre_drop=self.dropout, training=self.training, film_params=film_params, lengths=lengths, pack=pack,
+            mailbox=mb,
         )
 
 

@@ -19,6 +19,7 @@ from . import reference as ref
 from .packing import PackInfo, pack as pack_rows, unpack as unpack_rows  # noqa: F401
 
 _FORCED = os.environ.get("SSAMD_BACKEND")  # "reference" | "hip" | None
+_NO_MAILBOX = os.environ.get("SSAMD_NO_MAILBOX") == "1"  # A/B switch for the residual-gradient fusion
 
 
 def set_backend(name: Optional[str]):
@@ -53,14 +54,25 @@ def linear(x, w, b=None, act=None):
     return ref.linear(x, w, b, act)
 
 
-def linear_group(x, weights, biases):
+def residual_mailbox(x, weights=None):
+    """A GradMailbox for a sub-layer whose input x is also its LayerNorm residual (HIP path
+    only; None otherwise): the residual gradient is added inside the first GEMM's backward."""
+    if not use_hip(x) or x.dtype != torch.bfloat16 or not x.requires_grad or _NO_MAILBOX:
+        return None
+    hip = _hip()
+    if weights is not None and hip.gradslots.fused_data(list(weights)) is None:
+        return None
+    return hip.GradMailbox()
+
+
+def linear_group(x, weights, biases, mailbox=None):
     """y = x @ cat(weights)^T + cat(biases): one GEMM for several projections (Q/K/V).
 
     On the HIP path, when the group is contiguous in the flat arena, the fused
     weight is a view (no concatenation) and its gradient is written in place.
     """
     if use_hip(x):
-        return _hip().linear_group(x, weights, biases)
+        return _hip().linear_group(x, weights, biases, mailbox)
     return ref.linear(x, torch.cat(list(weights), 0), torch.cat(list(biases), 0))
 
 
@@ -70,12 +82,12 @@ def conv1d(x, w, b=None, pad=0, dil=1, act=None):
     return ref.conv1d(x, w, b, pad, dil, act)
 
 
-def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None):
+def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None, mailbox=None):
     """Position-wise FFN core: conv(k0) -> ReLU -> conv(k1) (``SubLayers.py:84-87``).
 
     ``pack``: x is packed ``[1, R, C]``; the convs zero-pad at every sequence end."""
     if use_hip(x):
-        return _hip().ffn(x, w1, b1, w2, b2, pack)
+        return _hip().ffn(x, w1, b1, w2, b2, pack, mailbox)
     if pack is not None:
         return pack_rows(ffn(unpack_rows(x, pack), w1, b1, w2, b2), pack)
     h = ref.conv1d(x, w1, b1, (w1.shape[2] - 1) // 2, 1, "relu")
@@ -90,9 +102,9 @@ def attention(qkv, lengths, n_head, pack: Optional[PackInfo] = None):
     return ref.attention(qkv, lengths, n_head)
 
 
-def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, **kw):
+def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, mailbox=None, **kw):
     if use_hip(a):
-        return _hip().add_layernorm(a, residual, ln_w, ln_b, pack=pack, **kw)
+        return _hip().add_layernorm(a, residual, ln_w, ln_b, pack=pack, mailbox=mailbox, **kw)
     if pack is not None:
         kw["lengths"] = pack.lens
         res = None if residual is None else unpack_rows(residual, pack)

@@ -355,18 +355,50 @@ def linear(x, w, b=None, act=None, out_f32=False):
     return y.reshape(*shp[:-1], w.shape[0])
 
 
+class GradMailbox:
+    """Hands the residual-branch gradient of a sub-layer input to the GEMM that consumes the same
+    input: ``add_layernorm(..., residual=x, mailbox=mb)`` puts d(residual) here instead of
+    returning it, and the first GEMM of the sub-layer (``linear_group`` / ``ffn`` on x, whose
+    backward runs later) adds it in its data-gradient epilogue (``resid``).  Autograd then sees
+    one gradient for x: no separate bf16 accumulation kernel per sub-layer."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def put(self, g):
+        self.grad = g if self.grad is None else self.grad + g
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
+def _resid_for(mailbox, like):
+    if mailbox is None:
+        return None
+    g = mailbox.take()
+    if g is None:
+        return None
+    g = g.to(torch.bfloat16).contiguous()
+    assert g.shape == like.shape, "mailbox gradient shape mismatch"
+    return g
+
+
 class _GroupLinearFn(torch.autograd.Function):
     """One GEMM for several Linear layers whose weights / biases are contiguous in the
     arena: ``wf`` / ``bf`` are the fused data views; the member parameters are inputs
     only so autograd routes each one its slice of the (in-place written) gradient."""
 
     @staticmethod
-    def forward(ctx, x, wf, bf, n, *params):
+    def forward(ctx, x, wf, bf, n, mailbox, *params):
         ws, bs = params[:n], params[n:]
         B, L, Cin = x.shape
         N = wf.shape[0]
         xc = x.contiguous()
         y = conv_gemm_raw(xc, weight_fwd(wf, owner=ws[0]), bf, B, L, Cin, 1, 1, 0, N, 0)
+        ctx.mailbox = mailbox
         ctx.save_for_backward(xc, wf)
         ctx.members = (ws, bs)
         ctx.dims = (B, L, Cin, N)
@@ -378,23 +410,26 @@ class _GroupLinearFn(torch.autograd.Function):
         ws, bs = ctx.members
         B, L, Cin, N = ctx.dims
         dy = dy.to(torch.bfloat16).contiguous()
-        dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin)
+        dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin,
+                           resid=_resid_for(ctx.mailbox, xc))
         sw, sb = gradslots.claim_fused(ws), gradslots.claim_fused(bs)
         dw, db = conv_wgrad_raw(xc, dy, B, L, Cin, 1, 1, 0, N, with_bias=True,
                                 dW=None if sw is None else sw.view(N, Cin, 1), db=sb)
         dw = dw.view(N, Cin)
-        return (dx, None, None, None, *gradslots.split_rows(dw, ws), *gradslots.split_rows(db, bs))
+        return (dx, None, None, None, None, *gradslots.split_rows(dw, ws), *gradslots.split_rows(db, bs))
 
 
-def linear_group(x, weights, biases):
+def linear_group(x, weights, biases, mailbox=None):
     weights, biases = list(weights), list(biases)
     wf, bf = gradslots.fused_data(weights), gradslots.fused_data(biases)
     if wf is None or bf is None:
+        if mailbox is not None:
+            raise ValueError("residual mailbox needs the fused (arena) projection path")
         w, b = torch.cat(weights, 0), torch.cat(biases, 0)
         return linear(x, w, b)
     shp = x.shape
     x3 = x.reshape(1, -1, shp[-1]) if x.dim() != 3 else x
-    y = _GroupLinearFn.apply(x3, wf, bf, len(weights), *weights, *biases)
+    y = _GroupLinearFn.apply(x3, wf, bf, len(weights), mailbox, *weights, *biases)
     return y.reshape(*shp[:-1], wf.shape[0])
 
 
@@ -403,8 +438,9 @@ class _FFNFn(torch.autograd.Function):
     data-gradient epilogue of the second conv (aux = h), so no extra pass."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, rinfo):
+    def forward(ctx, x, w1, b1, w2, b2, rinfo, mailbox):
         B, L, C = x.shape
+        ctx.mailbox = mailbox
         k1, k2 = w1.shape[2], w2.shape[2]
         H = w1.shape[0]
         xc = x.contiguous()
@@ -431,16 +467,17 @@ class _FFNFn(torch.autograd.Function):
         dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
         dw2, db2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=gradslots.claim(w2),
                                   db=gradslots.claim(b2), rinfo=r2, cu=ctx.cu[1])
-        dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1)
+        dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1,
+                           resid=_resid_for(ctx.mailbox, xc))
         dw1, db1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=gradslots.claim(w1),
                                   db=gradslots.claim(b1), rinfo=r1, cu=ctx.cu[0])
-        return dx, dw1, db1, dw2, db2, None
+        return dx, dw1, db1, dw2, db2, None, None
 
 
-def ffn(x, w1, b1, w2, b2, pack=None):
+def ffn(x, w1, b1, w2, b2, pack=None, mailbox=None):
     if pack is not None:
         assert x.shape[0] == 1 and x.shape[1] == pack.R, "packed FFN expects [1, R, C]"
-    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu))
+    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu), mailbox)
 
 
 # ------------------------------------------------------------------------ add + LayerNorm
@@ -458,7 +495,7 @@ def set_seed(s: int):
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom):
+    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox):
         B, L, C = a.shape if geom is None else geom  # packed: (sequences, longest, C) over [1, R, C] rows
         ac = a.contiguous()
         rc_ = None if res is None else res.contiguous()
@@ -472,6 +509,7 @@ class _AddLNFn(torch.autograd.Function):
                                    seed, eps, _stream())
         _check(rc, "ssamd_addln_fwd")
         ctx.cu = cu
+        ctx.mailbox = mailbox
         ctx.save_for_backward(ac, rc_, w, b, gf, bf, sg, sb, lens, mean, rstd)
         ctx.cfg = (B, L, C, pre_p, post_p, seed, res is not None, g is not None)
         ctx.gdtype = None if g is None else (g.dtype, bt.dtype)
@@ -497,17 +535,20 @@ class _AddLNFn(torch.autograd.Function):
         _check(rc, "ssamd_addln_bwd")
         d_a = da if da is not None else dh
         d_res = dh if has_res else None
+        if d_res is not None and ctx.mailbox is not None:  # the consumer GEMM adds it (GradMailbox)
+            ctx.mailbox.put(d_res)
+            d_res = None
         dg = dbt = dsg = dsb = None
         if has_film:
             dg = (S1 * sg).to(ctx.gdtype[0])
             dbt = (S2 * sb).to(ctx.gdtype[1])
             dsg = (S1 * gf).sum().reshape(1)
             dsb = (S2 * bf).sum().reshape(1)
-        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None
+        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None
 
 
 def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None,
-                  lengths=None, eps=1e-5, pack=None):
+                  lengths=None, eps=1e-5, pack=None, mailbox=None):
     C = a.shape[-1]
     if C not in (256, 512, 1024) or a.dtype != torch.bfloat16:
         if pack is not None:
@@ -528,7 +569,7 @@ def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, train
     if residual is not None:
         residual = residual.to(a.dtype)
     out = _AddLNFn.apply(a, residual, ln_w, ln_b, g, bt, sg, sb, lens, float(pre_drop), float(post_drop),
-                         _next_seed(), float(eps), cu, geom)
+                         _next_seed(), float(eps), cu, geom, mailbox)
     return out
 
 
