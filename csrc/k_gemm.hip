@@ -2185,7 +2185,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   const long total4 = total / 4;
   for (long e4 = blockIdx.x * (long)blockDim.x + threadIdx.x; e4 < total4; e4 += (long)gridDim.x * blockDim.x) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp = 0; sp < splits; ++sp) {
+#pragma unroll 8
+    for (int sp = 0; sp < splits; ++sp) {  // unrolled: 8 independent slab loads in flight
       const float4 v = reinterpret_cast<const float4*>(slabs + (long)sp * total)[e4];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
@@ -2199,6 +2200,42 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     dst[2 * ks] = acc.z;
     dst[3 * ks] = acc.w;
   }
+}
+
+// ks > 1: one block per output row n; slab row read coalesced (float4 over k = tap*Cin + cin),
+// summed over splits, transposed through LDS to the [cin][tap] order of dW, written contiguously.
+__global__ void __launch_bounds__(256) wgrad_reduce_rows_kernel(const float* __restrict__ slabs,
+                                                                float* __restrict__ dW,
+                                                                const float* __restrict__ bslabs,
+                                                                float* __restrict__ db, int splits, int N, int Cin,
+                                                                int ks) {
+  extern __shared__ float row[];
+  const int n = blockIdx.x;
+  const int K = Cin * ks;
+  const long total = (long)N * K;
+  const float* src = slabs + (long)n * K;
+  for (int k4 = threadIdx.x; k4 < K / 4; k4 += 256) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4 v = reinterpret_cast<const float4*>(src + (long)sp * total)[k4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    const int k = k4 * 4;
+    const int tap = k / Cin, cin = k - tap * Cin;  // the 4 k share a tap (Cin % 4 == 0)
+    row[(cin + 0) * ks + tap] = acc.x;
+    row[(cin + 1) * ks + tap] = acc.y;
+    row[(cin + 2) * ks + tap] = acc.z;
+    row[(cin + 3) * ks + tap] = acc.w;
+  }
+  if (bslabs && threadIdx.x == 0) {
+    float sb = 0.f;
+    for (int sp = 0; sp < splits; ++sp) sb += bslabs[(long)sp * N + n];
+    db[n] = sb;
+  }
+  __syncthreads();
+  float* dst = dW + (long)n * K;
+  for (int k = threadIdx.x; k < K; k += 256) dst[k] = row[k];
 }
 
 // db[n] = sum_m dY[m, n]  (column sums; fp32 atomics after block reduction)
@@ -2400,6 +2437,15 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
 
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.
 // ws: splits*N*ks*Cin (+ splits*N when db != null) floats.  db (optional): fused bias gradient.
+static void launch_reduce(const float* ws, float* dW, const float* bws, float* db, int splits, int N, int Cin, int ks,
+                          int blocks, hipStream_t s) {
+  const int K = Cin * ks;
+  if (ks > 1 && (size_t)K * 4 <= 65536)  // transposed through LDS: contiguous dW rows
+    hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(N), dim3(256), (size_t)K * 4, s, ws, dW, bws, db, splits, N, Cin, ks);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+}
+
 static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64), 0: 128x128, 1: 256x128 ring, 2: 256x256 BK=32 ring
 static int g_wgrad_blocks = 512;  // split-M target: blocks per launch
 SSAMD_API void ssamd_wgrad_set_blocks(int b) { g_wgrad_blocks = b > 0 ? b : 512; }
@@ -2450,7 +2496,7 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     auto wb = packed ? conv_wgrad_big64_kernel<true> : conv_wgrad_big64_kernel<false>;
     hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+    launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);
     return (int)hipGetLastError();
   }
   if (big) {
@@ -2475,7 +2521,7 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     auto wb = packed ? conv_wgrad_big_kernel<true> : conv_wgrad_big_kernel<false>;
     hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+    launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);
     return (int)hipGetLastError();
   }
   if (ring) {
@@ -2500,7 +2546,7 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     auto wr = packed ? conv_wgrad_ring_kernel<true> : conv_wgrad_ring_kernel<false>;
     hipLaunchKernelGGL(wr, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+    launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);
     return (int)hipGetLastError();
   }
   const int tiles = ((N + 127) / 128) * ((g.K + 127) / 128);
@@ -2524,7 +2570,7 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
                        rows_per_split);
   const long total = slab;
   int blocks = (int)min((total + 255) / 256, 8192L);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+  launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);
   return (int)hipGetLastError();
 }
 
