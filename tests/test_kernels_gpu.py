@@ -619,3 +619,23 @@ def test_conv_post(C):
     yi = hip.conv_post(x, w, b, 0.01, int16_scale=32768.0)
     yri = (yr * 32768.0).clamp(-32768, 32767)
     assert yi.dtype == torch.int16 and (yi.float() - yri).abs().max().item() <= 70
+
+
+@pytest.mark.parametrize("dma,nf", [(0, 1), (1, 1), (1, 2)])
+def test_attention_fwd_variants(dma, nf):
+    """D=128 forward: register-staged and LDS-DMA kernels (NF 1/2) vs fp32, padded and packed."""
+    from speakingstyle_amd.ops.packing import pack, unpack
+
+    torch.manual_seed(21)
+    H, D = 2, 128
+    pk, lens, M = _pack_case()
+    qkv = torch.randn(pk.B, M, 3 * H * D, device=DEV).to(torch.bfloat16)
+    hip.lib().ssamd_attn_set_fwd(dma, nf)
+    try:
+        o = hip.attention(qkv, lens, H)
+        op = hip.attention(pack(qkv, pk).contiguous(), None, H, pk)
+    finally:
+        hip.lib().ssamd_attn_set_fwd(1, 2)
+    orr = ref.attention(qkv.float(), lens, H)
+    assert _rel(o, orr) < 1e-2
+    assert _rel(unpack(op, pk), orr) < 1e-2

@@ -122,6 +122,11 @@ def main():
         tb = timeit(lambda: torch.autograd.grad(o, qh, g, retain_graph=True), args.iters)
         row = {"op": f"attention H{H} D{D} L{Lq}", "fwd_ms": round(tf, 3), "fwd_TF": round(fl / tf / 1e9, 1),
                "bwd_ms": round(tb, 3), "bwd_TF": round(2.5 * fl / tb / 1e9, 1)}
+        if D == 128:  # forward variants: register-staged (NF=1) / LDS-DMA NF=1 / NF=2
+            for dma, nf in ((0, 1), (1, 1), (1, 2)):
+                hip.lib().ssamd_attn_set_fwd(dma, nf)
+                row[f"fwd_ms_dma{dma}_nf{nf}"] = round(timeit(lambda: hip.attention(qh, lens, H), args.iters), 3)
+            hip.lib().ssamd_attn_set_fwd(1, 2)
         if D == 128:  # fragments-per-wave of the dK/dV and dQ kernels
             for nkv, nq in ((1, 1), (1, 2), (2, 2)):
                 hip.lib().ssamd_attn_set_nf(nkv, nq)
