@@ -598,6 +598,176 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   }
 }
 
+template <int NF, int MINB>
+__global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv_dma_kernel(const bf16_t* __restrict__ qkv,
+                                                           const int64_t* __restrict__ lens,
+                                                           const int64_t* __restrict__ cu,
+                                                           const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                           int L, int H, float scale_log2, float scale) {
+  constexpr int D = 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // per buffer: Q image, dO image (unified swizzle, DMA'd), lse[64], delta[64]
+  constexpr int BUFB = 2 * TQ * D * 2 + 2 * TQ * 4;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int RS = 3 * H * D, OS = H * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
+  const int len = (int)lens[b];
+  // packed variable-length rows (cu = row offsets): only rows < len exist for sequence b
+  const long rowb = cu ? (long)cu[b] : (long)b * L;
+  const int Lq = cu ? len : L;
+  const int kblk0 = blockIdx.x * (64 * NF);
+  auto load_ld = [&](int q0) -> float {  // thread t < 64: lse of query q0+t; 64 <= t < 128: delta
+    const int qq = q0 + (tid & 63);
+    if (tid >= 128 || qq >= len) return 0.f;
+    return tid < 64 ? lse[(long)bh * L + qq] : delta[(rowb + qq) * H + h];
+  };
+  const bf16_t* Qp = qkv + h * D;
+  const bf16_t* Kp = qkv + H * D + h * D;
+  const bf16_t* Vp = qkv + 2 * H * D + h * D;
+  const bf16_t* dOp = dO + h * D;
+
+  int keyv[NF];
+  bool kval[NF];
+  short8 kb[NF][D / 32], vb[NF][D / 32];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    keyv[f] = kblk0 + wave * (16 * NF) + f * 16 + (lane & 15);
+    kval[f] = keyv[f] < len;
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      short8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (keyv[f] < Lq) {
+        kv = *reinterpret_cast<const short8*>(Kp + (rowb + keyv[f]) * RS + s * 32 + 8 * g);
+        vv = *reinterpret_cast<const short8*>(Vp + (rowb + keyv[f]) * RS + s * 32 + 8 * g);
+      }
+      kb[f][s] = kv;
+      vb[f][s] = vv;
+    }
+  }
+  float4v dk[NF][D / 16], dv[NF][D / 16];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dk[f][i] = dv[f][i] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  // fully masked key block -> zero grads; query rows >= len have zero output -> no contribution
+  const int nqt = (kblk0 < len) ? (len + TQ - 1) / TQ : 0;
+  auto issue = [&](int q0, int buf) {
+    char* Qd = smem + buf * BUFB;
+    char* Dd = Qd + TQ * D * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (i * 4 + wave) * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ uni_h(row);
+      const int qq = q0 + row;
+      const bool ok = qq < len;
+      a_glds16(ok ? (const void*)(Qp + (rowb + qq) * (long)RS + c * 8) : (const void*)a_zero_chunk,
+               Qd + (i * 4 + wave) * 1024);
+      a_glds16(ok ? (const void*)(dOp + (rowb + qq) * (long)OS + c * 8) : (const void*)a_zero_chunk,
+               Dd + (i * 4 + wave) * 1024);
+    }
+  };
+  auto stash_ld = [&](int buf, float v) {
+    if (tid < 128) reinterpret_cast<float*>(smem + buf * BUFB + 2 * TQ * D * 2)[tid] = v;
+  };
+  if (nqt > 0) {
+    issue(0, 0);
+    stash_ld(0, load_ld(0));
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int buf = qt & 1;
+    float rld = 0.f;
+    if (qt + 1 < nqt) {
+      issue((qt + 1) * TQ, buf ^ 1);
+      rld = load_ld((qt + 1) * TQ);
+    }
+    const char* Qr = smem + buf * BUFB;
+    const char* Dr = Qr + TQ * D * 2;
+    const char* Qt = Qr;  // unified swizzle: transposed reads from the same images
+    const char* Dt = Dr;
+    const float* Ls = reinterpret_cast<const float*>(Qr + 2 * TQ * D * 2);
+    const float* Ds = Ls + TQ;
+    float4v sp[NF][4], dp[NF][4];
+#pragma unroll
+    for (int qf = 0; qf < 4; ++qf) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) sp[f][qf] = dp[f][qf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) {
+        const short8 aq = *reinterpret_cast<const short8*>(Qr + row_off<D>(qf * 16 + (lane & 15), s * 4 + g));
+        const short8 ad = *reinterpret_cast<const short8*>(Dr + row_off<D>(qf * 16 + (lane & 15), s * 4 + g));
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          sp[f][qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, kb[f][s], sp[f][qf], 0, 0, 0);
+          dp[f][qf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad, vb[f][s], dp[f][qf], 0, 0, 0);
+        }
+      }
+    }
+    // P = exp2(S*c - lse2[q]); dS = P * (dP - delta[q]); rows = queries qt*64 + qf*16 + 4g + r
+#pragma unroll
+    for (int qf = 0; qf < 4; ++qf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = qf * 16 + 4 * g + r;
+        const bool qok = qt * TQ + ql < len;
+        const float lq = Ls[ql];
+        const float dq = Ds[ql];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          float pv = 0.f, ds = 0.f;
+          if (qok && kval[f]) {
+            pv = exp2f(sp[f][qf][r] * scale_log2 - lq);
+            ds = pv * (dp[f][qf][r] - dq);
+          }
+          sp[f][qf][r] = pv;
+          dp[f][qf][r] = ds;
+        }
+      }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      short8 pb[NF], sb[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        pb[f] = pack8(sp[f][2 * hh], sp[f][2 * hh + 1]);
+        sb[f] = pack8(dp[f][2 * hh], dp[f][2 * hh + 1]);
+      }
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) {
+        const short8 ado = tr_frag<D>(Dt, hh * 32, df * 16, lane);
+        const short8 aq = tr_frag<D>(Qt, hh * 32, df * 16, lane);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          dv[f][df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ado, pb[f], dv[f][df], 0, 0, 0);
+          dk[f][df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq, sb[f], dk[f][df], 0, 0, 0);
+        }
+      }
+    }
+    if (qt + 1 < nqt) stash_ld(buf ^ 1, rld);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    if (keyv[f] >= Lq) continue;
+    bf16_t* dkp = dqkv + (rowb + keyv[f]) * RS + H * D + h * D;
+    bf16_t* dvp = dqkv + (rowb + keyv[f]) * RS + 2 * H * D + h * D;
+#pragma unroll
+    for (int df = 0; df < D / 16; ++df) {
+      short4v a, c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = (short)f2bf(dk[f][df][r] * scale);
+        c[r] = (short)f2bf(dv[f][df][r]);
+      }
+      *reinterpret_cast<short4v*>(dkp + df * 16 + 4 * g) = a;
+      *reinterpret_cast<short4v*>(dvp + df * 16 + 4 * g) = c;
+    }
+  }
+}
+
 // NF = query fragments per wave; block = 4 waves x 16*NF queries
 template <int D, int NF>
 __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
@@ -749,7 +919,9 @@ SSAMD_API void ssamd_attn_set_fwd(int dma, int nf) {
   g_fwd_dma = dma;
   g_fwd_nf = nf;
 }
-static int g_nf_kv = 2, g_nf_q = 1;  // measured on MI355X (D=128): dK/dV NF=2, dQ NF=1 -> -14 %
+static int g_nf_kv = 2, g_nf_q = 1;
+static int g_kv_dma = 1;
+SSAMD_API void ssamd_attn_set_kv_dma(int v) { g_kv_dma = v; }  // measured on MI355X (D=128): dK/dV NF=2, dQ NF=1 -> -14 %
 SSAMD_API void ssamd_attn_set_nf(int nf_kv, int nf_q) {
   g_nf_kv = nf_kv;
   g_nf_q = nf_q;
@@ -805,7 +977,20 @@ SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const int64
   if ((long)B * L == 0 || rows == 0) return 0;
   hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
   if (D == 128) {  // fragments per wave of the two kernels: runtime-tunable (measured defaults)
-    if (g_nf_kv == 1) launch_dkdv<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+    if (g_kv_dma) {
+      constexpr size_t lds = 2 * (2 * TQ * 128 * 2 + 2 * TQ * 4);
+      if (g_nf_kv == 1) {
+        static const bool once1 = (allow_lds(attn_bwd_dkdv_dma_kernel<1, 2>, lds), true);
+        (void)once1;
+        hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<1, 2>), dim3(cdiv(L, 64), B * H), dim3(NT), lds, s, qkv, lens,
+                           cu, dO, lse, delta, dqkv, L, H, scale * kLog2e, scale);
+      } else {
+        static const bool once2 = (allow_lds(attn_bwd_dkdv_dma_kernel<2, 1>, lds), true);
+        (void)once2;
+        hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<2, 1>), dim3(cdiv(L, 128), B * H), dim3(NT), lds, s, qkv, lens,
+                           cu, dO, lse, delta, dqkv, L, H, scale * kLog2e, scale);
+      }
+    } else if (g_nf_kv == 1) launch_dkdv<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
     else launch_dkdv<128, 2>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
     if (g_nf_q == 1) launch_dq<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
     else launch_dq<128, 2>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);

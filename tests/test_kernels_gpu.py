@@ -639,3 +639,24 @@ def test_attention_fwd_variants(dma, nf):
     orr = ref.attention(qkv.float(), lens, H)
     assert _rel(o, orr) < 1e-2
     assert _rel(unpack(op, pk), orr) < 1e-2
+
+
+@pytest.mark.parametrize("dma,nf", [(0, 2), (1, 1), (1, 2)])
+def test_attention_bwd_variants(dma, nf):
+    """D=128 dK/dV kernels (register-staged / LDS-DMA, 1 or 2 key fragments per wave) vs fp32."""
+    torch.manual_seed(22)
+    H, D = 2, 128
+    pk, lens, M = _pack_case()
+    qkv = torch.randn(pk.B, M, 3 * H * D, device=DEV).to(torch.bfloat16)
+    g = torch.randn(pk.B, M, H * D, device=DEV).to(torch.bfloat16)
+    hip.lib().ssamd_attn_set_kv_dma(dma)
+    hip.lib().ssamd_attn_set_nf(nf, 1)
+    try:
+        qh = qkv.clone().requires_grad_(True)
+        hip.attention(qh, lens, H).backward(g)
+    finally:
+        hip.lib().ssamd_attn_set_kv_dma(1)
+        hip.lib().ssamd_attn_set_nf(1, 1)
+    qr = qkv.float().requires_grad_(True)
+    ref.attention(qr, lens, H).backward(g.float())
+    assert _rel(qh.grad, qr.grad) < 2e-2

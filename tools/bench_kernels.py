@@ -127,12 +127,14 @@ def main():
                 hip.lib().ssamd_attn_set_fwd(dma, nf)
                 row[f"fwd_ms_dma{dma}_nf{nf}"] = round(timeit(lambda: hip.attention(qh, lens, H), args.iters), 3)
             hip.lib().ssamd_attn_set_fwd(1, 2)
-        if D == 128:  # fragments-per-wave of the dK/dV and dQ kernels
-            for nkv, nq in ((1, 1), (1, 2), (2, 2)):
-                hip.lib().ssamd_attn_set_nf(nkv, nq)
+        if D == 128:  # dK/dV kernel (register-staged / LDS-DMA) x fragments per wave; dQ NF = 1
+            for dma, nkv in ((0, 2), (1, 1), (1, 2)):
+                hip.lib().ssamd_attn_set_kv_dma(dma)
+                hip.lib().ssamd_attn_set_nf(nkv, 1)
                 t2 = timeit(lambda: torch.autograd.grad(o, qh, g, retain_graph=True), args.iters)
-                row[f"bwd_ms_nf{nkv}{nq}"] = round(t2, 3)
-            hip.lib().ssamd_attn_set_nf(2, 1)
+                row[f"bwd_ms_kvdma{dma}_nf{nkv}"] = round(t2, 3)
+            hip.lib().ssamd_attn_set_kv_dma(1)
+            hip.lib().ssamd_attn_set_nf(1, 1)
         print(json.dumps(row), flush=True)
 
 
