@@ -919,7 +919,7 @@ SSAMD_API void ssamd_attn_set_fwd(int dma, int nf) {
   g_fwd_dma = dma;
   g_fwd_nf = nf;
 }
-static int g_nf_kv = 2, g_nf_q = 1;
+static int g_nf_kv = 1, g_nf_q = 1;  // measured (D=128, L=800): LDS-DMA dK/dV NF=1 at 2 waves/SIMD 0.675 ms vs 0.793 (registers, NF=2)
 static int g_kv_dma = 1;
 SSAMD_API void ssamd_attn_set_kv_dma(int v) { g_kv_dma = v; }  // measured on MI355X (D=128): dK/dV NF=2, dQ NF=1 -> -14 %
 SSAMD_API void ssamd_attn_set_nf(int nf_kv, int nf_q) {
