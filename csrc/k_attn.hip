@@ -901,6 +901,146 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
   }
 }
 
+template <int NF, int MINB>
+__global__ void __launch_bounds__(NT, MINB) attn_bwd_dq_dma_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
+                                                         const int64_t* __restrict__ cu,
+                                                         const bf16_t* __restrict__ dO, const float* __restrict__ lse,
+                                                         const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                         int L, int H, float scale_log2, float scale) {
+  constexpr int D = 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K, V) unified images, DMA'd
+  constexpr int BUFB = 2 * TK * D * 2;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int RS = 3 * H * D, OS = H * D;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4;
+  const int len = (int)lens[b];
+  // packed variable-length rows (cu = row offsets): only rows < len exist for sequence b
+  const long rowb = cu ? (long)cu[b] : (long)b * L;
+  const int Lq = cu ? len : L;
+  const bf16_t* Qp = qkv + h * D;
+  const bf16_t* Kp = qkv + H * D + h * D;
+  const bf16_t* Vp = qkv + 2 * H * D + h * D;
+
+  int qv[NF];
+  float lq[NF], dd[NF];
+  short8 qf[NF][D / 32], df_[NF][D / 32];
+  if (blockIdx.x * (64 * NF) >= len) {  // padded query block: dQ = 0
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int q = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
+      if (q >= Lq) continue;
+      bf16_t* dqp = dqkv + (rowb + q) * RS + h * D;
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) *reinterpret_cast<short4v*>(dqp + df * 16 + 4 * g) = (short4v){0, 0, 0, 0};
+    }
+    return;
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    qv[f] = blockIdx.x * (64 * NF) + wave * (16 * NF) + f * 16 + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) {
+      short8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (qv[f] < len) {
+        a = *reinterpret_cast<const short8*>(Qp + (rowb + qv[f]) * RS + s * 32 + 8 * g);
+        c = *reinterpret_cast<const short8*>(dO + (rowb + qv[f]) * OS + h * D + s * 32 + 8 * g);
+      }
+      qf[f][s] = a;
+      df_[f][s] = c;
+    }
+    lq[f] = qv[f] < len ? lse[(long)bh * L + qv[f]] : 0.f;
+    dd[f] = qv[f] < len ? delta[(rowb + qv[f]) * H + h] : 0.f;
+  }
+  float4v dq[NF][D / 16];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) dq[f][i] = (float4v){0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (len + TK - 1) / TK;
+  auto issue = [&](int key0, int buf) {
+    char* Kd = smem + buf * BUFB;
+    char* Vd = Kd + TK * D * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (i * 4 + wave) * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ uni_h(row);
+      const int key = key0 + row;
+      const bool ok = key < len;
+      const long off = (rowb + key) * (long)RS + c * 8;
+      a_glds16(ok ? (const void*)(Kp + off) : (const void*)a_zero_chunk, Kd + (i * 4 + wave) * 1024);
+      a_glds16(ok ? (const void*)(Vp + off) : (const void*)a_zero_chunk, Vd + (i * 4 + wave) * 1024);
+    }
+  };
+  if (nkt > 0) issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) issue((kt + 1) * TK, buf ^ 1);
+    const char* Kr = smem + buf * BUFB;
+    const char* Kt = Kr;
+    const char* Vr = Kr + TK * D * 2;
+    float4v st[NF][4], dpt[NF][4];
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) st[f][kf] = dpt[f][kf] = (float4v){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < D / 32; ++s) {
+        const short8 ak = *reinterpret_cast<const short8*>(Kr + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
+        const short8 av = *reinterpret_cast<const short8*>(Vr + row_off<D>(kf * 16 + (lane & 15), s * 4 + g));
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          st[f][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[f][s], st[f][kf], 0, 0, 0);
+          dpt[f][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, df_[f][s], dpt[f][kf], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * TK + kf * 16 + 4 * g + r;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          float ds = 0.f;
+          if (key < len && qv[f] < len) {
+            const float pv = exp2f(st[f][kf][r] * scale_log2 - lq[f]);
+            ds = pv * (dpt[f][kf][r] - dd[f]);
+          }
+          st[f][kf][r] = ds;
+        }
+      }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      short8 sb[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) sb[f] = pack8(st[f][2 * hh], st[f][2 * hh + 1]);
+#pragma unroll
+      for (int df = 0; df < D / 16; ++df) {
+        const short8 ak = tr_frag<D>(Kt, hh * 32, df * 16, lane);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) dq[f][df] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, sb[f], dq[f][df], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    if (qv[f] >= Lq) continue;
+    bf16_t* dqp = dqkv + (rowb + qv[f]) * RS + h * D;
+#pragma unroll
+    for (int df = 0; df < D / 16; ++df) {
+      short4v a;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = (short)f2bf(dq[f][df][r] * scale);
+      *reinterpret_cast<short4v*>(dqp + df * 16 + 4 * g) = a;
+    }
+  }
+}
+
 }  // namespace
 
 // NF (fragments per wave) chosen from measurement on MI355X: the forward keeps 2 waves/SIMD
@@ -919,9 +1059,13 @@ SSAMD_API void ssamd_attn_set_fwd(int dma, int nf) {
   g_fwd_dma = dma;
   g_fwd_nf = nf;
 }
-static int g_nf_kv = 1, g_nf_q = 1;  // measured (D=128, L=800): LDS-DMA dK/dV NF=1 at 2 waves/SIMD 0.675 ms vs 0.793 (registers, NF=2)
-static int g_kv_dma = 1;
-SSAMD_API void ssamd_attn_set_kv_dma(int v) { g_kv_dma = v; }  // measured on MI355X (D=128): dK/dV NF=2, dQ NF=1 -> -14 %
+static int g_nf_kv = 1, g_nf_q = 2;  // measured (D=128, L=800): LDS-DMA dK/dV NF=1 (2 waves/SIMD), LDS-DMA dQ NF=2: bwd 0.599 ms (from 0.793)
+static int g_kv_dma = 1, g_q_dma = 1;
+SSAMD_API void ssamd_attn_set_kv_dma(int v) { g_kv_dma = v; }
+SSAMD_API void ssamd_attn_set_q_dma(int v, int nf) {
+  g_q_dma = v;
+  g_nf_q = nf;
+}  // measured on MI355X (D=128): dK/dV NF=2, dQ NF=1 -> -14 %
 SSAMD_API void ssamd_attn_set_nf(int nf_kv, int nf_q) {
   g_nf_kv = nf_kv;
   g_nf_q = nf_q;
@@ -992,7 +1136,15 @@ SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const int64
       }
     } else if (g_nf_kv == 1) launch_dkdv<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
     else launch_dkdv<128, 2>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
-    if (g_nf_q == 1) launch_dq<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
+    if (g_q_dma) {
+      constexpr size_t lds = 2 * 2 * TK * 128 * 2;  // 64 KiB
+      if (g_nf_q == 1)
+        hipLaunchKernelGGL((attn_bwd_dq_dma_kernel<1, 2>), dim3(cdiv(L, 64), B * H), dim3(NT), lds, s, qkv, lens, cu,
+                           dO, lse, delta, dqkv, L, H, scale * kLog2e, scale);
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_dma_kernel<2, 2>), dim3(cdiv(L, 128), B * H), dim3(NT), lds, s, qkv, lens,
+                           cu, dO, lse, delta, dqkv, L, H, scale * kLog2e, scale);
+    } else if (g_nf_q == 1) launch_dq<128, 1>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
     else launch_dq<128, 2>(qkv, lens, cu, dO, lse, delta, dqkv, B, L, H, scale, s);
   } else {
     ATTN_DISPATCH(D, false, {

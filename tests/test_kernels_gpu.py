@@ -641,8 +641,8 @@ def test_attention_fwd_variants(dma, nf):
     assert _rel(unpack(op, pk), orr) < 1e-2
 
 
-@pytest.mark.parametrize("dma,nf", [(0, 2), (1, 1), (1, 2)])
-def test_attention_bwd_variants(dma, nf):
+@pytest.mark.parametrize("dma,nf,qdma,nq", [(0, 2, 0, 1), (1, 1, 1, 1), (1, 2, 1, 2), (1, 1, 0, 1)])
+def test_attention_bwd_variants(dma, nf, qdma, nq):
     """D=128 dK/dV kernels (register-staged / LDS-DMA, 1 or 2 key fragments per wave) vs fp32."""
     torch.manual_seed(22)
     H, D = 2, 128
@@ -651,12 +651,14 @@ def test_attention_bwd_variants(dma, nf):
     g = torch.randn(pk.B, M, H * D, device=DEV).to(torch.bfloat16)
     hip.lib().ssamd_attn_set_kv_dma(dma)
     hip.lib().ssamd_attn_set_nf(nf, 1)
+    hip.lib().ssamd_attn_set_q_dma(qdma, nq)
     try:
         qh = qkv.clone().requires_grad_(True)
         hip.attention(qh, lens, H).backward(g)
     finally:
         hip.lib().ssamd_attn_set_kv_dma(1)
-        hip.lib().ssamd_attn_set_nf(1, 1)
+        hip.lib().ssamd_attn_set_nf(1, 2)
+        hip.lib().ssamd_attn_set_q_dma(1, 2)
     qr = qkv.float().requires_grad_(True)
     ref.attention(qr, lens, H).backward(g.float())
     assert _rel(qh.grad, qr.grad) < 2e-2

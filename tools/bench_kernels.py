@@ -134,7 +134,12 @@ def main():
                 t2 = timeit(lambda: torch.autograd.grad(o, qh, g, retain_graph=True), args.iters)
                 row[f"bwd_ms_kvdma{dma}_nf{nkv}"] = round(t2, 3)
             hip.lib().ssamd_attn_set_kv_dma(1)
-            hip.lib().ssamd_attn_set_nf(1, 1)
+            hip.lib().ssamd_attn_set_nf(1, 2)
+            for qd, nq in ((0, 1), (1, 1), (1, 2)):  # dQ kernel variants
+                hip.lib().ssamd_attn_set_q_dma(qd, nq)
+                t2 = timeit(lambda: torch.autograd.grad(o, qh, g, retain_graph=True), args.iters)
+                row[f"bwd_ms_qdma{qd}_nf{nq}"] = round(t2, 3)
+            hip.lib().ssamd_attn_set_q_dma(1, 2)
         print(json.dumps(row), flush=True)
 
 
