@@ -420,6 +420,49 @@ __global__ void __launch_bounds__(256) weight_prep_kernel(const WDesc* __restric
 }
 }  // namespace
 
+namespace {
+// Tiled variant: one block per 64 (cout) x 64 (j = cin*ks + tap) tile of one weight, staged in LDS, so
+// both the fp32 reads (along j) and the transposed dgrad-image writes (along cout) are coalesced.
+__global__ void __launch_bounds__(256) weight_prep_tiled_kernel(const WDesc* __restrict__ tab,
+                                                                const int4* __restrict__ tiles) {
+  __shared__ float t[64][65];
+  const int4 tl = tiles[blockIdx.x];
+  const WDesc d = tab[tl.x];
+  const int co0 = tl.y, j0 = tl.z;
+  const int K = d.cin * d.ks;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    const int co = co0 + r, j = j0 + c;
+    t[r][c] = (co < d.cout && j < K) ? d.src[(long)co * K + j] : 0.f;
+  }
+  __syncthreads();
+  if (d.mode == 1) {  // dgrad image [cin][ks - 1 - tap][cout]: consecutive threads -> consecutive cout
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+      const int jr = e >> 6, c = e & 63;
+      const int co = co0 + c, j = j0 + jr;
+      if (co >= d.cout || j >= K) continue;
+      const int ci = j / d.ks, tap = j - ci * d.ks;
+      d.dst[((long)ci * d.ks + (d.ks - 1 - tap)) * d.cout + co] = f2bf(t[c][jr]);
+    }
+  } else {  // forward image [cout][tap][cin]
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      const int co = co0 + r, j = j0 + c;
+      if (co >= d.cout || j >= K) continue;
+      const int ci = j / d.ks, tap = j - ci * d.ks;
+      d.dst[(long)co * K + (long)tap * d.cin + ci] = f2bf(t[r][c]);
+    }
+  }
+}
+}  // namespace
+
+SSAMD_API int ssamd_weight_prep_tiled(const void* table, const void* tiles, int ntiles, hipStream_t s) {
+  if (ntiles == 0) return 0;
+  hipLaunchKernelGGL(weight_prep_tiled_kernel, dim3(ntiles), dim3(256), 0, s, reinterpret_cast<const WDesc*>(table),
+                     reinterpret_cast<const int4*>(tiles));
+  return (int)hipGetLastError();
+}
+
 SSAMD_API int ssamd_weight_prep(const void* table, const long* cum, int n, long total, hipStream_t s) {
   if (n == 0 || total == 0) return 0;
   hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_for(total, 4)), dim3(256), 0, s,

@@ -63,6 +63,7 @@ _SIGS = {
     "ssamd_gemm_set_epilogue": [I],
     "ssamd_gemm_set_variant": [I],
     "ssamd_weight_prep": [P, P, I, L_, P],
+    "ssamd_weight_prep_tiled": [P, P, I, P],
 }
 
 
@@ -155,16 +156,27 @@ def _refresh_all(device):
         desc = np.zeros(len(live), dtype=[("src", "<u8"), ("dst", "<u8"), ("cout", "<i4"), ("cin", "<i4"),
                                           ("ks", "<i4"), ("mode", "<i4")])
         cum = np.zeros(len(live) + 1, dtype=np.int64)
+        tiles = []
         for i, (e, w) in enumerate(live):
             ks = w.shape[2] if w.dim() == 3 else 1
             desc[i] = (w.data_ptr(), e[3].data_ptr(), w.shape[0], w.shape[1], ks, e[4])
             cum[i + 1] = cum[i] + w.numel()
+            K = w.shape[1] * ks
+            for co0 in range(0, w.shape[0], 64):
+                for j0 in range(0, K, 64):
+                    tiles.append((i, co0, j0, 0))
+        tiles = np.asarray(tiles, dtype=np.int32).reshape(-1, 4)
         _wtable.update(n=len(live), dev=device, total=int(cum[-1]),
                        desc=torch.from_numpy(desc.view(np.uint8).copy()).to(device),
-                       cum=torch.from_numpy(cum).to(device))
+                       cum=torch.from_numpy(cum).to(device),
+                       tiles=torch.from_numpy(tiles).to(device), ntiles=len(tiles))
     if _wtable["n"]:
-        rc = lib().ssamd_weight_prep(_ptr(_wtable["desc"]), _ptr(_wtable["cum"]), _wtable["n"], _wtable["total"],
-                                     _stream())
+        if has("ssamd_weight_prep_tiled"):  # 64x64 LDS tiles: coalesced reads and transposed writes
+            rc = lib().ssamd_weight_prep_tiled(_ptr(_wtable["desc"]), _ptr(_wtable["tiles"]), _wtable["ntiles"],
+                                               _stream())
+        else:
+            rc = lib().ssamd_weight_prep(_ptr(_wtable["desc"]), _ptr(_wtable["cum"]), _wtable["n"], _wtable["total"],
+                                         _stream())
         _check(rc, "ssamd_weight_prep")
     for e, w in live:
         owner = e[2]()

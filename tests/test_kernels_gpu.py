@@ -662,3 +662,24 @@ def test_attention_bwd_variants(dma, nf, qdma, nq):
     qr = qkv.float().requires_grad_(True)
     ref.attention(qr, lens, H).backward(g.float())
     assert _rel(qh.grad, qr.grad) < 2e-2
+
+
+def test_weight_prep_batched_refresh_exact():
+    """Batched (tiled) image refresh == freshly built images, for conv and linear weights."""
+    torch.manual_seed(23)
+    ps = [torch.nn.Parameter(torch.randn(1024, 256, 9, device=DEV)), torch.nn.Parameter(torch.randn(80, 512, 5, device=DEV)),
+          torch.nn.Parameter(torch.randn(768, 256, device=DEV)), torch.nn.Parameter(torch.randn(70, 24, device=DEV))]
+    for p in ps:
+        hip.weight_fwd(p), hip.weight_dgrad(p)
+    with torch.no_grad():
+        for p in ps:
+            p.data.mul_(-0.5).add_(0.25)  # raw write: versions do not move
+    hip.bump_weight_generation()
+    for p in ps:
+        f, d = hip.weight_fwd(p), hip.weight_dgrad(p)  # first lookup refreshes all images in one launch
+        x = p.detach()
+        if x.dim() == 2:
+            ef, ed = x.to(torch.bfloat16), x.t().to(torch.bfloat16)
+        else:
+            ef, ed = x.permute(0, 2, 1).to(torch.bfloat16), x.flip(2).permute(1, 2, 0).to(torch.bfloat16)
+        assert torch.equal(f, ef.contiguous()) and torch.equal(d, ed.contiguous())
