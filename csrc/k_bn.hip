@@ -1,6 +1,7 @@
 // BatchNorm1d (channel-last, training batch statistics over all B*L rows incl. padding,
-// the reference PostNet semantics -- transformer/Layers.py:78-148) fused with tanh and
-// dropout, forward and backward.
+// the reference PostNet semantics -- transformer/Layers.py:78-148) fused with tanh (or ReLU:
+// the GST Conv2d + BatchNorm2d stack on NHWC rows) and dropout, forward and backward.
+// The int argument `act_tanh` is an activation code: 0 none, 1 tanh, 2 ReLU.
 //
 //   stats:    per-block partial (sum, sum of squares) per channel  -> [nblk][C] fp32
 //   finalize: combine partials (fp64), mean / biased var -> rstd, scale = g*rstd,
@@ -20,6 +21,19 @@ __device__ __forceinline__ float fast_tanh(float z) {
   // 1 - 2/(exp(2z)+1): one exp + one rcp; saturates correctly for |z| large
   const float e = __expf(2.f * z);
   return 1.f - 2.f / (e + 1.f);
+}
+
+// act: 0 none, 1 tanh (PostNet), 2 ReLU (GST Conv2d stack)
+__device__ __forceinline__ float act_fwd(int act, float z) {
+  if (act == 1) return fast_tanh(z);
+  if (act == 2) return fmaxf(z, 0.f);
+  return z;
+}
+// derivative of act at the pre-activation z
+__device__ __forceinline__ float act_grad(int act, float z) {
+  if (act == 1) { const float t = fast_tanh(z); return 1.f - t * t; }
+  if (act == 2) return z > 0.f ? 1.f : 0.f;
+  return 1.f;
 }
 
 struct RowMap {
@@ -129,7 +143,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float z = v[i] * sc[i] + sh[i];
-      if (act_tanh) z = fast_tanh(z);
+      z = act_fwd(act_tanh, z);
       v[i] = z * drop_scale(seed, (uint64_t)(r * C + c0 + i), p);
     }
     if constexpr (OUT_F32) {
@@ -184,10 +198,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restric
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
-        if (act_tanh) {
-          const float t = fast_tanh(hv[i] * sc[i] + sh[i]);
-          dz *= 1.f - t * t;
-        }
+        if (act_tanh) dz *= act_grad(act_tanh, hv[i] * sc[i] + sh[i]);
         a[i] += dz;
         b[i] += dz * (hv[i] - mu[i]) * rs[i];
       }
@@ -262,10 +273,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
-      if (act_tanh) {
-        const float t = fast_tanh(hv[i] * sc[i] + sh[i]);
-        dz *= 1.f - t * t;
-      }
+      if (act_tanh) dz *= act_grad(act_tanh, hv[i] * sc[i] + sh[i]);
       o[i] = (short)f2bf(k1[i] * dz + k2[i] * hv[i] + k3[i]);
     }
     *reinterpret_cast<short8*>(dh + off) = o;

@@ -97,28 +97,37 @@ class GlobalStyleTokens(nn.Module):
         self.feature_wise_affine = LinearNorm(self.token_size, 2 * d)
 
     def reference_embedding(self, mel, mel_lens):
-        x = mel.float().unsqueeze(1)  # [B,1,T,n_mel]
+        """mel [B, T, n_mel] -> last valid GRU state [B, H] (fp32).
+
+        Channel-last throughout: the mel is an NHWC image [B, T, n_mel, 1]; each layer is
+        ``ops.conv2d_s2`` (im2col + MFMA GEMM on the GPU) and ``ops.bn_act`` (BatchNorm2d batch
+        statistics over all B*H*W positions, fused ReLU).  The GRU input features are ordered
+        (channel, frequency) like the NCHW formulation, so the GRU weights mean the same thing."""
+        x = mel.unsqueeze(-1)
+        if not ops.use_hip(x):
+            x = x.float()
         lens = mel_lens.clone()
         for conv, bn in zip(self.convs, self.bns):
-            x = F.relu(bn(conv(x)))
+            y = ops.conv2d_s2(x, conv.weight, conv.bias)
+            B, Ho, Wo, C = y.shape
+            x = ops.bn_act(y.reshape(B, Ho * Wo, C), bn, self.training, "relu", 0.0).view(B, Ho, Wo, C)
             lens = (lens - 1) // 2 + 1
-        B, C, T, Fq = x.shape
-        x = x.permute(0, 2, 1, 3).reshape(B, T, C * Fq)
-        out, _ = self.gru(x)
-        idx = (lens.clamp(min=1, max=T) - 1).view(B, 1, 1).expand(-1, 1, out.shape[-1])
-        return out.gather(1, idx).squeeze(1)  # last valid GRU state [B, H]
+        B, T, Fq, C = x.shape
+        x = x.permute(0, 1, 3, 2).reshape(B, T, C * Fq)
+        return ops.gru_last(x, self.gru, lens.clamp(min=1, max=T) - 1)
+
+    def token_bank(self):
+        """Keys / values of the style-token bank, [heads, n_tok, token_size/heads] each."""
+        keys = torch.tanh(self.embed)  # [N, ts/h]
+        d = self.token_size // self.n_head
+        k = self.w_key(keys).view(-1, self.n_head, d).transpose(0, 1).contiguous()
+        v = self.w_value(keys).view(-1, self.n_head, d).transpose(0, 1).contiguous()
+        return k, v
 
     def token_attention(self, query):
         """query [B, token_size] -> style embedding [B, token_size] and weights [B, heads, n_tok]."""
-        keys = torch.tanh(self.embed)  # [N, ts/h]
-        B = query.shape[0]
-        q = query.view(B, self.n_head, 1, -1)
-        k = self.w_key(keys).view(-1, self.n_head, self.token_size // self.n_head).transpose(0, 1)  # [h,N,d]
-        v = self.w_value(keys).view(-1, self.n_head, self.token_size // self.n_head).transpose(0, 1)
-        s = torch.matmul(q, k.transpose(-1, -2).unsqueeze(0)) / (k.shape[-1] ** 0.5)  # [B,h,1,N]
-        w = torch.softmax(s, -1)
-        o = torch.matmul(w, v.unsqueeze(0)).reshape(B, self.token_size)
-        return o, w.squeeze(2)
+        k, v = self.token_bank()
+        return ops.token_attention(query, k, v)
 
     def _film(self, style_emb):
         gb = self.feature_wise_affine(style_emb)
@@ -126,7 +135,8 @@ class GlobalStyleTokens(nn.Module):
 
     def forward(self, mel, mel_lens, max_len=None):
         ref = self.reference_embedding(mel, mel_lens)
-        style, _ = self.token_attention(self.w_query(ref))
+        q = ops.linear(ref.to(mel.dtype), self.w_query.weight, None)
+        style, _ = self.token_attention(q)
         return self._film(style.to(mel.dtype))
 
     def from_token_weights(self, weights):

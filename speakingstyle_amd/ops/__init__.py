@@ -14,6 +14,7 @@ import os
 from typing import Optional
 
 import torch
+import torch.nn.functional as F
 
 from . import reference as ref
 from .packing import PackInfo, pack as pack_rows, unpack as unpack_rows  # noqa: F401
@@ -152,17 +153,58 @@ def predictor_head(h, w, b, lengths=None):
 
 
 def bn_act(h, bn, training, act_tanh, p, out_f32=False):
-    """PostNet stage: BatchNorm1d (batch stats over all B*L rows) -> [tanh] -> dropout."""
+    """PostNet stage: BatchNorm1d (batch stats over all B*L rows) -> [tanh] -> dropout.
+    ``act_tanh="relu"`` applies ReLU instead (GST BatchNorm2d over NHWC rows)."""
     if use_hip(h):
         return _hip().bn_act(h, bn, training, act_tanh, p, out_f32)
-    import torch.nn.functional as F
-
     B, L, C = h.shape
     y = F.batch_norm(h.reshape(B * L, C), bn.running_mean, bn.running_var, bn.weight, bn.bias, training,
                      bn.momentum, bn.eps).reshape(B, L, C)
     if training and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
-    if act_tanh:
+    if act_tanh == "relu":
+        y = F.relu(y)
+    elif act_tanh:
         y = torch.tanh(y)
     y = F.dropout(y, p, training) if p > 0 else y
     return y.float() if out_f32 else y
+
+
+# ------------------------------------------------------------------ GST reference encoder
+def conv2d_s2(x, w, b=None):
+    """Conv2d(3x3, stride 2, pad 1) on channel-last x [B, H, W, Cin] -> [B, Ho, Wo, Cout]."""
+    if use_hip(x):
+        return _hip().conv2d_s2(x, w, b)
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.to(x.dtype), None if b is None else b.to(x.dtype), stride=2, padding=1)
+    return y.permute(0, 2, 3, 1)
+
+
+def gru_last(x, gru, last):
+    """Batch-first single-layer GRU over x [B, T, I]; returns the hidden state at step last[b] (fp32)."""
+    if use_hip(x):
+        return _hip().gru_last(x, gru, last)
+    # explicit cell loop (torch gate order r, z, n): device-agnostic and differentiable in eval mode
+    # (the MIOpen RNN refuses a backward outside training mode)
+    gi = F.linear(x.float(), gru.weight_ih_l0, gru.bias_ih_l0)
+    h = x.new_zeros(x.shape[0], gru.hidden_size, dtype=torch.float32)
+    outs = []
+    for t in range(x.shape[1]):
+        gr, gz, gn = gi[:, t].chunk(3, -1)
+        hr, hz, hn = F.linear(h, gru.weight_hh_l0, gru.bias_hh_l0).chunk(3, -1)
+        r, z = torch.sigmoid(gr + hr), torch.sigmoid(gz + hz)
+        h = (1 - z) * torch.tanh(gn + r * hn) + z * h
+        outs.append(h)
+    out = torch.stack(outs, 1)
+    idx = last.to(torch.int64).view(-1, 1, 1).expand(-1, 1, out.shape[-1])
+    return out.gather(1, idx).squeeze(1)
+
+
+def token_attention(q, K, V):
+    """Multi-head attention of q [B, NH*D] over a token bank K/V [NH, N, D]:
+    returns (style [B, NH*D] fp32, weights [B, NH, N])."""
+    if use_hip(q):
+        return _hip().token_attention(q, K, V)
+    NH, N, D = K.shape
+    qh = q.float().view(q.shape[0], NH, 1, D)
+    w = torch.softmax(torch.matmul(qh, K.float().transpose(-1, -2).unsqueeze(0)) / (D ** 0.5), -1)
+    return torch.matmul(w, V.float().unsqueeze(0)).reshape(q.shape[0], NH * D), w.squeeze(2)

@@ -854,12 +854,186 @@ class _BNActFn(torch.autograd.Function):
 
 
 def bn_act(h, bn, training, act_tanh, p, out_f32=False):
-    """BatchNorm1d over all rows of channel-last h (+tanh) + dropout, one fused op."""
+    """BatchNorm over all rows of channel-last h (+tanh, or ReLU with ``act_tanh="relu"``) + dropout,
+    one fused op."""
     momentum = bn.momentum if bn.momentum is not None else 0.1
     if training and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
+    act = 2 if act_tanh == "relu" else int(bool(act_tanh))
     return _BNActFn.apply(h.to(torch.bfloat16), bn.weight, bn.bias, bn.running_mean, bn.running_var, bool(training),
-                          momentum, bn.eps, bool(act_tanh), float(p if training else 0.0), bool(out_f32), _next_seed())
+                          momentum, bn.eps, act, float(p if training else 0.0), bool(out_f32), _next_seed())
+
+
+# ------------------------------------------------------------------------ GST reference encoder
+_SIGS.update({
+    "ssamd_im2col_s2": [P, P, I, I, I, I, I, P],
+    "ssamd_col2im_s2": [P, P, I, I, I, I, I, P],
+    "ssamd_gru_fwd": [P, P, P, P, I, I, I, P, P, P, P],
+    "ssamd_gru_bwd": [P, P, P, P, I, I, I, P, P, P],
+    "ssamd_token_attn_fwd": [P, P, P, I, I, I, I, F, P, P, P],
+    "ssamd_token_attn_bwd": [P, P, P, P, P, I, I, I, I, F, P, P, P, P],
+})
+
+
+def _s2(n):
+    return (n - 1) // 2 + 1  # Conv2d k3 / s2 / p1 output size
+
+
+def im2col_s2(x, Kp):
+    """NHWC x [B, H, W, C] bf16 -> patch rows [B*Ho*Wo, Kp] (k = (ky*3 + kx)*C + c, zero padded)."""
+    _need(x, torch.bfloat16, "im2col.x")
+    B, H, W, C = x.shape
+    col = torch.empty(B * _s2(H) * _s2(W), Kp, device=x.device, dtype=torch.bfloat16)
+    _check(lib().ssamd_im2col_s2(_ptr(x), _ptr(col), B, H, W, C, Kp, _stream()), "ssamd_im2col_s2")
+    return col
+
+
+def _conv2d_wimg(w, Kp):
+    """[Cout, Cin, 3, 3] fp32 -> bf16 [Cout, Kp] in the im2col k order (tiny: rebuilt per call)."""
+    m = w.detach().permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+    img = torch.zeros(w.shape[0], Kp, device=w.device, dtype=torch.bfloat16)
+    img[:, : m.shape[1]] = m
+    return img
+
+
+class _Conv2dS2Fn(torch.autograd.Function):
+    """Conv2d(k3, s2, p1) on NHWC bf16: im2col + MFMA GEMM; backward = GEMM + col2im gather and the
+    split-M weight-gradient kernel on the (recomputed) patch rows with the fused bias gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        B, H, W, C = x.shape
+        Cout = w.shape[0]
+        assert w.shape[1:] == (C, 3, 3), "conv2d_s2 expects a [Cout, Cin, 3, 3] weight"
+        Kp = (9 * C + 7) // 8 * 8
+        Ho, Wo = _s2(H), _s2(W)
+        xc = x.to(torch.bfloat16).contiguous()
+        col = im2col_s2(xc, Kp)
+        wimg = _conv2d_wimg(w, Kp)
+        bf = None if b is None else b.detach().float().contiguous()
+        y = conv_gemm_raw(col, wimg, bf, 1, B * Ho * Wo, Kp, 1, 1, 0, Cout)
+        ctx.save_for_backward(xc, w, wimg)
+        ctx.b = b
+        ctx.dims = (B, H, W, C, Ho, Wo, Cout, Kp)
+        return y.view(B, Ho, Wo, Cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, w, wimg = ctx.saved_tensors
+        B, H, W, C, Ho, Wo, Cout, Kp = ctx.dims
+        rows = B * Ho * Wo
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcol = conv_gemm_raw(dy, wimg.t().contiguous(), None, 1, rows, Cout, 1, 1, 0, Kp)
+            dx = torch.empty_like(xc)
+            _check(lib().ssamd_col2im_s2(_ptr(dcol), _ptr(dx), B, H, W, C, Kp, _stream()), "ssamd_col2im_s2")
+        col = im2col_s2(xc, Kp)  # recomputed: cheaper than keeping [rows, 9C] alive over the step
+        want_b = ctx.b is not None and ctx.needs_input_grad[2]
+        res = conv_wgrad_raw(col, dy, 1, rows, Kp, 1, 1, 0, Cout, with_bias=want_b,
+                             db=gradslots.claim(ctx.b) if want_b else None)
+        dWp, db = res if want_b else (res, None)
+        dw = dWp.view(Cout, Kp)[:, : 9 * C].reshape(Cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
+        return dx, dw, db
+
+
+def conv2d_s2(x, w, b=None):
+    """NHWC [B, H, W, Cin] -> [B, ceil(H/2), ceil(W/2), Cout] bf16 (Conv2d 3x3, stride 2, pad 1)."""
+    return _Conv2dS2Fn.apply(x, w, b)
+
+
+class _GRUFn(torch.autograd.Function):
+    """Single-layer batch-first GRU returning the hidden state at step ``last[b]`` of every row.
+
+    Input projection and all weight / input gradients are MFMA GEMMs; the recurrence is the
+    persistent ``gru_fwd`` / ``gru_bwd`` kernel pair (csrc/k_gst.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, last):
+        B, T, I = x.shape
+        G, Hd = w_hh.shape
+        assert G == 3 * Hd and tuple(w_ih.shape) == (G, I), "GRU weight shapes"
+        _need(last, torch.int64, "gru.last")
+        xc = x.to(torch.bfloat16).contiguous()
+        gi = conv_gemm_raw(xc, weight_fwd(w_ih), b_ih.detach().float().contiguous(), 1, B * T, I, 1, 1, 0, G,
+                           out_f32=True)
+        hlast = torch.empty(B, Hd, device=x.device, dtype=torch.float32)
+        sv = torch.empty(B, T, 5, Hd, device=x.device, dtype=torch.float32)
+        hprev = torch.empty(B, T, Hd, device=x.device, dtype=torch.bfloat16)
+        rc = lib().ssamd_gru_fwd(_ptr(gi), _ptr(weight_fwd(w_hh)), _ptr(b_hh.detach().float().contiguous()), _ptr(last),
+                                 B, T, Hd, _ptr(hlast), _ptr(sv), _ptr(hprev), _stream())
+        _check(rc, "ssamd_gru_fwd")
+        ctx.save_for_backward(xc, w_ih, w_hh, last, sv, hprev)
+        ctx.biases = (b_ih, b_hh)
+        return hlast
+
+    @staticmethod
+    def backward(ctx, dh):
+        xc, w_ih, w_hh, last, sv, hprev = ctx.saved_tensors
+        b_ih, b_hh = ctx.biases
+        B, T, I = xc.shape
+        G, Hd = w_hh.shape
+        dgi = torch.empty(B, T, G, device=xc.device, dtype=torch.bfloat16)
+        dgh = torch.empty_like(dgi)
+        rc = lib().ssamd_gru_bwd(_ptr(dh.float().contiguous()), _ptr(sv), _ptr(weight_dgrad(w_hh)), _ptr(last), B, T,
+                                 Hd, _ptr(dgi), _ptr(dgh), _stream())
+        _check(rc, "ssamd_gru_bwd")
+
+        def wgrad(inp, dY, w, b, cin):
+            sw = gradslots.claim(w)
+            dw, db = conv_wgrad_raw(inp, dY, 1, B * T, cin, 1, 1, 0, G, with_bias=True,
+                                    dW=None if sw is None else sw.view(G, cin, 1), db=gradslots.claim(b))
+            return dw.view(G, cin), db
+
+        dw_hh, db_hh = wgrad(hprev, dgh, w_hh, b_hh, Hd)
+        dw_ih, db_ih = wgrad(xc, dgi, w_ih, b_ih, I)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_gemm_raw(dgi, weight_dgrad(w_ih), None, 1, B * T, G, 1, 1, 0, I).view(B, T, I)
+        return dx, dw_ih, dw_hh, db_ih, db_hh, None
+
+
+def gru_last(x, gru, last):
+    """``nn.GRU`` (1 layer, batch_first) parameters; x [B, T, I] -> h at step last[b] [B, H] fp32."""
+    if gru.num_layers != 1 or gru.bidirectional or not gru.batch_first or not gru.bias:
+        raise ValueError("gru_last supports a single-layer, unidirectional, batch-first GRU with biases")
+    return _GRUFn.apply(x, gru.weight_ih_l0, gru.weight_hh_l0, gru.bias_ih_l0, gru.bias_hh_l0,
+                        last.to(torch.int64).contiguous())
+
+
+class _TokenAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, K, V):
+        B = q.shape[0]
+        NH, N, D = K.shape
+        qc, Kc, Vc = q.float().contiguous(), K.float().contiguous(), V.float().contiguous()
+        assert qc.shape[1] == NH * D and Vc.shape == Kc.shape
+        o = torch.empty(B, NH * D, device=q.device, dtype=torch.float32)
+        w = torch.empty(B, NH, N, device=q.device, dtype=torch.float32)
+        scale = 1.0 / math.sqrt(D)
+        _check(lib().ssamd_token_attn_fwd(_ptr(qc), _ptr(Kc), _ptr(Vc), B, NH, N, D, scale, _ptr(o), _ptr(w),
+                                          _stream()), "ssamd_token_attn_fwd")
+        ctx.save_for_backward(qc, Kc, Vc, w)
+        ctx.mark_non_differentiable(w)
+        return o, w
+
+    @staticmethod
+    def backward(ctx, do, _dw):
+        qc, Kc, Vc, w = ctx.saved_tensors
+        B = qc.shape[0]
+        NH, N, D = Kc.shape
+        dq = torch.empty_like(qc)
+        part = _workspace(qc.device, B * 2 * NH * N * D)
+        dkv = torch.empty(2, NH, N, D, device=qc.device, dtype=torch.float32)
+        rc = lib().ssamd_token_attn_bwd(_ptr(do.float().contiguous()), _ptr(qc), _ptr(Kc), _ptr(Vc), _ptr(w), B, NH, N,
+                                        D, 1.0 / math.sqrt(D), _ptr(dq), _ptr(part), _ptr(dkv), _stream())
+        _check(rc, "ssamd_token_attn_bwd")
+        return dq, dkv[0], dkv[1]
+
+
+def token_attention(q, K, V):
+    """q [B, NH*D], K/V [NH, N, D] -> (style [B, NH*D] fp32, weights [B, NH, N])."""
+    return _TokenAttnFn.apply(q, K, V)
 
 
 # ------------------------------------------------------------------------ N = 1 heads

@@ -233,10 +233,11 @@ def test_attention(D, H):
     assert _rel(qh.grad, qr.grad) < 3e-2
 
 
-def test_model_step_hip_vs_reference():
-    """Full FastSpeech2 (BC2013 config, FiLM style) forward+backward, HIP vs torch fp32."""
+@pytest.mark.parametrize("cfg", ["BC2013", "BC2013_GST"])
+def test_model_step_hip_vs_reference(cfg):
+    """Full FastSpeech2 (BC2013 config: FiLM reference encoder, or the GST variant) forward+backward,
+    HIP vs torch fp32."""
     import copy
-    import os
 
     from speakingstyle_amd import ops
     from speakingstyle_amd.config import load_named
@@ -244,7 +245,7 @@ def test_model_step_hip_vs_reference():
     from speakingstyle_amd.models.fastspeech2 import FastSpeech2
     from speakingstyle_amd.models.loss import FastSpeech2Loss
 
-    pp, mc, tc = load_named("BC2013")
+    pp, mc, tc = load_named(cfg)
     torch.manual_seed(9)
     m = FastSpeech2(pp, mc).to(DEV).eval()
     mr = copy.deepcopy(m)
@@ -272,11 +273,18 @@ def test_model_step_hip_vs_reference():
     for a, c in zip(lo[:6], lr_[:6]):
         assert abs(a.item() - c.item()) <= 3e-2 * abs(c.item()) + 1e-3
     gr = dict(mr.named_parameters())
+    # FiLM scale scalars: each gradient is one global sum over (batch, channel) that can cancel
+    # down to a few % of its terms, so they get an absolute floor from the largest scalar gradient
+    scal = max([gr[n].grad.abs().item() for n, p in m.named_parameters()
+                if p.numel() == 1 and gr[n].grad is not None] or [0.0])
     bad = []
     for n, p in m.named_parameters():
         if p.grad is None or gr[n].grad is None:
             continue
-        if gr[n].grad.norm() > 1e-6 and _rel(p.grad, gr[n].grad) > 0.15:
+        if p.numel() == 1:
+            if abs(p.grad.item() - gr[n].grad.item()) > 0.15 * abs(gr[n].grad.item()) + 0.03 * scal:
+                bad.append((n, p.grad.item(), gr[n].grad.item()))
+        elif gr[n].grad.norm() > 1e-6 and _rel(p.grad, gr[n].grad) > 0.15:
             bad.append((n, _rel(p.grad, gr[n].grad)))
     assert not bad, bad[:10]
 
