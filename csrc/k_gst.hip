@@ -310,10 +310,12 @@ __global__ void __launch_bounds__(64) token_attn_fwd_kernel(const float* __restr
   }
 }
 
-// dq [B, NH*D]; part [B, 2, NH, N, D] = per-utterance (dK, dV) contributions
+// dq [B, NH*D]; part [B, 2, NH, N, D] = per-utterance (dK, dV) contributions.  dwts (optional):
+// gradient w.r.t. the returned attention weights (e.g. a loss on the weights themselves).
 __global__ void __launch_bounds__(64) token_attn_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ q,
                                                             const float* __restrict__ K, const float* __restrict__ V,
-                                                            const float* __restrict__ wts, int NH, int N, int D,
+                                                            const float* __restrict__ wts,
+                                                            const float* __restrict__ dwts, int NH, int N, int D,
                                                             float scale, float* __restrict__ dq,
                                                             float* __restrict__ part) {
   const int b = blockIdx.x, l = threadIdx.x;
@@ -327,6 +329,7 @@ __global__ void __launch_bounds__(64) token_attn_bwd_kernel(const float* __restr
     for (int n = 0; n < N; ++n) {
       wn[n] = wts[((long)b * NH + hh) * N + n];
       dw[n] = wave_sum(l < D ? dov * V[((long)hh * N + n) * D + l] : 0.f);
+      if (dwts) dw[n] += dwts[((long)b * NH + hh) * N + n];
       sdw += wn[n] * dw[n];
     }
     float dql = 0.f;
@@ -404,15 +407,15 @@ SSAMD_API int ssamd_token_attn_fwd(const float* q, const float* K, const float* 
 
 // part: B * 2*NH*N*D floats of workspace; dKV [2, NH, N, D] = (dK, dV)
 SSAMD_API int ssamd_token_attn_bwd(const float* dout, const float* q, const float* K, const float* V, const float* w,
-                                   int B, int NH, int N, int D, float scale, float* dq, float* part, float* dKV,
-                                   hipStream_t s) {
+                                   const float* dw, int B, int NH, int N, int D, float scale, float* dq, float* part,
+                                   float* dKV, hipStream_t s) {
   if (N > NTOK_MAX || D > 64) return -2;
   const long ncol = 2L * NH * N * D;
   if (B == 0) {
     hipMemsetAsync(dKV, 0, ncol * sizeof(float), s);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(token_attn_bwd_kernel, dim3(B), dim3(64), 0, s, dout, q, K, V, w, NH, N, D, scale, dq, part);
+  hipLaunchKernelGGL(token_attn_bwd_kernel, dim3(B), dim3(64), 0, s, dout, q, K, V, w, dw, NH, N, D, scale, dq, part);
   hipLaunchKernelGGL(colsum_f32_kernel, dim3(cdiv(ncol, 256)), dim3(256), 0, s, part, (long)B, ncol, dKV);
   return (int)hipGetLastError();
 }

@@ -38,10 +38,29 @@ class TacotronSTFT(torch.nn.Module):
                           pad_mode="reflect", return_complex=True)
         return spec.abs()  # [B, n_fft/2+1, frames]
 
+    def fft_window(self, device) -> torch.Tensor:
+        """The win_length window centred in n_fft (torch.stft's convention), fp32 on ``device``."""
+        w = self.window.to(device=device, dtype=torch.float32)
+        if self.win < self.n_fft:
+            left = (self.n_fft - self.win) // 2
+            w = torch.nn.functional.pad(w, (left, self.n_fft - self.win - left))
+        return w.contiguous()
+
     def mel_spectrogram(self, y: torch.Tensor):
-        """y [B, N] in [-1, 1] -> (mel [B, n_mel, frames], energy [B, frames])."""
+        """y [B, N] in [-1, 1] -> (mel [B, n_mel, frames], energy [B, frames]).
+
+        On the GPU (no autograd) one fused HIP kernel does framing + FFT + |X| + mel + log +
+        energy (``csrc/k_audio.hip``); the differentiable / CPU path is torch.stft."""
         if not y.requires_grad and not y.is_cuda:  # reference range check (audio/stft.py:169-170), host tensors only
             assert float(y.min()) >= -1 and float(y.max()) <= 1
+        from .. import ops
+
+        if y.is_cuda and ops.use_hip(y) and not (torch.is_grad_enabled() and y.requires_grad) \
+                and y.shape[-1] > self.n_fft // 2:
+            from ..ops import hip
+
+            return hip.logmel(y.float().contiguous(), self.n_fft, self.hop, self.fft_window(y.device),
+                              self.mel_basis.to(y.device).contiguous(), 1e-5)
         mag = self.magnitudes(y)
         mel = dynamic_range_compression(torch.matmul(self.mel_basis.to(y.device), mag))
         energy = torch.norm(mag, dim=1)

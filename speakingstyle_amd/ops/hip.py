@@ -871,7 +871,7 @@ _SIGS.update({
     "ssamd_gru_fwd": [P, P, P, P, I, I, I, P, P, P, P],
     "ssamd_gru_bwd": [P, P, P, P, I, I, I, P, P, P],
     "ssamd_token_attn_fwd": [P, P, P, I, I, I, I, F, P, P, P],
-    "ssamd_token_attn_bwd": [P, P, P, P, P, I, I, I, I, F, P, P, P, P],
+    "ssamd_token_attn_bwd": [P, P, P, P, P, P, I, I, I, I, F, P, P, P, P],
 })
 
 
@@ -1014,18 +1014,19 @@ class _TokenAttnFn(torch.autograd.Function):
         _check(lib().ssamd_token_attn_fwd(_ptr(qc), _ptr(Kc), _ptr(Vc), B, NH, N, D, scale, _ptr(o), _ptr(w),
                                           _stream()), "ssamd_token_attn_fwd")
         ctx.save_for_backward(qc, Kc, Vc, w)
-        ctx.mark_non_differentiable(w)
         return o, w
 
     @staticmethod
-    def backward(ctx, do, _dw):
+    def backward(ctx, do, dw):
         qc, Kc, Vc, w = ctx.saved_tensors
         B = qc.shape[0]
         NH, N, D = Kc.shape
         dq = torch.empty_like(qc)
         part = _workspace(qc.device, B * 2 * NH * N * D)
         dkv = torch.empty(2, NH, N, D, device=qc.device, dtype=torch.float32)
-        rc = lib().ssamd_token_attn_bwd(_ptr(do.float().contiguous()), _ptr(qc), _ptr(Kc), _ptr(Vc), _ptr(w), B, NH, N,
+        do = torch.zeros_like(qc) if do is None else do.float().contiguous()
+        dw = None if dw is None else dw.float().contiguous()
+        rc = lib().ssamd_token_attn_bwd(_ptr(do), _ptr(qc), _ptr(Kc), _ptr(Vc), _ptr(w), _ptr(dw), B, NH, N,
                                         D, 1.0 / math.sqrt(D), _ptr(dq), _ptr(part), _ptr(dkv), _stream())
         _check(rc, "ssamd_token_attn_bwd")
         return dq, dkv[0], dkv[1]
@@ -1034,6 +1035,29 @@ class _TokenAttnFn(torch.autograd.Function):
 def token_attention(q, K, V):
     """q [B, NH*D], K/V [NH, N, D] -> (style [B, NH*D] fp32, weights [B, NH, N])."""
     return _TokenAttnFn.apply(q, K, V)
+
+
+# ------------------------------------------------------------------------ audio front-end
+_SIGS.update({"ssamd_logmel": [P, I, L_, I, I, P, P, I, F, P, P, P]})
+
+
+def logmel(y, n_fft, hop, window, basis, clip=1e-5):
+    """y [B, N] fp32 -> (log-mel [B, n_mel, N // hop + 1], energy [B, frames]): TacotronSTFT semantics
+    (centre reflect padding, |FFT|, mel basis, log(clamp)), one fused kernel (csrc/k_audio.hip)."""
+    _need(y, torch.float32, "logmel.y")
+    _need(window, torch.float32, "logmel.window")
+    _need(basis, torch.float32, "logmel.basis")
+    y2 = y.reshape(-1, y.shape[-1])
+    B, N = y2.shape
+    n_mel = basis.shape[0]
+    assert window.numel() == n_fft and basis.shape[1] == n_fft // 2 + 1
+    frames = N // hop + 1
+    mel = torch.empty(B, n_mel, frames, device=y.device, dtype=torch.float32)
+    energy = torch.empty(B, frames, device=y.device, dtype=torch.float32)
+    rc = lib().ssamd_logmel(_ptr(y2), B, N, n_fft, hop, _ptr(window), _ptr(basis), n_mel, float(clip), _ptr(mel),
+                            _ptr(energy), _stream())
+    _check(rc, "ssamd_logmel")
+    return mel, energy
 
 
 # ------------------------------------------------------------------------ N = 1 heads

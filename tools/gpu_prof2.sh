@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of a short bench.py run (pre-built tree).  BENCHARGS, TAG.
+set -o pipefail
+R="$(cd "$(dirname "$0")/.." && pwd)"
+cd "$R"
+TAG=${TAG:-prof}
+mkdir -p gpurun_out/$TAG
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$TAG" -o run -- python3 "$R/bench.py" --steps 3 --warmup 2 ${BENCHARGS} > "$R/gpurun_out/$TAG.log" 2>&1 || { tail -30 "$R/gpurun_out/$TAG.log"; exit 1; }
+cd "$R"
+f=$(find gpurun_out/$TAG -name "*kernel_stats.csv" | head -1)
+t=$(find gpurun_out/$TAG -name "*kernel_trace.csv" | head -1)
+python tools/prof_summary.py "$f" "$t" > gpurun_out/${TAG}_summary.txt
+head -40 gpurun_out/${TAG}_summary.txt
