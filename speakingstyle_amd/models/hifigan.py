@@ -86,14 +86,38 @@ class ResBlock1(nn.Module):
             x = xt + x
         return x
 
-    def forward_cl(self, x):
-        """Channel-last inference path [B, T, C] through the HIP conv kernel."""
+    def fused_ok(self, x) -> bool:
+        return (x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] in (32, 64)
+                and self.kernel_size in (3, 7, 11) and max(self.dilation) <= 5)
+
+    def forward_cl(self, x, acc=None, out_scale=1.0, x_act=None):
+        """Channel-last inference path [B, T, C].  Returns ``(acc +) block(x) * out_scale``.
+
+        GPU: the narrow stages (C = 32 / 64) run each layer as ONE fused kernel (lrelu -> dilated
+        conv -> lrelu -> conv -> + x [-> + acc, * scale], ``csrc/k_vocoder.hip``); the wide stages
+        use the implicit-GEMM conv with the lrelu in the first conv's epilogue and the residual in
+        the second's.  ``x_act``: lrelu(x) when the caller already has it (shared by the MRF branches)."""
         k = self.kernel_size
-        for c1, c2, d in zip(self.convs1, self.convs2, self.dilation):
-            xt = ops.conv1d(_lrelu(x), _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
-            xt = ops.conv1d(xt, _w(c2), c2.bias, get_padding(k, 1), 1, None)
-            x = xt + x
-        return x
+        n = len(self.convs1)
+        if self.fused_ok(x):
+            hip = ops._hip()
+            for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
+                last = i == n - 1
+                x = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE, acc=acc if last else None,
+                                       out_scale=out_scale if last else 1.0)
+            return x
+        hip = ops._hip() if (x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16) else None
+        for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
+            a = x_act if (i == 0 and x_act is not None) else _lrelu(x)
+            if hip is not None:
+                xt = hip.conv1d_infer(a, _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
+                x = hip.conv1d_infer(xt, _w(c2), c2.bias, get_padding(k, 1), 1, None, resid=x)
+            else:
+                xt = ops.conv1d(a, _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
+                x = ops.conv1d(xt, _w(c2), c2.bias, get_padding(k, 1), 1, None) + x
+        if acc is not None:
+            x = acc.add_(x)
+        return x * out_scale if out_scale != 1.0 else x
 
 
 def _lrelu(x, slope=LRELU_SLOPE):
@@ -143,11 +167,14 @@ class Generator(nn.Module):
         for i in range(self.num_upsamples):
             up = self.ups[i]
             x = conv_transpose_polyphase(_lrelu(x), _w(up), up.bias, up.stride[0], up.padding[0])
+            # MRF: mean of the branches, accumulated in place into the first branch's output
+            blocks = [self.resblocks[i * self.num_kernels + j] for j in range(self.num_kernels)]
+            x_act = None if blocks[0].fused_ok(x) else _lrelu(x)  # shared first-layer input of the branches
             xs = None
-            for j in range(self.num_kernels):
-                y = self.resblocks[i * self.num_kernels + j].forward_cl(x)
-                xs = y if xs is None else xs + y
-            x = xs * (1.0 / self.num_kernels)
+            for j, blk in enumerate(blocks):
+                last = j == self.num_kernels - 1
+                xs = blk.forward_cl(x, acc=xs, out_scale=(1.0 / self.num_kernels) if last else 1.0, x_act=x_act)
+            x = xs
         w = _w(self.conv_post)  # [1, C, 7]: N = 1 output -> VALU kernel (lrelu + conv + tanh [+ int16] fused)
         if x.is_cuda and ops.use_hip(x) and x.shape[-1] in (8, 32):
             return ops._hip().conv_post(x, w, self.conv_post.bias, 0.01, int16_scale)

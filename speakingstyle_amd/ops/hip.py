@@ -1037,6 +1037,42 @@ def token_attention(q, K, V):
     return _TokenAttnFn.apply(q, K, V)
 
 
+# ------------------------------------------------------------------------ vocoder (inference)
+_SIGS.update({"ssamd_resblock_layer": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, P]})
+
+
+def resblock_layer(x, c1, c2, d, slope, acc=None, out_scale=1.0):
+    """One fused HiFi-GAN ResBlock1 layer (csrc/k_vocoder.hip), channel-last bf16, no autograd:
+    ``(acc +) x + conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2``, times ``out_scale``.  With ``acc``
+    the result is written into ``acc`` in place (the MRF branch sum)."""
+    _need(x, torch.bfloat16, "resblock.x")
+    B, T, C = x.shape
+    K = c1.weight.shape[2]
+    assert tuple(c1.weight.shape) == (C, C, K) and tuple(c2.weight.shape) == (C, C, K)
+    w1, w2 = weight_fwd(c1.weight), weight_fwd(c2.weight)
+    b1 = c1.bias.detach().float().contiguous()
+    b2 = c2.bias.detach().float().contiguous()
+    if acc is not None:
+        _need(acc, torch.bfloat16, "resblock.acc")
+        assert acc.shape == x.shape and acc.data_ptr() != x.data_ptr(), "acc must be a separate [B, T, C] buffer"
+        out = acc
+    else:
+        out = torch.empty_like(x)
+    rc = lib().ssamd_resblock_layer(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(acc), _ptr(out), B, T, C,
+                                    K, int(d), float(slope), float(out_scale), _stream())
+    _check(rc, "ssamd_resblock_layer")
+    return out
+
+
+def conv1d_infer(x, w, b, pad, dil, act=None, resid=None):
+    """Inference conv (no autograd) with an optional residual added in the GEMM epilogue."""
+    B, L, Cin = x.shape
+    ks = 1 if w.dim() == 2 else w.shape[2]
+    bf = None if b is None else b.detach().float().contiguous()
+    return conv_gemm_raw(x.contiguous(), weight_fwd(w), bf, B, L, Cin, ks, dil, pad, w.shape[0], _ACT[act],
+                         resid=None if resid is None else resid.contiguous())
+
+
 # ------------------------------------------------------------------------ audio front-end
 _SIGS.update({"ssamd_logmel": [P, I, L_, I, I, P, P, I, F, P, P, P]})
 

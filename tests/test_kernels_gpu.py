@@ -691,3 +691,30 @@ def test_weight_prep_batched_refresh_exact():
         else:
             ef, ed = x.permute(0, 2, 1).to(torch.bfloat16), x.flip(2).permute(1, 2, 0).to(torch.bfloat16)
         assert torch.equal(f, ef.contiguous()) and torch.equal(d, ed.contiguous())
+
+
+@pytest.mark.parametrize("C,K,d,T", [(32, 3, 1, 300), (32, 11, 5, 1000), (64, 7, 3, 129), (64, 11, 5, 40), (32, 7, 1, 5)])
+def test_resblock_layer_fused(C, K, d, T):
+    """Fused HiFi-GAN ResBlock1 layer (lrelu -> dilated conv -> lrelu -> conv -> + x [+ acc, * scale])
+    vs fp32 torch, incl. sequences shorter than the halo and the in-place MRF accumulation."""
+    from speakingstyle_amd.models.hifigan import LRELU_SLOPE
+
+    torch.manual_seed(24)
+    B = 3
+    c1 = torch.nn.Conv1d(C, C, K, dilation=d, padding=d * (K - 1) // 2).to(DEV)
+    c2 = torch.nn.Conv1d(C, C, K, padding=(K - 1) // 2).to(DEV)
+    for c in (c1, c2):
+        c.weight.data.normal_(0, 0.5 / math.sqrt(C * K))
+        c.weight.data = c.weight.data.to(torch.bfloat16).float()
+    x = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    acc = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        xr = x.float().transpose(1, 2)
+        yr = xr + c2(F.leaky_relu(c1(F.leaky_relu(xr, LRELU_SLOPE)), LRELU_SLOPE))
+        yr = yr.transpose(1, 2)
+        y = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE)
+        assert _rel(y, yr) < 1e-2
+        expect = (acc.float() + yr) * (1 / 3)
+        out = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE, acc=acc, out_scale=1 / 3)
+        assert out.data_ptr() == acc.data_ptr()
+        assert _rel(out, expect) < 1e-2
