@@ -3,14 +3,15 @@
 //     y = x + conv2( lrelu( conv1_d( lrelu(x) ) + b1 ) ) + b2          [channel-last, C channels]
 //     out = (acc_in + y) * out_scale   (optional: the MRF branch sum / mean, in place)
 //
-// for the narrow high-rate stages (C = 32 / 64 at 128-256x the mel rate), where a generic GEMM
-// tile wastes most of its N width and every separate lrelu / add pass re-streams GBs of
-// activations.  One workgroup owns BM = 128 output rows of one utterance:
+// for the high-rate stages (C = 32 / 64 / 128 at 256 / 128 / 64x the mel rate), where a generic
+// GEMM tile wastes N width and every separate lrelu / add pass re-streams GBs of activations.
+// One workgroup (4 waves; 8 for C = 128) owns BM = 128 output rows of one utterance:
 //   1. stage lrelu(x) for the rows both convs need (halo d*(K-1)/2 + (K-1)/2 each side, zero
 //      outside [0, T)) into LDS;
 //   2. conv1 (dilation d) for BM + K-1 rows on v_mfma_f32_16x16x32_bf16: A fragments from the
 //      LDS tile at row offset tap*d, B fragments (weights [C][K][C], L2-resident, shared by all
-//      blocks) streamed per tap; + b1, lrelu, zero outside [0, T) -> t1 tile in LDS (bf16);
+//      blocks) DMA-staged per (tap, 32-deep chunk) into an LDS ring; + b1, lrelu, zero outside
+//      [0, T) -> t1 tile in LDS (bf16);
 //   3. conv2 (dilation 1) over the t1 tile, + b2 -> fp32 tile in LDS (aliases the x tile);
 //   4. coalesced 16-B epilogue: + x (residual), + acc_in, * out_scale -> out.
 // Each activation byte is read once (plus the halo) and written once per layer: the unfused
@@ -19,12 +20,13 @@
 
 namespace {
 
-constexpr int NT = 256;
 constexpr int BM = 128;
 constexpr int MAXD = 5;
 
 template <int C, int K>
 struct RB {
+  static constexpr int NW = C >= 128 ? 8 : 4;       // waves per block
+  static constexpr int NT = 64 * NW;
   static constexpr int H2 = (K - 1) / 2;
   static constexpr int R1 = BM + 2 * H2;           // t1 rows the second conv needs
   static constexpr int R1P = (R1 + 15) / 16 * 16;  // padded to whole 16-row MFMA blocks
@@ -34,87 +36,155 @@ struct RB {
   static constexpr int NS = C / 16;                // 16-wide output sub-tiles
   static constexpr int KC = C / 32;                // 32-deep K chunks per tap
   static constexpr int XS_BYTES = RX * LDC * 2;
-  static constexpr int OUT_BYTES = BM * C * 4;
+  static constexpr int OSP = C + 4;                // fp32 output-tile pitch (skewed banks)
+  static constexpr int OUT_BYTES = BM * OSP * 4;
   static constexpr int R0_BYTES = ((XS_BYTES > OUT_BYTES ? XS_BYTES : OUT_BYTES) + 15) / 16 * 16;
-  static constexpr int LDS = R0_BYTES + R1P * LDC * 2;
-  static constexpr int MAXRB = (NRB1 + 3) / 4;     // row blocks per wave (4 waves)
+  static constexpr int T1_BYTES = R1P * LDC * 2;
+  static constexpr int LDS = R0_BYTES + T1_BYTES + 3 * C * 64;  // + the weight-slice ring
+  static constexpr int MAXRB = (NRB1 + NW - 1) / NW;  // row blocks per wave
 };
 
 __device__ __forceinline__ float lrelu(float v, float s) { return v >= 0.f ? v : v * s; }
 
-// acc[r][s] += A(rows of `src` at offset row_off + rb*16, K-chunk) * W[:, tap, chunk]
+// acc[r][s] = sum over (tap, 32-deep chunk) of A(src rows rb*16 + tap*row_step) * W[:, tap, chunk].
+// Weight fragments are staged per step into a 3-slot LDS ring by LDS-DMA (global_load_lds: one
+// 16-B chunk per lane, no VGPR round trip), two steps ahead, so the four waves share one copy
+// of each weight slice (NWx less L2->CU traffic than per-wave loads) and its latency is hidden.
+// Slot layout: [C rows (output channel)][32 k] bf16 = 64-B rows with the 16-B chunk index XORed
+// by (row >> 2) & 3 (source-side swizzle; the DMA image is lane-linear) -> conflict-free reads.
+__device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <int C, int K>
+__device__ __forceinline__ void stage_b(const bf16_t* __restrict__ w, int step, char* slot, int tid, int wave) {
+  using R = RB<C, K>;
+  constexpr int CHUNKS = C * 4;  // 16-B chunks per slot
+  if (wave * 64 < CHUNKS) {      // wave-uniform
+    const int tap = step / R::KC, kc = step - tap * R::KC;
+    const int n = tid >> 2, p = tid & 3;
+    const int lc = p ^ ((n >> 2) & 3);  // logical chunk stored at physical chunk p
+    glds16(w + (n * K + tap) * C + kc * 32 + 8 * lc, slot + wave * 1024);
+  }
+}
+
 template <int C, int K>
 __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int row_step, const bf16_t* __restrict__ w,
-                                          int nrb, int wave, int lane, float4v (&acc)[RB<C, K>::MAXRB][RB<C, K>::NS]) {
+                                          char* bring, int nrb, int wave, int tid,
+                                          float4v (&acc)[RB<C, K>::MAXRB][RB<C, K>::NS]) {
   using R = RB<C, K>;
-  const int col = lane & 15, quad = lane >> 4;
+  constexpr int STEPS = K * R::KC;
+  constexpr int SLOT = C * 64;
+  const int lane = tid & 63, col = lane & 15, quad = lane >> 4;
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r)
 #pragma unroll
     for (int s = 0; s < R::NS; ++s) acc[r][s] = float4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int tap = 0; tap < K; ++tap) {
+  stage_b<C, K>(w, 0, bring, tid, wave);
+  if (STEPS > 1) stage_b<C, K>(w, 1, bring + SLOT, tid, wave);
+  if (STEPS > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const bf16_t* arow = src + (wave * 16 + col) * R::LDC + 8 * quad;  // row block wave + NW*r
+  // B-fragment read offsets (bytes) within a slot, per 16-column sub-tile
+  int boff[R::NS];
 #pragma unroll
-    for (int kc = 0; kc < R::KC; ++kc) {
-      short8 bf[R::NS];
+  for (int s = 0; s < R::NS; ++s) {
+    const int n = s * 16 + col;
+    boff[s] = n * 64 + ((quad ^ ((n >> 2) & 3)) << 4);
+  }
 #pragma unroll
-      for (int s = 0; s < R::NS; ++s)
-        bf[s] = *reinterpret_cast<const short8*>(w + ((long)(s * 16 + col) * K + tap) * C + kc * 32 + 8 * quad);
+  for (int step = 0; step < STEPS; ++step) {
+    if (step + 2 < STEPS) stage_b<C, K>(w, step + 2, bring + ((step + 2) % 3) * SLOT, tid, wave);
+    const int tap = step / R::KC, kc = step - tap * R::KC;
+    const bf16_t* ap = arow + tap * row_step * R::LDC + kc * 32;
+    const char* bs = bring + (step % 3) * SLOT;
+    short8 a[R::MAXRB], bf[R::NS];
 #pragma unroll
-      for (int r = 0; r < R::MAXRB; ++r) {
-        const int rb = wave + 4 * r;
-        if (rb < nrb) {
-          const short8 a = *reinterpret_cast<const short8*>(
-              src + (long)(rb * 16 + col + tap * row_step) * R::LDC + kc * 32 + 8 * quad);
+    for (int s = 0; s < R::NS; ++s) bf[s] = *reinterpret_cast<const short8*>(bs + boff[s]);
 #pragma unroll
-          for (int s = 0; s < R::NS; ++s) acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bf[s], acc[r][s], 0, 0, 0);
-        }
+    for (int r = 0; r < R::MAXRB; ++r)
+      if (wave + R::NW * r < nrb) a[r] = *reinterpret_cast<const short8*>(ap + r * R::NW * 16 * R::LDC);
+#pragma unroll
+    for (int r = 0; r < R::MAXRB; ++r) {
+      if (wave + R::NW * r < nrb) {
+#pragma unroll
+        for (int s = 0; s < R::NS; ++s)
+          acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r], bf[s], acc[r][s], 0, 0, 0);
       }
+    }
+    if (step + 1 < STEPS) {
+      // step+1's slice landed (only step+2's DMA may still be in flight), and every wave is done
+      // reading this step's slot before step+1 re-fills it with step+3
+      if (step + 2 < STEPS) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
   }
 }
 
 template <int C, int K>
-__global__ void __launch_bounds__(NT) resblock_layer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
+__global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
                                                             const float* __restrict__ b1, const bf16_t* __restrict__ w2,
                                                             const float* __restrict__ b2, const bf16_t* acc_in,
                                                             bf16_t* out, int T, int tiles, int d, float slope,
-                                                            float out_scale) {
+                                                            float out_scale, int dbg) {
   using R = RB<C, K>;
+  constexpr int NT = R::NT;
+  constexpr int CH = C / 8;                                  // 16-B chunks per row
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  bf16_t* xs = reinterpret_cast<bf16_t*>(lds);               // [RX][LDC]  lrelu(x) tile
-  float* os = reinterpret_cast<float*>(lds);                 // [BM][C]    conv2 + b2 (after conv1)
-  bf16_t* t1 = reinterpret_cast<bf16_t*>(lds + R::R0_BYTES);  // [R1P][LDC] lrelu(conv1 + b1)
+  bf16_t* xs = reinterpret_cast<bf16_t*>(lds);               // [RX][LDC]   lrelu(x) tile
+  float* os = reinterpret_cast<float*>(lds);                 // [BM][OSP]   conv2 + b2 (after conv1)
+  bf16_t* t1 = reinterpret_cast<bf16_t*>(lds + R::R0_BYTES);  // [R1P][LDC]  lrelu(conv1 + b1)
+  char* bring = reinterpret_cast<char*>(lds + R::R0_BYTES + R::T1_BYTES);  // 3 x [C][32] weight slices
   const int b = blockIdx.x / tiles, t0 = (blockIdx.x - b * tiles) * BM;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row-block tests are scalar
   const int col = lane & 15, quad = lane >> 4;
   const int h1 = d * (K - 1) / 2;
   const bf16_t* xb = x + (long)b * T * C;
 
-  // 1. lrelu(x) rows [t0 - h1 - H2, ...): only the rows this dilation reads
-  const int rows_x = R::R1P + (K - 1) * d;
-  for (int q = tid; q < rows_x * (C / 8); q += NT) {
-    const int r = q / (C / 8), c0 = (q - r * (C / 8)) * 8;
-    const int t = t0 - h1 - R::H2 + r;
-    short8 v;
-    if (t >= 0 && t < T) {
-      v = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
+  // 1. lrelu(x) rows [t0 - h1 - H2, ...) -- all global loads of the thread first, then convert + store
+  {
+    constexpr int IT = (R::RX * CH + NT - 1) / NT;
+    const int rows_x = R::R1P + (K - 1) * d;
+    short8 v[IT];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = (short)f2bf(lrelu(bf2f((bf16_t)v[i]), slope));
-    } else {
+    for (int it = 0; it < IT; ++it) {
+      const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
+      const int t = t0 - h1 - R::H2 + r;
+      if (r < rows_x && t >= 0 && t < T && !(dbg & 4)) {
+        v[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = 0;
+        for (int i = 0; i < 8; ++i) v[it][i] = 0;
+      }
     }
-    *reinterpret_cast<short8*>(xs + r * R::LDC + c0) = v;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
+      if (r < rows_x) {
+        short8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(lrelu(bf2f((bf16_t)v[it][i]), slope));
+        *reinterpret_cast<short8*>(xs + r * R::LDC + c0) = o;
+      }
+    }
   }
   __syncthreads();
 
   // 2. conv1 (dilation d): t1 row i <- x rows i + tap*d
   float4v acc[R::MAXRB][R::NS];
-  conv_tile<C, K>(xs, d, w1, R::NRB1, wave, lane, acc);
+  if (!(dbg & 1)) conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
+  else
+#pragma unroll
+    for (int r = 0; r < R::MAXRB; ++r)
+#pragma unroll
+      for (int s = 0; s < R::NS; ++s) acc[r][s] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
-    const int rb = wave + 4 * r;
+    const int rb = wave + R::NW * r;
     if (rb < R::NRB1) {
 #pragma unroll
       for (int s = 0; s < R::NS; ++s) {
@@ -133,42 +203,58 @@ __global__ void __launch_bounds__(NT) resblock_layer_kernel(const bf16_t* __rest
   __syncthreads();  // t1 complete; the x tile is dead from here on (os aliases it)
 
   // 3. conv2 (dilation 1): out row j <- t1 rows j + tap
-  conv_tile<C, K>(t1, 1, w2, R::NRB2, wave, lane, acc);
+  if (!(dbg & 2)) conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
-    const int rb = wave + 4 * r;
+    const int rb = wave + R::NW * r;
     if (rb < R::NRB2) {
 #pragma unroll
       for (int s = 0; s < R::NS; ++s) {
         const int ch = s * 16 + col;
         const float bias = b2[ch];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * C + ch] = acc[r][s][i] + bias;
+        for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + ch] = acc[r][s][i] + bias;
       }
     }
   }
   __syncthreads();
 
-  // 4. + residual (+ MRF accumulator), scale, coalesced 16-B stores
-  bf16_t* ob = out + (long)b * T * C;
-  const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
-  for (int q = tid; q < BM * (C / 8); q += NT) {
-    const int j = q / (C / 8), c0 = (q - j * (C / 8)) * 8;
-    const int t = t0 + j;
-    if (t >= T) continue;
-    const short8 xr = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
-    short8 ar;
-    if (ab) ar = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
-    short8 o;
+  // 4. + residual (+ MRF accumulator), scale, coalesced 16-B stores (loads batched first)
+  {
+    constexpr int IT = BM * CH / NT;
+    bf16_t* ob = out + (long)b * T * C;
+    const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
+    short8 xr[IT], ar[IT];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float v = os[j * C + c0 + i] + bf2f((bf16_t)xr[i]);
-      if (ab) v += bf2f((bf16_t)ar[i]);
-      o[i] = (short)f2bf(v * out_scale);
+    for (int it = 0; it < IT; ++it) {
+      const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+      const int t = t0 + j;
+      if (t < T) {
+        xr[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
+        if (ab) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
+      }
     }
-    *reinterpret_cast<short8*>(ob + (long)t * C + c0) = o;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+      const int t = t0 + j;
+      if (t >= T) continue;
+      const float4 o0 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0);
+      const float4 o1 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0 + 4);
+      const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+      short8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v = ov[i] + bf2f((bf16_t)xr[it][i]);
+        if (ab) v += bf2f((bf16_t)ar[it][i]);
+        o[i] = (short)f2bf(v * out_scale);
+      }
+      *reinterpret_cast<short8*>(ob + (long)t * C + c0) = o;
+    }
   }
 }
+
+static int g_rb_debug = 0;  // A/B timing switch: bit 0 skip conv1 MFMAs, bit 1 conv2, bit 2 x loads
 
 template <int C, int K>
 int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
@@ -180,15 +266,17 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
     lds_set = true;
   }
   const int tiles = (T + BM - 1) / BM;
-  hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3((long)B * tiles), dim3(NT), R::LDS, s, x, w1, b1, w2, b2,
-                     acc_in, out, T, tiles, d, slope, out_scale);
+  hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
+                     acc_in, out, T, tiles, d, slope, out_scale, g_rb_debug);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
+SSAMD_API void ssamd_resblock_debug(int v) { g_rb_debug = v; }
+
 // x / out / acc_in [B, T, C] bf16 (acc_in may alias out, or be null); w1 / w2 bf16 [C][K][C] (the
-// implicit-GEMM forward image); b1 / b2 fp32 [C].  C in {32, 64}, K in {3, 7, 11}, 1 <= d <= 5.
+// implicit-GEMM forward image); b1 / b2 fp32 [C].  C in {32, 64, 128}, K in {3, 7, 11}, 1 <= d <= 5.
 SSAMD_API int ssamd_resblock_layer(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
                                    const float* b2, const bf16_t* acc_in, bf16_t* out, int B, int T, int C, int K,
                                    int d, float slope, float out_scale, hipStream_t s) {
@@ -198,6 +286,7 @@ SSAMD_API int ssamd_resblock_layer(const bf16_t* x, const bf16_t* w1, const floa
   if (C == CC && K == KK) return launch_rb<CC, KK>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, s);
   RB_CASE(32, 3) RB_CASE(32, 7) RB_CASE(32, 11)
   RB_CASE(64, 3) RB_CASE(64, 7) RB_CASE(64, 11)
+  RB_CASE(128, 3) RB_CASE(128, 7) RB_CASE(128, 11)
 #undef RB_CASE
   return -2;
 }

@@ -87,13 +87,13 @@ class ResBlock1(nn.Module):
         return x
 
     def fused_ok(self, x) -> bool:
-        return (x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] in (32, 64)
+        return (x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] in (32, 64, 128)
                 and self.kernel_size in (3, 7, 11) and max(self.dilation) <= 5)
 
     def forward_cl(self, x, acc=None, out_scale=1.0, x_act=None):
         """Channel-last inference path [B, T, C].  Returns ``(acc +) block(x) * out_scale``.
 
-        GPU: the narrow stages (C = 32 / 64) run each layer as ONE fused kernel (lrelu -> dilated
+        GPU: the high-rate stages (C = 32 / 64 / 128) run each layer as ONE fused kernel (lrelu -> dilated
         conv -> lrelu -> conv -> + x [-> + acc, * scale], ``csrc/k_vocoder.hip``); the wide stages
         use the implicit-GEMM conv with the lrelu in the first conv's epilogue and the residual in
         the second's.  ``x_act``: lrelu(x) when the caller already has it (shared by the MRF branches)."""
