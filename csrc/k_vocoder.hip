@@ -5,7 +5,7 @@
 //
 // for the high-rate stages (C = 32 / 64 / 128 at 256 / 128 / 64x the mel rate), where a generic
 // GEMM tile wastes N width and every separate lrelu / add pass re-streams GBs of activations.
-// One workgroup (4 waves; 8 for C = 128) owns BM = 128 output rows of one utterance:
+// One workgroup (4 waves; 8 for C = 128) owns BM (~118-250, see RB) output rows of one utterance:
 //   1. stage lrelu(x) for the rows both convs need (halo d*(K-1)/2 + (K-1)/2 each side, zero
 //      outside [0, T)) into LDS;
 //   2. conv1 (dilation d) for BM + K-1 rows on v_mfma_f32_16x16x32_bf16: A fragments from the
@@ -20,35 +20,48 @@
 
 namespace {
 
-constexpr int BM = 128;
 constexpr int MAXD = 5;
 
+// Work split: NW waves = WR (row groups) x WC (column groups); each wave owns RPW 16-row blocks
+// x NSW 16-column sub-tiles, so a 32-deep step costs RPW + NSW ds_read_b128 for RPW * NSW MFMAs
+// (C = 128: 2 + 4 reads / 8 MFMAs, under the LDS array's 1 read per 16-cycle MFMA at 2 waves per
+// SIMD).  The output tile BM = 16 * RPW * WR - (K - 1) is chosen so that conv1's BM + K - 1 rows
+// fill the row blocks exactly (no straggler block on one wave).
 template <int C, int K>
 struct RB {
   static constexpr int NW = C >= 128 ? 8 : 4;       // waves per block
   static constexpr int NT = 64 * NW;
+  static constexpr int WC = C >= 128 ? 2 : 1;       // column groups
+  static constexpr int WR = NW / WC;                // row groups
+  static constexpr int RPW = 2;                     // row blocks per wave
   static constexpr int H2 = (K - 1) / 2;
-  static constexpr int R1 = BM + 2 * H2;           // t1 rows the second conv needs
-  static constexpr int R1P = (R1 + 15) / 16 * 16;  // padded to whole 16-row MFMA blocks
-  static constexpr int NRB1 = R1P / 16, NRB2 = BM / 16;
+  static constexpr int NRB1 = RPW * WR;             // conv1 row blocks
+  static constexpr int R1P = NRB1 * 16;             // t1 rows (= R1: no padding)
+  static constexpr int R1 = R1P;
+  static constexpr int BM = R1 - 2 * H2;            // output rows per block
+  static constexpr int NRB2 = (BM + 15) / 16;
   static constexpr int LDC = C + 8;                // LDS pitch (bf16): 16-B rows, conflict-free row reads
   static constexpr int RX = R1P + (K - 1) * MAXD;  // staged x rows at the largest dilation
   static constexpr int NS = C / 16;                // 16-wide output sub-tiles
+  static constexpr int NSW = NS / WC;              // sub-tiles per wave
   static constexpr int KC = C / 32;                // 32-deep K chunks per tap
+  static constexpr int KC2 = KC >= 2 ? 2 : 1;      // 32-deep chunks per pipeline step (one barrier each)
+  static constexpr int SLOT = KC2 * C * 64;        // ring slot: KC2 sub-slices [C][32] bf16
   static constexpr int XS_BYTES = RX * LDC * 2;
   static constexpr int OSP = C + 4;                // fp32 output-tile pitch (skewed banks)
-  static constexpr int OUT_BYTES = BM * OSP * 4;
+  static constexpr int OUT_BYTES = NRB2 * 16 * OSP * 4;
   static constexpr int R0_BYTES = ((XS_BYTES > OUT_BYTES ? XS_BYTES : OUT_BYTES) + 15) / 16 * 16;
   static constexpr int T1_BYTES = R1P * LDC * 2;
-  static constexpr int LDS = R0_BYTES + T1_BYTES + 3 * C * 64;  // + the weight-slice ring
-  static constexpr int MAXRB = (NRB1 + NW - 1) / NW;  // row blocks per wave
+  static constexpr int LDS = R0_BYTES + T1_BYTES + 3 * SLOT;  // + the weight-slice ring
+  static constexpr int MAXRB = RPW;
+  static_assert(NRB2 <= NRB1 && LDS <= 160 * 1024, "resblock tile");
 };
 
 __device__ __forceinline__ float lrelu(float v, float s) { return v >= 0.f ? v : v * s; }
 
 // acc[r][s] = sum over (tap, 32-deep chunk) of A(src rows rb*16 + tap*row_step) * W[:, tap, chunk].
 // Weight fragments are staged per step into a 3-slot LDS ring by LDS-DMA (global_load_lds: one
-// 16-B chunk per lane, no VGPR round trip), two steps ahead, so the four waves share one copy
+// 16-B chunk per lane, no VGPR round trip), three steps ahead, so the waves share one copy
 // of each weight slice (NWx less L2->CU traffic than per-wave loads) and its latency is hidden.
 // Slot layout: [C rows (output channel)][32 k] bf16 = 64-B rows with the 16-B chunk index XORed
 // by (row >> 2) & 3 (source-side swizzle; the DMA image is lane-linear) -> conflict-free reads.
@@ -60,68 +73,88 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
 template <int C, int K>
 __device__ __forceinline__ void stage_b(const bf16_t* __restrict__ w, int step, char* slot, int tid, int wave) {
   using R = RB<C, K>;
-  constexpr int CHUNKS = C * 4;  // 16-B chunks per slot
+  constexpr int CHUNKS = C * 4;  // 16-B chunks per [C][32] sub-slice
   if (wave * 64 < CHUNKS) {      // wave-uniform
-    const int tap = step / R::KC, kc = step - tap * R::KC;
+    const int c0 = step * R::KC2, tap = c0 / R::KC, kc = c0 - tap * R::KC;
     const int n = tid >> 2, p = tid & 3;
     const int lc = p ^ ((n >> 2) & 3);  // logical chunk stored at physical chunk p
-    glds16(w + (n * K + tap) * C + kc * 32 + 8 * lc, slot + wave * 1024);
+#pragma unroll
+    for (int j = 0; j < R::KC2; ++j)
+      glds16(w + (n * K + tap) * C + (kc + j) * 32 + 8 * lc, slot + j * C * 64 + wave * 1024);
   }
 }
 
 template <int C, int K>
 __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int row_step, const bf16_t* __restrict__ w,
                                           char* bring, int nrb, int wave, int tid,
-                                          float4v (&acc)[RB<C, K>::MAXRB][RB<C, K>::NS]) {
+                                          float4v (&acc)[RB<C, K>::MAXRB][RB<C, K>::NSW]) {
   using R = RB<C, K>;
-  constexpr int STEPS = K * R::KC;
-  constexpr int SLOT = C * 64;
+  constexpr int STEPS = K * R::KC / R::KC2;
+  constexpr int SLOT = R::SLOT;
   const int lane = tid & 63, col = lane & 15, quad = lane >> 4;
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r)
 #pragma unroll
-    for (int s = 0; s < R::NS; ++s) acc[r][s] = float4v{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < R::NSW; ++s) acc[r][s] = float4v{0.f, 0.f, 0.f, 0.f};
+  const int wr = wave % R::WR, wc = wave / R::WR;
+  // Ring: slot j % 3 holds step j.  DMA runs three steps ahead of the MFMAs and the fragments of
+  // step+1 are read into registers while step's MFMAs run, so one barrier per step only has to
+  // cover "slot step+1 landed" and "everyone is done reading slot step" (re-filled with step+3).
   stage_b<C, K>(w, 0, bring, tid, wave);
   if (STEPS > 1) stage_b<C, K>(w, 1, bring + SLOT, tid, wave);
-  if (STEPS > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  if (STEPS > 2) stage_b<C, K>(w, 2, bring + 2 * SLOT, tid, wave);
+  // (vmcnt counts this thread's DMA pieces: KC2 per step)
+  if (STEPS > 2 && R::KC2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (STEPS > 2 || (STEPS > 1 && R::KC2 == 2)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (STEPS > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  const bf16_t* arow = src + (wave * 16 + col) * R::LDC + 8 * quad;  // row block wave + NW*r
-  // B-fragment read offsets (bytes) within a slot, per 16-column sub-tile
-  int boff[R::NS];
+  const bf16_t* arow = src + (wr * 16 + col) * R::LDC + 8 * quad;  // row block wr + WR*r
+  // B-fragment read offsets (bytes) within a slot, per 16-column sub-tile of this wave
+  int boff[R::NSW];
 #pragma unroll
-  for (int s = 0; s < R::NS; ++s) {
-    const int n = s * 16 + col;
+  for (int s = 0; s < R::NSW; ++s) {
+    const int n = (wc * R::NSW + s) * 16 + col;
     boff[s] = n * 64 + ((quad ^ ((n >> 2) & 3)) << 4);
   }
+  short8 a[2][R::KC2][R::MAXRB], bf[2][R::KC2][R::NSW];
+  auto load = [&](int step, int buf) {
+    const int c0 = step * R::KC2, tap = c0 / R::KC, kc = c0 - tap * R::KC;
+#pragma unroll
+    for (int j = 0; j < R::KC2; ++j) {
+      const bf16_t* ap = arow + tap * row_step * R::LDC + (kc + j) * 32;
+      const char* bs = bring + (step % 3) * SLOT + j * C * 64;
+#pragma unroll
+      for (int s = 0; s < R::NSW; ++s) bf[buf][j][s] = *reinterpret_cast<const short8*>(bs + boff[s]);
+#pragma unroll
+      for (int r = 0; r < R::MAXRB; ++r)
+        if (wr + R::WR * r < nrb) a[buf][j][r] = *reinterpret_cast<const short8*>(ap + r * R::WR * 16 * R::LDC);
+    }
+  };
+  load(0, 0);
 #pragma unroll
   for (int step = 0; step < STEPS; ++step) {
-    if (step + 2 < STEPS) stage_b<C, K>(w, step + 2, bring + ((step + 2) % 3) * SLOT, tid, wave);
-    const int tap = step / R::KC, kc = step - tap * R::KC;
-    const bf16_t* ap = arow + tap * row_step * R::LDC + kc * 32;
-    const char* bs = bring + (step % 3) * SLOT;
-    short8 a[R::MAXRB], bf[R::NS];
-#pragma unroll
-    for (int s = 0; s < R::NS; ++s) bf[s] = *reinterpret_cast<const short8*>(bs + boff[s]);
-#pragma unroll
-    for (int r = 0; r < R::MAXRB; ++r)
-      if (wave + R::NW * r < nrb) a[r] = *reinterpret_cast<const short8*>(ap + r * R::NW * 16 * R::LDC);
-#pragma unroll
-    for (int r = 0; r < R::MAXRB; ++r) {
-      if (wave + R::NW * r < nrb) {
-#pragma unroll
-        for (int s = 0; s < R::NS; ++s)
-          acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r], bf[s], acc[r][s], 0, 0, 0);
-      }
-    }
+    const int cur = step & 1;
     if (step + 1 < STEPS) {
-      // step+1's slice landed (only step+2's DMA may still be in flight), and every wave is done
-      // reading this step's slot before step+1 re-fills it with step+3
-      if (step + 2 < STEPS) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+      if (step + 2 < STEPS && R::KC2 == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      else if (step + 2 < STEPS) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      if (step + 3 < STEPS) stage_b<C, K>(w, step + 3, bring + (step % 3) * SLOT, tid, wave);
+      load(step + 1, cur ^ 1);
+    }
+#pragma unroll
+    for (int r = 0; r < R::MAXRB; ++r) {
+      if (wr + R::WR * r < nrb) {
+#pragma unroll
+        for (int j = 0; j < R::KC2; ++j)
+#pragma unroll
+          for (int s = 0; s < R::NSW; ++s)
+            acc[r][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cur][j][r], bf[cur][j][s], acc[r][s], 0, 0, 0);
+      }
     }
   }
+  // the caller's next phase re-uses the ring / tiles only after its own __syncthreads
 }
 
 template <int C, int K>
@@ -135,10 +168,10 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   constexpr int CH = C / 8;                                  // 16-B chunks per row
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(lds);               // [RX][LDC]   lrelu(x) tile
-  float* os = reinterpret_cast<float*>(lds);                 // [BM][OSP]   conv2 + b2 (after conv1)
+  float* os = reinterpret_cast<float*>(lds);                 // [NRB2*16][OSP] conv2 + b2 (after conv1)
   bf16_t* t1 = reinterpret_cast<bf16_t*>(lds + R::R0_BYTES);  // [R1P][LDC]  lrelu(conv1 + b1)
   char* bring = reinterpret_cast<char*>(lds + R::R0_BYTES + R::T1_BYTES);  // 3 x [C][32] weight slices
-  const int b = blockIdx.x / tiles, t0 = (blockIdx.x - b * tiles) * BM;
+  const int b = blockIdx.x / tiles, t0 = (blockIdx.x - b * tiles) * R::BM;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row-block tests are scalar
   const int col = lane & 15, quad = lane >> 4;
@@ -175,20 +208,21 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   __syncthreads();
 
   // 2. conv1 (dilation d): t1 row i <- x rows i + tap*d
-  float4v acc[R::MAXRB][R::NS];
+  float4v acc[R::MAXRB][R::NSW];
+  const int wr = wave % R::WR, wc = wave / R::WR;
   if (!(dbg & 1)) conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
   else
 #pragma unroll
     for (int r = 0; r < R::MAXRB; ++r)
 #pragma unroll
-      for (int s = 0; s < R::NS; ++s) acc[r][s] = float4v{0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < R::NSW; ++s) acc[r][s] = float4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
-    const int rb = wave + R::NW * r;
+    const int rb = wr + R::WR * r;
     if (rb < R::NRB1) {
 #pragma unroll
-      for (int s = 0; s < R::NS; ++s) {
-        const int ch = s * 16 + col;
+      for (int s = 0; s < R::NSW; ++s) {
+        const int ch = (wc * R::NSW + s) * 16 + col;
         const float bias = b1[ch];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -206,11 +240,11 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   if (!(dbg & 2)) conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
-    const int rb = wave + R::NW * r;
+    const int rb = wr + R::WR * r;
     if (rb < R::NRB2) {
 #pragma unroll
-      for (int s = 0; s < R::NS; ++s) {
-        const int ch = s * 16 + col;
+      for (int s = 0; s < R::NSW; ++s) {
+        const int ch = (wc * R::NSW + s) * 16 + col;
         const float bias = b2[ch];
 #pragma unroll
         for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + ch] = acc[r][s][i] + bias;
@@ -221,7 +255,8 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
 
   // 4. + residual (+ MRF accumulator), scale, coalesced 16-B stores (loads batched first)
   {
-    constexpr int IT = BM * CH / NT;
+    constexpr int BM = R::BM;
+    constexpr int IT = (BM * CH + NT - 1) / NT;
     bf16_t* ob = out + (long)b * T * C;
     const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
     short8 xr[IT], ar[IT];
@@ -229,7 +264,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     for (int it = 0; it < IT; ++it) {
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
       const int t = t0 + j;
-      if (t < T) {
+      if (j < BM && t < T) {
         xr[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
         if (ab) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
       }
@@ -238,7 +273,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     for (int it = 0; it < IT; ++it) {
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
       const int t = t0 + j;
-      if (t >= T) continue;
+      if (j >= BM || t >= T) continue;
       const float4 o0 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0);
       const float4 o1 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0 + 4);
       const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
@@ -265,7 +300,7 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
     allow_lds(resblock_layer_kernel<C, K>, R::LDS);
     lds_set = true;
   }
-  const int tiles = (T + BM - 1) / BM;
+  const int tiles = (T + R::BM - 1) / R::BM;
   hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
                      acc_in, out, T, tiles, d, slope, out_scale, g_rb_debug);
   return (int)hipGetLastError();
