@@ -1,38 +1,47 @@
 #!/usr/bin/env python
-"""Headline benchmark: FastSpeech2 training throughput in mel-frames/s (node).
+"""Headline benchmark: FastSpeech2 training throughput (mel-frames/s, node) + synthesis RTF.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
-is launched by torch.distributed.run with one rank per GPU (RCCL over xGMI).
-W untimed warm-up steps, then exactly K full training steps (forward + loss +
-backward + bucketed gradient all-reduce + clip + Adam + LR schedule) bracketed
-by barrier + device synchronise on both sides; the time is the MAX over ranks;
-rank 0 prints one JSON line.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  For N>1 the
+driver launches it under torch.distributed.run (one rank per GPU, RCCL over
+xGMI); run directly with ``--gpus N`` and no torchrun environment, this script
+starts the N ranks itself (``speakingstyle_amd.benchmark.launch``: a torchrun
+child process of a parent that never initialises the GPU) and exits with the
+child's status.  Every rank asserts WORLD_SIZE == N.
 
+Training (headline ``value``): W untimed warm-up steps (>= 1 under DP: the
+gradient-bucket calibration pass), then exactly K full training steps (forward
++ loss + backward + bucketed gradient all-reduce + clip + Adam + LR schedule)
+bracketed by barrier + device synchronise on both sides; time = MAX over ranks;
+value = valid mel frames of the K steps summed over ranks / that time.
 Config = BASELINE.json's headline: LJSpeech FastSpeech2 (model.yaml shape: 4+6
 FFT blocks, d=256, no style encoder), bf16 compute with fp32 master weights /
 Adam state, synthetic LJSpeech-shaped data (phoneme counts drawn from the real
 LJSpeech metadata, ~8.1 frames per phoneme, groups of 4 batches sorted by text
 length exactly like the reference loader), random-init weights.  Scaling is
 weak: every rank runs ``--batch`` utterances (default: the config's
-``optimizer.batch_size`` = 200), so the global batch is N*200.
-``value`` = total valid mel frames consumed by the K timed steps over all ranks
-divided by the max-over-ranks wall time.
+``optimizer.batch_size`` = 200), global batch N*200.  (``train.py`` instead
+splits ``batch_size`` across ranks -- the reference semantics of a global batch.)
+
+Synthesis (``synth_rtf`` field, BASELINE's second metric): text ids -> int16 wav
+through FastSpeech2 + style encoder (``--synth-config``, default BC2013 = FiLM
+reference encoder on a reference mel) + HiFi-GAN V1, batch 256 per GPU,
+independent shards per rank; RTF = max-over-ranks wall / total audio seconds.
+See ``speakingstyle_amd/benchmark.py`` for the duration-injection detail.
 """
 from __future__ import annotations
 
 import argparse
-import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_FRAMES_PER_S = 2.5e4  # derived GTX-1080Ti lower bound (train mel-frames/s)
+BASELINE_RTF = 1.33  # batch-1 E2E synthesis on the authors' GPU node (notebooks/control.ipynb:778)
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -41,103 +50,92 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (default: config batch_size)")
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic batches cycled through")
     ap.add_argument("--backend", default=None, choices=[None, "hip", "reference"])
-    ap.add_argument("--profile-steps", type=int, default=0)
-    args = ap.parse_args()
+    ap.add_argument("--synth-config", default="BC2013")
+    ap.add_argument("--synth-batch", type=int, default=256)
+    ap.add_argument("--synth-steps", type=int, default=3, help="0 disables the synthesis phase")
+    ap.add_argument("--synth-warmup", type=int, default=1)
+    ap.add_argument("--frames-per-phone", type=float, default=8.1)
+    ap.add_argument("--tiny", action="store_true", help="plumbing-size model (CPU launcher tests only)")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse()
+    from speakingstyle_amd import benchmark as B
+
+    if B.needs_launch(args.gpus):
+        sys.exit(B.launch(os.path.abspath(__file__), args.gpus, sys.argv[1:]))
+
+    from speakingstyle_amd.parallel import ddp
+
+    ddp.fail_fast(run, args)
+
+
+def run(args):
     # variable-shape batches: let the caching allocator grow segments instead of re-mallocing
     os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
-    os.environ.setdefault("PYTORCH_CUDA_ALLOC_CONF", "expandable_segments:True")
-
     import torch
 
+    from speakingstyle_amd import benchmark as B
     from speakingstyle_amd import ops
-    from speakingstyle_amd.config import load_named
-    from speakingstyle_amd.data.synthetic import SyntheticBatches
-    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
     from speakingstyle_amd.parallel import ddp
-    from speakingstyle_amd.train.trainer import Trainer
 
     if args.backend:
         ops.set_backend(args.backend)
-    rank, world, local_rank = ddp.init_distributed()
+    rank, world, local_rank = ddp.init_distributed(expect_world=args.gpus)
     cuda = torch.cuda.is_available()
     device = torch.device("cuda", local_rank) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(device)
-    pp, mc, tc = load_named(args.config)
-    batch = args.batch or int(tc["optimizer"]["batch_size"])
-    torch.manual_seed(1234)
-    model = FastSpeech2(pp, mc).to(device)
-    model.set_compute_dtype(torch.bfloat16 if cuda else torch.float32)
-    ddp.broadcast_module_state(model)
-    trainer = Trainer(model, (pp, mc, tc))
+    seen = torch.distributed.get_world_size() if world > 1 else 1
 
-    gen = SyntheticBatches(batch, device=device, max_seq_len=mc["max_seq_len"], seed=1000 + rank,
-                           frame_level=pp["preprocessing"]["pitch"]["feature"] == "frame_level")
-    pool = []
-    for _ in range(args.pool):
-        b = gen.make_batch()
-        pool.append((b, gen.last_valid_frames))
-    # largest padded batch first: the first warm-up step sizes the allocator for all others
-    pool.sort(key=lambda e: -(e[0][0].__len__() * e[0][8]))
+    tr = B.train_phase(args, rank, world, device)
+    sy = B.synth_phase(args, rank, world, device) if args.synth_steps > 0 else None
 
-    def step(i):
-        b, frames = pool[i % len(pool)]
-        trainer.train_step(b)
-        return frames
-
-    for i in range(args.warmup):
-        step(i)
-    if cuda:
-        torch.cuda.synchronize()
-    ddp.barrier()
-    if cuda:
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    frames = 0
-    for i in range(args.steps):
-        frames += step(args.warmup + i)
-    if cuda:
-        torch.cuda.synchronize()
-    ddp.barrier()
-    if cuda:
-        torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-
-    stats = torch.tensor([elapsed, float(frames)], dtype=torch.float64, device=device)
-    if world > 1:
-        import torch.distributed as dist
-
-        t_max = stats[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        f_sum = stats[1:2].clone()
-        dist.all_reduce(f_sum, op=dist.ReduceOp.SUM)
-        elapsed, frames = float(t_max.item()), float(f_sum.item())
-    value = frames / elapsed
-    if rank == 0:
-        print(json.dumps({
-            "metric": "train mel-frames/sec (node)",
-            "value": round(value, 1),
-            "unit": "mel-frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_FRAMES_PER_S, 3),
-            "dtype": "bf16" if cuda else "fp32",
-            "data": "synthetic (LJSpeech-shaped lengths, random-init weights)",
-            "config": {
-                "model": f"FastSpeech2 ({args.config} model.yaml)",
-                "global_batch": batch * world,
-                "seq_len": "T~LJSpeech phonemes, M<=1000 mel frames",
-                "parallelism": f"dp{world}",
+    value = tr["frames"] / tr["elapsed"]
+    rec = {
+        "metric": "train mel-frames/sec (node)",
+        "value": round(value, 1),
+        "unit": "mel-frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": tr["warmup"],
+        "ms_per_step": round(1000.0 * tr["elapsed"] / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_FRAMES_PER_S, 3),
+        "dtype": "bf16" if cuda else "fp32",
+        "data": "synthetic (LJSpeech-shaped lengths, random-init weights)",
+        "config": {
+            "model": f"FastSpeech2 ({args.config} model.yaml)" + (" tiny" if args.tiny else ""),
+            "global_batch": tr["batch"] * world,
+            "seq_len": "T~LJSpeech phonemes, M<=1000 mel frames",
+            "parallelism": f"dp{world}",
+        },
+        "world_size_seen": seen,
+        "grad_buckets": tr["buckets"],
+        "bucket_overlap": tr["overlap"],
+        "skipped_steps": tr["skipped_steps"],
+    }
+    if sy is not None:
+        rec.update({
+            "synth_rtf": sy["rtf"],
+            "synth_vs_baseline": round(BASELINE_RTF / sy["rtf"], 1),
+            "synth": {
+                "metric": "synth RTF (text ids -> int16 wav; lower is better)",
+                "model": f"FastSpeech2 ({args.synth_config}, style encoder on a reference mel) + HiFi-GAN V1"
+                         + (" tiny" if args.tiny else ""),
+                "batch_per_gpu": args.synth_batch, "steps": args.synth_steps, "warmup": args.synth_warmup,
+                "audio_seconds": round(sy["audio_s"], 2), "wall_s": round(sy["wall"], 4),
+                "mel_frames_per_utt": round(sy["frames_per_utt"], 1),
+                "parallelism": f"dp{world} (independent shards)",
             },
-        }), flush=True)
+        })
+    if rank == 0:
+        B.report(rec)
     if world > 1:
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+        ddp.barrier()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,229 @@
+"""Benchmark harness behind ``bench.py`` / ``bench_synth.py``.
+
+Two measurements (BASELINE.json: "train mel-frames/sec (node) + synth RTF"):
+
+* ``train_phase`` -- W untimed + K timed full training steps of FastSpeech2
+  (forward + loss + backward + bucketed RCCL gradient all-reduce + clip + Adam +
+  LR schedule) on synthetic LJSpeech-shaped batches; value = valid mel frames
+  summed over ranks / max-over-ranks wall time.
+* ``synth_phase`` -- text ids -> int16 waveform with the style encoder in the
+  loop (FastSpeech2 + FiLM reference encoder or GST on a reference mel, +
+  HiFi-GAN V1 generator, int16 conversion on the device), batch 256 per GPU;
+  RTF = max-over-ranks wall time / seconds of audio summed over ranks.  The
+  random-init duration predictor would emit ~0 frames, so its
+  output layer is re-initialised to predict ~``frames_per_phone`` frames with a
+  little spread (bias = log(fpp + 1), weight ~ N(0, 0.005)); everything else --
+  duration rounding, the one D2H of the mel lengths, length regulation, decoder,
+  PostNet, vocoder -- is the real inference path (reference
+  ``synthesize.py:128-150``, ``utils/model.py:97-115``).
+
+Multi-GPU: ``launch()`` starts one rank per GPU with ``torch.distributed.run``
+as a *child process* of a parent that never touched the GPU (re-exec'ing a
+process that initialised HIP is forbidden on this platform), and every rank
+asserts the world size it was promised.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def needs_launch(n_gpus: int) -> bool:
+    return n_gpus > 1 and "WORLD_SIZE" not in os.environ
+
+
+def launch(script: str, n: int, argv) -> int:
+    """Run ``script argv`` on ``n`` local ranks (torchrun child process); returns its exit code."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------- helpers
+def _sync(cuda):
+    import torch
+
+    if cuda:
+        torch.cuda.synchronize()
+
+
+def _max_sum(world, device, t_local, x_local):
+    """(max over ranks of t, sum over ranks of x)."""
+    if world <= 1:
+        return t_local, x_local
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([t_local], dtype=torch.float64, device=device)
+    x = torch.tensor([x_local], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(x, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(x.item())
+
+
+def tiny_overrides(mc):
+    """Plumbing-size model (CPU tests of the launcher): 1+1 layers, small widths."""
+    mc["transformer"].update(encoder_layer=1, decoder_layer=1, conv_filter_size=64, encoder_hidden=32,
+                             decoder_hidden=32, encoder_head=2, decoder_head=2)
+    mc["variance_predictor"]["filter_size"] = 32
+    if mc.get("reference_encoder"):
+        mc["reference_encoder"].update(encoder_layer=1, encoder_head=2, encoder_hidden=32, conv_layer=1,
+                                       conv_filter_size=32)
+    if mc.get("gst"):
+        mc["gst"].update(conv_filters=[4, 4, 8, 8, 16, 16], gru_hidden=16, token_size=16, n_style_token=4,
+                         attn_head=2)
+
+
+# ---------------------------------------------------------------------- training
+def train_phase(args, rank, world, device):
+    import torch
+
+    from .config import load_named
+    from .data.synthetic import SyntheticBatches
+    from .models.fastspeech2 import FastSpeech2
+    from .parallel import ddp
+    from .train.trainer import Trainer
+
+    cuda = device.type == "cuda"
+    pp, mc, tc = load_named(args.config)
+    if args.tiny:
+        tiny_overrides(mc)
+    batch = args.batch or int(tc["optimizer"]["batch_size"])
+    torch.manual_seed(1234)
+    model = FastSpeech2(pp, mc).to(device)
+    model.set_compute_dtype(torch.bfloat16 if cuda else torch.float32)
+    ddp.broadcast_module_state(model)
+    trainer = Trainer(model, (pp, mc, tc))
+
+    gen = SyntheticBatches(batch, device=device, max_seq_len=mc["max_seq_len"], seed=1000 + rank,
+                           frame_level=pp["preprocessing"]["pitch"]["feature"] == "frame_level")
+    pool = []
+    for _ in range(args.pool):
+        b = gen.make_batch()
+        pool.append((b, gen.last_valid_frames))
+    # largest padded batch first: the first warm-up step sizes the allocator for all others
+    pool.sort(key=lambda e: -(len(e[0][0]) * e[0][8]))
+
+    fail_rank = os.environ.get("SSAMD_FAIL_RANK")  # fault injection (launcher failure-path test)
+
+    def step(i):
+        if fail_rank is not None and int(fail_rank) == rank and i == 1:
+            raise RuntimeError(f"injected failure on rank {rank}")
+        b, frames = pool[i % len(pool)]
+        trainer.train_step(b)
+        return frames
+
+    # at least one untimed step under DP: the gradient-bucket calibration pass (ddp.GradBuckets)
+    warm = max(args.warmup, 1 if world > 1 else 0)
+    for i in range(warm):
+        step(i)
+    _sync(cuda)
+    ddp.barrier()
+    _sync(cuda)
+    t0 = time.perf_counter()
+    frames = 0
+    for i in range(args.steps):
+        frames += step(warm + i)
+    _sync(cuda)
+    ddp.barrier()
+    _sync(cuda)
+    elapsed = time.perf_counter() - t0
+    elapsed, frames_all = _max_sum(world, device, elapsed, float(frames))
+    info = {
+        "elapsed": elapsed, "frames": frames_all, "batch": batch, "warmup": warm,
+        "buckets": len(trainer.buckets.buckets), "overlap": trainer.buckets.calibrated() if world > 1 else None,
+        "skipped_steps": int(trainer.opt.skipped_steps),
+    }
+    del trainer, model, pool
+    if cuda:
+        torch.cuda.empty_cache()
+    return info
+
+
+# ---------------------------------------------------------------------- synthesis
+def synth_phase(args, rank, world, device):
+    import torch
+
+    from .config import load_named
+    from .data.synthetic import SyntheticBatches
+    from .models.fastspeech2 import FastSpeech2
+    from .parallel import ddp
+    from .utils.model import get_vocoder
+
+    cuda = device.type == "cuda"
+    pp, mc, tc = load_named(args.synth_config)
+    if args.tiny:
+        tiny_overrides(mc)
+    torch.manual_seed(0)
+    model = FastSpeech2(pp, mc).to(device)
+    with torch.no_grad():  # ~frames_per_phone frames per phoneme (see module docstring)
+        lin = model.variance_adaptor.duration_predictor.linear_layer
+        lin.weight.normal_(0.0, 0.005)
+        lin.bias.fill_(math.log(args.frames_per_phone + 1.0))
+    model.eval().set_compute_dtype(torch.bfloat16 if cuda else torch.float32)
+    model.requires_grad_(False)
+    voc = get_vocoder(mc, device)
+    hop = pp["preprocessing"]["stft"]["hop_length"]
+    sr = pp["preprocessing"]["audio"]["sampling_rate"]
+    mx = float(pp["preprocessing"]["audio"]["max_wav_value"])
+    # texts + a reference mel per utterance (the style input of synthesize.py single/batch mode)
+    gen = SyntheticBatches(args.synth_batch, device=device, seed=7 + rank, max_seq_len=mc["max_seq_len"])
+    b = gen.make_batch()
+    speakers, texts, src_lens, max_src = b[2], b[3], b[4], b[5]
+    ref_mels, ref_lens, ref_max = b[6], b[7], b[8]
+
+    @torch.no_grad()
+    def synth():
+        out = model(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
+        mel, mel_len = out[1], out[9]
+        if cuda:  # int16 conversion fused into the vocoder's conv_post kernel
+            pcm = voc.infer(mel.to(torch.bfloat16).contiguous(), int16_scale=mx)
+        else:
+            wav = voc(mel.transpose(1, 2)).squeeze(1)
+            pcm = (wav.float() * mx).clamp(-32768, 32767).to(torch.int16)
+        return pcm, mel_len
+
+    for _ in range(args.synth_warmup):
+        synth()
+    _sync(cuda)
+    ddp.barrier()
+    _sync(cuda)
+    t0 = time.perf_counter()
+    samples = 0
+    for _ in range(args.synth_steps):
+        pcm, mel_len = synth()
+        samples += int(mel_len.sum().item()) * hop  # valid audio (the D2H of lengths is part of the pipeline)
+    _sync(cuda)
+    ddp.barrier()
+    _sync(cuda)
+    wall = time.perf_counter() - t0
+    wall, audio_s = _max_sum(world, device, wall, samples / sr)
+    info = {"wall": wall, "audio_s": audio_s, "rtf": wall / max(audio_s, 1e-12),
+            "frames_per_utt": samples / hop / max(1, args.synth_steps * args.synth_batch)}
+    del model, voc
+    if cuda:
+        torch.cuda.empty_cache()
+    return info
+
+
+def report(rec: dict):
+    print(json.dumps(rec), flush=True)

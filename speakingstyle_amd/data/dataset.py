@@ -111,6 +111,64 @@ class Dataset(_TorchDataset):
             groups = [g[rank::world] for g in groups if len(g[rank::world])]
         return [self.reprocess(data, g) for g in groups]
 
+    def text_lengths(self) -> np.ndarray:
+        """Phoneme count per utterance from the metadata alone (no .npy reads)."""
+        if getattr(self, "_tlens", None) is None:
+            self._tlens = np.array([len(text_to_sequence(t, self.cleaners)) for t in self.text], dtype=np.int64)
+        return self._tlens
+
+    def collate_local(self, data):
+        """Collate for ``ShardedGroupSampler``: ``data`` is this rank's rows of one global
+        group, already in the global (length-sorted) batch order; split it back into
+        the per-batch shards."""
+        sizes = self._local_sizes
+        out, o = [], 0
+        for n in sizes:
+            if n:
+                out.append(self.reprocess(data, list(range(o, o + n))))
+            o += n
+        return out
+
+
+class ShardedGroupSampler:
+    """Batch sampler with the reference loader's grouping (``train.py:27-41``,
+    ``dataset.py:127-146``: shuffle, groups of ``batch_size * group`` utterances,
+    each group sorted by text length and split into ``group`` batches) that shards
+    *before* loading: every rank draws the same shuffled group and yields only
+    its own rows (``batch[rank::world]`` of each sorted batch), so ``__getitem__``
+    -- the .npy reads -- runs on the local shard only.
+
+    ``epoch`` / ``start`` (groups already consumed) make the order resumable:
+    the permutation is a pure function of ``seed + epoch``."""
+
+    def __init__(self, dataset: "Dataset", batch_size: int, group: int = 4, rank: int = 0, world: int = 1,
+                 seed: int = 1234, epoch: int = 0, start: int = 0, drop_last: bool = True):
+        self.ds = dataset
+        self.bs = int(batch_size)
+        self.group = int(group)
+        self.rank, self.world = int(rank), int(world)
+        self.seed, self.epoch, self.start = int(seed), int(epoch), int(start)
+        self.drop_last = drop_last
+        self.tlens = dataset.text_lengths()
+        dataset._local_sizes = [len(range(self.rank, self.bs, self.world))] * self.group
+
+    def __len__(self):
+        n = len(self.tlens) // (self.bs * self.group)
+        return max(0, n - self.start)
+
+    def __iter__(self):
+        g = torch.Generator().manual_seed(self.seed + self.epoch)
+        perm = torch.randperm(len(self.tlens), generator=g).numpy()
+        gs = self.bs * self.group
+        n = len(perm) // gs
+        for gi in range(self.start, n):
+            idx = perm[gi * gs:(gi + 1) * gs]
+            idx = idx[np.argsort(-self.tlens[idx], kind="stable")]
+            local = []
+            for k in range(self.group):
+                local.extend(idx[k * self.bs:(k + 1) * self.bs][self.rank::self.world].tolist())
+            yield local
+
 
 class TextDataset(_TorchDataset):
     """Synthesis-time dataset: (id, speaker, phones, raw, mel) per metadata line."""

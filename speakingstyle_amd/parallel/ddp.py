@@ -11,19 +11,31 @@ Design (MI355X-first):
   in reverse registration order ~= backward production order.  A bucket is a
   contiguous slice of that arena -- no copy-in/copy-out, the collective runs on
   the arena memory directly.
-* Each parameter carries a post-accumulate-grad hook; when the last parameter of
-  a bucket has its gradient, the bucket's ``all_reduce(SUM)`` is issued
-  asynchronously.  With the ``nccl`` backend (= RCCL on ROCm) the collective runs
-  on RCCL's internal stream after an event wait on the compute stream, so it
-  overlaps the rest of backward.  ``finish()`` makes the compute stream wait for
-  all buckets before the fused clip+Adam kernel reads the arena.
+* Each parameter carries a post-accumulate-grad hook.  The hook fires once per
+  *accumulation* (a parameter used twice in the graph fires twice), so the first
+  backward is a calibration pass: it counts the firings per parameter, checks
+  that every rank saw the same counts (one tiny MIN/MAX all-reduce) and then
+  all-reduces every bucket at ``finish()``.  From the second step on (static
+  graph), a parameter is final when its count is reached; a bucket is ready when
+  all its counted parameters are final, and ready buckets are launched strictly
+  in bucket-index order (bucket i only after 0..i-1), so every rank issues the
+  identical collective sequence regardless of hook timing.  With the ``nccl``
+  backend (= RCCL on ROCm) the collective runs on RCCL's internal stream after
+  an event wait on the compute stream, so it overlaps the rest of backward.
+  ``finish()`` makes the compute stream wait for all buckets before the fused
+  clip+Adam kernel reads the arena.
+* Gradients the HIP backward kernels wrote straight into the arena slot
+  (``ops/gradslots.py``) are adopted by AccumulateGrad without a copy; the hook
+  copies the few produced elsewhere (plain-torch ops) into the slot before the
+  bucket can launch.  Later accumulations into a slot are in place.
 * Buckets default to 32 MiB: the LJSpeech model's 140 MB of fp32 gradients
   become 5 buckets -- large enough that each ring all-reduce runs near the
-  per-link xGMI bandwidth, small enough that the first bucket launches early
-  in backward (the decoder/PostNet grads arrive first).
+  per-link xGMI bandwidth (7 links x ~153 GB/s per GPU on MI355X, so a 32 MiB
+  ring pass is ~0.1 ms of wire time per hop), small enough that the first
+  bucket launches early in backward (the decoder/PostNet grads arrive first).
 * Parameters that receive no gradient in a step (e.g. the pitch/energy FiLM
-  scalars, which the reference never applies -- SURVEY D7) leave their bucket
-  incomplete; ``finish()`` launches any such bucket at the end.
+  scalars, which the reference never applies -- SURVEY D7) have count 0 and do
+  not hold their bucket back.
 * Loss normalisation uses *global* valid-element counts (all-reduced at step
   start, see ``models/loss.py``), so summed gradients equal the single-process
   full-batch gradient exactly; no 1/world rescale is needed.
@@ -37,19 +49,61 @@ import torch
 import torch.distributed as dist
 
 
-def init_distributed(backend: Optional[str] = None):
-    """torchrun-style env init.  Returns (rank, world, local_rank)."""
+DEFAULT_TIMEOUT_S = float(os.environ.get("SSAMD_DIST_TIMEOUT_S", "600"))
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None,
+                     expect_world: Optional[int] = None):
+    """torchrun-style env init.  Returns (rank, world, local_rank).
+
+    Failure handling: every collective has a deadline
+    (``timeout_s``, default ``SSAMD_DIST_TIMEOUT_S`` = 600 s); with RCCL the
+    process group runs with asynchronous error handling, so a collective that
+    times out or fails on a peer tears the communicator down and raises in
+    this rank instead of hanging (the launcher then ends the job, see
+    ``fail_fast``).  ``expect_world`` asserts the world size the launcher
+    promised (bench.py ``--gpus``)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
+        import datetime
+
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
+            # RCCL reads the same knobs as NCCL on ROCm: surface async errors, abort the comm on timeout
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+            os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "0")
             torch.cuda.set_device(local_rank)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        t = datetime.timedelta(seconds=float(timeout_s or DEFAULT_TIMEOUT_S))
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=t)
+    if expect_world is not None and world != expect_world:
+        raise RuntimeError(f"rank {rank}: launched with WORLD_SIZE={world} but {expect_world} ranks were requested")
+    if world > 1 and dist.get_world_size() != world:
+        raise RuntimeError(f"rank {rank}: process group has {dist.get_world_size()} ranks, env says {world}")
     return rank, world, local_rank
+
+
+def fail_fast(fn, *args, **kwargs):
+    """Run ``fn``; on any exception print it tagged with this rank and exit non-zero
+    without waiting on peers (``os._exit`` skips atexit hooks that could block in a
+    dead communicator).  torchrun sees the non-zero exit and terminates the other ranks."""
+    try:
+        return fn(*args, **kwargs)
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 -- report every failure with its rank
+        import sys
+        import traceback
+
+        r = os.environ.get("RANK", "0")
+        sys.stderr.write(f"[rank {r}] FAILED: {type(e).__name__}: {e}\n")
+        traceback.print_exc(file=sys.stderr)
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(3)
 
 
 def world_size() -> int:
@@ -93,38 +147,83 @@ class GradBuckets:
             cur_end = e_al
         if members:
             self.buckets.append([start, cur_end, members])
-        self.pending = [b[2] for b in self.buckets]
-        self.works: List[Optional[object]] = [None] * len(self.buckets)
+        nb = len(self.buckets)
+        self.bucket_of = [self.param_bucket[id(p)] for p in arena.params]
+        self.counts: Optional[List[int]] = None  # hook firings per parameter per backward (learned)
+        self.fired = [0] * len(arena.params)
+        self.pending = [0] * nb
+        self.works: List[Optional[object]] = [None] * nb
+        self.next_launch = 0
+        self.launch_order: List[int] = []  # bucket indices in issue order (current step)
+        self.last_launch_order: List[int] = []
         self.enabled = True
         self._handles = []
         if self.world > 1:
             for p in arena.params:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
 
+    # ------------------------------------------------------------------ internals
     def _launch(self, bi):
         s, e, _ = self.buckets[bi]
+        self.launch_order.append(bi)
         self.works[bi] = dist.all_reduce(self.arena.grad[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
+    def _launch_ready(self):
+        """Issue every ready bucket from the next unlaunched index on, in index order."""
+        while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
+            self._launch(self.next_launch)
+            self.next_launch += 1
+
+    def _reset_step(self):
+        self.fired = [0] * len(self.arena.params)
+        self.works = [None] * len(self.buckets)
+        self.next_launch = 0
+        if self.counts is not None:
+            self.pending = [0] * len(self.buckets)
+            for i, c in enumerate(self.counts):
+                if c > 0:
+                    self.pending[self.bucket_of[i]] += 1
+
     def _hook(self, p):
+        i = self.param_index[id(p)]
+        self.fired[i] += 1
         if not self.enabled:
             return
-        self.arena.ensure_slot(p, self.param_index[id(p)])  # gradients from plain-torch ops: into the bucket
-        bi = self.param_bucket[id(p)]
+        self.arena.ensure_slot(p, i)  # gradients from plain-torch ops: into the bucket
+        if self.counts is None or self.fired[i] != self.counts[i]:
+            return
+        bi = self.bucket_of[i]
         self.pending[bi] -= 1
-        if self.pending[bi] == 0 and self.works[bi] is None:
-            self._launch(bi)
+        if self.pending[bi] == 0 and bi == self.next_launch:
+            self._launch_ready()
+
+    def _calibrate(self):
+        """First synchronised backward: adopt its per-parameter hook counts if all ranks agree."""
+        dev = self.arena.grad.device
+        c = torch.tensor(self.fired, dtype=torch.int64, device=dev)
+        lo, hi = c.clone(), c.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        if torch.equal(lo, hi):
+            self.counts = list(self.fired)
+        # else: rank-dependent graph -> stay in launch-at-finish mode (correct, no overlap)
+
+    # ------------------------------------------------------------------ API
+    def calibrated(self) -> bool:
+        return self.counts is not None
 
     def finish(self):
-        """Launch stragglers, make the current stream wait for every bucket, reset."""
+        """Launch stragglers in order, make the current stream wait for every bucket, reset."""
         if self.world <= 1:
             return
-        for bi in range(len(self.buckets)):
-            if self.works[bi] is None:
-                self._launch(bi)
+        if self.counts is None:
+            self._calibrate()
+        for bi in range(self.next_launch, len(self.buckets)):
+            self._launch(bi)
         for w in self.works:
             w.wait()
-        self.works = [None] * len(self.buckets)
-        self.pending = [b[2] for b in self.buckets]
+        self.last_launch_order, self.launch_order = self.launch_order, []
+        self._reset_step()
 
     def no_sync(self):
         """Context for gradient-accumulation micro-steps (no collectives)."""
@@ -136,7 +235,7 @@ class GradBuckets:
 
             def __exit__(self, *a):
                 outer.enabled = True
-                outer.pending = [b[2] for b in outer.buckets]
+                outer._reset_step()
 
         return _Ctx()
 

@@ -32,12 +32,10 @@ from ..utils.tb import SummaryWriter
 from .trainer import Trainer
 
 
-class _Preempted(Exception):
-    pass
-
-
-def _batches(configs, device, rank, world, synthetic: bool, seed: int):
-    """Yields lists of batches (one DataLoader item = group_size sorted batches)."""
+def _batches(configs, device, rank, world, synthetic: bool, seed: int, pos=None):
+    """Yields (epoch, group_index, [batches]); one item = one global group of
+    ``group`` length-sorted batches, this rank's shard of each.  ``pos`` =
+    (epoch, groups consumed) resumes the data order exactly where a checkpoint left it."""
     preprocess_config, model_config, train_config = configs
     bs = int(train_config["optimizer"]["batch_size"])
     if synthetic:
@@ -45,20 +43,24 @@ def _batches(configs, device, rank, world, synthetic: bool, seed: int):
         gen = SyntheticBatches(per_rank, device=device, max_seq_len=model_config["max_seq_len"], seed=seed + rank,
                                n_speakers=_n_speakers(preprocess_config),
                                frame_level=preprocess_config["preprocessing"]["pitch"]["feature"] == "frame_level")
+        gi = 0
         while True:
-            yield [gen.make_batch()]
-    dataset = Dataset("train.txt", preprocess_config, train_config, sort=True, drop_last=True, shard=(rank, world))
+            yield 0, gi, [gen.make_batch()]
+            gi += 1
+    from ..data.dataset import ShardedGroupSampler
+
+    dataset = Dataset("train.txt", preprocess_config, train_config, sort=True, drop_last=True)
     group = 4
     assert bs * group < len(dataset), "batch_size * group_size must be < dataset size"
-    epoch = 0
+    epoch, start = pos if pos else (0, 0)
     while True:
-        g = torch.Generator().manual_seed(seed + epoch)  # identical shuffle on every rank
-        loader = DataLoader(dataset, batch_size=bs * group, shuffle=True, generator=g, collate_fn=dataset.collate_fn,
+        sampler = ShardedGroupSampler(dataset, bs, group, rank, world, seed=seed, epoch=epoch, start=start)
+        loader = DataLoader(dataset, batch_sampler=sampler, collate_fn=dataset.collate_local,
                             num_workers=int(train_config.get("mi355x", {}).get("num_workers", 4)),
-                            pin_memory=torch.cuda.is_available(), drop_last=True)
-        for batchs in loader:
-            yield [to_device(b, device) for b in batchs]
-        epoch += 1
+                            pin_memory=torch.cuda.is_available())
+        for gi, batchs in enumerate(loader, start=start):
+            yield epoch, gi, [to_device(b, device) for b in batchs]
+        epoch, start = epoch + 1, 0
 
 
 def _n_speakers(preprocess_config):
@@ -125,41 +127,66 @@ def train(args, configs):
     fail_at = int(getattr(args, "fail_at_step", 0) or 0)
 
     state = {"step": restore}
+    pos0 = ckpt.get("data_pos") if ckpt is not None else None  # (epoch, group, batches done in group)
+    check_every = int(train_config.get("mi355x", {}).get("preempt_check_steps", 10))
 
-    def save(step):
+    def save(step, pos):
         if rank == 0:
             mutil.save_checkpoint(mutil.ckpt_file(train_config, step), model, trainer.opt, step,
-                                  extra={"rng": torch.get_rng_state()})
+                                  extra={"rng": torch.get_rng_state(), "data_pos": list(pos)})
+
+    # SIGTERM (SLURM preemption) on ANY rank sets a flag; ranks agree on it at a step
+    # boundary (every ``preempt_check_steps`` under DP: one tiny all-reduce), then rank 0
+    # saves and everybody leaves the loop together -- no rank is left inside a collective.
+    flag = {"term": False}
 
     def on_term(signum, frame):
-        raise _Preempted()
+        flag["term"] = True
 
-    prev = signal.signal(signal.SIGTERM, on_term) if rank == 0 or world == 1 else None
+    prev = signal.signal(signal.SIGTERM, on_term)
+
+    def preempted(step):
+        if world == 1:
+            return flag["term"]
+        if step % check_every:
+            return False
+        t = torch.tensor([1.0 if flag["term"] else 0.0], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return bool(t.item() > 0)
+
     step = restore + 1
-    frames_acc = 0
     t_last = time.perf_counter()
     synthetic = getattr(args, "synthetic", False) or not os.path.exists(
         os.path.join(preprocess_config["path"]["preprocessed_path"], "train.txt"))
+    start_pos = (pos0[0], pos0[1]) if pos0 else None
+    skip = int(pos0[2]) if pos0 else 0
     try:
-        for batchs in _batches(configs, device, rank, world, synthetic, seed):
-            for batch in batchs:
+        for epoch, gi, batchs in _batches(configs, device, rank, world, synthetic, seed, start_pos):
+            for k, batch in enumerate(batchs):
+                if skip:  # resumed inside a group: these batches were consumed before the checkpoint
+                    skip -= 1
+                    continue
                 if fail_at and step == fail_at:
                     raise RuntimeError(f"fault injection at step {step}")
                 losses, output, lr = trainer.train_step(batch)
-                frames_acc += int(batch[7].clamp(max=model_config["max_seq_len"]).sum()) if step % log_step == 0 else 0
-                if rank == 0 and step % log_step == 0:
-                    vals = [float(l) for l in losses[:-1]]
+                # position AFTER this batch: the next run starts at the following batch
+                pos = (epoch, gi + 1, 0) if k + 1 == len(batchs) else (epoch, gi, k + 1)
+                if step % log_step == 0:
+                    vals = trainer.reduce_losses(losses)  # collective on every rank
+                    frames = trainer.take_frames()
                     dt = time.perf_counter() - t_last
                     t_last = time.perf_counter()
-                    msg1 = "Step {}/{}, ".format(step, total_step)
-                    msg2 = ("Total Loss: {:.4f}, Mel Loss: {:.4f}, Mel PostNet Loss: {:.4f}, Pitch Loss: {:.4f}, "
-                            "Energy Loss: {:.4f}, Duration Loss: {:.4f}").format(*vals)
-                    with open(os.path.join(train_log_path, "log.txt"), "a") as f:
-                        f.write(msg1 + msg2 + "\n")
-                    print(msg1 + msg2, flush=True)
-                    log_scalars(train_logger, step, losses=vals, lr=trainer.last_lr, lambdas=losses[-1])
-                    train_logger.add_scalar("Perf/step_ms", 1000.0 * dt / log_step, step)
-                    train_logger.add_scalar("Perf/skipped_steps", float(trainer.opt.skipped_steps), step)
+                    if rank == 0:
+                        msg1 = "Step {}/{}, ".format(step, total_step)
+                        msg2 = ("Total Loss: {:.4f}, Mel Loss: {:.4f}, Mel PostNet Loss: {:.4f}, Pitch Loss: {:.4f}, "
+                                "Energy Loss: {:.4f}, Duration Loss: {:.4f}").format(*vals)
+                        with open(os.path.join(train_log_path, "log.txt"), "a") as f:
+                            f.write(msg1 + msg2 + "\n")
+                        print(msg1 + msg2, flush=True)
+                        log_scalars(train_logger, step, losses=vals, lr=trainer.last_lr, lambdas=losses[-1])
+                        train_logger.add_scalar("Perf/step_ms", 1000.0 * dt / log_step, step)
+                        train_logger.add_scalar("Perf/mel_frames_per_s", frames / max(dt, 1e-9), step)
+                        train_logger.add_scalar("Perf/skipped_steps", float(trainer.opt.skipped_steps), step)
                 if rank == 0 and synth_step and step % synth_step == 0:
                     synth_one_sample(batch, output, vocoder, model_config, preprocess_config, train_logger, step, "Training")
                 if val_step and step % val_step == 0 and not synthetic:
@@ -173,18 +200,18 @@ def train(args, configs):
                         print(msg, flush=True)
                     model.train()
                 if save_step and step % save_step == 0:
-                    save(step)
+                    save(step, pos)
                 state["step"] = step
                 if step >= total_step:
                     return step
+                if preempted(step):
+                    save(step, pos)
+                    if rank == 0:
+                        print(f"SIGTERM: checkpoint saved at step {step}", flush=True)
+                    return step
                 step += 1
-    except _Preempted:
-        save(state["step"])
-        print(f"SIGTERM: checkpoint saved at step {state['step']}", flush=True)
-        return state["step"]
     finally:
-        if prev is not None:
-            signal.signal(signal.SIGTERM, prev)
+        signal.signal(signal.SIGTERM, prev)
         for lg in (train_logger, val_logger):
             if lg is not None:
                 lg.close()

@@ -20,6 +20,7 @@ from __future__ import annotations
 import time
 from typing import Optional
 
+import numpy as np
 import torch
 
 from ..models.loss import FastSpeech2Loss
@@ -42,6 +43,37 @@ class Trainer:
         self.max_seq_len = model_config["max_seq_len"]
         self.micro = 0
         self.last_lr = self.opt._get_lr()
+        self.frames = torch.zeros((), dtype=torch.int64, device=self.opt.arena.data.device)
+        self.frames_host = 0
+
+    def take_frames(self) -> int:
+        """Valid mel frames consumed since the last call, summed over ranks (host sync: log steps only)."""
+        f = self.frames.clone() + self.frames_host
+        self.frames.zero_()
+        self.frames_host = 0
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(f)
+        return int(f)
+
+    def reduce_losses(self, losses):
+        """Host floats of the 6 loss terms of the *global* batch.
+
+        Each rank's masked terms are its share of the global mean (they divide by the
+        all-reduced valid counts), so the global value is their SUM over ranks; the
+        ``lambda_f * sum(s^2)`` FiLM term is identical on every rank and is added once."""
+        terms = torch.stack([l.detach().float().reshape(()) for l in losses[1:6]])
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(terms)
+        vals = [float(v) for v in terms]
+        total = sum(vals)
+        named = self.model.film_scalars()
+        if named is not None and self.loss_fn.lambda_f > 0:
+            total += float(self.loss_fn.lambda_f * torch.sum(torch.square(named.detach().float())))
+        return [total] + vals
 
     def _global_counts(self, batch):
         """[mel elements, phonemes, mel frames] valid in this rank's batch (device, fp32)."""
@@ -71,6 +103,11 @@ class Trainer:
                 (total / self.grad_acc).backward()
         self.opt.arena.finalize_grads()
         self.micro += 1
+        hl = getattr(batch[7], "host_lengths", None)
+        if hl is not None:  # host copy from the loader: no device work
+            self.frames_host += int(np.minimum(hl, self.max_seq_len).sum())
+        else:
+            self.frames += batch[7].clamp(max=self.max_seq_len).sum()
         lr = None
         if last_micro:
             self.buckets.finish()

@@ -92,6 +92,35 @@ def test_sigterm_checkpoint_and_fault_injection(tmp_path):
     assert "Step 4/4" in out
 
 
+def test_sigterm_saves_at_step_boundary(tmp_path):
+    """SIGTERM sets a flag; the loop saves at the next step boundary (with the data
+    position) and exits 0 -- no exception from inside a step or a collective."""
+    import signal
+    import time
+
+    p, m, t = _tiny_configs(tmp_path)
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", PYTHONUNBUFFERED="1")
+    proc = subprocess.Popen([sys.executable, "train.py", "-p", p, "-m", m, "-t", t, "--synthetic", "--cpu",
+                             "--no_vocoder", "--max_steps", "100000"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+    try:
+        deadline = time.time() + 600
+        for line in proc.stdout:
+            if line.startswith("Step 2/"):
+                break
+            assert time.time() < deadline
+        proc.send_signal(signal.SIGTERM)
+        out, err = proc.communicate(timeout=300)
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+    assert proc.returncode == 0, err[-3000:]
+    assert "SIGTERM: checkpoint saved at step" in out
+    step = int(out.split("SIGTERM: checkpoint saved at step")[1].split()[0])
+    blob = torch.load(tmp_path / "ckpt_path" / f"{step}.pth.tar", weights_only=True)
+    assert blob["step"] == step and len(blob["data_pos"]) == 3
+
+
 def test_synthesize_single_cli(tmp_path):
     p, m, t = _tiny_configs(tmp_path, style="gst")
     _run(["train.py", "-p", p, "-m", m, "-t", t, "--synthetic", "--cpu", "--no_vocoder", "--max_steps", "2"])
