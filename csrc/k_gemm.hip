@@ -49,6 +49,18 @@ __device__ __forceinline__ int2 row_pos(const ConvGeom& g, int m) {
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
 
+// Extended epilogue (bf16 output; 256x256 "big64" and 256x128 "ring" kernels), applied after
+// bias -> act -> aux -> residual -> row mask:  v = (v + acc) * scale;  y2 = lrelu_0.1(v);
+// Y = post_act(v).  acc may alias Y (in-place MRF branch sum: every element is read before it
+// is written, by the same thread).  Used by the HiFi-GAN inference path so that no activation
+// or accumulation pass runs outside a GEMM (models/hifigan.py).
+struct EpiX {
+  const bf16_t* acc;
+  bf16_t* y2;
+  float scale;
+  int post_act;
+};
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   // bijective: consecutive remapped ids land on the same XCD (round-robin dispatch)
   const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, k = bid / 8;
@@ -453,7 +465,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ aux,
                                                                 const bf16_t* __restrict__ resid,
                                                                 const int64_t* __restrict__ lens, void* __restrict__ Yv,
-                                                                ConvGeom g, int act, int ldy) {
+                                                                ConvGeom g, int act, int ldy, EpiX ex) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BN - 1) / BN;
   const int nM = (g.M + BM3 - 1) / BM3;
@@ -619,6 +631,23 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
       if constexpr (OUT_F32) {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
+        if (ex.acc) {
+          const short4v x = *reinterpret_cast<const short4v*>(ex.acc + off);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = valid ? v[q] * ex.scale : 0.f;
+        if (ex.y2) {
+          short4v o2;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o2[q] = (short)f2bf(v[q] > 0.f ? v[q] : 0.1f * v[q]);
+          *reinterpret_cast<short4v*>(ex.y2 + off) = o2;
+        }
+        if (ex.post_act == ACT_LRELU) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+        }
         short4v o;
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
@@ -837,7 +866,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
                                                                const bf16_t* __restrict__ aux,
                                                                const bf16_t* __restrict__ resid,
                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
-                                                               ConvGeom g, int act, int ldy) {
+                                                               ConvGeom g, int act, int ldy, EpiX ex) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BG - 1) / BG;
   const int nM = (g.M + BG - 1) / BG;
@@ -993,6 +1022,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       }
       __syncthreads();
       bf16_t* Y = reinterpret_cast<bf16_t*>(Yv);
+      const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f;
       for (int e = tid; e < BG * 32; e += NT3) {
         const int r = e >> 5, c = e & 31;
         const int m = m0 + r, n = n0 + c * 8;
@@ -1004,7 +1034,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
           valid = tt < (int)lens[bb];
         }
         const long off = (long)m * ldy + n;
-        if (aux || resid || !valid) {
+        if (aux || resid || !valid || xon) {
           float f[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)v[q]);
@@ -1018,8 +1048,25 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)rr[q]);
           }
+          if (ex.acc) {
+            const short8 aa = *reinterpret_cast<const short8*>(ex.acc + off);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = valid ? (short)f2bf(f[q]) : (short)0;
+            for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)aa[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = valid ? f[q] * ex.scale : 0.f;
+          if (ex.y2) {
+            short8 o2;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o2[q] = (short)f2bf(f[q] > 0.f ? f[q] : 0.1f * f[q]);
+            *reinterpret_cast<short8*>(ex.y2 + off) = o2;
+          }
+          if (ex.post_act == ACT_LRELU) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = f[q] > 0.f ? f[q] : 0.1f * f[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = (short)f2bf(f[q]);
         }
         *reinterpret_cast<short8*>(Y + off) = v;
       }
@@ -2271,9 +2318,9 @@ static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N
   return g;
 }
 
-SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
-                              const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
-                              int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, hipStream_t s) {
+static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
+                          const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
+                          int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, EpiX ex, hipStream_t s) {
   if (Cin % 8 != 0) return -2;
   if ((long)B * L == 0 || N == 0) return 0;
   ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
@@ -2294,6 +2341,12 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
   // every N >= 256 shape (+3..15 % over the 256x128 ring, +4..8 % over 256x256 with a BK=32 4-stage ring);
   // the 256x128 ring for narrower N when K-slabs are tap-aligned, LDS-DMA 128x128 otherwise
   if (variant < 0) variant = N >= 256 ? 4 : (Cin % BK == 0) ? 2 : 1;
+  const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f;
+  if (xon) {  // only the big64 (LDS-staged bf16 epilogue) and ring kernels implement EpiX
+    if (out_f32 || !reg || (N % 8) || (ldy % 8) || act < 0) return -3;
+    if (N >= 256) variant = 4;
+    else if (variant != 2) return -3;
+  }
   if (g_debug_nostore && variant >= 3) act = -1;
   if (reg && variant == 3 && N >= 256) {
     static bool big_set = false;
@@ -2376,7 +2429,7 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true> : conv_gemm_big64_kernel<F32, FK, false>; \
-      hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy);     \
+      hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
     if (out_f32) {
       if (fastk) B64_LAUNCH(true, true); else B64_LAUNCH(true, false);
@@ -2403,7 +2456,7 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
 #define RING_LAUNCH(F32, FK)                                                                        \
     do {                                                                                            \
       auto kfn = g.rinfo ? conv_gemm_ring_kernel<F32, FK, true> : conv_gemm_ring_kernel<F32, FK, false>; \
-      hipLaunchKernelGGL(kfn, dim3(nwg3), dim3(NT3), L3, s, X, W, bias, aux, resid, lens, Y, g, act, ldy); \
+      hipLaunchKernelGGL(kfn, dim3(nwg3), dim3(NT3), L3, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
     if (out_f32) {
       if (fastk) RING_LAUNCH(true, true); else RING_LAUNCH(true, false);
@@ -2433,6 +2486,21 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
                        g, act, ldy);
   }
   return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
+                              const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
+                              int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, hipStream_t s) {
+  const EpiX ex{nullptr, nullptr, 1.f, 0};
+  return conv_gemm_impl(X, W, bias, aux, resid, lens, Y, out_f32, B, L, Cin, ks, dil, pad, N, act, ldy, rinfo, ex, s);
+}
+
+// conv_gemm with the extended epilogue (see EpiX): acc (may alias Y), y2 = lrelu(v), scale, post_act.
+SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* resid, void* Y,
+                                 int B, int L, int Cin, int ks, int dil, int pad, int N, int act, const bf16_t* acc,
+                                 bf16_t* y2, float scale, int post_act, hipStream_t s) {
+  const EpiX ex{acc, y2, scale, post_act};
+  return conv_gemm_impl(X, W, bias, nullptr, resid, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, nullptr, ex, s);
 }
 
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.

@@ -2,6 +2,7 @@
 //
 //     y = x + conv2( lrelu( conv1_d( lrelu(x) ) + b1 ) ) + b2          [channel-last, C channels]
 //     out = (acc_in + y) * out_scale   (optional: the MRF branch sum / mean, in place)
+//     [-> lrelu(out): the next upsampling conv's input activation, when post_lrelu]
 //
 // for the high-rate stages (C = 32 / 64 / 128 at 256 / 128 / 64x the mel rate), where a generic
 // GEMM tile wastes N width and every separate lrelu / add pass re-streams GBs of activations.
@@ -162,7 +163,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
                                                             const float* __restrict__ b1, const bf16_t* __restrict__ w2,
                                                             const float* __restrict__ b2, const bf16_t* acc_in,
                                                             bf16_t* out, int T, int tiles, int d, float slope,
-                                                            float out_scale, int dbg) {
+                                                            float out_scale, int post_lrelu, int dbg) {
   using R = RB<C, K>;
   constexpr int NT = R::NT;
   constexpr int CH = C / 8;                                  // 16-B chunks per row
@@ -282,7 +283,9 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
       for (int i = 0; i < 8; ++i) {
         float v = ov[i] + bf2f((bf16_t)xr[it][i]);
         if (ab) v += bf2f((bf16_t)ar[it][i]);
-        o[i] = (short)f2bf(v * out_scale);
+        v *= out_scale;
+        if (post_lrelu) v = lrelu(v, slope);  // the next upsampling conv's pre-activation
+        o[i] = (short)f2bf(v);
       }
       *reinterpret_cast<short8*>(ob + (long)t * C + c0) = o;
     }
@@ -293,7 +296,8 @@ static int g_rb_debug = 0;  // A/B timing switch: bit 0 skip conv1 MFMAs, bit 1 
 
 template <int C, int K>
 int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
-              const bf16_t* acc_in, bf16_t* out, int B, int T, int d, float slope, float out_scale, hipStream_t s) {
+              const bf16_t* acc_in, bf16_t* out, int B, int T, int d, float slope, float out_scale, int post_lrelu,
+              hipStream_t s) {
   using R = RB<C, K>;
   static bool lds_set = false;
   if (!lds_set) {
@@ -302,7 +306,7 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
   }
   const int tiles = (T + R::BM - 1) / R::BM;
   hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
-                     acc_in, out, T, tiles, d, slope, out_scale, g_rb_debug);
+                     acc_in, out, T, tiles, d, slope, out_scale, post_lrelu, g_rb_debug);
   return (int)hipGetLastError();
 }
 
@@ -314,11 +318,12 @@ SSAMD_API void ssamd_resblock_debug(int v) { g_rb_debug = v; }
 // implicit-GEMM forward image); b1 / b2 fp32 [C].  C in {32, 64, 128}, K in {3, 7, 11}, 1 <= d <= 5.
 SSAMD_API int ssamd_resblock_layer(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
                                    const float* b2, const bf16_t* acc_in, bf16_t* out, int B, int T, int C, int K,
-                                   int d, float slope, float out_scale, hipStream_t s) {
+                                   int d, float slope, float out_scale, int post_lrelu, hipStream_t s) {
   if (d < 1 || d > MAXD) return -2;
   if ((long)B * T == 0) return 0;
 #define RB_CASE(CC, KK) \
-  if (C == CC && K == KK) return launch_rb<CC, KK>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, s);
+  if (C == CC && K == KK) \
+    return launch_rb<CC, KK>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s);
   RB_CASE(32, 3) RB_CASE(32, 7) RB_CASE(32, 11)
   RB_CASE(64, 3) RB_CASE(64, 7) RB_CASE(64, 11)
   RB_CASE(128, 3) RB_CASE(128, 7) RB_CASE(128, 11)

@@ -13,10 +13,11 @@ State-dict keys of the generator match the reference (``conv_pre``, ``ups.i``,
 replaces every weight-normed conv by its folded weight (reference
 ``remove_weight_norm``) for inference.
 
-Inference runs channel-last through ``ops.conv1d`` (HIP implicit-GEMM conv with
-fused LeakyReLU / tanh epilogues on the GPU); the transposed convolutions use a
-polyphase decomposition into ``stride`` ordinary convolutions whose outputs
-interleave, so they run on the same MFMA kernel.  Training runs in PyTorch NCL
+Inference runs channel-last on the HIP kernels (``Generator._infer_hip``): each
+transposed convolution is ONE 3-tap implicit GEMM with N = stride * Cout whose
+output rows are the interleaved phases (``convT_as_conv3``), activations / bias /
+residual / MRF mean sit in GEMM epilogues, the C <= 128 ResBlocks are single fused
+layer kernels.  The CPU path (tests) uses the polyphase decomposition.  Training runs in PyTorch NCL
 layout with autograd (vocoder training is not a headline config).
 """
 from __future__ import annotations
@@ -86,17 +87,23 @@ class ResBlock1(nn.Module):
             x = xt + x
         return x
 
-    def fused_ok(self, x) -> bool:
-        return (x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] in (32, 64, 128)
-                and self.kernel_size in (3, 7, 11) and max(self.dilation) <= 5)
+    def fusable(self, channels: int) -> bool:
+        """Geometry covered by the fused ResBlock1 layer kernel (csrc/k_vocoder.hip)."""
+        return channels in (32, 64, 128) and self.kernel_size in (3, 7, 11) and max(self.dilation) <= 5
 
-    def forward_cl(self, x, acc=None, out_scale=1.0, x_act=None):
-        """Channel-last inference path [B, T, C].  Returns ``(acc +) block(x) * out_scale``.
+    def fused_ok(self, x) -> bool:
+        return x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16 and self.fusable(x.shape[-1])
+
+    def forward_cl(self, x, acc=None, out_scale=1.0, x_act=None, post_lrelu=False):
+        """Channel-last inference path [B, T, C].  Returns ``(acc +) block(x) * out_scale`` (then
+        ``lrelu`` when ``post_lrelu``: the next upsampling conv's input activation).
 
         GPU: the high-rate stages (C = 32 / 64 / 128) run each layer as ONE fused kernel (lrelu -> dilated
-        conv -> lrelu -> conv -> + x [-> + acc, * scale], ``csrc/k_vocoder.hip``); the wide stages
-        use the implicit-GEMM conv with the lrelu in the first conv's epilogue and the residual in
-        the second's.  ``x_act``: lrelu(x) when the caller already has it (shared by the MRF branches)."""
+        conv -> lrelu -> conv -> + x [-> + acc, * scale, lrelu], ``csrc/k_vocoder.hip``); the wide stages
+        use the implicit-GEMM conv with everything in its epilogues: lrelu after the first conv, the
+        residual + a second lrelu'd output (the next layer's input) after the second, and the MRF
+        accumulate / mean / post-activation after the block's last conv -- no elementwise pass.
+        ``x_act``: lrelu(x) when the caller already has it (shared by the MRF branches)."""
         k = self.kernel_size
         n = len(self.convs1)
         if self.fused_ok(x):
@@ -104,20 +111,27 @@ class ResBlock1(nn.Module):
             for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
                 last = i == n - 1
                 x = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE, acc=acc if last else None,
-                                       out_scale=out_scale if last else 1.0)
+                                       out_scale=out_scale if last else 1.0, post_lrelu=post_lrelu and last)
             return x
-        hip = ops._hip() if (x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16) else None
+        if x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16:
+            hip = ops._hip()
+            a = x_act if x_act is not None else _lrelu(x)
+            for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
+                t = hip.conv1d_infer(a, _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
+                if i < n - 1:
+                    x, a = hip.conv1d_infer(t, _w(c2), c2.bias, get_padding(k, 1), 1, None, resid=x, dual_lrelu=True)
+                else:
+                    x = hip.conv1d_infer(t, _w(c2), c2.bias, get_padding(k, 1), 1, None, resid=x, acc=acc,
+                                         scale=out_scale, post_act="lrelu" if post_lrelu else None)
+            return x
         for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
             a = x_act if (i == 0 and x_act is not None) else _lrelu(x)
-            if hip is not None:
-                xt = hip.conv1d_infer(a, _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
-                x = hip.conv1d_infer(xt, _w(c2), c2.bias, get_padding(k, 1), 1, None, resid=x)
-            else:
-                xt = ops.conv1d(a, _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
-                x = ops.conv1d(xt, _w(c2), c2.bias, get_padding(k, 1), 1, None) + x
+            xt = ops.conv1d(a, _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
+            x = ops.conv1d(xt, _w(c2), c2.bias, get_padding(k, 1), 1, None) + x
         if acc is not None:
             x = acc.add_(x)
-        return x * out_scale if out_scale != 1.0 else x
+        x = x * out_scale if out_scale != 1.0 else x
+        return _lrelu(x) if post_lrelu else x
 
 
 def _lrelu(x, slope=LRELU_SLOPE):
@@ -163,21 +177,83 @@ class Generator(nn.Module):
     def infer(self, mel_cl: torch.Tensor, int16_scale=None) -> torch.Tensor:
         """mel [B, T, n_mel] (channel-last) -> wav [B, T*hop] in [-1, 1] (or int16 samples
         scaled by ``int16_scale``, fused into the conv_post kernel)."""
+        if mel_cl.is_cuda and ops.use_hip(mel_cl):
+            return self._infer_hip(mel_cl.to(torch.bfloat16).contiguous(), int16_scale)
         x = ops.conv1d(mel_cl, _w(self.conv_pre), self.conv_pre.bias, 3, 1, None)
         for i in range(self.num_upsamples):
             up = self.ups[i]
             x = conv_transpose_polyphase(_lrelu(x), _w(up), up.bias, up.stride[0], up.padding[0])
-            # MRF: mean of the branches, accumulated in place into the first branch's output
             blocks = [self.resblocks[i * self.num_kernels + j] for j in range(self.num_kernels)]
-            x_act = None if blocks[0].fused_ok(x) else _lrelu(x)  # shared first-layer input of the branches
+            x_act = _lrelu(x)
             xs = None
             for j, blk in enumerate(blocks):
                 last = j == self.num_kernels - 1
                 xs = blk.forward_cl(x, acc=xs, out_scale=(1.0 / self.num_kernels) if last else 1.0, x_act=x_act)
             x = xs
+        w = _w(self.conv_post)
+        y = torch.tanh(ref_conv_post(_lrelu(x, 0.01), w, self.conv_post.bias)).squeeze(-1)
+        if int16_scale is not None:
+            y = (y * int16_scale).clamp(-32768, 32767).to(torch.int16)
+        return y
+
+    def _ups_image(self, i):
+        """(fp32 [s*Cout, Cin, 3] weight, bf16 [s*Cout][3][Cin] operand image, tiled bias) of
+        upsampling layer i as one 3-tap convolution (``convT_as_conv3``), cached per weight version."""
+        up = self.ups[i]
+        w = _w(up)
+        key = (w.data_ptr(), w._version, None if up.bias is None else up.bias._version)
+        cache = self.__dict__.setdefault("_ups_cache", {})
+        hit = cache.get(i)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        wu = convT_as_conv3(w.detach().float(), up.stride[0], up.padding[0])
+        if wu is None:
+            val = None
+        else:
+            s = up.stride[0]
+            bt = None if up.bias is None else up.bias.detach().float().repeat(s).contiguous()
+            val = (wu, wu.permute(0, 2, 1).to(torch.bfloat16).contiguous(), bt)
+        cache[i] = (key, val)
+        return val
+
+    def _infer_hip(self, mel, int16_scale):
+        """GPU inference: every op is a HIP kernel, every activation / bias / accumulate sits in a
+        GEMM epilogue.  conv_pre writes lrelu(x) (its only consumer is ups[0]); each upsampling conv
+        is ONE implicit GEMM over a 3-tap window with N = stride * Cout whose output rows ARE the
+        interleaved phases (no pad / stack / bias pass); each MRF's last branch writes
+        lrelu(mean) for the next upsampling conv, or the raw mean for conv_post (slope 0.01, fused)."""
+        hip = ops._hip()
+        x = hip.conv1d_infer(mel, _w(self.conv_pre), self.conv_pre.bias, 3, 1, "lrelu")
+        nk = self.num_kernels
+        for i in range(self.num_upsamples):
+            up = self.ups[i]
+            s = up.stride[0]
+            blocks = [self.resblocks[i * nk + j] for j in range(nk)]
+            B, T, _ = x.shape
+            img = self._ups_image(i)
+            fused = blocks[0].fusable(up.weight.shape[1])
+            x_act = None
+            if img is None:  # generic ConvTranspose geometry: polyphase fallback on the same GEMM kernel
+                y = conv_transpose_polyphase(x, _w(up), up.bias, s, up.padding[0])
+            else:
+                wu, wimg, bt = img
+                if fused:
+                    y = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg)
+                else:
+                    y, x_act = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, dual_lrelu=True)
+                y = y.view(B, T * s, -1)
+                if x_act is not None:
+                    x_act = x_act.view(B, T * s, -1)
+            post = i < self.num_upsamples - 1
+            xs = None
+            for j, blk in enumerate(blocks):
+                last = j == nk - 1
+                xs = blk.forward_cl(y, acc=xs, out_scale=(1.0 / nk) if last else 1.0, x_act=x_act,
+                                    post_lrelu=post and last)
+            x = xs
         w = _w(self.conv_post)  # [1, C, 7]: N = 1 output -> VALU kernel (lrelu + conv + tanh [+ int16] fused)
-        if x.is_cuda and ops.use_hip(x) and x.shape[-1] in (8, 32):
-            return ops._hip().conv_post(x, w, self.conv_post.bias, 0.01, int16_scale)
+        if x.shape[-1] in (8, 32):
+            return hip.conv_post(x, w, self.conv_post.bias, 0.01, int16_scale)
         y = torch.tanh(ref_conv_post(_lrelu(x, 0.01), w, self.conv_post.bias)).squeeze(-1)
         if int16_scale is not None:
             y = (y * int16_scale).clamp(-32768, 32767).to(torch.int16)
@@ -194,6 +270,29 @@ class Generator(nn.Module):
 
 def ref_conv_post(x, w, b):
     return ops.ref.conv1d(x.float(), w.float(), None if b is None else b.float(), 3, 1, None)
+
+
+def convT_as_conv3(w, stride: int, pad: int):
+    """ConvTranspose1d weight [Cin, Cout, K] -> an ordinary 3-tap conv weight [stride*Cout, Cin, 3].
+
+    y[s*q + r] = sum_k x[q + (r + pad - k)/s] w[:, :, k] over the taps k with (r + pad - k) divisible
+    by s.  When K == s + 2*pad and pad <= s (every HiFi-GAN upsampler: K = 2s, pad = s/2) the input
+    offset (r + pad - k)/s is always -1, 0 or +1, so output phase r of frame q is a 3-tap conv of
+    x[q-1 .. q+1] with W3[r*Cout + co, cin, t] = w[cin, co, r + pad - s*(t-1)] (zero where that tap does
+    not exist).  The GEMM output [B, T, s*Cout] then IS the interleaved [B, T*s, Cout] result.  1.5x the
+    MACs of the exact polyphase form, but one wide GEMM (N = s*Cout) with no interleave / pad / bias
+    pass.  Returns None for other geometries."""
+    Cin, Cout, K = w.shape
+    s = int(stride)
+    if K != s + 2 * pad or pad > s or pad < 0:
+        return None
+    wu = w.new_zeros(s, Cout, Cin, 3)
+    for r in range(s):
+        for t in range(3):
+            k = r + pad - s * (t - 1)
+            if 0 <= k < K:
+                wu[r, :, :, t] = w[:, :, k].t()
+    return wu.reshape(s * Cout, Cin, 3).contiguous()
 
 
 def conv_transpose_polyphase(x, w, b, stride: int, pad: int):

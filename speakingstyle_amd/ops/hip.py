@@ -1038,13 +1038,15 @@ def token_attention(q, K, V):
 
 
 # ------------------------------------------------------------------------ vocoder (inference)
-_SIGS.update({"ssamd_resblock_layer": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, P]})
+_SIGS.update({"ssamd_resblock_layer": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P],
+              "ssamd_conv_gemm_ex": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, F, I, P]})
 
 
-def resblock_layer(x, c1, c2, d, slope, acc=None, out_scale=1.0):
+def resblock_layer(x, c1, c2, d, slope, acc=None, out_scale=1.0, post_lrelu=False):
     """One fused HiFi-GAN ResBlock1 layer (csrc/k_vocoder.hip), channel-last bf16, no autograd:
-    ``(acc +) x + conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2``, times ``out_scale``.  With ``acc``
-    the result is written into ``acc`` in place (the MRF branch sum)."""
+    ``(acc +) x + conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2``, times ``out_scale`` [then lrelu when
+    ``post_lrelu``: the next upsampling conv's input].  With ``acc`` the result is written into
+    ``acc`` in place (the MRF branch sum)."""
     _need(x, torch.bfloat16, "resblock.x")
     B, T, C = x.shape
     K = c1.weight.shape[2]
@@ -1059,18 +1061,42 @@ def resblock_layer(x, c1, c2, d, slope, acc=None, out_scale=1.0):
     else:
         out = torch.empty_like(x)
     rc = lib().ssamd_resblock_layer(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(acc), _ptr(out), B, T, C,
-                                    K, int(d), float(slope), float(out_scale), _stream())
+                                    K, int(d), float(slope), float(out_scale), int(bool(post_lrelu)), _stream())
     _check(rc, "ssamd_resblock_layer")
     return out
 
 
-def conv1d_infer(x, w, b, pad, dil, act=None, resid=None):
-    """Inference conv (no autograd) with an optional residual added in the GEMM epilogue."""
+def conv1d_infer(x, w, b, pad, dil, act=None, resid=None, acc=None, scale=1.0, post_act=None, dual_lrelu=False,
+                 wimg=None):
+    """Inference conv (no autograd), channel-last bf16, everything in the GEMM epilogue:
+    ``v = act(conv(x) + b) [+ resid]``; ``v = (v [+ acc]) * scale``; returns ``post_act(v)``
+    (and ``lrelu(v)`` as a second output when ``dual_lrelu``).  ``acc`` may be the output
+    buffer itself (in-place accumulation; it is then returned).  ``wimg``: a prepared bf16
+    [N][ks][Cin] operand image (with ``w`` the fp32 [N, Cin, ks] it came from, for shapes)."""
     B, L, Cin = x.shape
     ks = 1 if w.dim() == 2 else w.shape[2]
+    N = w.shape[0]
     bf = None if b is None else b.detach().float().contiguous()
-    return conv_gemm_raw(x.contiguous(), weight_fwd(w), bf, B, L, Cin, ks, dil, pad, w.shape[0], _ACT[act],
-                         resid=None if resid is None else resid.contiguous())
+    wi = weight_fwd(w) if wimg is None else wimg
+    if acc is None and scale == 1.0 and post_act is None and not dual_lrelu:
+        return conv_gemm_raw(x.contiguous(), wi, bf, B, L, Cin, ks, dil, pad, N, _ACT[act],
+                             resid=None if resid is None else resid.contiguous())
+    xc = x.contiguous()
+    _need(xc, torch.bfloat16, "conv_ex.x")
+    _need(wi, torch.bfloat16, "conv_ex.w")
+    assert wi.numel() == N * ks * Cin and N % 8 == 0 and Cin % 8 == 0, "conv_ex: shape"
+    if bf is not None:
+        assert bf.numel() == N
+    for t in (resid, acc):
+        if t is not None:
+            _need(t, torch.bfloat16, "conv_ex.operand")
+            assert t.numel() == B * L * N, "conv_ex: operand shape"
+    y = acc if acc is not None else torch.empty(B, L, N, device=x.device, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y) if dual_lrelu else None
+    rc = lib().ssamd_conv_gemm_ex(_ptr(xc), _ptr(wi), _ptr(bf), _ptr(resid), _ptr(y), B, L, Cin, ks, dil, pad, N,
+                                  _ACT[act], _ptr(acc), _ptr(y2), float(scale), _ACT[post_act], _stream())
+    _check(rc, "ssamd_conv_gemm_ex")
+    return (y, y2) if dual_lrelu else y
 
 
 # ------------------------------------------------------------------------ audio front-end

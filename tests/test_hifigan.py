@@ -19,6 +19,24 @@ def test_polyphase_conv_transpose(k, s, cin, cout, T):
     torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("k,s,cin,cout,T", [(16, 8, 16, 8, 9), (4, 2, 8, 8, 13), (16, 8, 8, 4, 1), (8, 4, 8, 8, 6)])
+def test_conv_transpose_as_3tap_conv(k, s, cin, cout, T):
+    """The GPU upsampler form: one 3-tap conv with N = s*Cout whose output rows are the phases."""
+    from speakingstyle_amd.ops import reference as R
+
+    torch.manual_seed(0)
+    x = torch.randn(2, T, cin)
+    w = torch.randn(cin, cout, k)
+    b = torch.randn(cout)
+    pad = (k - s) // 2
+    wu = H.convT_as_conv3(w, s, pad)
+    assert wu is not None and wu.shape == (s * cout, cin, 3)
+    y = R.conv1d(x, wu, b.repeat(s), 1, 1, None).reshape(2, T * s, cout)
+    yr = F.conv_transpose1d(x.transpose(1, 2), w, b, stride=s, padding=pad).transpose(1, 2)
+    torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+    assert H.convT_as_conv3(torch.randn(4, 4, 7), 3, 1) is None  # K != s + 2*pad: polyphase fallback
+
+
 def _small_cfg():
     h = H.default_config()
     h.update(upsample_initial_channel=32, resblock_kernel_sizes=[3, 7], resblock_dilation_sizes=[[1, 3, 5], [1, 3, 5]])

@@ -358,6 +358,49 @@ def test_hifigan_infer_gpu():
     assert _rel(w, ref_w) < 5e-2
 
 
+@pytest.mark.parametrize("N,Cin,ks", [(256, 256, 3), (128, 128, 3), (2048, 512, 3), (64, 64, 3)])
+@pytest.mark.parametrize("mode", ["dual", "acc_post", "acc_scale"])
+def test_conv_extended_epilogue(N, Cin, ks, mode):
+    """EpiX: (v + acc) * scale -> y2 = lrelu(v), Y = post_act(v), on the big64 (N >= 256) and ring kernels."""
+    torch.manual_seed(2)
+    B, L = 3, 301
+    x = torch.randn(B, L, Cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, Cin, ks, device=DEV) / math.sqrt(Cin * ks)
+    b = torch.randn(N, device=DEV)
+    res = torch.randn(B, L, N, device=DEV).to(torch.bfloat16)
+    acc0 = torch.randn(B, L, N, device=DEV).to(torch.bfloat16)
+    v = ref.conv1d(x.float(), w.to(torch.bfloat16).float(), b, 1, 1, None) + res.float()
+    if mode == "dual":
+        y, y2 = hip.conv1d_infer(x, w, b, 1, 1, None, resid=res, dual_lrelu=True)
+        assert _rel(y, v) < 1e-2 and _rel(y2, F.leaky_relu(v, 0.1)) < 1e-2
+    elif mode == "acc_post":
+        acc = acc0.clone()
+        y = hip.conv1d_infer(x, w, b, 1, 1, None, resid=res, acc=acc, scale=1 / 3, post_act="lrelu")
+        assert y.data_ptr() == acc.data_ptr()
+        assert _rel(y, F.leaky_relu((v + acc0.float()) / 3, 0.1)) < 1e-2
+    else:
+        acc = acc0.clone()
+        y = hip.conv1d_infer(x, w, b, 1, 1, None, resid=res, acc=acc, scale=0.5)
+        assert _rel(y, (v + acc0.float()) * 0.5) < 1e-2
+
+
+def test_hifigan_batch_infer_gpu():
+    """The RTF path at a realistic length: batched HIP generator vs the fp32 NCL forward, with
+    unequal content per utterance (upsampler 3-tap GEMMs, fused MRF epilogues, post-activations)."""
+    from speakingstyle_amd.models import hifigan as H
+
+    torch.manual_seed(21)
+    g = H.Generator(H.default_config()).eval().fold_weight_norm().to(DEV)
+    mel = torch.randn(3, 80, 130, device=DEV) * 2 - 5
+    with torch.no_grad():
+        ref_w = g(mel).squeeze(1)
+        w = g.infer(mel.transpose(1, 2).contiguous().to(torch.bfloat16)).float()
+        pcm = g.infer(mel.transpose(1, 2).contiguous().to(torch.bfloat16), int16_scale=32768.0)
+    assert w.shape == ref_w.shape == (3, 130 * 256)
+    assert _rel(w, ref_w) < 5e-2
+    assert pcm.dtype == torch.int16 and _rel(pcm.float() / 32768.0, ref_w) < 5e-2
+
+
 def test_weight_images_follow_optimizer():
     """bf16 weight images must be re-derived after the fused Adam step (raw-pointer writes)."""
     import copy
