@@ -58,3 +58,10 @@ template <typename Kern>
 static inline void allow_lds(Kern k, size_t bytes) {
   if (bytes > 65536) hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
+
+// Deterministic fixed-order reductions (csrc/k_reduce.hip), callable from every kernel file's host code.
+SSAMD_API int ssamd_seg_colsum(const float* P, long ld, int nseg, int rows, int ncols, float* out, long out_ld,
+                               int accumulate, int ncols1, float* out2, float* ws, long ws_floats, hipStream_t s);
+SSAMD_API int ssamd_small_sum(const float* P, int rows, int k, float* out, hipStream_t s);
+// scratch floats seg_colsum needs for its two-level form
+static inline long seg_colsum_ws(int nseg, int ncols) { return (long)nseg * 16 * ncols; }

@@ -2285,15 +2285,16 @@ __global__ void __launch_bounds__(256) wgrad_reduce_rows_kernel(const float* __r
   for (int k = threadIdx.x; k < K; k += 256) dst[k] = row[k];
 }
 
-// db[n] = sum_m dY[m, n]  (column sums; fp32 atomics after block reduction)
-__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ dY, float* __restrict__ db, long M,
+// db[n] = sum_m dY[m, n]: per row-chunk partials part[chunk][n], finished by a fixed-order column
+// sum (k_reduce.hip) -- deterministic
+__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ dY, float* __restrict__ part, long M,
                                                      int N, int rows_per_block) {
   const long r0 = (long)blockIdx.y * rows_per_block;
   const long r1 = min(M, r0 + rows_per_block);
   for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
     float s = 0.f;
     for (long r = r0; r < r1; ++r) s += bf2f(dY[r * N + n]);
-    atomicAdd(db + n, s);
+    part[(long)blockIdx.y * N + n] = s;
   }
 }
 
@@ -2642,11 +2643,16 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   return (int)hipGetLastError();
 }
 
-SSAMD_API int ssamd_colsum(const bf16_t* dY, float* db, long M, int N, hipStream_t s) {
-  hipMemsetAsync(db, 0, (size_t)N * sizeof(float), s);
-  if (M == 0) return (int)hipGetLastError();
+SSAMD_API long ssamd_colsum_ws(long M, int N) { return (long)cdiv(M, 256) * N + seg_colsum_ws(1, N); }
+
+SSAMD_API int ssamd_colsum(const bf16_t* dY, float* db, long M, int N, float* ws, long ws_floats, hipStream_t s) {
+  if (M == 0) return (int)hipMemsetAsync(db, 0, (size_t)N * sizeof(float), s);
   const int rpb = 256;
-  dim3 grid((N + 255) / 256, (int)((M + rpb - 1) / rpb));
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, dY, db, M, N, rpb);
-  return (int)hipGetLastError();
+  const int chunks = cdiv(M, rpb);
+  if (ws_floats < ssamd_colsum_ws(M, N)) return -3;
+  dim3 grid((N + 255) / 256, chunks);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, dY, ws, M, N, rpb);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  return ssamd_seg_colsum(ws, N, 1, chunks, N, db, 0, 0, N, nullptr, ws + (long)chunks * N, seg_colsum_ws(1, N), s);
 }

@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) lr_bwd_kernel(const bf16_t* __restrict__ 
 // energy bucketized embeddings, modules.py:83-101).
 //   mode 0: out[r] = table[ids[r]] + pe[r % L]            (ids int64)
 //   mode 1: out[r] = x[r] + table[bucketize(vals[r], bins)]  (torch.bucketize, right=False)
-// Backward: dtable[id] += dout[r] with fp32 atomics on 256-B row segments.
+// Backward: dtable[v] = sum of dout rows with id v, deterministic (one block per table row).
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ int bucketize_lower(float v, const float* bins, int nb) {
   int lo = 0, hi = nb;  // number of bins strictly less than v
@@ -123,14 +123,82 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(int mode, const int64_t*
   }
 }
 
+// Deterministic backward: block v owns table row v.  It scans the saved bucket ids in row order
+// (wave ballots, order-preserving compaction into an LDS hit list) and sums the dout rows of its
+// hits in that order -- every dtable element is produced by one thread in a fixed order, no atomics.
+constexpr int EB_UNROLL = 4, EB_HITS = 2048;
+
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const int* __restrict__ idx, const bf16_t* __restrict__ dout,
                                                         float* __restrict__ dtable, long rows, int C) {
-  const long total = rows * C;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const long r = e / C;
-    const int c = (int)(e % C);
-    const float g = bf2f(dout[e]);
-    if (g != 0.f) atomicAdd(dtable + (long)idx[r] * C + c, g);
+  __shared__ int hits[EB_HITS + 256 * EB_UNROLL];
+  __shared__ int wcnt[4 * EB_UNROLL];
+  const int v = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int MAXC = 4;  // channels per thread: C <= 1024
+  float acc[MAXC] = {0.f, 0.f, 0.f, 0.f};
+  int nh = 0;
+  auto flush = [&](int n) {
+    int k = 0;
+    for (; k + 4 <= n; k += 4) {  // 4 independent row loads in flight, added in row order
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = tid + j * 256;
+        if (c < C) {
+          const float x0 = bf2f(dout[(long)hits[k] * C + c]), x1 = bf2f(dout[(long)hits[k + 1] * C + c]);
+          const float x2 = bf2f(dout[(long)hits[k + 2] * C + c]), x3 = bf2f(dout[(long)hits[k + 3] * C + c]);
+          acc[j] = (((acc[j] + x0) + x1) + x2) + x3;
+        }
+      }
+    }
+    for (; k < n; ++k)
+#pragma unroll
+      for (int j = 0; j < MAXC; ++j) {
+        const int c = tid + j * 256;
+        if (c < C) acc[j] += bf2f(dout[(long)hits[k] * C + c]);
+      }
+  };
+  for (long base = 0; base < rows; base += 256 * EB_UNROLL) {
+    int id[EB_UNROLL];
+#pragma unroll
+    for (int u = 0; u < EB_UNROLL; ++u) {
+      const long r = base + u * 256 + tid;
+      id[u] = r < rows ? idx[r] : -1;
+    }
+    unsigned long long m[EB_UNROLL];
+#pragma unroll
+    for (int u = 0; u < EB_UNROLL; ++u) {
+      m[u] = __ballot(id[u] == v);
+      if (lane == 0) wcnt[u * 4 + wave] = __popcll(m[u]);
+    }
+    __syncthreads();
+    int off = nh;
+#pragma unroll
+    for (int u = 0; u < EB_UNROLL; ++u) {
+      int before = 0, tot = 0;
+      for (int w = 0; w < 4; ++w) {
+        const int cw = wcnt[u * 4 + w];
+        if (w < wave) before += cw;
+        tot += cw;
+      }
+      if (id[u] == v) {
+        const int pos = __popcll(m[u] & ((1ull << lane) - 1ull));
+        hits[off + before + pos] = (int)(base + u * 256 + tid);
+      }
+      off += tot;
+    }
+    __syncthreads();
+    nh = off;
+    if (nh >= EB_HITS) {
+      flush(nh);
+      nh = 0;
+      __syncthreads();
+    }
+  }
+  flush(nh);
+#pragma unroll
+  for (int j = 0; j < MAXC; ++j) {
+    const int c = tid + j * 256;
+    if (c < C) dtable[(long)v * C + c] = acc[j];
   }
 }
 
@@ -140,7 +208,7 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int* __restrict__ 
 // ----------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) l1pair_fwd_kernel(const float* __restrict__ p1, const float* __restrict__ p2,
                                                          const float* __restrict__ tgt, const int64_t* __restrict__ lens,
-                                                         int M, int Mt, int C, float* __restrict__ sums, long rows) {
+                                                         int M, int Mt, int C, float* __restrict__ part, long rows) {
   float s1 = 0.f, s2 = 0.f;
   const long total = rows * C;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -158,9 +226,9 @@ __global__ void __launch_bounds__(256) l1pair_fwd_kernel(const float* __restrict
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane == 0) { red[0][wave] = s1; red[1][wave] = s2; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd(sums, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    atomicAdd(sums + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  if (threadIdx.x == 0) {  // per-block partial; finished by a fixed-order sum (k_reduce.hip)
+    part[2 * blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    part[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   }
 }
 
@@ -190,8 +258,8 @@ __global__ void __launch_bounds__(256) l1pair_bwd_kernel(const float* __restrict
 
 // ----------------------------------------------------------------------------
 // Global-norm clip + Adam over the flat fp32 arena (model/optimizer.py:10-15,
-// train.py:97).  Pass 1: sum of squares -> ws[0] (fp32 atomics after wave+block
-// reduction).  Pass 2: coef = min(1, clip / (sqrt(ss) + 1e-6)); a non-finite norm
+// train.py:97).  Pass 1: sum of squares -> per-block partials ws[1..], summed in a fixed order
+// into ws[0] (deterministic).  Pass 2: coef = min(1, clip / (sqrt(ss) + 1e-6)); a non-finite norm
 // skips the update (and counts it) -- no host synchronisation anywhere.
 // ----------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g, long n, float* __restrict__ out) {
@@ -208,7 +276,7 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g,
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const float* __restrict__ g,
@@ -322,19 +390,27 @@ SSAMD_API int ssamd_embed_fwd(int mode, const int64_t* ids, const float* vals, c
   return (int)hipGetLastError();
 }
 
-SSAMD_API int ssamd_embed_bwd(const int* idx, const bf16_t* dout, float* dtable, long rows, int C, hipStream_t s) {
-  if (rows == 0) return 0;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(rows * C)), dim3(256), 0, s, idx, dout, dtable, rows, C);
+// dtable [V, C] is overwritten (rows of unused ids become 0).  C <= 1024.
+SSAMD_API int ssamd_embed_bwd(const int* idx, const bf16_t* dout, float* dtable, long rows, int C, int V,
+                              hipStream_t s) {
+  if (C > 1024 || V <= 0) return -1;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(V), dim3(256), 0, s, idx, dout, dtable, rows, C);
   return (int)hipGetLastError();
 }
 
+SSAMD_API long ssamd_l1pair_ws(int B, int M, int C) { return 2L * grid_for((long)B * M * C, 4); }
+
+// sums[0..1] = (sum |p1 - t|, sum |p2 - t|) over valid frames; ws: ssamd_l1pair_ws floats of partials.
 SSAMD_API int ssamd_l1pair_fwd(const float* p1, const float* p2, const float* tgt, const int64_t* lens, int B, int M,
-                               int Mt, int C, float* sums, hipStream_t s) {
+                               int Mt, int C, float* sums, float* ws, long ws_floats, hipStream_t s) {
   long rows = (long)B * M;
-  if (rows == 0) return 0;
-  hipLaunchKernelGGL(l1pair_fwd_kernel, dim3(grid_for(rows * C, 4)), dim3(256), 0, s, p1, p2, tgt, lens, M, Mt, C,
-                     sums, rows);
-  return (int)hipGetLastError();
+  if (rows == 0) return (int)hipMemsetAsync(sums, 0, 2 * sizeof(float), s);
+  const int nblk = grid_for(rows * C, 4);
+  if (ws_floats < 2L * nblk) return -3;
+  hipLaunchKernelGGL(l1pair_fwd_kernel, dim3(nblk), dim3(256), 0, s, p1, p2, tgt, lens, M, Mt, C, ws, rows);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  return ssamd_small_sum(ws, nblk, 2, sums, s);
 }
 
 SSAMD_API int ssamd_l1pair_bwd(const float* p1, const float* p2, const float* tgt, const int64_t* lens, int B, int M,
@@ -347,11 +423,15 @@ SSAMD_API int ssamd_l1pair_bwd(const float* p1, const float* p2, const float* tg
   return (int)hipGetLastError();
 }
 
+SSAMD_API long ssamd_clip_adam_ws(long n) { return 1L + grid_for(n, 16); }
+
+// ws: ssamd_clip_adam_ws(n) floats (ws[0] = global sum of squares, ws[1..] = block partials)
 SSAMD_API int ssamd_clip_adam(float* p, const float* g, float* m, float* v, long n, float* ws, float clip, float lr,
                               float b1, float b2, float eps, float wd, int step, float* norm_out, long long* skipped,
                               hipStream_t s) {
-  hipMemsetAsync(ws, 0, sizeof(float), s);
-  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n, 16)), dim3(256), 0, s, g, n, ws);
+  const int nblk = grid_for(n, 16);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, s, g, n, ws + 1);
+  ssamd_small_sum(ws + 1, nblk, 1, ws, s);
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2 = 1.f - powf(b2, (float)step);
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 8)), dim3(256), 0, s, p, g, m, v, n, ws, clip, lr, b1, b2, eps, wd,

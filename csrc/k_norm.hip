@@ -130,9 +130,11 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
 }
 
 // Backward.  dh = d(pre_drop(a) + res); da = dh * pre_mask; dres = dh.
-// Accumulates (fp32, atomics after an in-block LDS reduction):
-//   dw[c], db[c]                       LayerNorm affine
-//   S1[b,c] = sum_t dout*yd, S2[b,c] = sum_t dout   (FiLM: dgamma = s_g*S1 ...)
+// Parameter gradients, deterministic: every block writes its (in-block LDS-reduced) partials
+//   part[blk][0..C)   dw        part[blk][C..2C)  db          (LayerNorm affine)
+//   part[blk][2C..3C) S1[b]     part[blk][3C..4C) S2[b]       (FiLM: S1 = sum_t dout*yd, S2 = sum_t dout)
+// (blk = b * gridDim.x + blockIdx.x) and the host finishes them with fixed-order column sums
+// (k_reduce.hip) -- no float atomics.
 template <int EPL>
 __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ a, const bf16_t* __restrict__ res,
@@ -140,8 +142,7 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const float* __restrict__ s_g, const int64_t* __restrict__ lens, const int64_t* __restrict__ cu,
     const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ da_out,
-    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ S1, float* __restrict__ S2, int L, int C,
-    float pre_p, float post_p, uint64_t seed) {
+    float* __restrict__ part, int film, int L, int C, float pre_p, float post_p, uint64_t seed) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][C]
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -149,7 +150,12 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
   const int len = lens ? (int)lens[b] : L;
   const long rowb = cu ? (long)cu[b] : (long)b * L;
   const int Lb = cu ? len : L;
-  if (blockIdx.x * ROWS_PER_BLOCK >= Lb) return;  // block-uniform: before any barrier
+  const int nk = film ? 4 : 2;
+  float* pb = part + ((long)b * gridDim.x + blockIdx.x) * nk * C;
+  if (blockIdx.x * ROWS_PER_BLOCK >= Lb) {  // block-uniform, before any barrier: a zero partial
+    for (int c = threadIdx.x; c < nk * C; c += 256) pb[c] = 0.f;
+    return;
+  }
   float wv[EPL], bv[EPL], G[EPL];
   float acc_w[EPL], acc_b[EPL], acc_s1[EPL], acc_s2[EPL];
   const float sg = fg ? *s_g : 0.f;
@@ -216,20 +222,17 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
       store_row<EPL>(da_out + row * C + c0, dh);
     }
   }
-  // block reduction of the four accumulators, then one atomic per channel
+  // block reduction of the accumulators in a fixed order -> this block's partial row
   float* accs[4] = {acc_w, acc_b, acc_s1, acc_s2};
-  float* dsts[4] = {dw, db, S1 ? S1 + (long)b * C : nullptr, S2 ? S2 + (long)b * C : nullptr};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    if (dsts[k] == nullptr) continue;
+    if (k >= nk) break;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < EPL; ++i) red[wave * C + c0 + i] = accs[k][i];
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += 256) {
-      float s = red[c] + red[C + c] + red[2 * C + c] + red[3 * C + c];
-      if (s != 0.f) atomicAdd(dsts[k] + c, s);
-    }
+    for (int c = threadIdx.x; c < C; c += 256)
+      pb[k * C + c] = (red[c] + red[C + c]) + (red[2 * C + c] + red[3 * C + c]);
   }
 }
 
@@ -256,16 +259,35 @@ SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w
   return (int)hipGetLastError();
 }
 
+// Workspace floats ssamd_addln_bwd needs (partials + the two-level column-sum scratch).
+SSAMD_API long ssamd_addln_bwd_ws(int B, int L, int C, int film) {
+  return (long)cdiv(L, ROWS_PER_BLOCK) * B * (film ? 4 : 2) * C + seg_colsum_ws(1, 2 * C);
+}
+
+// dw / db / S1 / S2 are overwritten (not accumulated).  S1 / S2 may be null (no FiLM).
 SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t* res, const float* w,
                               const float* bias, const float* fg, const float* s_g, const int64_t* lens,
                               const int64_t* cu, const float* mean, const float* rstd, bf16_t* dh, bf16_t* da, float* dw, float* db,
                               float* S1, float* S2, int B, int L, int C, float pre_p, float post_p,
-                              unsigned long long seed, hipStream_t stream) {
+                              unsigned long long seed, float* ws, long ws_floats, hipStream_t stream) {
   if (B == 0 || L == 0) return 0;
-  dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
+  const int film = S1 != nullptr && S2 != nullptr;
+  const int gx = cdiv(L, ROWS_PER_BLOCK);
+  const long nblk = (long)gx * B;
+  const int nk = film ? 4 : 2;
+  if (ws_floats < ssamd_addln_bwd_ws(B, L, C, film)) return -3;
+  dim3 grid(gx, B);
   size_t lds = (size_t)WAVES * C * sizeof(float);
   DISPATCH_EPL(C, hipLaunchKernelGGL(addln_bwd_kernel<EPL>, grid, dim3(256), lds, stream, dout, a, res, w, bias, fg,
-                                     s_g, lens, cu, mean, rstd, dh, da, dw, db, S1, S2, L, C, pre_p, post_p,
+                                     s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
                                      (uint64_t)seed));
-  return (int)hipGetLastError();
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  float* scratch = ws + nblk * nk * C;
+  // dw | db over every block, in block order
+  rc = ssamd_seg_colsum(ws, (long)nk * C, 1, (int)nblk, 2 * C, dw, 0, 0, C, db, scratch, seg_colsum_ws(1, 2 * C),
+                        stream);
+  if (rc || !film) return rc;
+  // S1[b] | S2[b] over the gx blocks of sequence b
+  return ssamd_seg_colsum(ws + 2 * C, (long)nk * C, B, gx, 2 * C, S1, C, 0, C, S2, nullptr, 0, stream);
 }

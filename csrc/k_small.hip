@@ -2,8 +2,8 @@
 //
 //  * variance-predictor head (reference model/modules.py:247,253-257):
 //    out[r] = (h[r,:] . w + b) masked to 0 at padded rows; one wave per row, fused mask.
-//    Backward: dh = g (x) w (masked), dw = sum_r g h, db = sum_r g -- block-reduced, then
-//    one fp32 atomic per channel per block.
+//    Backward: dh = g (x) w (masked), dw = sum_r g h, db = sum_r g -- block-reduced into one
+//    partial row per block, finished by a fixed-order column sum (deterministic, no atomics).
 //  * HiFi-GAN conv_post (K V4/V6, reference hifigan/models.py:145,161-163 +
 //    utils/model.py:105-113): LeakyReLU(0.01) -> Conv1d(C -> 1, k=7, pad 3) -> tanh, and
 //    optionally * max_wav_value -> clamp -> int16, channel-last input read once through an
@@ -45,8 +45,8 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const bf16_t* __restrict_
 template <int EPL>
 __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__ g, const bf16_t* __restrict__ h,
                                                        const float* __restrict__ w, const int64_t* __restrict__ lens,
-                                                       long R, int L, bf16_t* __restrict__ dh, float* __restrict__ dw,
-                                                       float* __restrict__ db) {
+                                                       long R, int L, bf16_t* __restrict__ dh,
+                                                       float* __restrict__ part) {
   __shared__ float red[4][64 * EPL + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float wv[EPL], acc[EPL];
@@ -77,14 +77,8 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__
   for (int i = 0; i < EPL; ++i) red[wave][lane * EPL + i] = acc[i];
   if (lane == 0) red[wave][64 * EPL] = gsum;
   __syncthreads();
-  for (int c = threadIdx.x; c <= 64 * EPL; c += 256) {
-    const float v = red[0][c] + red[1][c] + red[2][c] + red[3][c];
-    if (c < 64 * EPL) {
-      if (v != 0.f) atomicAdd(dw + c, v);
-    } else if (db && v != 0.f) {
-      atomicAdd(db, v);
-    }
-  }
+  float* pb = part + (long)blockIdx.x * (64 * EPL + 1);
+  for (int c = threadIdx.x; c <= 64 * EPL; c += 256) pb[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 
 // conv_post: block = 256 output samples of one utterance; LDS tile of (256 + 6) input rows x C
@@ -155,13 +149,19 @@ SSAMD_API int ssamd_head_fwd(const bf16_t* h, const float* w, const float* b, co
   return (int)hipGetLastError();
 }
 
-// dw / db must be zeroed by the caller (they accumulate)
+SSAMD_API long ssamd_head_bwd_ws(long R, int C) { return (long)cdiv(R, HEAD_ROWS) * (C + 1) + seg_colsum_ws(1, C + 1); }
+
+// dw / db (db may be null) are overwritten with fixed-order sums of the per-block partials.
 SSAMD_API int ssamd_head_bwd(const float* g, const bf16_t* h, const float* w, const int64_t* lens, long R, int L,
-                             int C, bf16_t* dh, float* dw, float* db, hipStream_t s) {
+                             int C, bf16_t* dh, float* dw, float* db, float* ws, long ws_floats, hipStream_t s) {
   if (R == 0) return 0;
-  HEAD_DISPATCH(C, hipLaunchKernelGGL(head_bwd_kernel<EPL>, dim3(cdiv(R, HEAD_ROWS)), dim3(256), 0, s, g, h, w, lens,
-                                      R, L, dh, dw, db));
-  return (int)hipGetLastError();
+  const int nblk = cdiv(R, HEAD_ROWS);
+  if (ws_floats < ssamd_head_bwd_ws(R, C)) return -3;
+  HEAD_DISPATCH(C, hipLaunchKernelGGL(head_bwd_kernel<EPL>, dim3(nblk), dim3(256), 0, s, g, h, w, lens, R, L, dh, ws));
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  return ssamd_seg_colsum(ws, C + 1, 1, nblk, db ? C + 1 : C, dw, 0, 0, C, db, ws + (long)nblk * (C + 1),
+                          seg_colsum_ws(1, C + 1), s);
 }
 
 SSAMD_API int ssamd_conv_post(const bf16_t* x, const float* w, const float* b, int B, int T, int C, float slope,

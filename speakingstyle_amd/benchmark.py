@@ -112,7 +112,7 @@ def train_phase(args, rank, world, device):
     model = FastSpeech2(pp, mc).to(device)
     model.set_compute_dtype(torch.bfloat16 if cuda else torch.float32)
     ddp.broadcast_module_state(model)
-    trainer = Trainer(model, (pp, mc, tc))
+    trainer = Trainer(model, (pp, mc, tc), seed=1234)
 
     gen = SyntheticBatches(batch, device=device, max_seq_len=mc["max_seq_len"], seed=1000 + rank,
                            frame_level=pp["preprocessing"]["pitch"]["feature"] == "frame_level")

@@ -244,6 +244,24 @@ def _load_stats(preprocess_config):
     return {"pitch": [-4.0, 12.0, 0.0, 1.0], "energy": [-2.0, 10.0, 0.0, 1.0]}
 
 
+def _spker_table(preprocess_config):
+    """[n_speakers, dim] fp32 table of ``spker_embed/{speaker}-spker_embed.npy`` (ordered by the
+    speakers.json ids), or None when no speaker embedder is configured.  Missing files are an error."""
+    emb = preprocess_config["preprocessing"].get("speaker_embedder", "none")
+    if emb in (None, "none"):
+        return None
+    root = preprocess_config["path"]["preprocessed_path"]
+    with open(os.path.join(root, "speakers.json")) as f:
+        smap = json.load(f)
+    import numpy as np
+
+    rows = [None] * len(smap)
+    for name, i in smap.items():
+        v = np.load(os.path.join(root, "spker_embed", f"{name}-spker_embed.npy"), allow_pickle=False)
+        rows[int(i)] = np.asarray(v, dtype=np.float32).reshape(-1)
+    return torch.from_numpy(np.stack(rows))
+
+
 def _n_speakers(preprocess_config):
     path = os.path.join(preprocess_config["path"]["preprocessed_path"], "speakers.json")
     if os.path.exists(path):
@@ -269,8 +287,19 @@ class FastSpeech2(nn.Module):
         self.mel_linear = nn.Linear(model_config["transformer"]["decoder_hidden"], n_mel)
         self.postnet = PostNet(n_mel)
         self.speaker_emb = None
+        d = model_config["transformer"]["encoder_hidden"]
         if model_config["multi_speaker"]:
-            self.speaker_emb = nn.Embedding(_n_speakers(preprocess_config), model_config["transformer"]["encoder_hidden"])
+            self.speaker_emb = nn.Embedding(_n_speakers(preprocess_config), d)
+        # external speaker embeddings (reference ``synthesize.py:268-277``: ``{spk}-spker_embed.npy`` under
+        # ``preprocessed_path/spker_embed`` when ``preprocessing.speaker_embedder != 'none'``).  The
+        # reference loads them and drops them; here they condition the model: a per-speaker table
+        # (non-persistent buffer, looked up by speaker id in training and synthesis alike) projected
+        # to the encoder width and added next to the speaker-id embedding.
+        table = _spker_table(preprocess_config) if model_config["multi_speaker"] else None
+        self.spker_embed_proj = None
+        if table is not None:
+            self.register_buffer("spker_table", table, persistent=False)
+            self.spker_embed_proj = nn.Linear(table.shape[1], d)
         self.compute_dtype = torch.float32
 
     # ------------------------------------------------------------------ helpers
@@ -318,7 +347,10 @@ class FastSpeech2(nn.Module):
         style = self.compute_style(mels, mel_lens, max_mel_len, texts.shape[0], dev, style_weights)
         x = self.encoder(texts, src_lens, style, cd)
         if self.speaker_emb is not None:
-            x = x + self.speaker_emb(speakers).to(cd).unsqueeze(1)
+            spk = self.speaker_emb(speakers)
+            if self.spker_embed_proj is not None:
+                spk = spk + self.spker_embed_proj(self.spker_table[speakers])
+            x = x + spk.to(cd).unsqueeze(1)
         training_lr = d_targets is not None
         packed = (self.training and training_lr and mel_lens is not None and mel_lens_host is not None
                   and max_mel_len is not None and self.variance_adaptor.packable())

@@ -44,17 +44,22 @@ _SIGS = {
     "ssamd_attn_set_q_dma": [I, I],
     "ssamd_wgrad_set_blocks": [I],
     "ssamd_head_fwd": [P, P, P, P, L_, I, I, P, P],
-    "ssamd_head_bwd": [P, P, P, P, L_, I, I, P, P, P, P],
+    "ssamd_head_bwd": [P, P, P, P, L_, I, I, P, P, P, P, L_, P],
+    "ssamd_head_bwd_ws": [L_, I],
     "ssamd_conv_post": [P, P, P, I, I, I, F, F, P, P, P],
-    "ssamd_colsum": [P, P, L_, I, P],
+    "ssamd_colsum": [P, P, L_, I, P, L_, P],
+    "ssamd_colsum_ws": [L_, I],
     "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
-    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P],
+    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P, L_, P],
+    "ssamd_addln_bwd_ws": [I, I, I, I],
     "ssamd_lr_fwd": [P, P, P, P, P, P, I, I, I, I, P],
     "ssamd_lr_bwd": [P, P, P, P, P, I, I, I, I, P],
     "ssamd_pack_info": [P, I, I, P, P, P, P],
     "ssamd_embed_fwd": [I, P, P, P, I, P, P, I, P, P, L_, I, P],
-    "ssamd_embed_bwd": [P, P, P, L_, I, P],
-    "ssamd_l1pair_fwd": [P, P, P, P, I, I, I, I, P, P],
+    "ssamd_embed_bwd": [P, P, P, L_, I, I, P],
+    "ssamd_l1pair_fwd": [P, P, P, P, I, I, I, I, P, P, L_, P],
+    "ssamd_l1pair_ws": [I, I, I],
+    "ssamd_clip_adam_ws": [L_],
     "ssamd_l1pair_bwd": [P, P, P, P, I, I, I, I, P, P, P, P, P],
     "ssamd_clip_adam": [P, P, P, P, L_, P, F, F, F, F, F, F, I, P, P, P],
     "ssamd_attn_fwd": [P, P, P, P, P, I, I, I, I, F, P],
@@ -65,6 +70,10 @@ _SIGS = {
     "ssamd_weight_prep": [P, P, I, L_, P],
     "ssamd_weight_prep_tiled": [P, P, I, P],
 }
+
+
+_RESTYPES = {"ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws": L_, "ssamd_embed_bwd_ws": L_,
+             "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_}
 
 
 def lib():
@@ -81,7 +90,7 @@ def lib():
                     fn = getattr(handle, name, None)
                     if fn is not None:
                         fn.argtypes = args
-                        fn.restype = I
+                        fn.restype = _RESTYPES.get(name, I)
                 _lib = handle
     return _lib
 
@@ -109,6 +118,24 @@ def _stream():
 def _check(rc, name):
     if rc != 0:
         raise RuntimeError(f"{name} failed with code {rc}")
+
+
+_FALLBACK_OK = os.environ.get("SSAMD_ALLOW_TORCH_FALLBACK") == "1"
+_fallback_seen = set()
+
+
+def _torch_fallback(what: str):
+    """A GPU op got a shape / dtype its HIP kernel does not cover.  That is an error (a silent
+    torch path on the GPU would hide itself in every benchmark) unless explicitly opted into
+    with ``SSAMD_ALLOW_TORCH_FALLBACK=1`` (then it warns once per site)."""
+    if not _FALLBACK_OK:
+        raise ValueError(f"{what}: not covered by the HIP kernels; set SSAMD_ALLOW_TORCH_FALLBACK=1 to run the "
+                         "torch reference op on the GPU instead")
+    if what not in _fallback_seen:
+        _fallback_seen.add(what)
+        import warnings
+
+        warnings.warn(f"torch fallback on the GPU: {what}")
 
 
 def _need(t, dtype, name):
@@ -300,7 +327,9 @@ def colsum_raw(dy, N, db=None):
     _need(dy, torch.bfloat16, "colsum.dy")
     if db is None:
         db = torch.empty(N, device=dy.device, dtype=torch.float32)
-    rc = lib().ssamd_colsum(_ptr(dy), _ptr(db), dy.numel() // N, N, _stream())
+    M = dy.numel() // N
+    ws = _workspace(dy.device, int(lib().ssamd_colsum_ws(M, N)))
+    rc = lib().ssamd_colsum(_ptr(dy), _ptr(db), M, N, _ptr(ws), ws.numel(), _stream())
     _check(rc, "ssamd_colsum")
     return db
 
@@ -364,7 +393,8 @@ def linear(x, w, b=None, act=None, out_f32=False):
     shp = x.shape
     x3 = x.reshape(1, -1, shp[-1]) if x.dim() != 3 else x
     if x3.shape[-1] % 8 or w.shape[0] % 8:
-        # tiny heads (e.g. the variance-predictor Linear(256 -> 1)): not MFMA-shaped
+        # not MFMA-shaped (the N = 1 variance-predictor head has its own kernel: predictor_head)
+        _torch_fallback(f"linear {x3.shape[-1]}->{w.shape[0]} (dims must be multiples of 8)")
         return ref.linear(x, w, b, act)
     y = _ConvFn.apply(x3, w, b, 0, 1, act, out_f32)
     return y.reshape(*shp[:-1], w.shape[0])
@@ -508,6 +538,10 @@ def set_seed(s: int):
     _seed_counter[0] = int(s) & ((1 << 64) - 1)
 
 
+def get_seed() -> int:
+    return _seed_counter[0]
+
+
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox):
@@ -537,16 +571,18 @@ class _AddLNFn(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous()
         dh = torch.empty_like(ac)
         da = torch.empty_like(ac) if pre_p > 0 else None
-        dw, db = gradslots.claim(w), gradslots.claim(b)  # zeroed slots double as the atomic accumulators
+        dw, db = gradslots.claim(w), gradslots.claim(b)  # written (not accumulated) by the fixed-order reduce
         if dw is None:
-            dw = torch.zeros(C, device=ac.device, dtype=torch.float32)
+            dw = torch.empty(C, device=ac.device, dtype=torch.float32)
         if db is None:
-            db = torch.zeros(C, device=ac.device, dtype=torch.float32)
-        S1 = torch.zeros(B, C, device=ac.device, dtype=torch.float32) if has_film else None
-        S2 = torch.zeros_like(S1) if has_film else None
+            db = torch.empty(C, device=ac.device, dtype=torch.float32)
+        S1 = torch.empty(B, C, device=ac.device, dtype=torch.float32) if has_film else None
+        S2 = torch.empty_like(S1) if has_film else None
+        nws = int(lib().ssamd_addln_bwd_ws(B, L, C, int(has_film)))
+        ws = _workspace(ac.device, nws)
         rc = lib().ssamd_addln_bwd(_ptr(dout), _ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(sg), _ptr(lens),
                                    _ptr(ctx.cu), _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da), _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
-                                   B, L, C, pre_p, post_p, seed, _stream())
+                                   B, L, C, pre_p, post_p, seed, _ptr(ws), ws.numel(), _stream())
         _check(rc, "ssamd_addln_bwd")
         d_a = da if da is not None else dh
         d_res = dh if has_res else None
@@ -568,6 +604,7 @@ def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, train
     if C not in (256, 512, 1024) or a.dtype != torch.bfloat16:
         if pack is not None:
             raise ValueError("packed add_layernorm needs C in (256, 512, 1024) and bf16")
+        _torch_fallback(f"add_layernorm C={C} dtype={a.dtype} (kernel: C in 256/512/1024, bf16)")
         return ref.add_layernorm(a, residual, ln_w, ln_b, pre_drop=pre_drop, post_drop=post_drop, training=training,
                                  film_params=film_params, lengths=lengths, eps=eps)
     if not training:
@@ -617,6 +654,7 @@ class _LRFn(torch.autograd.Function):
 
 def length_regulate(x, durations, max_len, pe=None):
     if x.dtype != torch.bfloat16 or x.shape[-1] % 8:
+        _torch_fallback(f"length_regulate C={x.shape[-1]} dtype={x.dtype} (kernel: bf16, C % 8 == 0)")
         out, ml = ref.length_regulate(x, durations, max_len)
         return (out + pe[: out.shape[1]].to(out.dtype) if pe is not None else out), ml
     dur = durations.to(torch.int64).contiguous()
@@ -692,8 +730,9 @@ class _EmbedFn(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous()
         dt = gradslots.claim(ctx.table) if ctx.needs_input_grad[4] else None
         if dt is None:
-            dt = torch.zeros(shape, device=dout.device, dtype=torch.float32)
-        rc = lib().ssamd_embed_bwd(_ptr(idx), _ptr(dout), _ptr(dt), idx.numel(), shape[1], _stream())
+            dt = torch.empty(shape, device=dout.device, dtype=torch.float32)
+        # one block per table row, fixed summation order (deterministic; every row is written)
+        rc = lib().ssamd_embed_bwd(_ptr(idx), _ptr(dout), _ptr(dt), idx.numel(), shape[1], shape[0], _stream())
         _check(rc, "ssamd_embed_bwd")
         d_add = dout if ctx.mode == 1 else None
         return None, None, None, None, dt if dtype == torch.float32 else dt.to(dtype), d_add, None
@@ -759,8 +798,10 @@ class _L1PairFn(torch.autograd.Function):
         B, M, C = p1.shape
         Mt = tgt.shape[1]
         p1c, p2c, tc = p1.float().contiguous(), p2.float().contiguous(), tgt.float().contiguous()
-        sums = torch.zeros(2, device=p1.device, dtype=torch.float32)
-        rc = lib().ssamd_l1pair_fwd(_ptr(p1c), _ptr(p2c), _ptr(tc), _ptr(lens), B, M, Mt, C, _ptr(sums), _stream())
+        sums = torch.empty(2, device=p1.device, dtype=torch.float32)
+        ws = _workspace(p1.device, int(lib().ssamd_l1pair_ws(B, M, C)))
+        rc = lib().ssamd_l1pair_fwd(_ptr(p1c), _ptr(p2c), _ptr(tc), _ptr(lens), B, M, Mt, C, _ptr(sums), _ptr(ws),
+                                    ws.numel(), _stream())
         _check(rc, "ssamd_l1pair_fwd")
         cnt = count.float().reshape(1).contiguous()
         ctx.save_for_backward(p1c, p2c, tc, lens, cnt)
@@ -792,9 +833,10 @@ def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped
     for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
         _need(t, torch.float32, "adam." + nm)
     assert p.numel() == g.numel() == m.numel() == v.numel()
+    n_ws = int(lib().ssamd_clip_adam_ws(p.numel()))
     ws = _adam_ws.get(p.device)
-    if ws is None:
-        ws = _adam_ws[p.device] = torch.zeros(4, device=p.device, dtype=torch.float32)
+    if ws is None or ws.numel() < n_ws:  # [global sum of squares, per-block partials]
+        ws = _adam_ws[p.device] = torch.zeros(n_ws, device=p.device, dtype=torch.float32)
     rc = lib().ssamd_clip_adam(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(ws), float(clip), float(lr),
                                float(betas[0]), float(betas[1]), float(eps), float(wd), int(step), _ptr(norm_out),
                                _ptr(skipped), _stream())
@@ -1147,16 +1189,17 @@ class _HeadFn(torch.autograd.Function):
         B, L, C = hc.shape
         g = g.float().contiguous()
         dh = torch.empty_like(hc)
-        dw = gradslots.claim(w)  # zeroed arena slot, or a fresh zeroed accumulator
+        dw = gradslots.claim(w)  # arena slot (overwritten by the fixed-order reduce) or a fresh buffer
         if dw is None:
-            dw = torch.zeros_like(w, dtype=torch.float32)
+            dw = torch.empty_like(w, dtype=torch.float32)
         db = None
         if b is not None:
             db = gradslots.claim(b)
             if db is None:
-                db = torch.zeros_like(b, dtype=torch.float32)
+                db = torch.empty_like(b, dtype=torch.float32)
+        ws = _workspace(hc.device, int(lib().ssamd_head_bwd_ws(B * L, C)))
         rc = lib().ssamd_head_bwd(_ptr(g), _ptr(hc), _ptr(wf), _ptr(lens), B * L, L, C, _ptr(dh), _ptr(dw), _ptr(db),
-                                  _stream())
+                                  _ptr(ws), ws.numel(), _stream())
         _check(rc, "ssamd_head_bwd")
         return dh.to(ctx.hdtype), dw, db, None
 

@@ -99,9 +99,11 @@ def train(args, configs):
         ckpt = mutil.load_checkpoint(mutil.ckpt_file(train_config, restore))
         mutil.restore_model(model, ckpt, train_config.get("ignore_layers", []))
     ddp.broadcast_module_state(model)
-    trainer = Trainer(model, configs, restore_step=restore)
+    trainer = Trainer(model, configs, restore_step=restore, seed=seed)
     if ckpt is not None and "optimizer" in ckpt:
         trainer.opt.load_state_dict(ckpt["optimizer"])
+    if ckpt is not None and isinstance(ckpt.get("rng"), torch.Tensor) and not cuda:
+        torch.set_rng_state(ckpt["rng"])  # CPU dropout (torch RNG); the GPU masks are step-seeded
     if rank == 0:
         print("Number of FastSpeech2 Parameters:", mutil.get_param_num(model), flush=True)
 

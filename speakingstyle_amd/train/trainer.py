@@ -29,7 +29,8 @@ from .optim import ScheduledOptim
 
 
 class Trainer:
-    def __init__(self, model, configs, restore_step: int = 0, bucket_mb: Optional[float] = None):
+    def __init__(self, model, configs, restore_step: int = 0, bucket_mb: Optional[float] = None,
+                 seed: Optional[int] = None):
         preprocess_config, model_config, train_config = configs
         self.model = model
         self.configs = configs
@@ -45,6 +46,11 @@ class Trainer:
         self.last_lr = self.opt._get_lr()
         self.frames = torch.zeros((), dtype=torch.int64, device=self.opt.arena.data.device)
         self.frames_host = 0
+        # dropout masks (counter-hash RNG in the HIP kernels) are seeded per micro-step from
+        # (seed, rank, optimizer step, micro-step): a resumed run reproduces the masks of an
+        # uninterrupted one bit for bit, with nothing extra stored in the checkpoint
+        self.seed = seed
+        self.rank = ddp.rank()
 
     def take_frames(self) -> int:
         """Valid mel frames consumed since the last call, summed over ranks (host sync: log steps only)."""
@@ -83,8 +89,17 @@ class Trainer:
         work = ddp.all_reduce_async(c)
         return c, work
 
+    def _step_seed(self):
+        if self.seed is None or not self.opt.arena.data.is_cuda:
+            return
+        from ..ops import hip
+
+        k = (self.seed * 1000003 + self.rank) * 1000003 + self.opt.current_step
+        hip.set_seed((k * 64 + self.micro % self.grad_acc) * 0x9E3779B97F4A7C15)
+
     def train_step(self, batch):
         self.model.train()
+        self._step_seed()
         counts, work = self._global_counts(batch) if self.world > 1 else (None, None)
         last_micro = (self.micro + 1) % self.grad_acc == 0
         output = self.model(*batch[2:])
