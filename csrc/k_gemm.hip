@@ -59,6 +59,27 @@ struct EpiX {
   bf16_t* y2;
   float scale;
   int post_act;
+  // Fused residual + LayerNorm tail (big64 only, N == 256: one 256x256 tile owns whole rows).
+  // With ln_out set, the GEMM output a (bias added, bf16) is stored as usual AND
+  //   ln_out = rowmask( FiLM( post_drop( LN( pre_drop(a) + ln_res ) ) ) ), mean / rstd per row,
+  // bit-identical to the separate addln_fwd kernel (k_norm.hip) on the same a, whose backward
+  // consumes (a, ln_res, mean, rstd) unchanged.  Rows: unpacked (m = b*Lseq + t, valid t < lens[b])
+  // or packed (dst[m] = b*Mseq + t, all rows valid).
+  const bf16_t* ln_res;
+  const float* ln_w;
+  const float* ln_b;
+  const float* film_g;
+  const float* film_b;
+  const float* s_g;
+  const float* s_b;
+  const int64_t* ln_lens;
+  const int64_t* dst;
+  bf16_t* ln_out;
+  float* mean;
+  float* rstd;
+  int Lseq, Mseq;
+  float pre_p, post_p, eps;
+  unsigned long long seed;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -1022,6 +1043,92 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       }
       __syncthreads();
       bf16_t* Y = reinterpret_cast<bf16_t*>(Yv);
+      if (ex.ln_out) {
+        // Residual + LayerNorm tail (N == 256, n0 == 0): half-wave h = tid >> 5 owns rows h, h+16, ...
+        // of the tile, lane c = tid & 31 owns columns 8c..8c+7.  Every global operand of the 16 rows
+        // (residual segments, row -> sequence / validity) is loaded up front and the FiLM rows one
+        // row ahead, so the epilogue is not a chain of exposed load latencies.
+        const int c = tid & 31, h = tid >> 5, n = c * 8;
+        float lw[8], lb[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          lw[q] = ex.ln_w[n + q];
+          lb[q] = ex.ln_b[n + q];
+        }
+        short8 rr[16];
+        int bq[16];
+        bool rv[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          const int m = m0 + h + it * 16;
+          const int mm = m < g.M ? m : g.M - 1;
+          rr[it] = *reinterpret_cast<const short8*>(ex.ln_res + (long)mm * 256 + n);
+          if (ex.dst) {
+            bq[it] = (int)(ex.dst[mm] / ex.Mseq);
+            rv[it] = true;
+          } else {
+            bq[it] = mm / ex.Lseq;
+            rv[it] = ex.ln_lens ? (mm - bq[it] * ex.Lseq) < (int)ex.ln_lens[bq[it]] : true;
+          }
+        }
+        const bool film = ex.film_g != nullptr;
+        const float sg = film ? *ex.s_g : 0.f, sb = film ? *ex.s_b : 0.f;
+        float fg[8], fb[8];
+        auto load_film = [&](int b) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            fg[q] = film ? ex.film_g[(long)b * 256 + n + q] : 0.f;
+            fb[q] = film ? ex.film_b[(long)b * 256 + n + q] : 0.f;
+          }
+        };
+        load_film(bq[0]);
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          const int r = h + it * 16, m = m0 + r;
+          float G[8], Bt[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            G[q] = sg * fg[q] + 1.f;
+            Bt[q] = sb * fb[q];
+          }
+          if (it + 1 < 16 && film && bq[it + 1] != bq[it]) load_film(bq[it + 1]);  // one row ahead
+          if (m >= g.M) continue;  // uniform over the half-wave
+          const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
+          const long ro = (long)m * 256 + n;
+          *reinterpret_cast<short8*>(Y + ro) = v;  // a (the pre-LN GEMM output: the backward reads it)
+          float hv[8], sum = 0.f;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            hv[q] = bf2f((bf16_t)v[q]);
+            if (ex.pre_p > 0.f) hv[q] *= drop_scale(ex.seed, (uint64_t)ro + q, ex.pre_p);
+            hv[q] += bf2f((bf16_t)rr[it][q]);
+            sum += hv[q];
+          }
+#pragma unroll
+          for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+          const float mu = sum * (1.f / 256.f);
+          float sq = 0.f;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) sq += (hv[q] - mu) * (hv[q] - mu);
+#pragma unroll
+          for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+          const float rs = rsqrtf(sq * (1.f / 256.f) + ex.eps);
+          short8 o8;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float y = (hv[q] - mu) * rs * lw[q] + lb[q];
+            if (ex.post_p > 0.f) y *= drop_scale(ex.seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)ro + q, ex.post_p);
+            y = G[q] * y + Bt[q];
+            o8[q] = (short)f2bf(rv[it] ? y : 0.f);
+          }
+          *reinterpret_cast<short8*>(ex.ln_out + ro) = o8;
+          if (c == 0) {
+            ex.mean[m] = mu;
+            ex.rstd[m] = rs;
+          }
+        }
+        return;
+      }
       const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f;
       for (int e = tid; e < BG * 32; e += NT3) {
         const int r = e >> 5, c = e & 31;
@@ -2348,6 +2455,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     if (N >= 256) variant = 4;
     else if (variant != 2) return -3;
   }
+  if (ex.ln_out) {  // the LayerNorm tail needs whole rows in one tile and the plain bf16 store
+    if (xon || N != 256 || ldy != 256 || out_f32 || !reg || act != 0 || aux || resid || lens) return -3;
+    variant = 4;
+  }
   if (g_debug_nostore && variant >= 3) act = -1;
   if (reg && variant == 3 && N >= 256) {
     static bool big_set = false;
@@ -2492,7 +2603,8 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
 SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
                               const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
                               int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, hipStream_t s) {
-  const EpiX ex{nullptr, nullptr, 1.f, 0};
+  EpiX ex{};
+  ex.scale = 1.f;
   return conv_gemm_impl(X, W, bias, aux, resid, lens, Y, out_f32, B, L, Cin, ks, dil, pad, N, act, ldy, rinfo, ex, s);
 }
 
@@ -2500,8 +2612,36 @@ SSAMD_API int ssamd_conv_gemm(const bf16_t* X, const bf16_t* W, const float* bia
 SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* resid, void* Y,
                                  int B, int L, int Cin, int ks, int dil, int pad, int N, int act, const bf16_t* acc,
                                  bf16_t* y2, float scale, int post_act, hipStream_t s) {
-  const EpiX ex{acc, y2, scale, post_act};
+  EpiX ex{};
+  ex.acc = acc;
+  ex.y2 = y2;
+  ex.scale = scale;
+  ex.post_act = post_act;
   return conv_gemm_impl(X, W, bias, nullptr, resid, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, nullptr, ex, s);
+}
+
+// conv_gemm (N = 256, bf16 out a) + the fused residual/LayerNorm/dropout/FiLM/mask tail (EpiX.ln_*).
+// rinfo: packed A-operand sequence table (k > 1 convs); dst: packed rows' b*Mseq + t (needed for FiLM
+// on packed rows); ln_lens: unpacked rows' valid lengths (rows t >= lens[b] -> 0).
+SSAMD_API int ssamd_conv_gemm_ln(const bf16_t* X, const bf16_t* W, const float* bias, void* Y, int B, int L, int Cin,
+                                 int ks, int dil, int pad, int N, const int* rinfo, const bf16_t* res,
+                                 const float* ln_w, const float* ln_b, const float* film_g, const float* film_b,
+                                 const float* s_g, const float* s_b, const int64_t* ln_lens, const int64_t* dst,
+                                 int Mseq, bf16_t* ln_out, float* mean, float* rstd, float pre_p, float post_p,
+                                 float eps, unsigned long long seed, hipStream_t s) {
+  if (!res || !ln_w || !ln_b || !ln_out || !mean || !rstd) return -2;
+  if ((film_g != nullptr) != (film_b != nullptr) || (film_g && (!s_g || !s_b))) return -2;
+  if (dst && ln_lens) return -2;  // packed rows (dst) are all valid; unpacked rows use lens
+  EpiX ex{};
+  ex.scale = 1.f;
+  ex.ln_res = res; ex.ln_w = ln_w; ex.ln_b = ln_b;
+  ex.film_g = film_g; ex.film_b = film_b; ex.s_g = s_g; ex.s_b = s_b;
+  ex.ln_lens = ln_lens;
+  ex.dst = dst;
+  ex.ln_out = ln_out; ex.mean = mean; ex.rstd = rstd;
+  ex.Lseq = L; ex.Mseq = Mseq > 0 ? Mseq : 1;
+  ex.pre_p = pre_p; ex.post_p = post_p; ex.eps = eps; ex.seed = seed;
+  return conv_gemm_impl(X, W, bias, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, rinfo, ex, s);
 }
 
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.

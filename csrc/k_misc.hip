@@ -390,6 +390,34 @@ SSAMD_API int ssamd_embed_fwd(int mode, const int64_t* ids, const float* vals, c
   return (int)hipGetLastError();
 }
 
+// One-hot expansion of the saved ids: oh[r, v] = (idx[r] == v) in bf16, [rows, Vpad] -- the
+// embedding backward then is the weight-gradient GEMM dtable = oh^T @ dout on the MFMA wgrad
+// kernel (exact: the one-hot factors are 0 / 1), deterministic through its fixed-order slab reduce,
+// and insensitive to skewed id distributions (pitch / energy buckets).
+namespace {
+__global__ void __launch_bounds__(256) onehot_kernel(const int* __restrict__ idx, long rows, int Vpad,
+                                                     bf16_t* __restrict__ oh) {
+  const int v8 = Vpad / 8;
+  const long total = rows * v8;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long r = e / v8;
+    const int c0 = (int)(e - r * v8) * 8;
+    const int id = idx[r];
+    short8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (c0 + i == id) ? (short)0x3F80 : (short)0;  // bf16 1.0
+    *reinterpret_cast<short8*>(oh + r * Vpad + c0) = o;
+  }
+}
+}  // namespace
+
+SSAMD_API int ssamd_onehot(const int* idx, long rows, int Vpad, bf16_t* oh, hipStream_t s) {
+  if (Vpad % 8) return -1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(onehot_kernel, dim3(grid_for(rows * (Vpad / 8))), dim3(256), 0, s, idx, rows, Vpad, oh);
+  return (int)hipGetLastError();
+}
+
 // dtable [V, C] is overwritten (rows of unused ids become 0).  C <= 1024.
 SSAMD_API int ssamd_embed_bwd(const int* idx, const bf16_t* dout, float* dtable, long rows, int C, int V,
                               hipStream_t s) {
@@ -547,5 +575,128 @@ SSAMD_API int ssamd_weight_prep(const void* table, const long* cum, int n, long 
   if (n == 0 || total == 0) return 0;
   hipLaunchKernelGGL(weight_prep_kernel, dim3(grid_for(total, 4)), dim3(256), 0, s,
                      reinterpret_cast<const WDesc*>(table), cum, n, total);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// Fused variance losses (reference model/loss.py:76-89): the masked MSE of pitch, energy
+// and log-duration in one pass.  Each term k reads pred_k [B, L_k] (row stride ldp_k), its target
+// (fp32, or int64 durations -> log(d + 1), row stride ldt_k) and its pad mask (bool [B, L_k],
+// true = padded).  Pass 1: per-block partial (sum, count) for the 3 terms; pass 2 (one block):
+// fixed-order sums, loss_k = sum_k / max(count_k, 1) with count_k from the masks or given
+// (the all-reduced global counts under data parallelism).  Backward: d pred_k = 2 g_k (pred - t)
+// * valid / count_k.  Deterministic, no atomics.
+// ----------------------------------------------------------------------------
+struct VTerm {
+  const float* pred;
+  const void* tgt;
+  const bool* mask;
+  float* grad;
+  int L, ldp, ldt, dur;
+};
+
+namespace {
+__device__ __forceinline__ float vterm_diff(const VTerm& t, int b, int j, bool& valid) {
+  valid = !t.mask[(long)b * t.L + j];
+  if (!valid) return 0.f;
+  const float p = t.pred[(long)b * t.ldp + j];
+  const float y = t.dur ? logf((float)reinterpret_cast<const int64_t*>(t.tgt)[(long)b * t.ldt + j] + 1.f)
+                        : reinterpret_cast<const float*>(t.tgt)[(long)b * t.ldt + j];
+  return p - y;
+}
+
+__global__ void __launch_bounds__(256) var_loss_fwd_kernel(VTerm t0, VTerm t1, VTerm t2, int B,
+                                                           float* __restrict__ part) {
+  const VTerm ts[3] = {t0, t1, t2};
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const long n0 = (long)B * t0.L, n1 = n0 + (long)B * t1.L, n2 = n1 + (long)B * t2.L;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n2; e += (long)gridDim.x * 256) {
+    const int k = e < n0 ? 0 : (e < n1 ? 1 : 2);
+    const long o = e - (k == 0 ? 0 : (k == 1 ? n0 : n1));
+    const int L = ts[k].L;
+    const int b = (int)(o / L), j = (int)(o - (long)b * L);
+    bool valid;
+    const float d = vterm_diff(ts[k], b, j, valid);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q == k) {
+        acc[q] += d * d;
+        acc[3 + q] += valid ? 1.f : 0.f;
+      }
+  }
+  __shared__ float red[6][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const float v = wave_sum(acc[q]);
+    if (lane == 0) red[q][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = (red[threadIdx.x][0] + red[threadIdx.x][1]) +
+                                                             (red[threadIdx.x][2] + red[threadIdx.x][3]);
+}
+
+__global__ void __launch_bounds__(256) var_loss_final_kernel(const float* __restrict__ part, int nblk,
+                                                             const float* __restrict__ ext_counts,
+                                                             float* __restrict__ loss, float* __restrict__ counts) {
+  __shared__ float red[6][256];
+  float a[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = threadIdx.x; r < nblk; r += 256)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) a[q] += part[r * 6 + q];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) red[q][threadIdx.x] = a[q];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) {
+    const float c = ext_counts ? ext_counts[threadIdx.x] : red[3 + threadIdx.x][0];
+    counts[threadIdx.x] = c;
+    loss[threadIdx.x] = red[threadIdx.x][0] / fmaxf(c, 1.f);
+  }
+}
+
+__global__ void __launch_bounds__(256) var_loss_bwd_kernel(VTerm t0, VTerm t1, VTerm t2, int B,
+                                                           const float* __restrict__ g,
+                                                           const float* __restrict__ counts) {
+  const VTerm ts[3] = {t0, t1, t2};
+  float sc[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) sc[q] = 2.f * g[q] / fmaxf(counts[q], 1.f);
+  const long n0 = (long)B * t0.L, n1 = n0 + (long)B * t1.L, n2 = n1 + (long)B * t2.L;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n2; e += (long)gridDim.x * 256) {
+    const int k = e < n0 ? 0 : (e < n1 ? 1 : 2);
+    const long o = e - (k == 0 ? 0 : (k == 1 ? n0 : n1));
+    const int L = ts[k].L;
+    const int b = (int)(o / L), j = (int)(o - (long)b * L);
+    bool valid;
+    const float d = vterm_diff(ts[k], b, j, valid);
+    const float s = k == 0 ? sc[0] : (k == 1 ? sc[1] : sc[2]);
+    ts[k].grad[(long)b * ts[k].ldp + j] = valid ? s * d : 0.f;
+  }
+}
+}  // namespace
+
+SSAMD_API long ssamd_var_loss_ws() { return 6L * 1024; }
+
+// loss[3] = masked MSE of the 3 terms; counts[3] = the divisors used (ext_counts or mask counts)
+SSAMD_API int ssamd_var_loss_fwd(VTerm t0, VTerm t1, VTerm t2, int B, const float* ext_counts, float* loss,
+                                 float* counts, float* ws, hipStream_t s) {
+  const long n = (long)B * (t0.L + t1.L + t2.L);
+  const int nblk = n ? (grid_for(n, 4) > 1024 ? 1024 : grid_for(n, 4)) : 1;
+  hipLaunchKernelGGL(var_loss_fwd_kernel, dim3(nblk), dim3(256), 0, s, t0, t1, t2, B, ws);
+  hipLaunchKernelGGL(var_loss_final_kernel, dim3(1), dim3(256), 0, s, ws, nblk, ext_counts, loss, counts);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_var_loss_bwd(VTerm t0, VTerm t1, VTerm t2, int B, const float* g, const float* counts,
+                                 hipStream_t s) {
+  const long n = (long)B * (t0.L + t1.L + t2.L);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(var_loss_bwd_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, t0, t1, t2, B, g, counts);
   return (int)hipGetLastError();
 }

@@ -49,10 +49,19 @@ lengths_to_mask = ref.lengths_to_mask
 sinusoid_table = ref.sinusoid_table
 
 
-def linear(x, w, b=None, act=None):
+def linear(x, w, b=None, act=None, ln=None):
+    """``ln``: an ``ln_spec`` whose LayerNorm tail the GEMM runs in its epilogue (HIP only)."""
     if use_hip(x):
-        return _hip().linear(x, w, b, act)
+        return _hip().linear(x, w, b, act, ln=ln)
     return ref.linear(x, w, b, act)
+
+
+def ln_spec(residual, ln_w, ln_b, **kw):
+    """The LayerNorm tail ``add_layernorm(a, residual, ln_w, ln_b, **kw)`` packaged for the GEMM that
+    produces ``a`` (HIP path, d_model = 256: fused into its epilogue); None where it does not apply."""
+    if use_hip(residual) and residual.dtype == torch.bfloat16:
+        return _hip().ln_spec(residual, ln_w, ln_b, **kw)
+    return None
 
 
 def residual_mailbox(x, weights=None):
@@ -83,12 +92,13 @@ def conv1d(x, w, b=None, pad=0, dil=1, act=None):
     return ref.conv1d(x, w, b, pad, dil, act)
 
 
-def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None, mailbox=None):
+def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None, mailbox=None, ln=None):
     """Position-wise FFN core: conv(k0) -> ReLU -> conv(k1) (``SubLayers.py:84-87``).
 
-    ``pack``: x is packed ``[1, R, C]``; the convs zero-pad at every sequence end."""
+    ``pack``: x is packed ``[1, R, C]``; the convs zero-pad at every sequence end.
+    ``ln``: an ``ln_spec`` run in the second conv's epilogue (HIP only)."""
     if use_hip(x):
-        return _hip().ffn(x, w1, b1, w2, b2, pack, mailbox)
+        return _hip().ffn(x, w1, b1, w2, b2, pack, mailbox, ln=ln)
     if pack is not None:
         return pack_rows(ffn(unpack_rows(x, pack), w1, b1, w2, b2), pack)
     h = ref.conv1d(x, w1, b1, (w1.shape[2] - 1) // 2, 1, "relu")
@@ -103,9 +113,10 @@ def attention(qkv, lengths, n_head, pack: Optional[PackInfo] = None):
     return ref.attention(qkv, lengths, n_head)
 
 
-def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, mailbox=None, **kw):
+def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, mailbox=None, fused=None, **kw):
+    """``fused``: the ``ln_spec`` the producing GEMM already evaluated (HIP): no kernel, same autograd."""
     if use_hip(a):
-        return _hip().add_layernorm(a, residual, ln_w, ln_b, pack=pack, mailbox=mailbox, **kw)
+        return _hip().add_layernorm(a, residual, ln_w, ln_b, pack=pack, mailbox=mailbox, fused=fused, **kw)
     if pack is not None:
         kw["lengths"] = pack.lens
         res = None if residual is None else unpack_rows(residual, pack)

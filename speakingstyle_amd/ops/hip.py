@@ -57,6 +57,7 @@ _SIGS = {
     "ssamd_pack_info": [P, I, I, P, P, P, P],
     "ssamd_embed_fwd": [I, P, P, P, I, P, P, I, P, P, L_, I, P],
     "ssamd_embed_bwd": [P, P, P, L_, I, I, P],
+    "ssamd_onehot": [P, L_, I, P, P],
     "ssamd_l1pair_fwd": [P, P, P, P, I, I, I, I, P, P, L_, P],
     "ssamd_l1pair_ws": [I, I, I],
     "ssamd_clip_adam_ws": [L_],
@@ -91,6 +92,8 @@ def lib():
                     if fn is not None:
                         fn.argtypes = args
                         fn.restype = _RESTYPES.get(name, I)
+                if os.environ.get("SSAMD_WGRAD_BLOCKS"):  # tuning knob: split-M target of the wgrad GEMMs
+                    handle.ssamd_wgrad_set_blocks(int(os.environ["SSAMD_WGRAD_BLOCKS"]))
                 _lib = handle
     return _lib
 
@@ -121,6 +124,11 @@ def _check(rc, name):
 
 
 _FALLBACK_OK = os.environ.get("SSAMD_ALLOW_TORCH_FALLBACK") == "1"
+# LayerNorm tails in the producing GEMM's epilogue (ssamd_conv_gemm_ln) are opt-in: measured on MI355X
+# (tools/exp_ln.py, 100k rows, profiles/README.md r2) the fused epilogue of the one-block-per-CU 256x256
+# GEMM costs more (+62 us at K=256) than the separate, fully occupied addln kernel (+31 us): the epilogue
+# does not overlap any MFMA work.  SSAMD_LN_FUSE=1 enables it.
+_NO_LN_FUSE = os.environ.get("SSAMD_LN_FUSE") != "1"
 _fallback_seen = set()
 
 
@@ -293,6 +301,82 @@ def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, re
     return y
 
 
+class LNSpec:
+    """A residual + LayerNorm (+ dropout, FiLM, row mask) tail that the producing GEMM runs in its
+    epilogue (``ssamd_conv_gemm_ln``; d_model = 256: one 256x256 tile owns whole rows).  Built by
+    ``ln_spec`` before the GEMM, filled by it (``out``, ``mean``, ``rstd``) and consumed by
+    ``add_layernorm(..., fused=spec)``, whose backward is the unchanged ``addln_bwd``."""
+
+    __slots__ = ("res", "w", "b", "g", "bt", "sg", "sb", "lens", "cu", "geom", "dst", "M", "pre_p", "post_p",
+                 "seed", "eps", "out", "mean", "rstd", "used")
+
+    def launch_args(self):
+        return (_ptr(self.res), _ptr(self.w), _ptr(self.b), _ptr(self.g), _ptr(self.bt), _ptr(self.sg),
+                _ptr(self.sb), _ptr(None if self.dst is not None else self.lens), _ptr(self.dst), int(self.M),
+                _ptr(self.out), _ptr(self.mean), _ptr(self.rstd), float(self.pre_p), float(self.post_p),
+                float(self.eps), ctypes.c_ulonglong(self.seed))
+
+
+_SIGS.update({"ssamd_conv_gemm_ln": [P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P, P,
+                                     F, F, F, U64, P]})
+
+
+def ln_spec(residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None, lengths=None,
+            eps=1e-5, pack=None):
+    """LNSpec for ``add_layernorm(a, residual, ...)`` when its ``a`` comes from a d=256 GEMM, else None."""
+    if _NO_LN_FUSE or residual.dtype != torch.bfloat16 or residual.shape[-1] != 256 or not residual.is_cuda:
+        return None
+    sp = LNSpec()
+    sp.res = residual.contiguous()
+    sp.w, sp.b = ln_w, ln_b
+    sp.g = sp.bt = sp.sg = sp.sb = None
+    if film_params is not None:
+        g, bt, sg, sb = film_params
+        sp.g, sp.bt = g.detach().float().contiguous(), bt.detach().float().contiguous()
+        sp.sg, sp.sb = sg, sb
+    sp.pre_p = float(pre_drop) if training else 0.0
+    sp.post_p = float(post_drop) if training else 0.0
+    sp.seed = _next_seed()
+    sp.eps = float(eps)
+    if pack is not None:
+        sp.lens, sp.cu, sp.geom, sp.dst, sp.M = pack.lens, pack.cu, (pack.B, pack.M, 256), pack.dst, pack.M
+    else:
+        sp.lens = None if lengths is None else lengths.to(torch.int64).contiguous()
+        sp.cu = sp.geom = sp.dst = None
+        sp.M = 1
+    sp.out = sp.mean = sp.rstd = None
+    sp.used = False
+    return sp
+
+
+def conv_gemm_ln_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, spec: LNSpec, rinfo=None):
+    """a = conv(x) + bias (bf16 [B, L, 256]) with the LayerNorm tail of ``spec`` in the epilogue."""
+    _need(x, torch.bfloat16, "conv_ln.x")
+    _need(wimg, torch.bfloat16, "conv_ln.w")
+    N = 256
+    assert x.numel() == B * L * Cin and wimg.numel() == N * ks * Cin, "conv_ln: shape"
+    assert spec.res.numel() == B * L * N, "conv_ln: residual shape"
+    _need(spec.w, torch.float32, "conv_ln.ln_w")
+    _need(spec.b, torch.float32, "conv_ln.ln_b")
+    if bias is not None:
+        _need(bias, torch.float32, "conv_ln.bias")
+    if spec.g is not None:
+        nb = spec.geom[0] if spec.geom is not None else B
+        assert spec.g.shape == (nb, N) and spec.bt.shape == (nb, N)
+        assert spec.dst is not None or spec.geom is None, "packed FiLM needs the row map"
+    if spec.lens is not None and spec.dst is None:
+        assert spec.lens.numel() == B
+    y = torch.empty(B, L, N, device=x.device, dtype=torch.bfloat16)
+    spec.out = torch.empty_like(y)
+    spec.mean = torch.empty(B * L, device=x.device, dtype=torch.float32)
+    spec.rstd = torch.empty_like(spec.mean)
+    rc = lib().ssamd_conv_gemm_ln(_ptr(x), _ptr(wimg), _ptr(bias), _ptr(y), B, L, Cin, ks, dil, pad, N,
+                                  _rinfo_ptr(rinfo, B * L), *spec.launch_args(), _stream())
+    _check(rc, "ssamd_conv_gemm_ln")
+    spec.used = True
+    return y
+
+
 def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, db=None, rinfo=None, cu=None):
     """-> dW [N, Cin, ks] fp32 (and db [N] when ``with_bias``: fused column sums of dY).
 
@@ -346,13 +430,17 @@ def relu_mask_(dy, y):
 # ------------------------------------------------------------------------ conv / linear
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, pad, dil, act, out_f32):
+    def forward(ctx, x, w, b, pad, dil, act, out_f32, ln=None):
         B, L, Cin = x.shape
         ks = 1 if w.dim() == 2 else w.shape[2]
         N = w.shape[0]
         xc = x.contiguous()
-        y = conv_gemm_raw(xc, weight_fwd(w), None if b is None else b.detach().float().contiguous(), B, L, Cin, ks,
-                          dil, pad, N, _ACT[act], out_f32=out_f32)
+        bf = None if b is None else b.detach().float().contiguous()
+        if ln is not None:
+            assert act is None and not out_f32 and N == 256
+            y = conv_gemm_ln_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, ln)
+        else:
+            y = conv_gemm_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, N, _ACT[act], out_f32=out_f32)
         ctx.geom = (B, L, Cin, ks, dil, pad, N)
         ctx.act = act
         ctx.has_b = b is not None
@@ -382,15 +470,20 @@ class _ConvFn(torch.autograd.Function):
                 dw = dw.view(N, Cin)
         elif want_b:
             db = colsum_raw(dy, N, sb)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv1d(x, w, b=None, pad=0, dil=1, act=None, out_f32=False):
     return _ConvFn.apply(x, w, b, pad, dil, act, out_f32)
 
 
-def linear(x, w, b=None, act=None, out_f32=False):
+def linear(x, w, b=None, act=None, out_f32=False, ln=None):
+    """``ln``: an LNSpec whose LayerNorm tail runs in this GEMM's epilogue (N must be 256)."""
     shp = x.shape
+    if ln is not None and (w.shape[0] != 256 or act is not None or out_f32 or x.dim() != 3):
+        ln = None
+    if ln is not None:
+        return _ConvFn.apply(x, w, b, 0, 1, None, False, ln)
     x3 = x.reshape(1, -1, shp[-1]) if x.dim() != 3 else x
     if x3.shape[-1] % 8 or w.shape[0] % 8:
         # not MFMA-shaped (the N = 1 variance-predictor head has its own kernel: predictor_head)
@@ -483,7 +576,7 @@ class _FFNFn(torch.autograd.Function):
     data-gradient epilogue of the second conv (aux = h), so no extra pass."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, rinfo, mailbox):
+    def forward(ctx, x, w1, b1, w2, b2, rinfo, mailbox, ln=None):
         B, L, C = x.shape
         ctx.mailbox = mailbox
         k1, k2 = w1.shape[2], w2.shape[2]
@@ -494,7 +587,10 @@ class _FFNFn(torch.autograd.Function):
         r2 = rinfo if k2 > 1 else None
         ctx.cu = (cu if k1 > 1 else None, cu if k2 > 1 else None)
         h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1, rinfo=r1)
-        z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0, rinfo=r2)
+        if ln is not None and C == 256:
+            z = conv_gemm_ln_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, ln, rinfo=r2)
+        else:
+            z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0, rinfo=r2)
         ctx.rinfo = (r1, r2)
         ctx.save_for_backward(xc, h, w1, w2)
         ctx.biases = (b1, b2)
@@ -516,13 +612,13 @@ class _FFNFn(torch.autograd.Function):
                            resid=_resid_for(ctx.mailbox, xc))
         dw1, db1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=gradslots.claim(w1),
                                   db=gradslots.claim(b1), rinfo=r1, cu=ctx.cu[0])
-        return dx, dw1, db1, dw2, db2, None, None
+        return dx, dw1, db1, dw2, db2, None, None, None
 
 
-def ffn(x, w1, b1, w2, b2, pack=None, mailbox=None):
+def ffn(x, w1, b1, w2, b2, pack=None, mailbox=None, ln=None):
     if pack is not None:
         assert x.shape[0] == 1 and x.shape[1] == pack.R, "packed FFN expects [1, R, C]"
-    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu), mailbox)
+    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu), mailbox, ln)
 
 
 # ------------------------------------------------------------------------ add + LayerNorm
@@ -544,19 +640,23 @@ def get_seed() -> int:
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox):
+    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox, fused=None):
         B, L, C = a.shape if geom is None else geom  # packed: (sequences, longest, C) over [1, R, C] rows
         ac = a.contiguous()
         rc_ = None if res is None else res.contiguous()
-        out = torch.empty_like(ac)
-        mean = torch.empty(a.numel() // C, device=a.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
         gf = None if g is None else g.detach().float().contiguous()
         bf = None if bt is None else bt.detach().float().contiguous()
-        rc = lib().ssamd_addln_fwd(_ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb),
-                                   _ptr(lens), _ptr(cu), _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, pre_p, post_p,
-                                   seed, eps, _stream())
-        _check(rc, "ssamd_addln_fwd")
+        if fused is not None:  # the producing GEMM already ran this LayerNorm in its epilogue
+            out, mean, rstd = fused.out, fused.mean, fused.rstd
+            gf, bf = fused.g, fused.bt
+        else:
+            out = torch.empty_like(ac)
+            mean = torch.empty(a.numel() // C, device=a.device, dtype=torch.float32)
+            rstd = torch.empty_like(mean)
+            rc = lib().ssamd_addln_fwd(_ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb),
+                                       _ptr(lens), _ptr(cu), _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, pre_p,
+                                       post_p, seed, eps, _stream())
+            _check(rc, "ssamd_addln_fwd")
         ctx.cu = cu
         ctx.mailbox = mailbox
         ctx.save_for_backward(ac, rc_, w, b, gf, bf, sg, sb, lens, mean, rstd)
@@ -595,12 +695,23 @@ class _AddLNFn(torch.autograd.Function):
             dbt = (S2 * sb).to(ctx.gdtype[1])
             dsg = (S1 * gf).sum().reshape(1)
             dsb = (S2 * bf).sum().reshape(1)
-        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None
+        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None, None
 
 
 def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None,
-                  lengths=None, eps=1e-5, pack=None, mailbox=None):
+                  lengths=None, eps=1e-5, pack=None, mailbox=None, fused=None):
     C = a.shape[-1]
+    if fused is not None and fused.used:
+        g = bt = sg = sb = None
+        if film_params is not None:
+            g, bt, sg, sb = film_params
+        cu = geom = None
+        if pack is not None:
+            lens, cu, geom = pack.lens, pack.cu, (pack.B, pack.M, C)
+        else:
+            lens = fused.lens
+        return _AddLNFn.apply(a, residual.to(a.dtype), ln_w, ln_b, g, bt, sg, sb, lens, fused.pre_p, fused.post_p,
+                              fused.seed, fused.eps, cu, geom, mailbox, fused)
     if C not in (256, 512, 1024) or a.dtype != torch.bfloat16:
         if pack is not None:
             raise ValueError("packed add_layernorm needs C in (256, 512, 1024) and bf16")
@@ -731,9 +842,23 @@ class _EmbedFn(torch.autograd.Function):
         dt = gradslots.claim(ctx.table) if ctx.needs_input_grad[4] else None
         if dt is None:
             dt = torch.empty(shape, device=dout.device, dtype=torch.float32)
-        # one block per table row, fixed summation order (deterministic; every row is written)
-        rc = lib().ssamd_embed_bwd(_ptr(idx), _ptr(dout), _ptr(dt), idx.numel(), shape[1], shape[0], _stream())
-        _check(rc, "ssamd_embed_bwd")
+        V, C = shape[0], shape[1]
+        rows = idx.numel()
+        if C % 8 == 0 and rows > 0:
+            # dtable = onehot(idx)^T @ dout on the MFMA weight-gradient GEMM (deterministic split-M reduce)
+            Vp = (V + 7) // 8 * 8
+            oh = torch.empty(rows, Vp, device=dout.device, dtype=torch.bfloat16)
+            rc = lib().ssamd_onehot(_ptr(idx), rows, Vp, _ptr(oh), _stream())
+            _check(rc, "ssamd_onehot")
+            if Vp == V:
+                conv_wgrad_raw(dout.view(1, rows, C), oh.view(1, rows, Vp), 1, rows, C, 1, 1, 0, Vp,
+                               dW=dt.view(V, C, 1))
+            else:
+                dt.copy_(conv_wgrad_raw(dout.view(1, rows, C), oh.view(1, rows, Vp), 1, rows, C, 1, 1, 0, Vp)
+                         .view(Vp, C)[:V])
+        else:  # one block per table row, fixed summation order (deterministic; every row is written)
+            rc = lib().ssamd_embed_bwd(_ptr(idx), _ptr(dout), _ptr(dt), rows, C, V, _stream())
+            _check(rc, "ssamd_embed_bwd")
         d_add = dout if ctx.mode == 1 else None
         return None, None, None, None, dt if dtype == torch.float32 else dt.to(dtype), d_add, None
 
@@ -819,6 +944,68 @@ class _L1PairFn(torch.autograd.Function):
                                     _ptr(cnt), _ptr(d1), _ptr(d2), _stream())
         _check(rc, "ssamd_l1pair_bwd")
         return d1, d2, None, None, None
+
+
+class VTerm(ctypes.Structure):
+    _fields_ = [("pred", P), ("tgt", P), ("mask", P), ("grad", P), ("L", I), ("ldp", I), ("ldt", I), ("dur", I)]
+
+
+_SIGS.update({"ssamd_var_loss_fwd": [VTerm, VTerm, VTerm, I, P, P, P, P, P],
+              "ssamd_var_loss_bwd": [VTerm, VTerm, VTerm, I, P, P, P],
+              "ssamd_var_loss_ws": []})
+_RESTYPES["ssamd_var_loss_ws"] = L_
+
+
+def _vterm(pred, tgt, mask, grad=None):
+    B, L = mask.shape
+    _need(pred, torch.float32, "var_loss.pred")
+    _need(mask, torch.bool, "var_loss.mask")
+    dur = tgt.dtype == torch.int64
+    if not dur:
+        _need(tgt, torch.float32, "var_loss.target")
+    assert pred.dim() == 2 and tgt.dim() == 2 and pred.shape[0] == tgt.shape[0] == B
+    assert pred.shape[1] >= L and tgt.shape[1] >= L and tgt.stride(1) == 1, "var_loss: operand shapes"
+    return VTerm(pred.data_ptr(), tgt.data_ptr(), mask.data_ptr(), 0 if grad is None else grad.data_ptr(), L,
+                 pred.stride(0), tgt.stride(0), int(dur))
+
+
+class _VarLossFn(torch.autograd.Function):
+    """pitch / energy / log-duration masked MSE (reference ``model/loss.py:76-89``) in one fused,
+    deterministic kernel pair; ``counts`` (3 fp32, optional): the all-reduced global divisors."""
+
+    @staticmethod
+    def forward(ctx, pp, pt, pm, ep, et, em, ld, dt, dm, counts):
+        tensors = [t.contiguous() for t in (pp, pt, ep, et, ld, dt)]
+        pp, pt, ep, et, ld, dt = tensors
+        pm, em, dm = pm.contiguous(), em.contiguous(), dm.contiguous()
+        B = pm.shape[0]
+        loss = torch.empty(3, device=pp.device, dtype=torch.float32)
+        cnt = torch.empty(3, device=pp.device, dtype=torch.float32)
+        ws = _workspace(pp.device, int(lib().ssamd_var_loss_ws()))
+        ext = None if counts is None else counts.float().contiguous()
+        rc = lib().ssamd_var_loss_fwd(_vterm(pp, pt, pm), _vterm(ep, et, em), _vterm(ld, dt, dm), B, _ptr(ext),
+                                      _ptr(loss), _ptr(cnt), _ptr(ws), _stream())
+        _check(rc, "ssamd_var_loss_fwd")
+        ctx.save_for_backward(pp, pt, pm, ep, et, em, ld, dt, dm, cnt)
+        return loss[0], loss[1], loss[2]
+
+    @staticmethod
+    def backward(ctx, g0, g1, g2):
+        pp, pt, pm, ep, et, em, ld, dt, dm, cnt = ctx.saved_tensors
+        gs = torch.stack([g.reshape(()) for g in (g0, g1, g2)]).float().contiguous()
+        # columns past the mask width (frame-level preds longer than the truncated mel) get no gradient
+        gp, ge, gd = [torch.empty_like(x) if x.shape[1] == m.shape[1] else torch.zeros_like(x)
+                      for x, m in ((pp, pm), (ep, em), (ld, dm))]
+        rc = lib().ssamd_var_loss_bwd(_vterm(pp, pt, pm, gp), _vterm(ep, et, em, ge), _vterm(ld, dt, dm, gd),
+                                      pm.shape[0], _ptr(gs), _ptr(cnt), _stream())
+        _check(rc, "ssamd_var_loss_bwd")
+        return gp, None, None, ge, None, None, gd, None, None, None
+
+
+def variance_losses(p_pred, p_t, p_mask, e_pred, e_t, e_mask, logd, d_t, src_mask, counts=None):
+    """-> (pitch, energy, duration) losses; masks are the reference's pad masks (True = padded)."""
+    return _VarLossFn.apply(p_pred.float(), p_t.float(), p_mask, e_pred.float(), e_t.float(), e_mask,
+                            logd.float(), d_t.to(torch.int64), src_mask, counts)
 
 
 def masked_l1_pair(mel_p, post_p, mel_t, mel_valid, count):

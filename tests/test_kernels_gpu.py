@@ -167,6 +167,94 @@ def test_embeddings():
     o2.backward(g.to(torch.bfloat16))
     o2r.backward(g.to(torch.bfloat16).float())
     assert _rel(t2.grad, t2r.grad) < 1e-2
+    # phoneme table (V = 361, not a multiple of 8) backward, and a skewed id distribution
+    for ids_ in (ids, torch.full_like(ids, 7)):
+        tb = torch.randn(V, C, device=DEV, requires_grad=True)
+        tr = tb.detach().clone().requires_grad_(True)
+        o = hip.embed_add_pe(ids_, tb, pe)
+        orf = F.embedding(ids_, tr.to(torch.bfloat16).float()) + pe.float()
+        gg = torch.randn_like(orf).to(torch.bfloat16)
+        o.backward(gg)
+        orf.backward(gg.float())
+        assert _rel(tb.grad, tr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("film", [False, True])
+def test_gemm_fused_layernorm(packed, film):
+    """FFT block with the residual+LayerNorm(+dropout, FiLM, mask) tails in the fc / w_2 GEMM epilogues
+    == the same block with separate addln kernels (same dropout seeds), forward and backward."""
+    from speakingstyle_amd import ops
+    from speakingstyle_amd.models.layers import FFTBlock
+
+    torch.manual_seed(3)
+    blk = FFTBlock(256, 2, 128, 128, 1024, (9, 1), dropout=0.1, film=True).to(DEV).train()
+    B, L = 4, 50
+    lens = torch.tensor([50, 31, 7, 44], device=DEV)
+    x0 = torch.randn(B, L, 256, device=DEV).to(torch.bfloat16)
+    style = (torch.randn(B, 256, device=DEV).to(torch.bfloat16), torch.randn(B, 256, device=DEV).to(torch.bfloat16))
+    with torch.no_grad():
+        blk.film.s_gamma.fill_(0.3)
+        blk.film.s_beta.fill_(-0.2)
+    pk = None
+    if packed:
+        R = int(lens.sum())
+        pk = ops.PackInfo.build(lens, L, R)
+        x0 = hip_pack(x0, lens)
+
+    def run(no_fuse):
+        hip._NO_LN_FUSE = no_fuse
+        hip.set_seed(77)
+        blk.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        y = blk(x, lens, style if film else None, pack=pk)
+        g = torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).to(torch.bfloat16)
+        y.backward(g)
+        grads = [p.grad.clone() for p in blk.parameters() if p.grad is not None]
+        return y.detach().float(), x.grad.float(), grads
+
+    old = hip._NO_LN_FUSE
+    try:
+        y1, gx1, gp1 = run(False)
+        y2, gx2, gp2 = run(True)
+    finally:
+        hip._NO_LN_FUSE = old
+    assert _rel(y1, y2) < 2e-3 and _rel(gx1, gx2) < 5e-3
+    assert len(gp1) == len(gp2)
+    for a, b in zip(gp1, gp2):
+        assert _rel(a, b) < 5e-3
+
+
+def hip_pack(x, lens):
+    return torch.cat([x[b, : int(lens[b])] for b in range(x.shape[0])], 0).unsqueeze(0).contiguous()
+
+
+@pytest.mark.parametrize("with_counts", [False, True])
+def test_variance_losses(with_counts):
+    """Fused pitch / energy / log-duration masked MSE (+ backward) vs the torch formula."""
+    torch.manual_seed(8)
+    B, T, M = 5, 23, 61
+    src_lens = torch.tensor([23, 7, 15, 1, 20], device=DEV)
+    mel_lens = torch.tensor([61, 30, 44, 3, 50], device=DEV)
+    sm = torch.arange(T, device=DEV)[None] >= src_lens[:, None]
+    mm = torch.arange(M, device=DEV)[None] >= mel_lens[:, None]
+    pp = torch.randn(B, T, device=DEV, requires_grad=True)   # phoneme-level pitch
+    ep = torch.randn(B, M + 4, device=DEV, requires_grad=True)  # frame-level energy, wider than the mask
+    ld = torch.randn(B, T, device=DEV, requires_grad=True)
+    pt, et = torch.randn(B, T, device=DEV), torch.randn(B, M + 9, device=DEV)
+    dt = torch.randint(0, 12, (B, T), device=DEV)
+    counts = torch.tensor([40.0, 100.0, 60.0], device=DEV) if with_counts else None
+    out = hip.variance_losses(pp, pt, sm, ep, et, mm, ld, dt, sm, counts)
+    c = counts if with_counts else torch.stack([(~sm).sum(), (~mm).sum(), (~sm).sum()]).float()
+    refs = [(((a[:, :w] - b[:, :w]) * ~m) ** 2).sum() / c[i]
+            for i, (a, b, m, w) in enumerate(((pp, pt, sm, T), (ep, et, mm, M), (ld, torch.log(dt.float() + 1), sm, T)))]
+    for o, r in zip(out, refs):
+        torch.testing.assert_close(o, r, rtol=1e-5, atol=1e-6)
+    g = [pp, ep, ld]
+    ga = torch.autograd.grad(sum(o * (i + 1) for i, o in enumerate(out)), g)
+    gr = torch.autograd.grad(sum(r * (i + 1) for i, r in enumerate(refs)), g)
+    for a, b in zip(ga, gr):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
 
 
 def test_l1_pair():
