@@ -56,6 +56,7 @@ def parse(argv=None):
     ap.add_argument("--synth-warmup", type=int, default=1)
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--tiny", action="store_true", help="plumbing-size model (CPU launcher tests only)")
+    ap.add_argument("--phase-times", action="store_true", help="per-phase host/device ms of the timed steps")
     return ap.parse_args(argv)
 
 
@@ -117,6 +118,9 @@ def run(args):
         "bucket_overlap": tr["overlap"],
         "skipped_steps": tr["skipped_steps"],
     }
+    if tr.get("phases"):
+        rec["phase_ms"] = {k: {"host": round(v["host_ms"], 3), "device": round(v["device_ms"], 3)}
+                           for k, v in tr["phases"].items()}
     if sy is not None:
         rec.update({
             "synth_rtf": sy["rtf"],

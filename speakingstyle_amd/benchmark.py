@@ -113,6 +113,7 @@ def train_phase(args, rank, world, device):
     model.set_compute_dtype(torch.bfloat16 if cuda else torch.float32)
     ddp.broadcast_module_state(model)
     trainer = Trainer(model, (pp, mc, tc), seed=1234)
+    trainer.timer.enabled = bool(getattr(args, "phase_times", False)) or trainer.timer.enabled
 
     gen = SyntheticBatches(batch, device=device, max_seq_len=mc["max_seq_len"], seed=1000 + rank,
                            frame_level=pp["preprocessing"]["pitch"]["feature"] == "frame_level")
@@ -136,6 +137,7 @@ def train_phase(args, rank, world, device):
     warm = max(args.warmup, 1 if world > 1 else 0)
     for i in range(warm):
         step(i)
+    trainer.timer.summary()  # drop the warm-up phases
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)
@@ -148,7 +150,9 @@ def train_phase(args, rank, world, device):
     _sync(cuda)
     elapsed = time.perf_counter() - t0
     elapsed, frames_all = _max_sum(world, device, elapsed, float(frames))
+    phases = trainer.timer.summary()
     info = {
+        "phases": phases,
         "elapsed": elapsed, "frames": frames_all, "batch": batch, "warmup": warm,
         "buckets": len(trainer.buckets.buckets), "overlap": trainer.buckets.calibrated() if world > 1 else None,
         "skipped_steps": int(trainer.opt.skipped_steps),

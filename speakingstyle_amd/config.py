@@ -96,6 +96,8 @@ _TRAIN_DEFAULTS: Config = {
         "seed": 1234,
         "num_workers": 4,
         "frames_per_gpu": None,   # optional frame budget per rank (overrides batch_size)
+        "phase_timing": False,    # per-phase host / device step timing (Perf/phase_* TB scalars)
+        "preempt_check_steps": 10,  # DP: steps between cross-rank SIGTERM agreements
         "nan_guard": True,        # skip the optimizer step if the loss is non-finite
         "hip_kernels": True,      # False => torch reference ops even on GPU (debug only)
     },

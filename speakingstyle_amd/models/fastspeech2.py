@@ -314,8 +314,12 @@ class FastSpeech2(nn.Module):
         return getattr(self, "reference_encoder", None) or getattr(self, "gst", None)
 
     def film_scalars(self):
-        """Stacked s_gamma/s_beta parameters (reference ``utils/model.py:53-59``)."""
-        ps = [p for n, p in self.named_parameters() if ("s_gamma" in n or "s_beta" in n)]
+        """Stacked s_gamma/s_beta parameters (reference ``utils/model.py:53-59``).  The parameter
+        list is collected once (named_parameters() walks the whole module tree every call)."""
+        ps = self.__dict__.get("_film_ps")
+        if ps is None:
+            ps = [p for n, p in self.named_parameters() if ("s_gamma" in n or "s_beta" in n)]
+            self.__dict__["_film_ps"] = ps
         return torch.cat(ps) if ps else None
 
     def compute_style(self, mels, mel_lens, max_mel_len, batch, device, style_weights=None):

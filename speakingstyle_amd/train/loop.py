@@ -189,6 +189,9 @@ def train(args, configs):
                         train_logger.add_scalar("Perf/step_ms", 1000.0 * dt / log_step, step)
                         train_logger.add_scalar("Perf/mel_frames_per_s", frames / max(dt, 1e-9), step)
                         train_logger.add_scalar("Perf/skipped_steps", float(trainer.opt.skipped_steps), step)
+                        for ph, v in trainer.timer.summary().items():  # empty unless phase timing is on
+                            train_logger.add_scalar(f"Perf/phase_{ph}_host_ms", v["host_ms"], step)
+                            train_logger.add_scalar(f"Perf/phase_{ph}_device_ms", v["device_ms"], step)
                 if rank == 0 and synth_step and step % synth_step == 0:
                     synth_one_sample(batch, output, vocoder, model_config, preprocess_config, train_logger, step, "Training")
                 if val_step and step % val_step == 0 and not synthetic:

@@ -51,6 +51,12 @@ class Trainer:
         # uninterrupted one bit for bit, with nothing extra stored in the checkpoint
         self.seed = seed
         self.rank = ddp.rank()
+        import os
+
+        from ..utils.timing import PhaseTimer
+
+        mi = train_config.get("mi355x", {}) or {}
+        self.timer = PhaseTimer(bool(mi.get("phase_timing", False)) or os.environ.get("SSAMD_PHASE_TIMING") == "1")
 
     def take_frames(self) -> int:
         """Valid mel frames consumed since the last call, summed over ranks (host sync: log steps only)."""
@@ -98,19 +104,25 @@ class Trainer:
         hip.set_seed((k * 64 + self.micro % self.grad_acc) * 0x9E3779B97F4A7C15)
 
     def train_step(self, batch):
-        self.model.train()
+        tm = self.timer
+        tm.phase("setup")
+        if not self.model.training:  # module.train() walks every submodule: only when needed
+            self.model.train()
         self._step_seed()
         counts, work = self._global_counts(batch) if self.world > 1 else (None, None)
         last_micro = (self.micro + 1) % self.grad_acc == 0
+        tm.phase("forward")
         output = self.model(*batch[2:])
         if work is not None:
             work.wait()
+        tm.phase("loss")
         named = self.model.film_scalars()
         losses = self.loss_fn(batch, output, named, global_counts=counts)
         total = losses[0]
         if self.world > 1 and named is not None and self.loss_fn.lambda_f > 0:
             # the FiLM L2 term is identical on every rank: scale so the SUM all-reduce counts it once
             total = total - (1.0 - 1.0 / self.world) * self.loss_fn.lambda_f * torch.sum(torch.square(named))
+        tm.phase("backward")
         if last_micro or self.world == 1:
             (total / self.grad_acc).backward()
         else:
@@ -125,8 +137,11 @@ class Trainer:
             self.frames += batch[7].clamp(max=self.max_seq_len).sum()
         lr = None
         if last_micro:
+            tm.phase("allreduce_wait")
             self.buckets.finish()
+            tm.phase("optimizer")
             lr = self.opt.step_and_update_lr()
             self.opt.zero_grad()
             self.last_lr = lr
+        tm.stop()
         return losses, output, lr
