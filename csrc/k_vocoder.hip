@@ -41,7 +41,12 @@ struct RB {
   static constexpr int R1 = R1P;
   static constexpr int BM = R1 - 2 * H2;            // output rows per block
   static constexpr int NRB2 = (BM + 15) / 16;
-  static constexpr int LDC = C + 8;                // LDS pitch (bf16): 16-B rows, conflict-free row reads
+  // LDS pitch (bf16) of the activation tiles: the A-fragment ds_read_b128 of lane l reads row l & 15 at
+  // 16-B column chunk l >> 4, so its bank quad is (p * row + chunk) mod 16 for a pitch of 4p dwords.
+  // The b128 lane groups ({0-3,12-15,20-27}, ...) hit 16 distinct quads iff p = 2 (mod 4), i.e. a pitch
+  // of C + 16 bf16 for C = 32 / 64 / 128 (p = 6 / 10 / 18).  C + 8 (p odd) left a 2-way conflict in
+  // every group: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.40-0.48 (profiles/r2_v2_pmc_step_summary.txt).
+  static constexpr int LDC = C + 16;
   static constexpr int RX = R1P + (K - 1) * MAXD;  // staged x rows at the largest dilation
   static constexpr int NS = C / 16;                // 16-wide output sub-tiles
   static constexpr int NSW = NS / WC;              // sub-tiles per wave
@@ -65,7 +70,10 @@ __device__ __forceinline__ float lrelu(float v, float s) { return v >= 0.f ? v :
 // 16-B chunk per lane, no VGPR round trip), three steps ahead, so the waves share one copy
 // of each weight slice (NWx less L2->CU traffic than per-wave loads) and its latency is hidden.
 // Slot layout: [C rows (output channel)][32 k] bf16 = 64-B rows with the 16-B chunk index XORed
-// by (row >> 2) & 3 (source-side swizzle; the DMA image is lane-linear) -> conflict-free reads.
+// by 2 * ((row >> 2) & 1) (source-side swizzle; the DMA image is lane-linear): lane (col, quad) of a
+// B-fragment ds_read_b128 then hits bank quad 4 * (row mod 4) + chunk, distinct within each of the
+// instruction's four 16-lane groups ({0-3,12-15,20-27}, ...; found by exhaustive search over XOR
+// swizzles -- the earlier (row >> 2) & 3 left a 2-way conflict in every group).
 __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
@@ -78,7 +86,7 @@ __device__ __forceinline__ void stage_b(const bf16_t* __restrict__ w, int step, 
   if (wave * 64 < CHUNKS) {      // wave-uniform
     const int c0 = step * R::KC2, tap = c0 / R::KC, kc = c0 - tap * R::KC;
     const int n = tid >> 2, p = tid & 3;
-    const int lc = p ^ ((n >> 2) & 3);  // logical chunk stored at physical chunk p
+    const int lc = p ^ (((n >> 2) & 1) << 1);  // logical chunk stored at physical chunk p (see conv_tile)
 #pragma unroll
     for (int j = 0; j < R::KC2; ++j)
       glds16(w + (n * K + tap) * C + (kc + j) * 32 + 8 * lc, slot + j * C * 64 + wave * 1024);
@@ -116,7 +124,7 @@ __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int ro
 #pragma unroll
   for (int s = 0; s < R::NSW; ++s) {
     const int n = (wc * R::NSW + s) * 16 + col;
-    boff[s] = n * 64 + ((quad ^ ((n >> 2) & 3)) << 4);
+    boff[s] = n * 64 + ((quad ^ (((n >> 2) & 1) << 1)) << 4);
   }
   short8 a[2][R::KC2][R::MAXRB], bf[2][R::KC2][R::NSW];
   auto load = [&](int step, int buf) {
