@@ -2449,6 +2449,12 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   // every N >= 256 shape (+3..15 % over the 256x128 ring, +4..8 % over 256x256 with a BK=32 4-stage ring);
   // the 256x128 ring for narrower N when K-slabs are tap-aligned, LDS-DMA 128x128 otherwise
   if (variant < 0) variant = N >= 256 ? 4 : (Cin % BK == 0) ? 2 : 1;
+  // Few 256x256 tiles (encoder / variance-predictor GEMMs at M = B*T ~ 5k-30k rows with N = 256): the
+  // big tile leaves most of the 256 CUs idle; the 256x128 ring (or the 128x128 LDS-DMA kernel) doubles
+  // (quadruples) the tile count.  Measured at M = 14k (tools/exp_small_m.py): -20..36 % time for every
+  // N = 256 shape (k9 dgrad 219 -> 141 us), while N >= 768 keeps the 256x256 tile.
+  if (g_gemm_variant < 0 && N >= 256 && N <= 256 && ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG) <= 64)
+    variant = (Cin % BK == 0) ? 2 : 1;
   const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f;
   if (xon) {  // only the big64 (LDS-staged bf16 epilogue) and ring kernels implement EpiX
     if (out_f32 || !reg || (N % 8) || (ldy % 8) || act < 0) return -3;
