@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--tiny", action="store_true", help="plumbing-size model (CPU launcher tests only)")
     ap.add_argument("--phase-times", action="store_true", help="per-phase host/device ms of the timed steps")
+    ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
+                    help="default: nccl (RCCL) on GPUs; gloo rehearses the multi-rank path on fewer GPUs")
     return ap.parse_args(argv)
 
 
@@ -83,12 +85,13 @@ def run(args):
 
     if args.backend:
         ops.set_backend(args.backend)
-    rank, world, local_rank = ddp.init_distributed(expect_world=args.gpus)
+    rank, world, local_rank = ddp.init_distributed(backend=args.dist_backend, expect_world=args.gpus)
     cuda = torch.cuda.is_available()
     device = torch.device("cuda", local_rank) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(device)
     seen = torch.distributed.get_world_size() if world > 1 else 1
+    comm = torch.distributed.get_backend() if world > 1 else None
 
     tr = B.train_phase(args, rank, world, device)
     sy = B.synth_phase(args, rank, world, device) if args.synth_steps > 0 else None
@@ -114,6 +117,7 @@ def run(args):
             "parallelism": f"dp{world}",
         },
         "world_size_seen": seen,
+        "comm_backend": comm,
         "grad_buckets": tr["buckets"],
         "bucket_overlap": tr["overlap"],
         "skipped_steps": tr["skipped_steps"],

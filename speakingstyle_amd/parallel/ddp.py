@@ -54,7 +54,10 @@ DEFAULT_TIMEOUT_S = float(os.environ.get("SSAMD_DIST_TIMEOUT_S", "600"))
 
 def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None,
                      expect_world: Optional[int] = None):
-    """torchrun-style env init.  Returns (rank, world, local_rank).
+    """torchrun-style env init.  Returns (rank, world, local device ordinal).
+
+    ``backend``: "nccl" (= RCCL on ROCm, the default with GPUs), "gloo" (CPU, or a multi-process
+    rehearsal with several ranks sharing the visible GPU(s)); ``SSAMD_DIST_BACKEND`` overrides.
 
     Failure handling: every collective has a deadline
     (``timeout_s``, default ``SSAMD_DIST_TIMEOUT_S`` = 600 s); with RCCL the
@@ -66,6 +69,14 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] =
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = backend or os.environ.get("SSAMD_DIST_BACKEND") or None
+    if torch.cuda.is_available():
+        n_dev = torch.cuda.device_count()
+        if local_rank >= n_dev:
+            if world > 1 and (backend or "nccl") == "nccl":
+                raise RuntimeError(f"rank {rank}: local rank {local_rank} but only {n_dev} GPU(s) visible; RCCL "
+                                   "needs one GPU per rank (use the gloo backend to rehearse on fewer GPUs)")
+            local_rank = local_rank % n_dev  # gloo rehearsal: several ranks share a GPU
     if world > 1 and not dist.is_initialized():
         import datetime
 
@@ -125,10 +136,13 @@ def barrier():
 class GradBuckets:
     """Bucketed, backward-overlapped gradient all-reduce over a FlatArena."""
 
-    def __init__(self, arena, bucket_mb: float = 32.0, group=None):
+    def __init__(self, arena, bucket_mb: float = 32.0, group=None, force: bool = False):
+        """``force``: run the hook / collective machinery even in a 1-rank group (tests of the RCCL
+        path on a single GPU)."""
         self.arena = arena
         self.group = group
         self.world = world_size()
+        self.active = self.world > 1 or (force and dist.is_available() and dist.is_initialized())
         cap = max(1, int(bucket_mb * 1024 * 1024 // 4))
         self.buckets: List[tuple] = []  # (start, end, n_params)
         self.param_bucket = {}
@@ -158,7 +172,7 @@ class GradBuckets:
         self.last_launch_order: List[int] = []
         self.enabled = True
         self._handles = []
-        if self.world > 1:
+        if self.active:
             for p in arena.params:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
 
@@ -214,7 +228,7 @@ class GradBuckets:
 
     def finish(self):
         """Launch stragglers in order, make the current stream wait for every bucket, reset."""
-        if self.world <= 1:
+        if not self.active:
             return
         if self.counts is None:
             self._calibrate()

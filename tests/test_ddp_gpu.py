@@ -1,0 +1,90 @@
+"""The data-parallel gradient path on a real GPU with RCCL (single-rank communicator -- a 1-GPU
+box cannot host two RCCL ranks): the HIP backward kernels write weight gradients into arena slots,
+post-accumulate hooks drive asynchronous RCCL all-reduces of arena slices in bucket order while
+the backward continues, ``finish()`` orders the compute stream after them.  With one rank every
+all-reduce is an identity, so the reduced gradients must equal a plain (non-DP) step's bitwise.
+
+The multi-rank launcher / gloo path is covered on the CPU (tests/test_bench_cpu.py,
+tests/test_ddp_cpu.py, tests/test_ddp_slots_cpu.py)."""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _trainer(cfg, seed=11):
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+    from speakingstyle_amd.train.trainer import Trainer
+
+    torch.manual_seed(seed)
+    m = FastSpeech2(*cfg[:2]).to("cuda").set_compute_dtype(torch.bfloat16)
+    return Trainer(m, cfg, seed=1234)
+
+
+def _capture(tr):
+    grads = []
+    orig = tr.opt.step_and_update_lr
+
+    def hook():
+        grads.append(tr.opt.arena.grad.clone())
+        return orig()
+
+    tr.opt.step_and_update_lr = hook
+    return grads
+
+
+def test_rccl_bucket_path_single_rank():
+    import torch.distributed as dist
+
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.parallel import ddp
+
+    pp, mc, tc = load_named("LJSpeech")
+    mc["transformer"]["encoder_layer"] = mc["transformer"]["decoder_layer"] = 2
+    cfg = (pp, mc, tc)
+    batches = [SyntheticBatches(8, device="cuda", seed=3 + i).make_batch() for i in range(3)]
+
+    ref = _trainer(cfg)
+    g_ref = _capture(ref)
+    for b in batches:
+        ref.train_step(b)
+
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_port()}")
+    try:
+        tr = _trainer(cfg)
+        tr.buckets = ddp.GradBuckets(tr.opt.arena, bucket_mb=4.0, force=True)  # many buckets
+        nb = len(tr.buckets.buckets)
+        assert nb >= 4
+        g = _capture(tr)
+        in_hooks = []
+        for i, b in enumerate(batches):
+            orig_finish = tr.buckets.finish
+
+            def finish():
+                in_hooks.append(list(tr.buckets.launch_order))  # issued during backward
+                return orig_finish()
+
+            tr.buckets.finish = finish
+            tr.train_step(b)
+            tr.buckets.finish = orig_finish
+            assert tr.buckets.last_launch_order == list(range(nb))
+        torch.cuda.synchronize()
+        assert in_hooks[0] == [] and tr.buckets.calibrated()
+        assert len(in_hooks[1]) >= nb // 2 and len(in_hooks[2]) >= nb // 2  # overlapped with backward
+        for a, r in zip(g, g_ref):
+            assert torch.equal(a, r)
+        assert torch.equal(tr.opt.arena.data, ref.opt.arena.data)
+    finally:
+        dist.destroy_process_group()
