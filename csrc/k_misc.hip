@@ -700,3 +700,156 @@ SSAMD_API int ssamd_var_loss_bwd(VTerm t0, VTerm t1, VTerm t2, int B, const floa
   hipLaunchKernelGGL(var_loss_bwd_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, t0, t1, t2, B, g, counts);
   return (int)hipGetLastError();
 }
+
+// ----------------------------------------------------------------------------
+// Inference duration rounding (reference model/modules.py:132-137):
+//   d = max(round(exp(log_d) - 1), 0);  d = max(round(d * control), 0);  d = 0 at t >= len[b]
+// and mel_len[b] = sum_t d -- one block per utterance, the row sum in a fixed order.
+// control: null (1.0), one scalar (ctl_stride 0) or a [B, T] per-phoneme factor (word-level control).
+// torch.round / rintf both round half to even.
+// ----------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) duration_round_kernel(const float* __restrict__ log_d,
+                                                             const float* __restrict__ ctl, int ctl_per_elem,
+                                                             const int64_t* __restrict__ lens, int T,
+                                                             int64_t* __restrict__ d_out, int64_t* __restrict__ mel_len) {
+  __shared__ long long red[256];
+  const int b = blockIdx.x;
+  const int len = lens ? (int)lens[b] : T;
+  long long s = 0;
+  for (int t = threadIdx.x; t < T; t += 256) {
+    long long d = 0;
+    if (t < len) {
+      float v = fmaxf(rintf(expf(log_d[(long)b * T + t]) - 1.f), 0.f);
+      if (ctl) v = fmaxf(rintf(v * (ctl_per_elem ? ctl[(long)b * T + t] : ctl[0])), 0.f);
+      d = (long long)v;
+    }
+    d_out[(long)b * T + t] = d;
+    s += d;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) mel_len[b] = red[0];
+}
+
+// Sequence mean pool (reference model/modules.py:396: enc_seq.mean(dim=1) over the padded length; SURVEY
+// K16): out[b, c] = sum_{t < rows_b} x[row(b, t), c] / div.  Padded layout (cu null): rows_b = L, row =
+// b*L + t.  Packed layout: sequence b owns rows cu[b] .. cu[b+1]-1.  One block per (b, 64-column tile),
+// 4 row lanes summed in order then combined in order: deterministic.
+__global__ void __launch_bounds__(256) seq_mean_kernel(const bf16_t* __restrict__ x, const int64_t* __restrict__ cu,
+                                                       int L, int C, float div, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane_r = threadIdx.x >> 6;
+  const long r0 = cu ? cu[b] : (long)b * L;
+  const long r1 = cu ? cu[b + 1] : r0 + L;
+  float s = 0.f;
+  if (c < C)
+    for (long r = r0 + lane_r; r < r1; r += 4) s += bf2f(x[r * C + c]);
+  red[lane_r][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (lane_r == 0 && c < C) out[(long)b * C + c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                                    (red[2][threadIdx.x] + red[3][threadIdx.x])) / div;
+}
+
+// backward: dx[row(b, t), c] = g[b, c] / div for every row of sequence b (padded: all L rows).
+__global__ void __launch_bounds__(256) seq_mean_bwd_kernel(const float* __restrict__ g, const int64_t* __restrict__ cu,
+                                                           int B, int L, int C, float div, bf16_t* __restrict__ dx,
+                                                           long rows) {
+  const int c8n = C / 8;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < rows * c8n; e += (long)gridDim.x * 256) {
+    const long r = e / c8n;
+    const int c0 = (int)(e - r * c8n) * 8;
+    int b;
+    if (cu) {  // sequence of packed row r (B is small: binary search over the offsets)
+      int lo = 0, hi = B;
+      while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cu[mid] <= r) lo = mid; else hi = mid; }
+      b = lo;
+    } else {
+      b = (int)(r / L);
+    }
+    short8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(g[(long)b * C + c0 + i] / div);
+    *reinterpret_cast<short8*>(dx + r * C + c0) = o;
+  }
+}
+
+// Per-utterance row vector add (the speaker embedding, reference model/fastspeech2.py:74-77):
+//   out[b, t, :] = x[b, t, :] + table[ids[b], :]      (bf16 out, fp32 table)
+__global__ void __launch_bounds__(256) add_rowvec_kernel(const bf16_t* __restrict__ x, const float* __restrict__ table,
+                                                         const int64_t* __restrict__ ids, int L, int C,
+                                                         bf16_t* __restrict__ out, long rows) {
+  const int c8n = C / 8;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < rows * c8n; e += (long)gridDim.x * 256) {
+    const long r = e / c8n;
+    const int c0 = (int)(e - r * c8n) * 8;
+    const float* tv = table + (ids ? ids[r / L] : r / L) * (long)C + c0;  // ids null: row b of table
+    const short8 v = *reinterpret_cast<const short8*>(x + r * C + c0);
+    short8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(bf2f((bf16_t)v[i]) + tv[i]);
+    *reinterpret_cast<short8*>(out + r * C + c0) = o;
+  }
+}
+
+// dtable[v, c] = sum over utterances b with ids[b] == v (in b order) of S[b, c] (S = per-utterance row sums)
+__global__ void __launch_bounds__(256) rowvec_grad_kernel(const float* __restrict__ S, const int64_t* __restrict__ ids,
+                                                          int B, int C, float* __restrict__ dtable) {
+  const int v = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b)
+    if (ids[b] == v) s += S[(long)b * C + c];
+  dtable[(long)v * C + c] = s;
+}
+}  // namespace
+
+SSAMD_API int ssamd_duration_round(const float* log_d, const float* ctl, int ctl_per_elem, const int64_t* lens, int B,
+                                   int T, int64_t* d_out, int64_t* mel_len, hipStream_t s) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(duration_round_kernel, dim3(B), dim3(256), 0, s, log_d, ctl, ctl_per_elem, lens, T, d_out,
+                     mel_len);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_seq_mean(const bf16_t* x, const int64_t* cu, int B, int L, int C, float div, float* out,
+                             hipStream_t s) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(seq_mean_kernel, dim3(cdiv(C, 64), B), dim3(256), 0, s, x, cu, L, C, div, out);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_seq_mean_bwd(const float* g, const int64_t* cu, int B, int L, int C, float div, bf16_t* dx,
+                                 long rows, hipStream_t s) {
+  if (C % 8) return -1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(seq_mean_bwd_kernel, dim3(grid_for(rows * (C / 8))), dim3(256), 0, s, g, cu, B, L, C, div, dx,
+                     rows);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_add_rowvec(const bf16_t* x, const float* table, const int64_t* ids, int B, int L, int C,
+                               bf16_t* out, hipStream_t s) {
+  if (C % 8) return -1;
+  const long rows = (long)B * L;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(add_rowvec_kernel, dim3(grid_for(rows * (C / 8))), dim3(256), 0, s, x, table, ids, L, C, out,
+                     rows);
+  return (int)hipGetLastError();
+}
+
+// dtable [V, C] (overwritten) from dout [B, L, C]: per-utterance fixed-order row sums, then per-row gather
+SSAMD_API int ssamd_rowvec_grad(const bf16_t* dout, const int64_t* ids, int B, int L, int C, int V, float* dtable,
+                                float* ws, long ws_floats, hipStream_t s) {
+  if ((long)B * C > ws_floats) return -3;
+  int rc = ssamd_seq_mean(dout, nullptr, B, L, C, 1.f, ws, s);  // S[b] = sum_t dout[b, t]
+  if (rc) return rc;
+  hipLaunchKernelGGL(rowvec_grad_kernel, dim3(cdiv(C, 256), V), dim3(256), 0, s, ws, ids, B, C, dtable);
+  return (int)hipGetLastError();
+}

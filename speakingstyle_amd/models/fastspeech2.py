@@ -217,10 +217,8 @@ class VarianceAdaptor(nn.Module):
             if mel_lens is not None:
                 mel_len = mel_lens
         else:
-            d_pred = torch.clamp(torch.round(torch.exp(log_d) - 1.0), min=0.0)
-            d_rounded = torch.clamp(torch.round(_apply_control(d_pred, d_control)), min=0.0)
-            d_rounded = d_rounded.masked_fill(ops.lengths_to_mask(src_lens, d_rounded.shape[1]), 0.0)
-            x, mel_len = ops.length_regulate(x, d_rounded.long(), None)
+            d_rounded, mel_len = ops.duration_round(log_d, src_lens, d_control)  # one kernel on the GPU
+            x, mel_len = ops.length_regulate(x, d_rounded, None, mel_len=mel_len)
 
         if self.pitch_feature_level == "frame_level":
             p_pred, x = self._variance(self.pitch_predictor, self.pitch_bins, self.pitch_embedding, x, pitch_target, mel_len, p_control)
@@ -354,7 +352,7 @@ class FastSpeech2(nn.Module):
             spk = self.speaker_emb(speakers)
             if self.spker_embed_proj is not None:
                 spk = spk + self.spker_embed_proj(self.spker_table[speakers])
-            x = x + spk.to(cd).unsqueeze(1)
+            x = ops.add_rowvec(x, spk)
         training_lr = d_targets is not None
         packed = (self.training and training_lr and mel_lens is not None and mel_lens_host is not None
                   and max_mel_len is not None and self.variance_adaptor.packable())

@@ -68,7 +68,7 @@ class ReferenceEncoder(nn.Module):
         if self.mean_over_valid:
             pooled = h.float().sum(1) / lens.clamp(min=1).unsqueeze(1).float()
         else:
-            pooled = h.float().mean(1)
+            pooled = ops.seq_mean(h)  # over the padded length, like the reference (D8)
         gb = self.feature_wise_affine(pooled.to(h.dtype))
         return gb[:, : self.d_model], gb[:, self.d_model:]
 

@@ -124,10 +124,41 @@ def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, mail
     return ref.add_layernorm(a, residual, ln_w, ln_b, **kw)
 
 
-def length_regulate(x, durations, max_len):
+def length_regulate(x, durations, max_len, mel_len=None):
     if use_hip(x):
-        return _hip().length_regulate(x, durations, max_len)
+        return _hip().length_regulate(x, durations, max_len, mel_len=mel_len)
     return ref.length_regulate(x, durations, max_len)
+
+
+def duration_round(log_d, lengths, control=1.0):
+    """Inference durations: max(round(exp(log_d)-1), 0) * control, rounded, 0 at pads -> (d, mel_len)."""
+    if use_hip(log_d):
+        return _hip().duration_round(log_d, lengths, control)
+    d = torch.clamp(torch.round(torch.exp(log_d) - 1.0), min=0.0)
+    if isinstance(control, torch.Tensor):
+        control = control.to(d.device, d.dtype)
+        if control.dim() == 2 and control.shape[1] != d.shape[1]:
+            control = F.pad(control, (0, d.shape[1] - control.shape[1]), value=1.0)[:, : d.shape[1]]
+        d = d * control
+    elif control != 1.0:
+        d = d * control
+    d = torch.clamp(torch.round(d), min=0.0)
+    d = d.masked_fill(ref.lengths_to_mask(lengths, d.shape[1]), 0.0).long()
+    return d, d.sum(1)
+
+
+def seq_mean(x, divisor=None):
+    """[B, L, C] -> [B, C] fp32 mean over the (padded) length L (``divisor`` overrides L)."""
+    if use_hip(x):
+        return _hip().seq_mean(x, divisor)
+    return x.float().sum(1) / float(divisor or x.shape[1])
+
+
+def add_rowvec(x, v):
+    """x [B, L, C] + v[:, None, :] (per-utterance vector, e.g. the speaker embedding)."""
+    if use_hip(x):
+        return _hip().add_rowvec(x, v)
+    return x + v.to(x.dtype).unsqueeze(1)
 
 
 def length_regulate_packed(x, durations, pack: PackInfo, pe):

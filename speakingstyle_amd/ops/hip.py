@@ -763,13 +763,15 @@ class _LRFn(torch.autograd.Function):
         return dx, None, None, None
 
 
-def length_regulate(x, durations, max_len, pe=None):
+def length_regulate(x, durations, max_len, pe=None, mel_len=None):
+    """``mel_len``: the row sums of ``durations`` when the caller already has them (duration_round)."""
     if x.dtype != torch.bfloat16 or x.shape[-1] % 8:
         _torch_fallback(f"length_regulate C={x.shape[-1]} dtype={x.dtype} (kernel: bf16, C % 8 == 0)")
         out, ml = ref.length_regulate(x, durations, max_len)
         return (out + pe[: out.shape[1]].to(out.dtype) if pe is not None else out), ml
     dur = durations.to(torch.int64).contiguous()
-    mel_len = dur.clamp(min=0).sum(1)
+    if mel_len is None:
+        mel_len = dur.clamp(min=0).sum(1)
     if max_len is None:
         max_len = int(mel_len.max().item()) if dur.shape[0] else 0  # inference: one D2H for allocation
     return _LRFn.apply(x, dur, int(max_len), pe), mel_len
@@ -1418,3 +1420,106 @@ def conv_post(x, w, b, slope=0.01, int16_scale=None):
                                    _ptr(out), _stream())
     _check(rc, "ssamd_conv_post")
     return out
+
+
+# ------------------------------------------------------------------------ small glue kernels
+_SIGS.update({"ssamd_duration_round": [P, P, I, P, I, I, P, P, P],
+              "ssamd_seq_mean": [P, P, I, I, I, F, P, P],
+              "ssamd_seq_mean_bwd": [P, P, I, I, I, F, P, L_, P],
+              "ssamd_add_rowvec": [P, P, P, I, I, I, P, P]})
+
+
+def duration_round(log_d, lengths, control=1.0):
+    """Inference durations (reference ``model/modules.py:132-137``): max(round(exp(log_d) - 1), 0),
+    times the control (scalar or per-phoneme [B, T]), rounded, 0 at padded phonemes; plus the mel
+    lengths.  -> (d int64 [B, T], mel_len int64 [B]); one kernel, no host sync."""
+    ld = log_d.float().contiguous()
+    B, T = ld.shape
+    ctl, per = None, 0
+    if isinstance(control, torch.Tensor):
+        c = control.to(ld.device, torch.float32)
+        if c.dim() == 2:
+            if c.shape[1] != T:
+                c = torch.nn.functional.pad(c, (0, max(0, T - c.shape[1])), value=1.0)[:, :T]
+            ctl, per = c.expand(B, T).contiguous(), 1
+        else:
+            ctl = c.reshape(-1)[:1].contiguous()
+    elif float(control) != 1.0:
+        ctl = torch.full((1,), float(control), device=ld.device, dtype=torch.float32)
+    lens = None if lengths is None else lengths.to(torch.int64).contiguous()
+    d = torch.empty(B, T, device=ld.device, dtype=torch.int64)
+    ml = torch.empty(B, device=ld.device, dtype=torch.int64)
+    rc = lib().ssamd_duration_round(_ptr(ld), _ptr(ctl), per, _ptr(lens), B, T, _ptr(d), _ptr(ml), _stream())
+    _check(rc, "ssamd_duration_round")
+    return d, ml
+
+
+class _SeqMeanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cu, B, L, div):
+        xc = x.to(torch.bfloat16).contiguous()
+        C = xc.shape[-1]
+        out = torch.empty(B, C, device=x.device, dtype=torch.float32)
+        rc = lib().ssamd_seq_mean(_ptr(xc), _ptr(cu), B, L, C, float(div), _ptr(out), _stream())
+        _check(rc, "ssamd_seq_mean")
+        ctx.save_for_backward(cu)
+        ctx.geom = (B, L, C, float(div), xc.shape, x.dtype, cu is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, L, C, div, shape, dtype, has_cu = ctx.geom
+        (cu,) = ctx.saved_tensors
+        dx = torch.empty(shape, device=g.device, dtype=torch.bfloat16)
+        rows = dx.numel() // C
+        rc = lib().ssamd_seq_mean_bwd(_ptr(g.float().contiguous()), _ptr(cu if has_cu else None), B, L, C, div,
+                                      _ptr(dx), rows, _stream())
+        _check(rc, "ssamd_seq_mean_bwd")
+        return dx.to(dtype), None, None, None, None
+
+
+def seq_mean(x, divisor=None, pack=None):
+    """[B, L, C] -> [B, C] fp32 mean over L (the reference's mean over the padded length; ``divisor``
+    overrides L), or per packed sequence ([1, R, C] rows, ``pack``) divided by ``divisor``."""
+    if pack is not None:
+        return _SeqMeanFn.apply(x, pack.cu, pack.B, pack.M, float(divisor or pack.M))
+    B, L, C = x.shape
+    if C % 8:
+        _torch_fallback(f"seq_mean C={C}")
+        return x.float().sum(1) / float(divisor or L)
+    return _SeqMeanFn.apply(x, None, B, L, float(divisor or L))
+
+
+class _AddRowVecFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, v):
+        xc = x.to(torch.bfloat16).contiguous()
+        B, L, C = xc.shape
+        vf = v.detach().float().contiguous()
+        assert vf.shape == (B, C), "add_rowvec: one vector per sequence"
+        out = torch.empty_like(xc)
+        rc = lib().ssamd_add_rowvec(_ptr(xc), _ptr(vf), None, B, L, C, _ptr(out), _stream())
+        _check(rc, "ssamd_add_rowvec")
+        ctx.geom = (B, L, C, v.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, L, C, vdtype = ctx.geom
+        gc = g.to(torch.bfloat16).contiguous()
+        dv = None
+        if ctx.needs_input_grad[1]:
+            dv = torch.empty(B, C, device=g.device, dtype=torch.float32)
+            rc = lib().ssamd_seq_mean(_ptr(gc), None, B, L, C, 1.0, _ptr(dv), _stream())  # fixed-order row sums
+            _check(rc, "ssamd_seq_mean")
+            dv = dv.to(vdtype)
+        return g, dv
+
+
+def add_rowvec(x, v):
+    """x [B, L, C] + v[b] broadcast over L (bf16 out): the speaker-embedding add (reference
+    ``model/fastspeech2.py:74-77``), backward = per-utterance fixed-order row sums."""
+    if x.shape[-1] % 8:
+        _torch_fallback(f"add_rowvec C={x.shape[-1]}")
+        return x + v.to(x.dtype).unsqueeze(1)
+    return _AddRowVecFn.apply(x, v)

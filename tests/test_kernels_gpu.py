@@ -854,3 +854,41 @@ def test_resblock_layer_fused(C, K, d, T):
         out = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE, acc=acc, out_scale=1 / 3)
         assert out.data_ptr() == acc.data_ptr()
         assert _rel(out, expect) < 1e-2
+
+
+def test_duration_round_seq_mean_add_rowvec():
+    """K12 duration rounding (+ scalar / per-phoneme control), K16 mean pool, K1 per-utterance add."""
+    from speakingstyle_amd import ops as O
+
+    torch.manual_seed(9)
+    B, T = 5, 37
+    log_d = torch.randn(B, T, device=DEV) * 1.5 + 1.0
+    lens = torch.tensor([37, 20, 1, 30, 12], device=DEV)
+    for ctl in (1.0, 1.3, torch.rand(B, 30, device=DEV) + 0.5):
+        d, ml = hip.duration_round(log_d, lens, ctl)
+        ref_d = torch.clamp(torch.round(torch.exp(log_d) - 1.0), min=0.0)
+        if isinstance(ctl, torch.Tensor):
+            c = F.pad(ctl, (0, T - ctl.shape[1]), value=1.0)
+            ref_d = ref_d * c
+        else:
+            ref_d = ref_d * ctl
+        ref_d = torch.clamp(torch.round(ref_d), min=0.0).masked_fill(ref.lengths_to_mask(lens, T), 0.0).long()
+        assert torch.equal(d, ref_d) and torch.equal(ml, ref_d.sum(1))
+    x = torch.randn(B, 50, 256, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    m = hip.seq_mean(x)
+    mr = xr.mean(1)
+    torch.testing.assert_close(m, mr, rtol=1e-4, atol=1e-5)
+    g = torch.randn_like(mr)
+    m.backward(g)
+    mr.backward(g)
+    assert _rel(x.grad, xr.grad) < 1e-2
+    v = torch.randn(B, 256, device=DEV, requires_grad=True)
+    vr = v.detach().clone().requires_grad_(True)
+    y = hip.add_rowvec(x.detach().clone().requires_grad_(True), v)
+    yr = x.detach().float() + vr.unsqueeze(1)
+    assert _rel(y, yr) < 1e-2
+    gy = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(gy)
+    yr.backward(gy.float())
+    assert _rel(v.grad, vr.grad) < 1e-3
