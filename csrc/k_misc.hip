@@ -853,3 +853,126 @@ SSAMD_API int ssamd_rowvec_grad(const bf16_t* dout, const int64_t* ids, int B, i
   hipLaunchKernelGGL(rowvec_grad_kernel, dim3(cdiv(C, 256), V), dim3(256), 0, s, ws, ids, B, C, dtable);
   return (int)hipGetLastError();
 }
+
+// ----------------------------------------------------------------------------
+// Packed <-> padded row layouts (ops/packing.py) without torch gather / scatter:
+//   pack:    out[r] = x[dst[r]] (+ pe[dst[r] % M])                bf16 [R, C]
+//   unpack:  out[b*M + t] = t < lens[b] ? src[cu[b] + t] : fill   bf16 or fp32 [B*M, C]
+//   pad_colsum: per-block partial column sums of dout over the padded rows only (the gradient
+//   of the fill row), finished by a fixed-order column sum.
+// ----------------------------------------------------------------------------
+namespace {
+template <typename T>
+__device__ __forceinline__ float ld_as_f(const T* p);
+template <>
+__device__ __forceinline__ float ld_as_f<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ld_as_f<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T>
+__device__ __forceinline__ void st_from_f(T* p, float v);
+template <>
+__device__ __forceinline__ void st_from_f<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void st_from_f<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+template <typename T>
+__global__ void __launch_bounds__(256) pack_rows_kernel(const T* __restrict__ x, const int64_t* __restrict__ dst,
+                                                        const bf16_t* __restrict__ pe, int M, long R, int C,
+                                                        T* __restrict__ out) {
+  const int c8n = C / 8;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < R * c8n; e += (long)gridDim.x * 256) {
+    const long r = e / c8n;
+    const int c0 = (int)(e - r * c8n) * 8;
+    const long s = dst[r];
+    const T* xs = x + s * C + c0;
+    T* o = out + r * C + c0;
+    if (pe) {
+      const bf16_t* p = pe + (s % M) * C + c0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) st_from_f<T>(o + i, ld_as_f<T>(xs + i) + bf2f(p[i]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = xs[i];
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) unpack_rows_kernel(const T* __restrict__ src, const int64_t* __restrict__ cu,
+                                                          const int64_t* __restrict__ lens, const float* __restrict__ fill,
+                                                          int M, int C, long rows, T* __restrict__ out) {
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < rows * C; e += (long)gridDim.x * 256) {
+    const long row = e / C;
+    const int c = (int)(e - row * C);
+    const int b = (int)(row / M), t = (int)(row - (long)b * M);
+    float v = fill ? fill[c] : 0.f;
+    if (t < lens[b]) v = ld_as_f<T>(src + (cu[b] + t) * C + c);
+    st_from_f<T>(out + e, v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) pad_colsum_kernel(const T* __restrict__ dout, const int64_t* __restrict__ lens,
+                                                         int M, int C, long rows, int rows_per_blk,
+                                                         float* __restrict__ part) {
+  const long r0 = (long)blockIdx.y * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
+    float s = 0.f;
+    for (long row = r0; row < r1; ++row) {
+      const int b = (int)(row / M), t = (int)(row - (long)b * M);
+      if (t >= lens[b]) s += ld_as_f<T>(dout + row * C + c);
+    }
+    part[(long)blockIdx.y * C + c] = s;
+  }
+}
+}  // namespace
+
+// f32: 1 = fp32 rows, 0 = bf16 rows; pe (bf16 [>=M, C]) optional
+SSAMD_API int ssamd_pack_rows(const void* x, const int64_t* dst, const bf16_t* pe, int M, long R, int C, int f32,
+                              void* out, hipStream_t s) {
+  if (C % 8) return -1;
+  if (R == 0) return 0;
+  const int g = grid_for(R * (C / 8));
+  if (f32)
+    hipLaunchKernelGGL(pack_rows_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, dst, pe, M, R, C,
+                       (float*)out);
+  else
+    hipLaunchKernelGGL(pack_rows_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)x, dst, pe, M, R, C,
+                       (bf16_t*)out);
+  return (int)hipGetLastError();
+}
+
+// f32: 1 = fp32 rows, 0 = bf16 rows
+SSAMD_API int ssamd_unpack_rows(const void* src, const int64_t* cu, const int64_t* lens, const float* fill, int B, int M,
+                                int C, int f32, void* out, hipStream_t s) {
+  const long rows = (long)B * M;
+  if (rows == 0) return 0;
+  const int g = grid_for(rows * C);
+  if (f32)
+    hipLaunchKernelGGL(unpack_rows_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)src, cu, lens, fill, M, C,
+                       rows, (float*)out);
+  else
+    hipLaunchKernelGGL(unpack_rows_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)src, cu, lens, fill, M, C,
+                       rows, (bf16_t*)out);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API long ssamd_pad_colsum_ws(int B, int M, int C) { return (long)cdiv((long)B * M, 256) * C + seg_colsum_ws(1, C); }
+
+// dfill[c] = sum over padded rows (t >= lens[b]) of dout[b*M + t, c]; fixed order
+SSAMD_API int ssamd_pad_colsum(const void* dout, int f32, const int64_t* lens, int B, int M, int C, float* dfill,
+                               float* ws, long ws_floats, hipStream_t s) {
+  const long rows = (long)B * M;
+  if (rows == 0) return (int)hipMemsetAsync(dfill, 0, C * sizeof(float), s);
+  const int chunks = cdiv(rows, 256);
+  if (ws_floats < ssamd_pad_colsum_ws(B, M, C)) return -3;
+  dim3 grid(cdiv(C, 256), chunks);
+  if (f32)
+    hipLaunchKernelGGL(pad_colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)dout, lens, M, C, rows, 256, ws);
+  else
+    hipLaunchKernelGGL(pad_colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dout, lens, M, C, rows, 256,
+                       ws);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  return ssamd_seg_colsum(ws, C, 1, chunks, C, dfill, 0, 0, C, nullptr, ws + (long)chunks * C, seg_colsum_ws(1, C), s);
+}

@@ -52,6 +52,10 @@ class ReferenceEncoder(nn.Module):
             conv, ln = seq[0], seq[2]
             h = conv(h, act="relu")
             h = ops.add_layernorm(h, None, ln.weight, ln.bias, post_drop=self.dropout, training=self.training)
+        host = getattr(mel_lens, "host_lengths", None)
+        if (host is not None and not self.mean_over_valid and ops.use_hip(h)
+                and (self.training or M <= self.max_seq_len)):
+            return self._forward_packed(h, mel_lens, host)
         # pad frames are zeroed once after the whole conv stack (modules.py:370-371)
         h = h.masked_fill(ops.lengths_to_mask(mel_lens, M).unsqueeze(-1), 0.0)
         if (not self.training) and M > self.max_seq_len:
@@ -70,6 +74,25 @@ class ReferenceEncoder(nn.Module):
         else:
             pooled = ops.seq_mean(h)  # over the padded length, like the reference (D8)
         gb = self.feature_wise_affine(pooled.to(h.dtype))
+        return gb[:, : self.d_model], gb[:, self.d_model:]
+
+    def _forward_packed(self, h, mel_lens, host):
+        """FFT blocks over the valid frames only (``ops/packing.py``), same result as the padded
+        path: pad rows there are zeroed after every sublayer, so they contribute nothing to the
+        attention (masked keys), to the k=3 FFN convs (zero padding at sequence ends) or to the
+        mean, which still divides by the padded length (D8).  The host lengths size the packed
+        rows without a device sync."""
+        M = min(h.shape[1], self.max_seq_len)
+        if h.shape[1] != M:
+            h = h[:, :M].contiguous()
+        R = int(sum(min(int(v), M) for v in host))
+        pk = ops.PackInfo.build(mel_lens, M, R)
+        x = ops.pack_rows(h, pk, self.position_enc[0, :M])
+        x = self.fftb_linear(x)
+        for blk in self.fftb_stack:
+            x = blk(x, pk.lens, None, pack=pk)
+        pooled = ops.seq_mean(x, divisor=M, pack=pk)
+        gb = self.feature_wise_affine(pooled.to(x.dtype))
         return gb[:, : self.d_model], gb[:, self.d_model:]
 
 

@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from . import reference as ref
-from .packing import PackInfo, pack as pack_rows, unpack as unpack_rows  # noqa: F401
+from .packing import PackInfo, pack as _pack, unpack as _unpack  # noqa: F401
 
 _FORCED = os.environ.get("SSAMD_BACKEND")  # "reference" | "hip" | None
 _NO_MAILBOX = os.environ.get("SSAMD_NO_MAILBOX") == "1"  # A/B switch for the residual-gradient fusion
@@ -147,10 +147,13 @@ def duration_round(log_d, lengths, control=1.0):
     return d, d.sum(1)
 
 
-def seq_mean(x, divisor=None):
-    """[B, L, C] -> [B, C] fp32 mean over the (padded) length L (``divisor`` overrides L)."""
+def seq_mean(x, divisor=None, pack: Optional[PackInfo] = None):
+    """[B, L, C] -> [B, C] fp32 mean over the (padded) length L (``divisor`` overrides L); with
+    ``pack``: x is packed ``[1, R, C]``, each sequence's rows summed and divided by ``divisor``."""
     if use_hip(x):
-        return _hip().seq_mean(x, divisor)
+        return _hip().seq_mean(x, divisor, pack)
+    if pack is not None:
+        x = _unpack(x, pack)
     return x.float().sum(1) / float(divisor or x.shape[1])
 
 
@@ -159,6 +162,20 @@ def add_rowvec(x, v):
     if use_hip(x):
         return _hip().add_rowvec(x, v)
     return x + v.to(x.dtype).unsqueeze(1)
+
+
+def pack_rows(x, pack: PackInfo, pe=None):
+    """[B, M, C] -> packed [1, R, C] (+ positional encoding ``pe[t]`` when given)."""
+    if use_hip(x):
+        return _hip().pack_rows(x, pack, pe)
+    return _pack(x if pe is None else x + pe[: pack.M].to(x.dtype).unsqueeze(0), pack)
+
+
+def unpack_rows(x, pack: PackInfo, fill=None):
+    """packed [1, R, C] -> [B, M, C]; padded rows = ``fill`` ([C], default 0)."""
+    if use_hip(x):
+        return _hip().unpack_rows(x, pack, fill)
+    return _unpack(x, pack, fill)
 
 
 def length_regulate_packed(x, durations, pack: PackInfo, pe):

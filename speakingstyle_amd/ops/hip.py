@@ -1523,3 +1523,89 @@ def add_rowvec(x, v):
         _torch_fallback(f"add_rowvec C={x.shape[-1]}")
         return x + v.to(x.dtype).unsqueeze(1)
     return _AddRowVecFn.apply(x, v)
+
+
+# ------------------------------------------------------------------------ packed <-> padded rows
+_SIGS.update({"ssamd_pack_rows": [P, P, P, I, L_, I, I, P, P],
+              "ssamd_unpack_rows": [P, P, P, P, I, I, I, I, P, P],
+              "ssamd_pad_colsum_ws": [I, I, I],
+              "ssamd_pad_colsum": [P, I, P, I, I, I, P, P, L_, P]})
+_RESTYPES["ssamd_pad_colsum_ws"] = L_
+
+
+def _pack_raw(x, pk, pe=None):
+    f32 = x.dtype == torch.float32
+    xc = x.contiguous() if f32 else x.to(torch.bfloat16).contiguous()
+    C = xc.shape[-1]
+    assert xc.numel() == pk.B * pk.M * C, "pack_rows: x must be [B, M, C]"
+    pec = None if pe is None else pe.to(torch.bfloat16).contiguous()
+    if pec is not None:
+        assert pec.shape[0] >= pk.M and pec.shape[-1] == C
+    out = torch.empty(1, pk.R, C, device=xc.device, dtype=xc.dtype)
+    rc = lib().ssamd_pack_rows(_ptr(xc), _ptr(pk.dst), _ptr(pec), pk.M, pk.R, C, int(f32), _ptr(out), _stream())
+    _check(rc, "ssamd_pack_rows")
+    return out
+
+
+def _unpack_raw(x, pk, fill=None):
+    f32 = x.dtype == torch.float32
+    xc = x.contiguous() if f32 else x.to(torch.bfloat16).contiguous()
+    C = xc.shape[-1]
+    assert xc.numel() == pk.R * C, "unpack_rows: x must be [1, R, C]"
+    fc = None if fill is None else fill.detach().float().reshape(C).contiguous()
+    out = torch.empty(pk.B, pk.M, C, device=xc.device, dtype=xc.dtype)
+    rc = lib().ssamd_unpack_rows(_ptr(xc), _ptr(pk.cu), _ptr(pk.lens), _ptr(fc), pk.B, pk.M, C, int(f32), _ptr(out),
+                                 _stream())
+    _check(rc, "ssamd_unpack_rows")
+    return out
+
+
+class _PackRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pk, pe):
+        ctx.pk, ctx.dtype = pk, x.dtype
+        return _pack_raw(x, pk, pe)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _unpack_raw(g, ctx.pk).to(ctx.dtype), None, None  # padded rows get zero gradient
+
+
+class _UnpackRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pk, fill):
+        ctx.pk, ctx.dtype = pk, x.dtype
+        ctx.fill_dtype = None if fill is None else fill.dtype
+        return _unpack_raw(x, pk, fill)
+
+    @staticmethod
+    def backward(ctx, g):
+        pk = ctx.pk
+        gc = g.contiguous() if g.dtype == torch.float32 else g.to(torch.bfloat16).contiguous()
+        dx = _pack_raw(gc, pk).to(ctx.dtype)
+        dfill = None
+        if ctx.fill_dtype is not None and ctx.needs_input_grad[2]:
+            C = gc.shape[-1]
+            dfill = torch.empty(C, device=g.device, dtype=torch.float32)
+            ws = _workspace(g.device, int(lib().ssamd_pad_colsum_ws(pk.B, pk.M, C)))
+            rc = lib().ssamd_pad_colsum(_ptr(gc), int(gc.dtype == torch.float32), _ptr(pk.lens), pk.B, pk.M, C,
+                                        _ptr(dfill), _ptr(ws), ws.numel(), _stream())
+            _check(rc, "ssamd_pad_colsum")
+            dfill = dfill.to(ctx.fill_dtype)
+        return dx, None, dfill
+
+
+def pack_rows(x, pk, pe=None):
+    """[B, M, C] -> [1, R, C] valid rows (+ ``pe[t]`` at position t); backward scatters, pads get 0."""
+    if x.shape[-1] % 8 or x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+        _torch_fallback(f"pack_rows C={x.shape[-1]}")
+        from .packing import pack
+
+        return pack(x if pe is None else x + pe[: pk.M].to(x.dtype).unsqueeze(0), pk)
+    return _PackRowsFn.apply(x, pk, pe)
+
+
+def unpack_rows(x, pk, fill=None):
+    """[1, R, C] -> [B, M, C], padded rows = ``fill`` ([C], default 0; its gradient = column sums of
+    the padded rows' gradient, fixed order)."""
+    return _UnpackRowsFn.apply(x, pk, fill)

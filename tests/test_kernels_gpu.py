@@ -661,10 +661,20 @@ def test_model_packed_vs_padded_gpu():
     lp[0].backward()
     ld[0].backward()
     g2 = dict(m2.named_parameters())
+    # exact gradient 0: the key bias shifts every score of a query by the same amount, a conv bias
+    # feeding a batch-statistics BatchNorm is subtracted again; both paths produce rounding noise
+    # there -> only check that it stays tiny
+    def zero_grad_exact(n):
+        return n.endswith("w_ks.bias") or (n.startswith("postnet.") and n.endswith("conv.bias"))
+
+    p1 = dict(m1.named_parameters())
+    for n, p in p1.items():
+        if zero_grad_exact(n) and p.grad is not None:
+            assert p.grad.norm() < 1e-2 * p1[n[:-4] + "weight"].grad.norm() + 1e-6, n
     bad = [(n, _rel(p.grad, g2[n].grad)) for n, p in m1.named_parameters()
            if p.grad is not None and g2[n].grad is not None and g2[n].grad.norm() > 1e-6
-           and _rel(p.grad, g2[n].grad) > 0.1]
-    assert not bad, bad[:10]
+           and not zero_grad_exact(n) and _rel(p.grad, g2[n].grad) > 0.1]
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("Cin,N,ks", [(256, 1024, 9), (1024, 256, 1), (512, 512, 5), (80, 512, 5)])
@@ -892,3 +902,76 @@ def test_duration_round_seq_mean_add_rowvec():
     y.backward(gy)
     yr.backward(gy.float())
     assert _rel(v.grad, vr.grad) < 1e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_pack_unpack_rows_gpu(dtype):
+    """HIP pack (+PE) / unpack (+fill row) and their backward vs the torch gather/scatter."""
+    from speakingstyle_amd.ops import packing
+
+    torch.manual_seed(31)
+    lens = torch.tensor([7, 0, 13, 5, 13], device=DEV)
+    B, M, C = 5, 13, 80
+    R = int(lens.sum())
+    pk = packing.PackInfo.build(lens, M, R)
+    x = torch.randn(B, M, C, device=DEV).to(dtype).requires_grad_(True)
+    pe = torch.randn(M + 3, C, device=DEV)
+    y = hip.pack_rows(x, pk, pe)
+    y_ref = packing.pack(x.detach().float() + pe[:M].to(torch.bfloat16).float().unsqueeze(0), pk)
+    assert _rel(y, y_ref) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    gx_ref = packing.unpack(g.float(), pk)
+    assert torch.allclose(x.grad.float(), gx_ref, atol=1e-2)
+    z = torch.randn(1, R, C, device=DEV).to(dtype).requires_grad_(True)
+    fill = torch.randn(C, device=DEV, requires_grad=True)
+    u = hip.unpack_rows(z, pk, fill)
+    u_ref = packing.unpack(z.detach().float(), pk, fill.detach())
+    assert torch.allclose(u.float(), u_ref, atol=1e-2)
+    gu = torch.randn(B, M, C, device=DEV).to(dtype)
+    u.backward(gu)
+    assert torch.allclose(z.grad.float(), packing.pack(gu.float(), pk), atol=1e-2)
+    pad = ~(torch.arange(M, device=DEV)[None] < lens[:, None])
+    dfill_ref = (gu.float() * pad[..., None]).sum((0, 1))
+    assert _rel(fill.grad, dfill_ref) < 1e-5
+
+
+def test_reference_encoder_packed_vs_padded_gpu():
+    """FiLM reference encoder: packed FFT blocks (host lengths) == padded path, values and grads."""
+    import copy
+
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.models.style import ReferenceEncoder
+
+    pp, mc, _ = load_named("BC2013")
+    mc["reference_encoder"]["dropout"] = 0.0
+    torch.manual_seed(32)
+    e1 = ReferenceEncoder(pp, mc).to(DEV)
+    e2 = copy.deepcopy(e1)
+    lens_h = [120, 37, 301, 5, 250]
+    B, M = len(lens_h), max(lens_h)
+    mel = torch.randn(B, M, 80, device=DEV)
+    for i, n in enumerate(lens_h):
+        mel[i, n:] = 0.0
+    mel = mel.to(torch.bfloat16)
+    lens = torch.tensor(lens_h, device=DEV)
+    lens_p = lens.clone()
+    lens_p.host_lengths = lens_h
+    calls = []
+    orig = e1._forward_packed
+    e1._forward_packed = lambda *a: calls.append(1) or orig(*a)
+    for train in (False, True):
+        e1.train(train)
+        e2.train(train)
+        g1, b1 = e1(mel, lens_p)
+        g2, b2 = e2(mel, lens)
+        assert _rel(g1, g2) < 2e-2 and _rel(b1, b2) < 2e-2
+    assert len(calls) == 2
+    w = torch.randn_like(g1.float())
+    ((g1.float() * w).sum() + b1.float().sum()).backward()
+    ((g2.float() * w).sum() + b2.float().sum()).backward()
+    p2 = dict(e2.named_parameters())
+    bad = [(n, _rel(p.grad, p2[n].grad)) for n, p in e1.named_parameters()
+           if p.grad is not None and p2[n].grad.norm() > 1e-6 and not n.endswith("w_ks.bias")  # exact grad 0
+           and _rel(p.grad, p2[n].grad) > 5e-2]
+    assert not bad, bad
