@@ -104,6 +104,68 @@ __device__ __forceinline__ short8 pack8(const float4v& a, const float4v& b) {
   return r;
 }
 
+// Online-softmax update of one 64-key tile (scores st = raw Q.K, query on the lane column, keys
+// 4g + r of each 16-key fragment on the lane's 4 accumulator slots).  VALU-lean form -- the
+// loop is VALU-issue bound (MI355X_MICROARCH: 4 cycles per VALU, 8 per v_exp beside 16-cycle
+// MFMAs): raw v_exp_f32 (no denormal-range fix-up: softmax terms below 2^-126 are 0 anyway),
+// the key mask only on the one tile that straddles len, scale and max folded into one FMA,
+// the O rescale skipped when no lane's running max moved, and l kept as a per-lane partial
+// (the 4 lane groups of a query share m, so the cross-group sum is deferred to the end).
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int NF, int D>
+__device__ __forceinline__ void online_softmax(float4v (&st)[NF][4], float (&m)[NF], float (&l)[NF],
+                                               float4v (&oacc)[NF][D / 16], int key0, int len, float scale_log2,
+                                               int g) {
+  if (key0 + TK > len) {
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (key0 + kf * 16 + 4 * g + r >= len)
+#pragma unroll
+          for (int f = 0; f < NF; ++f) st[f][kf][r] = -INFINITY;
+  }
+  bool rescale = false;
+  float alpha[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    float mx = fmaxf(fmaxf(st[f][0][0], st[f][0][1]), fmaxf(st[f][0][2], st[f][0][3]));
+#pragma unroll
+    for (int kf = 1; kf < 4; ++kf)
+      mx = fmaxf(mx, fmaxf(fmaxf(st[f][kf][0], st[f][kf][1]), fmaxf(st[f][kf][2], st[f][kf][3])));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m[f], mx * scale_log2);  // the tile always holds a valid key: mn finite
+    alpha[f] = fast_exp2(m[f] - mn);                 // m = -inf on the first tile -> 0
+    rescale |= m[f] != mn;
+    const float nb = -mn;
+    float ls = 0.f;
+#pragma unroll
+    for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = fast_exp2(fmaf(st[f][kf][r], scale_log2, nb));
+        st[f][kf][r] = pv;
+        ls += pv;
+      }
+    l[f] = fmaf(l[f], alpha[f], ls);
+    m[f] = mn;
+  }
+  if (__any(rescale)) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int i = 0; i < D / 16; ++i) oacc[f][i] *= alpha[f];
+  }
+}
+
+// per-lane partial -> the query's full softmax denominator (sum over the 4 lane groups)
+__device__ __forceinline__ float lsum_groups(float l) {
+  l += __shfl_xor(l, 16, 64);
+  return l + __shfl_xor(l, 32, 64);
+}
+
 // A fragment (16 rows x 32) of a transposed image: rows = reduction keys/queries in the
 // permuted order {base + 4g + q} u {base + 16 + 4g + q}, columns col0 .. col0+15.
 template <int D>
@@ -199,39 +261,7 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
         for (int f = 0; f < NF; ++f) st[f][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[f][s], st[f][kf], 0, 0, 0);
       }
     }
-    const int key0 = kt * TK;
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = key0 + kf * 16 + 4 * g + r;
-          const float x = key < len ? st[f][kf][r] * scale_log2 : -INFINITY;
-          st[f][kf][r] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[f], mx);
-      const float alpha = exp2f(m[f] - mn);
-      float ls = 0.f;
-#pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = exp2f(st[f][kf][r] - mn);
-          st[f][kf][r] = pv;
-          ls += pv;
-        }
-      ls += __shfl_xor(ls, 16, 64);
-      ls += __shfl_xor(ls, 32, 64);
-      l[f] = l[f] * alpha + ls;
-      m[f] = mn;
-#pragma unroll
-      for (int i = 0; i < D / 16; ++i) oacc[f][i] *= alpha;
-    }
+    online_softmax<NF, D>(st, m, l, oacc, kt * TK, len, scale_log2, g);
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       short8 pb[NF];
@@ -245,6 +275,8 @@ __global__ void __launch_bounds__(NT) attn_fwd_kernel(const bf16_t* __restrict__
       }
     }
   }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) l[f] = lsum_groups(l[f]);
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     if (qv[f] >= Lq) continue;
@@ -358,39 +390,7 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_dma_kernel(const bf16_t* __res
         for (int f = 0; f < NF; ++f) st[f][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[f][s], st[f][kf], 0, 0, 0);
       }
     }
-    const int key0 = kt * TK;
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = key0 + kf * 16 + 4 * g + r;
-          const float x = key < len ? st[f][kf][r] * scale_log2 : -INFINITY;
-          st[f][kf][r] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[f], mx);
-      const float alpha = exp2f(m[f] - mn);
-      float ls = 0.f;
-#pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = exp2f(st[f][kf][r] - mn);
-          st[f][kf][r] = pv;
-          ls += pv;
-        }
-      ls += __shfl_xor(ls, 16, 64);
-      ls += __shfl_xor(ls, 32, 64);
-      l[f] = l[f] * alpha + ls;
-      m[f] = mn;
-#pragma unroll
-      for (int i = 0; i < D / 16; ++i) oacc[f][i] *= alpha;
-    }
+    online_softmax<NF, D>(st, m, l, oacc, kt * TK, len, scale_log2, g);
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       short8 pb[NF];
@@ -406,6 +406,8 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_dma_kernel(const bf16_t* __res
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // next tile landed, this one consumed
     __builtin_amdgcn_s_barrier();
   }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) l[f] = lsum_groups(l[f]);
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     if (qv[f] >= Lq) continue;
@@ -468,7 +470,8 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
   const int kblk0 = blockIdx.x * (64 * NF);
   auto load_ld = [&](int q0) -> float {  // thread t < 64: lse of query q0+t; 64 <= t < 128: delta
     const int qq = q0 + (tid & 63);
-    if (tid >= 128 || qq >= len) return 0.f;
+    if (tid >= 128) return 0.f;
+    if (qq >= len) return tid < 64 ? INFINITY : 0.f;  // P = exp2(-inf) = 0, dS = 0: no query mask
     return tid < 64 ? lse[(long)bh * L + qq] : delta[(rowb + qq) * H + h];
   };
   const bf16_t* Qp = qkv + h * D;
@@ -544,19 +547,15 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
     for (int qf = 0; qf < 4; ++qf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // key columns past len only feed their own (discarded) dK / dV column: no key mask
         const int ql = qf * 16 + 4 * g + r;
-        const bool qok = qt * TQ + ql < len;
-        const float lq = Ls[ql];
+        const float nlq = -Ls[ql];
         const float dq = Ds[ql];
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          float pv = 0.f, ds = 0.f;
-          if (qok && kval[f]) {
-            pv = exp2f(sp[f][qf][r] * scale_log2 - lq);
-            ds = pv * (dp[f][qf][r] - dq);
-          }
+          const float pv = fast_exp2(fmaf(sp[f][qf][r], scale_log2, nlq));
           sp[f][qf][r] = pv;
-          dp[f][qf][r] = ds;
+          dp[f][qf][r] = pv * (dp[f][qf][r] - dq);
         }
       }
 #pragma unroll
@@ -589,8 +588,8 @@ __global__ void __launch_bounds__(NT) attn_bwd_dkdv_kernel(const bf16_t* __restr
       short4v a, c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        a[r] = (short)f2bf(dk[f][df][r] * scale);
-        c[r] = (short)f2bf(dv[f][df][r]);
+        a[r] = (short)f2bf(kval[f] ? dk[f][df][r] * scale : 0.f);
+        c[r] = (short)f2bf(kval[f] ? dv[f][df][r] : 0.f);
       }
       *reinterpret_cast<short4v*>(dkp + df * 16 + 4 * g) = a;
       *reinterpret_cast<short4v*>(dvp + df * 16 + 4 * g) = c;
@@ -619,7 +618,8 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv_dma_kernel(const bf16_
   const int kblk0 = blockIdx.x * (64 * NF);
   auto load_ld = [&](int q0) -> float {  // thread t < 64: lse of query q0+t; 64 <= t < 128: delta
     const int qq = q0 + (tid & 63);
-    if (tid >= 128 || qq >= len) return 0.f;
+    if (tid >= 128) return 0.f;
+    if (qq >= len) return tid < 64 ? INFINITY : 0.f;  // P = exp2(-inf) = 0, dS = 0: no query mask
     return tid < 64 ? lse[(long)bh * L + qq] : delta[(rowb + qq) * H + h];
   };
   const bf16_t* Qp = qkv + h * D;
@@ -711,19 +711,15 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv_dma_kernel(const bf16_
     for (int qf = 0; qf < 4; ++qf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // key columns past len only feed their own (discarded) dK / dV column: no key mask
         const int ql = qf * 16 + 4 * g + r;
-        const bool qok = qt * TQ + ql < len;
-        const float lq = Ls[ql];
+        const float nlq = -Ls[ql];
         const float dq = Ds[ql];
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          float pv = 0.f, ds = 0.f;
-          if (qok && kval[f]) {
-            pv = exp2f(sp[f][qf][r] * scale_log2 - lq);
-            ds = pv * (dp[f][qf][r] - dq);
-          }
+          const float pv = fast_exp2(fmaf(sp[f][qf][r], scale_log2, nlq));
           sp[f][qf][r] = pv;
-          dp[f][qf][r] = ds;
+          dp[f][qf][r] = pv * (dp[f][qf][r] - dq);
         }
       }
 #pragma unroll
@@ -759,8 +755,8 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv_dma_kernel(const bf16_
       short4v a, c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        a[r] = (short)f2bf(dk[f][df][r] * scale);
-        c[r] = (short)f2bf(dv[f][df][r]);
+        a[r] = (short)f2bf(kval[f] ? dk[f][df][r] * scale : 0.f);
+        c[r] = (short)f2bf(kval[f] ? dv[f][df][r] : 0.f);
       }
       *reinterpret_cast<short4v*>(dkp + df * 16 + 4 * g) = a;
       *reinterpret_cast<short4v*>(dvp + df * 16 + 4 * g) = c;
@@ -863,15 +859,17 @@ __global__ void __launch_bounds__(NT) attn_bwd_dq_kernel(const bf16_t* __restric
     for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = kt * TK + kf * 16 + 4 * g + r;
+        // queries past len have zero Q / dO, lse = delta = 0 -> dS = 0: no query mask.  Keys past
+        // len (zero K / V rows) are masked on the one tile that straddles len only: their dS
+        // meets a zero K row, but exp2(-lse) could overflow for a row of very negative scores.
+        if (kt * TK + TK > len && kt * TK + kf * 16 + 4 * g + r >= len) {
+#pragma unroll
+          for (int f = 0; f < NF; ++f) st[f][kf][r] = -INFINITY;
+        }
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          float ds = 0.f;
-          if (key < len && qv[f] < len) {
-            const float pv = exp2f(st[f][kf][r] * scale_log2 - lq[f]);
-            ds = pv * (dpt[f][kf][r] - dd[f]);
-          }
-          st[f][kf][r] = ds;
+          const float pv = fast_exp2(fmaf(st[f][kf][r], scale_log2, -lq[f]));
+          st[f][kf][r] = pv * (dpt[f][kf][r] - dd[f]);
         }
       }
 #pragma unroll
@@ -1001,15 +999,17 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dq_dma_kernel(const bf16_t*
     for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int key = kt * TK + kf * 16 + 4 * g + r;
+        // queries past len have zero Q / dO, lse = delta = 0 -> dS = 0: no query mask.  Keys past
+        // len (zero K / V rows) are masked on the one tile that straddles len only: their dS
+        // meets a zero K row, but exp2(-lse) could overflow for a row of very negative scores.
+        if (kt * TK + TK > len && kt * TK + kf * 16 + 4 * g + r >= len) {
+#pragma unroll
+          for (int f = 0; f < NF; ++f) st[f][kf][r] = -INFINITY;
+        }
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-          float ds = 0.f;
-          if (key < len && qv[f] < len) {
-            const float pv = exp2f(st[f][kf][r] * scale_log2 - lq[f]);
-            ds = pv * (dpt[f][kf][r] - dd[f]);
-          }
-          st[f][kf][r] = ds;
+          const float pv = fast_exp2(fmaf(st[f][kf][r], scale_log2, -lq[f]));
+          st[f][kf][r] = pv * (dpt[f][kf][r] - dd[f]);
         }
       }
 #pragma unroll
@@ -1045,9 +1045,21 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dq_dma_kernel(const bf16_t*
 
 // NF (fragments per wave) chosen from measurement on MI355X: the forward keeps 2 waves/SIMD
 // with NF = 1; the D >= 64 backward is LDS-read bound and gains from NF = 2.
+static int g_nf32_fwd = 2, g_nf32_bwd = 2;  // D = 32 (reference encoder, 8 heads): measured NF=2 -6 % fwd, -2 % bwd vs 1; 4 spills
+SSAMD_API void ssamd_attn_set_nf32(int fwd, int bwd) {
+  g_nf32_fwd = fwd;
+  g_nf32_bwd = bwd;
+}
 #define ATTN_DISPATCH(D, FWD, ...)                                                                 \
   switch (D) {                                                                                     \
-    case 32: { constexpr int DD = 32; constexpr int NF = 1; __VA_ARGS__; break; }                 \
+    case 32: {                                                                                     \
+      constexpr int DD = 32;                                                                       \
+      const int nf32 = FWD ? g_nf32_fwd : g_nf32_bwd;                                              \
+      if (nf32 == 4) { constexpr int NF = 4; __VA_ARGS__; }                                         \
+      else if (nf32 == 2) { constexpr int NF = 2; __VA_ARGS__; }                                    \
+      else { constexpr int NF = 1; __VA_ARGS__; }                                                   \
+      break;                                                                                       \
+    }                                                                                              \
     case 64: { constexpr int DD = 64; constexpr int NF = FWD ? 1 : 2; __VA_ARGS__; break; }       \
     case 128: { constexpr int DD = 128; constexpr int NF = FWD ? 1 : 2; __VA_ARGS__; break; }     \
     default: return -1;                                                                            \

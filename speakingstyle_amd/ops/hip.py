@@ -39,6 +39,7 @@ _SIGS = {
     "ssamd_conv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, P, P, I, P],
     "ssamd_wgrad_set_variant": [I],
     "ssamd_attn_set_nf": [I, I],
+    "ssamd_attn_set_nf32": [I, I],
     "ssamd_attn_set_fwd": [I, I],
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],

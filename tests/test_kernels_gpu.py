@@ -975,3 +975,39 @@ def test_reference_encoder_packed_vs_padded_gpu():
            if p.grad is not None and p2[n].grad.norm() > 1e-6 and not n.endswith("w_ks.bias")  # exact grad 0
            and _rel(p.grad, p2[n].grad) > 5e-2]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("nf", [1, 2, 4])
+def test_attention_d32_nf_variants(nf, packed):
+    """D=32 / 8-head attention (reference encoder) with 1, 2 or 4 fragments per wave, padded and
+    packed rows, ragged lengths incl. a partial last tile: forward and backward vs fp32."""
+    torch.manual_seed(24)
+    H, D = 8, 32
+    pk, lens, M = _pack_case()
+    qkv = torch.randn(pk.B, M, 3 * H * D, device=DEV).to(torch.bfloat16)
+    g = torch.randn(pk.B, M, H * D, device=DEV).to(torch.bfloat16)
+    mask = (torch.arange(M, device=DEV)[None] < lens[:, None]).unsqueeze(-1)
+    g = g * mask
+    hip.lib().ssamd_attn_set_nf32(nf, nf)
+    try:
+        if packed:
+            from speakingstyle_amd.ops import packing
+
+            qp = packing.pack(qkv, pk).requires_grad_(True)
+            o = hip.attention(qp, pk.lens, H, pk)
+            o.backward(packing.pack(g, pk))
+            o = packing.unpack(o.detach(), pk)
+            gq = packing.unpack(qp.grad, pk)
+        else:
+            qh = qkv.clone().requires_grad_(True)
+            o = hip.attention(qh, lens, H)
+            o.backward(g)
+            gq = qh.grad
+    finally:
+        hip.lib().ssamd_attn_set_nf32(2, 2)
+    qr = qkv.float().requires_grad_(True)
+    o_ref = ref.attention(qr, lens, H)
+    o_ref.backward(g.float())
+    assert _rel(o.float() * mask, o_ref * mask) < 2e-2
+    assert _rel(gq.float() * mask, qr.grad * mask) < 2e-2

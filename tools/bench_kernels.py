@@ -140,6 +140,14 @@ def main():
                 t2 = timeit(lambda: torch.autograd.grad(o, qh, g, retain_graph=True), args.iters)
                 row[f"bwd_ms_qdma{qd}_nf{nq}"] = round(t2, 3)
             hip.lib().ssamd_attn_set_q_dma(1, 2)
+        if D == 32:  # query / key fragments per wave of the D = 32 kernels
+            for nf in (1, 2, 4):
+                hip.lib().ssamd_attn_set_nf32(nf, nf)
+                row[f"fwd_ms_nf{nf}"] = round(timeit(lambda: hip.attention(qh, lens, H), args.iters), 3)
+                o2 = hip.attention(qh, lens, H)
+                row[f"bwd_ms_nf{nf}"] = round(timeit(lambda: torch.autograd.grad(o2, qh, g, retain_graph=True),
+                                                     args.iters), 3)
+            hip.lib().ssamd_attn_set_nf32(2, 2)
         print(json.dumps(row), flush=True)
 
 
