@@ -300,6 +300,18 @@ __device__ __forceinline__ void a_glds16(const void* src, char* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// Buffer-resource LDS-DMA: a descriptor over the rows of ONE sequence (bytes = len rows), so a
+// tile row past len is out of range and lands as zeros (no per-row select, no 64-bit address
+// math per tile); the per-lane part is a loop-invariant 32-bit voffset, the tile offset a
+// scalar soffset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seq_rsrc(const bf16_t* base, int nrows, int row_stride) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, nrows * row_stride * 2, 0x00020000);
+}
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff,
+                                           0, 0);
+}
+
 template <int NF>
 __global__ void __launch_bounds__(NT, 2) attn_fwd_dma_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ lens,
                                                       const int64_t* __restrict__ cu,
@@ -356,18 +368,21 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_dma_kernel(const bf16_t* __res
   const int nkt = (len + TK - 1) / TK;
   // K / V tiles go global -> LDS by DMA (no staging registers, no ds_write), row-major with the
   // unified swizzle applied on the source side; V^T fragments are read with ds_read_b64_tr_b16.
+  const __amdgpu_buffer_rsrc_t rK = seq_rsrc(Kp + rowb * RS, len, RS), rV = seq_rsrc(Vp + rowb * RS, len, RS);
+  int voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 4 + wave) * 4 + (lane >> 4);
+    voff[i] = (row * RS + ((lane & 15) ^ uni_h(row)) * 8) * 2;
+  }
   auto issue = [&](int key0, int buf) {
     char* Kd = smem + buf * (2 * TK * D * 2);
     char* Vd = Kd + TK * D * 2;
+    const int soff = key0 * RS * 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = (i * 4 + wave) * 4 + (lane >> 4);
-      const int c = (lane & 15) ^ uni_h(row);
-      const int key = key0 + row;
-      const bool ok = key < len;
-      const long off = (rowb + key) * (long)RS + c * 8;
-      a_glds16(ok ? (const void*)(Kp + off) : (const void*)a_zero_chunk, Kd + (i * 4 + wave) * 1024);
-      a_glds16(ok ? (const void*)(Vp + off) : (const void*)a_zero_chunk, Vd + (i * 4 + wave) * 1024);
+      buf_lds16(rK, voff[i], soff, Kd + (i * 4 + wave) * 1024);
+      buf_lds16(rV, voff[i], soff, Vd + (i * 4 + wave) * 1024);
     }
   };
   if (nkt > 0) issue(0, 0);
@@ -653,19 +668,22 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv_dma_kernel(const bf16_
 
   // fully masked key block -> zero grads; query rows >= len have zero output -> no contribution
   const int nqt = (kblk0 < len) ? (len + TQ - 1) / TQ : 0;
+  const __amdgpu_buffer_rsrc_t rQ = seq_rsrc(Qp + rowb * RS, len, RS), rD = seq_rsrc(dOp + rowb * OS, len, OS);
+  int voq[4], vod[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 4 + wave) * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ uni_h(row);
+    voq[i] = (row * RS + c * 8) * 2;
+    vod[i] = (row * OS + c * 8) * 2;
+  }
   auto issue = [&](int q0, int buf) {
     char* Qd = smem + buf * BUFB;
     char* Dd = Qd + TQ * D * 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = (i * 4 + wave) * 4 + (lane >> 4);
-      const int c = (lane & 15) ^ uni_h(row);
-      const int qq = q0 + row;
-      const bool ok = qq < len;
-      a_glds16(ok ? (const void*)(Qp + (rowb + qq) * (long)RS + c * 8) : (const void*)a_zero_chunk,
-               Qd + (i * 4 + wave) * 1024);
-      a_glds16(ok ? (const void*)(dOp + (rowb + qq) * (long)OS + c * 8) : (const void*)a_zero_chunk,
-               Dd + (i * 4 + wave) * 1024);
+      buf_lds16(rQ, voq[i], q0 * RS * 2, Qd + (i * 4 + wave) * 1024);
+      buf_lds16(rD, vod[i], q0 * OS * 2, Dd + (i * 4 + wave) * 1024);
     }
   };
   auto stash_ld = [&](int buf, float v) {
@@ -956,18 +974,21 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dq_dma_kernel(const bf16_t*
     for (int i = 0; i < D / 16; ++i) dq[f][i] = (float4v){0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (len + TK - 1) / TK;
+  const __amdgpu_buffer_rsrc_t rK = seq_rsrc(Kp + rowb * RS, len, RS), rV = seq_rsrc(Vp + rowb * RS, len, RS);
+  int voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 4 + wave) * 4 + (lane >> 4);
+    voff[i] = (row * RS + ((lane & 15) ^ uni_h(row)) * 8) * 2;
+  }
   auto issue = [&](int key0, int buf) {
     char* Kd = smem + buf * BUFB;
     char* Vd = Kd + TK * D * 2;
+    const int soff = key0 * RS * 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = (i * 4 + wave) * 4 + (lane >> 4);
-      const int c = (lane & 15) ^ uni_h(row);
-      const int key = key0 + row;
-      const bool ok = key < len;
-      const long off = (rowb + key) * (long)RS + c * 8;
-      a_glds16(ok ? (const void*)(Kp + off) : (const void*)a_zero_chunk, Kd + (i * 4 + wave) * 1024);
-      a_glds16(ok ? (const void*)(Vp + off) : (const void*)a_zero_chunk, Vd + (i * 4 + wave) * 1024);
+      buf_lds16(rK, voff[i], soff, Kd + (i * 4 + wave) * 1024);
+      buf_lds16(rV, voff[i], soff, Vd + (i * 4 + wave) * 1024);
     }
   };
   if (nkt > 0) issue(0, 0);
