@@ -440,21 +440,23 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_dma_kernel(const bf16_t* __res
 }
 
 // ------------------------------------------------------------------------------ backward
+// delta[row * H + h] = sum_d dO * O: 8 channels (16 B) per lane, D/8 lanes per (row, head)
 __global__ void __launch_bounds__(NT) attn_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dO,
                                                         float* __restrict__ delta, long rows, int H, int D) {
-  // one wave per (row, head): delta[row * H + h] = sum_d dO * O
-  const long wid = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wid >= rows * H) return;
-  const long row = wid / H;
-  const int h = (int)(wid % H);
+  const int lpr = D / 8;  // lanes per (row, head): 4 (D=32) .. 16 (D=128), a power of two
+  const long e = blockIdx.x * (long)NT + threadIdx.x;
+  const long wid = e / lpr;
+  const int c = (int)(e - wid * lpr);
   float s = 0.f;
-  for (int d = lane; d < D; d += 64) {
-    const long idx = row * (long)H * D + h * D + d;
-    s += bf2f(o[idx]) * bf2f(dO[idx]);
+  if (wid < rows * H) {
+    const long off = wid * D + c * 8;  // [rows, H*D] row-major == (row*H + h)*D
+    const short8 a = *reinterpret_cast<const short8*>(o + off);
+    const short8 b = *reinterpret_cast<const short8*>(dO + off);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += bf2f((bf16_t)a[q]) * bf2f((bf16_t)b[q]);
   }
-  s = wave_sum(s);
-  if (lane == 0) delta[wid] = s;
+  for (int w = lpr >> 1; w > 0; w >>= 1) s += __shfl_xor(s, w, 64);
+  if (c == 0 && wid < rows * H) delta[wid] = s;
 }
 
 // NF = key fragments (of 16) per wave; block = 4 waves x 16*NF keys
@@ -1152,7 +1154,7 @@ SSAMD_API int ssamd_attn_bwd(const bf16_t* qkv, const int64_t* lens, const int64
                              const float* lse, const bf16_t* dO, bf16_t* dqkv, float* delta, long rows, int B, int L,
                              int H, int D, float scale, hipStream_t s) {
   if ((long)B * L == 0 || rows == 0) return 0;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * 64, NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
+  hipLaunchKernelGGL(attn_delta_kernel, dim3(cdiv(rows * H * (D / 8), NT)), dim3(NT), 0, s, o, dO, delta, rows, H, D);
   if (D == 128) {  // fragments per wave of the two kernels: runtime-tunable (measured defaults)
     if (g_kv_dma) {
       constexpr size_t lds = 2 * (2 * TQ * 128 * 2 + 2 * TQ * 4);

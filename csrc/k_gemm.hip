@@ -22,6 +22,7 @@
 // ds_read_b128 / tr reads), XCD-aware bijective block remap so that the 8 blocks
 // that share an A panel run on one XCD's L2.
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
@@ -332,7 +333,16 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restri
 // per-lane SOURCE address (the LDS image is lane-linear per wave instruction).  Lanes
 // whose chunk is conv padding / out of range read a 16-B zero block instead.
 // ----------------------------------------------------------------------------
-__device__ __attribute__((aligned(16))) bf16_t g_zero_chunk[8];
+__device__ __attribute__((aligned(16))) bf16_t g_zero_chunk_mem[8];
+// The zero chunk's address, produced by an opaque asm so it stays in an SGPR pair for the whole
+// kernel: read directly, the global's GOT entry is reloaded (s_load + lgkmcnt wait) before every
+// LDS-DMA issue, because the loops' s_waitcnt asm carries a "memory" clobber.  Each kernel below
+// shadows g_zero_chunk with this local.
+__device__ __forceinline__ const void* zero_chunk_ptr() {
+  const void* p = g_zero_chunk_mem;
+  asm volatile("" : "+s"(p));
+  return p;
+}
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -346,6 +356,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
                                                                const bf16_t* __restrict__ resid,
                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
                                                                ConvGeom g, int act, int ldy) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BN - 1) / BN;
   const int nM = (g.M + BM - 1) / BM;
@@ -487,6 +498,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ resid,
                                                                 const int64_t* __restrict__ lens, void* __restrict__ Yv,
                                                                 ConvGeom g, int act, int ldy, EpiX ex) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BN - 1) / BN;
   const int nM = (g.M + BM3 - 1) / BM3;
@@ -740,6 +752,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
                                                                const bf16_t* __restrict__ resid,
                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
                                                                ConvGeom g, int act, int ldy) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BG - 1) / BG;
   const int nM = (g.M + BG - 1) / BG;
@@ -888,6 +901,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
                                                                const bf16_t* __restrict__ resid,
                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
                                                                ConvGeom g, int act, int ldy, EpiX ex) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BG - 1) / BG;
   const int nM = (g.M + BG - 1) / BG;
@@ -1214,6 +1228,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_pers_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ resid,
                                                                 const int64_t* __restrict__ lens, void* __restrict__ Yv,
                                                                 ConvGeom g, int act, int ldy) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BG - 1) / BG;
   const int nM = (g.M + BG - 1) / BG;
@@ -1398,6 +1413,7 @@ template <bool PACKED>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
                                                            float* __restrict__ slabs, float* __restrict__ bias_slabs,
                                                            ConvGeom g, int rows_per_split) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + 127) / 128;  // cout tiles
   const int nK = (g.K + 127) / 128;  // k tiles
@@ -1588,6 +1604,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_ring_kernel(const bf16_t* _
                                                                  float* __restrict__ slabs,
                                                                  float* __restrict__ bias_slabs, ConvGeom g,
                                                                  int rows_per_split) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + 255) / 256;
   const int nK = (g.K + 127) / 128;
@@ -1781,6 +1798,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big_kernel(const bf16_t* __
                                                                 float* __restrict__ slabs,
                                                                 float* __restrict__ bias_slabs, ConvGeom g,
                                                                 int rows_per_split) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + 255) / 256;
   const int nK = (g.K + 255) / 256;
@@ -1955,12 +1973,13 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big_kernel(const bf16_t* __
 
 constexpr int WB64_STAGE = 2 * 64 * 512;  // 64 KiB: dY [64][256] + X [64][256]
 
-template <bool PACKED>
+template <bool PACKED, bool IMM>
 __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* __restrict__ X,
                                                                 const bf16_t* __restrict__ dY,
                                                                 float* __restrict__ slabs,
                                                                 float* __restrict__ bias_slabs, ConvGeom g,
                                                                 int rows_per_split) {
+  const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + 255) / 256;
   const int nK = (g.K + 255) / 256;
@@ -1975,11 +1994,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wk = wave & 3;
   const float invCin = 1.f / (float)g.Cin;
-  int* cu_s = reinterpret_cast<int*>(smem + 2 * WB64_STAGE);
-  if constexpr (PACKED) {
-    for (int i = tid; i <= g.nseq; i += NT3) cu_s[i] = (int)g.cu[i];
-    __syncthreads();
-  }
 
   float4v acc[8][4];
 #pragma unroll
@@ -1993,7 +2007,10 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
   bool yok[4];
   int xshift[4], xcin[4];
   bool xkok[4];
-  int t_cur[4], s0[4], s1[4], sb[4];
+  int t_cur[4];
+  // packed rows: (position, length) of each staged row from the rinfo table, prefetched one stage
+  // ahead of its use so the DMA issue never waits on it (no per-step sequence walk)
+  int2 ri_nxt[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = 2 * (i * 8 + wave) + (lane >> 5);
@@ -2009,19 +2026,21 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
     xcin[i] = k - tap * g.Cin;
     xshift[i] = tap * g.dil - g.pad;
     const int m = r_begin + row;
-    if constexpr (PACKED) {
-      int lo = 0, hi = g.nseq;
-      while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cu_s[mid] <= m) lo = mid; else hi = mid; }
-      sb[i] = lo;
-      s0[i] = cu_s[lo];
-      s1[i] = cu_s[lo + 1];
-    } else {
-      t_cur[i] = m % g.L;
-    }
+    if constexpr (!PACKED) t_cur[i] = m % g.L;
   }
+  auto load_ri = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + drow[i];
+      ri_nxt[i] = m < r_end ? g.rinfo[m] : make_int2(0, 0);
+    }
+  };
+  if constexpr (PACKED) load_ri(r_begin);
+  // LDS: dY images of the two stages at 0 / 32 KiB, X images at 64 / 96 KiB, so that every
+  // fragment read is a loop-invariant per-lane base + an immediate (stage, k-half, +4 rows)
   auto stage = [&](int r0, int buf) {
-    char* Ys = smem + buf * WB64_STAGE;
-    char* Xs = Ys + 64 * 512;
+    char* Ys = smem + buf * 32768;
+    char* Xs = smem + 65536 + buf * 32768;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + drow[i];
@@ -2033,13 +2052,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
       const int m = r0 + drow[i];
       int ts, lim;
       if constexpr (PACKED) {
-        while (m >= s1[i] && sb[i] + 1 < g.nseq) {
-          ++sb[i];
-          s0[i] = s1[i];
-          s1[i] = cu_s[sb[i] + 1];
-        }
-        ts = m - s0[i] + xshift[i];
-        lim = s1[i] - s0[i];
+        ts = ri_nxt[i].x + xshift[i];
+        lim = ri_nxt[i].y;
       } else {
         ts = t_cur[i] + xshift[i];
         lim = g.L;
@@ -2058,15 +2072,27 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
 
   const int nsteps = (r_end - r_begin + 64 - 1) / 64;
   if (nsteps > 0) stage(r_begin, 0);
+  if constexpr (PACKED) load_ri(r_begin + 64);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nsteps) stage(r_begin + (s + 1) * 64, buf ^ 1);
-    const char* Ys = smem + buf * WB64_STAGE;
-    const char* Xs = Ys + 64 * 512;
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  const __attribute__((address_space(3))) char* lds0 = (const __attribute__((address_space(3))) char*)smem;
+  int fa_off[8], fb_off[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa_off[i] = swz_tr512(grp * 8 + q, (wn * 128 + i * 16) / 4 + p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb_off[j] = 65536 + swz_tr512(grp * 8 + q, (wk * 64 + j * 16) / 4 + p);
+  auto tr = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(lds0 + off)); };
+  auto step = [&](int st, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    if (st + 1 < nsteps) {
+      stage(r_begin + (st + 1) * 64, buf ^ 1);
+      if constexpr (PACKED) load_ri(r_begin + (st + 2) * 64);
+    }
     if (do_bias) {
+      const char* Ys = smem + buf * 32768;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = (tid >> 5) + 16 * j;
@@ -2078,25 +2104,18 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int rbase = kk * 32 + grp * 8 + q;
+      const int imm = buf * 32768 + kk * 16384;  // compile-time after unrolling
       short8 fa[8], fb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int cb = (wk * 64 + j * 16) / 4 + p;
-        short4v b0 = ds_read_tr_asm(Xs + swz_tr512(rbase, cb));
-        short4v b1 = ds_read_tr_asm(Xs + swz_tr512(rbase + 4, cb));
+        const short4v b0 = tr(fb_off[j] + imm), b1 = tr(fb_off[j] + imm + 2048);
         fb[j] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int ca = (wn * 128 + i * 16) / 4 + p;
-        short4v a0 = ds_read_tr_asm(Ys + swz_tr512(rbase, ca));
-        short4v a1 = ds_read_tr_asm(Ys + swz_tr512(rbase + 4, ca));
+        const short4v a0 = tr(fa_off[i] + imm), a1 = tr(fa_off[i] + imm + 2048);
         fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
       }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
-                     "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -2104,6 +2123,62 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  };
+  if constexpr (IMM) {
+    // two steps per iteration: the stage index is a compile-time constant in each body
+    for (int st = 0; st < nsteps; st += 2) {
+      step(st, std::integral_constant<int, 0>{});
+      if (st + 1 < nsteps) step(st + 1, std::integral_constant<int, 1>{});
+    }
+  } else {  // all 24 fragment reads of a k-half issued, one wait, 32 MFMAs (runtime stage base)
+    for (int st = 0; st < nsteps; ++st) {
+      const int buf = st & 1;
+      if (st + 1 < nsteps) {
+        stage(r_begin + (st + 1) * 64, buf ^ 1);
+        if constexpr (PACKED) load_ri(r_begin + (st + 2) * 64);
+      }
+      const char* Ys = smem + buf * 32768;
+      const char* Xs = smem + 65536 + buf * 32768;
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = (tid >> 5) + 16 * j;
+          const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
+          const short8 v = *reinterpret_cast<const short8*>(Ys + row * 512 + ((bc16 ^ (f >> 1)) << 4));
+#pragma unroll
+          for (int t = 0; t < 8; ++t) bsum[t] += bf2f((bf16_t)v[t]);
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int rbase = kk * 32 + grp * 8 + q;
+        short8 fa[8], fb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cb = (wk * 64 + j * 16) / 4 + p;
+          short4v b0 = ds_read_tr_asm(Xs + swz_tr512(rbase, cb));
+          short4v b1 = ds_read_tr_asm(Xs + swz_tr512(rbase + 4, cb));
+          fb[j] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int ca = (wn * 128 + i * 16) / 4 + p;
+          short4v a0 = ds_read_tr_asm(Ys + swz_tr512(rbase, ca));
+          short4v a1 = ds_read_tr_asm(Ys + swz_tr512(rbase + 4, ca));
+          fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
+                       "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
   if (do_bias) {
     float* red = reinterpret_cast<float*>(smem);  // [16][256]
@@ -2353,6 +2428,69 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     dst[ks] = acc.y;
     dst[2 * ks] = acc.z;
     dst[3 * ks] = acc.w;
+  }
+}
+
+// Split-parallel slab reduction: block = 64 float4 columns x 4 split lanes; lane l sums the slabs
+// l, l+4, ... (4 independent float4 loads in flight per thread, every block of the grid busy even
+// for a single 256x256 weight), the 4 lane sums are combined in LDS in a fixed order -> the same
+// bits on every run.  Blocks past the dW part reduce the bias slabs the same way.
+__global__ void __launch_bounds__(256) wgrad_reduce4_kernel(const float* __restrict__ slabs, float* __restrict__ dW,
+                                                            const float* __restrict__ bslabs, float* __restrict__ db,
+                                                            int splits, int N, int Cin, int ks, int nb_main) {
+  __shared__ float4 red[4][64];
+  const long K = (long)Cin * ks;
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const bool bias_blk = (int)blockIdx.x >= nb_main;
+  const long stride = bias_blk ? (long)N : (long)N * K;   // floats between consecutive slabs
+  const long ncol4 = bias_blk ? (N + 3) / 4 : (long)N * K / 4;
+  const long c4 = (long)(bias_blk ? blockIdx.x - nb_main : blockIdx.x) * 64 + cl;
+  const float* base = bias_blk ? bslabs : slabs;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c4 < ncol4) {
+    if (bias_blk && (N & 3)) {  // scalar tail-safe bias path (N % 4 != 0)
+      for (int q = 0; q < 4; ++q) {
+        const long n = c4 * 4 + q;
+        if (n >= N) break;
+        float t = 0.f;
+        for (int sp = sl; sp < splits; sp += 4) t += base[(long)sp * stride + n];
+        (&acc.x)[q] = t;
+      }
+    } else {
+#pragma unroll 4
+      for (int sp = sl; sp < splits; sp += 4) {
+        const float4 v = reinterpret_cast<const float4*>(base + (long)sp * stride)[c4];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+  }
+  red[sl][cl] = acc;
+  __syncthreads();
+  if (sl != 0 || c4 >= ncol4) return;
+  const float4 a = red[0][cl], b = red[1][cl], c = red[2][cl], d = red[3][cl];
+  const float4 t = make_float4((a.x + b.x) + (c.x + d.x), (a.y + b.y) + (c.y + d.y), (a.z + b.z) + (c.z + d.z),
+                               (a.w + b.w) + (c.w + d.w));
+  if (bias_blk) {
+    for (int q = 0; q < 4; ++q)
+      if (c4 * 4 + q < N) db[c4 * 4 + q] = (&t.x)[q];
+    return;
+  }
+  const long e = c4 * 4;
+  const long n = e / K;
+  const int k = (int)(e - n * K);
+  const int tap = k / Cin, cin = k - tap * Cin;  // the 4 k share a tap (Cin % 4 == 0)
+  if (ks == 1) {  // scalar stores: dW may be an arena slot without 16-B alignment
+    float* dst = dW + n * Cin + cin;
+    dst[0] = t.x;
+    dst[1] = t.y;
+    dst[2] = t.z;
+    dst[3] = t.w;
+  } else {
+    float* dst = dW + (n * Cin + cin) * ks + tap;
+    dst[0] = t.x;
+    dst[ks] = t.y;
+    dst[2 * ks] = t.z;
+    dst[3 * ks] = t.w;
   }
 }
 
@@ -2650,15 +2788,36 @@ SSAMD_API int ssamd_conv_gemm_ln(const bf16_t* X, const bf16_t* W, const float* 
   return conv_gemm_impl(X, W, bias, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, rinfo, ex, s);
 }
 
+static int g_wgrad_imm = -1;  // -1 auto, 0 / 1: force the big64 wgrad read schedule
+SSAMD_API void ssamd_wgrad_set_imm(int v) { g_wgrad_imm = v; }
+static int g_wgrad_reduce_old = 0;  // 1: the pre-split-parallel reduction kernels (A/B measurement)
+SSAMD_API void ssamd_wgrad_set_reduce(int old) { g_wgrad_reduce_old = old; }
+
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.
 // ws: splits*N*ks*Cin (+ splits*N when db != null) floats.  db (optional): fused bias gradient.
 static void launch_reduce(const float* ws, float* dW, const float* bws, float* db, int splits, int N, int Cin, int ks,
                           int blocks, hipStream_t s) {
   const int K = Cin * ks;
-  if (ks > 1 && (size_t)K * 4 <= 65536)  // transposed through LDS: contiguous dW rows
-    hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(N), dim3(256), (size_t)K * 4, s, ws, dW, bws, db, splits, N, Cin, ks);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+  (void)blocks;
+  if (g_wgrad_reduce_old) {
+    if (ks > 1 && (size_t)K * 4 <= 65536)  // transposed through LDS: contiguous dW rows
+      hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(N), dim3(256), (size_t)K * 4, s, ws, dW, bws, db, splits, N, Cin,
+                         ks);
+    else
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
+    return;
+  }
+  // many output rows of a k > 1 conv: one block per row keeps the dW stores contiguous; otherwise
+  // (Linear / k = 1 weights, few rows) the split-parallel kernel keeps every CU busy
+  if (ks > 1 && N >= 256 && (size_t)K * 4 <= 65536) {
+    hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(N), dim3(256), (size_t)K * 4, s, ws, dW, bws, db, splits, N, Cin,
+                       ks);
+    return;
+  }
+  const int nb_main = (int)cdiv((long)N * K / 4, 64L);
+  const int nb_bias = bws ? (int)cdiv((long)(N + 3) / 4, 64L) : 0;
+  hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3(nb_main + nb_bias), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin,
+                     ks, nb_main);
 }
 
 static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64), 0: 128x128, 1: 256x128 ring, 2: 256x256 BK=32 ring
@@ -2691,8 +2850,10 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   if (big && g_wgrad_variant != 2) {
     static bool b64_set = false;
     if (!b64_set) {
-      allow_lds(conv_wgrad_big64_kernel<false>, 160 * 1024);
-      allow_lds(conv_wgrad_big64_kernel<true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<false, false>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true, false>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<false, true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true, true>, 160 * 1024);
       b64_set = true;
     }
     const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
@@ -2706,9 +2867,13 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     rows_per_split = (rows_per_split + 63) / 64 * 64;
     splits = (g.M + rows_per_split - 1) / rows_per_split;
     float* bws = db ? ws + (long)splits * slab : nullptr;
-    size_t lds = 2 * WB64_STAGE + (packed ? (size_t)(nseq + 1) * 4 : 0);
+    size_t lds = 2 * WB64_STAGE;
     if (lds < 128 * 1088) lds = 128 * 1088;  // the LDS-staged slab epilogue tile
-    auto wb = packed ? conv_wgrad_big64_kernel<true> : conv_wgrad_big64_kernel<false>;
+    // immediate-offset fragment reads: measured faster on packed rows (the decoder FFN), the
+    // single-wait schedule on plain rows (tools/exp_packed_wgrad.py); g_wgrad_imm overrides
+    const bool imm = g_wgrad_imm < 0 ? packed : g_wgrad_imm != 0;
+    auto wb = packed ? (imm ? conv_wgrad_big64_kernel<true, true> : conv_wgrad_big64_kernel<true, false>)
+                     : (imm ? conv_wgrad_big64_kernel<false, true> : conv_wgrad_big64_kernel<false, false>);
     hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);
     launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);

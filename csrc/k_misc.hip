@@ -911,19 +911,26 @@ __global__ void __launch_bounds__(256) unpack_rows_kernel(const T* __restrict__ 
   }
 }
 
+// block = 64 columns x 4 row lanes over a 256-row chunk: coalesced 64-column row pieces, 64 rows
+// per thread, lanes combined in LDS in a fixed order
 template <typename T>
 __global__ void __launch_bounds__(256) pad_colsum_kernel(const T* __restrict__ dout, const int64_t* __restrict__ lens,
                                                          int M, int C, long rows, int rows_per_blk,
                                                          float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
-  for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
-    float s = 0.f;
-    for (long row = r0; row < r1; ++row) {
+  float s = 0.f;
+  if (c < C) {
+    for (long row = r0 + rl; row < r1; row += 4) {
       const int b = (int)(row / M), t = (int)(row - (long)b * M);
       if (t >= lens[b]) s += ld_as_f<T>(dout + row * C + c);
     }
-    part[(long)blockIdx.y * C + c] = s;
   }
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) part[(long)blockIdx.y * C + c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 }  // namespace
 
@@ -966,7 +973,7 @@ SSAMD_API int ssamd_pad_colsum(const void* dout, int f32, const int64_t* lens, i
   if (rows == 0) return (int)hipMemsetAsync(dfill, 0, C * sizeof(float), s);
   const int chunks = cdiv(rows, 256);
   if (ws_floats < ssamd_pad_colsum_ws(B, M, C)) return -3;
-  dim3 grid(cdiv(C, 256), chunks);
+  dim3 grid(cdiv(C, 64), chunks);
   if (f32)
     hipLaunchKernelGGL(pad_colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)dout, lens, M, C, rows, 256, ws);
   else

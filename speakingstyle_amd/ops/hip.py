@@ -40,6 +40,8 @@ _SIGS = {
     "ssamd_wgrad_set_variant": [I],
     "ssamd_attn_set_nf": [I, I],
     "ssamd_attn_set_nf32": [I, I],
+    "ssamd_wgrad_set_reduce": [I],
+    "ssamd_wgrad_set_imm": [I],
     "ssamd_attn_set_fwd": [I, I],
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],
@@ -186,14 +188,14 @@ def _refresh_all(device):
             del _wcache[k]
             _wtable["n"] = -1
         elif w.device == device and _eligible(w):
-            live.append((e, w))
+            live.append((e, w, owner))  # strong ref: the owner cannot die before its image is stamped
     if _wtable.get("n") != len(live) or _wtable.get("dev") != device:
         import numpy as np
         desc = np.zeros(len(live), dtype=[("src", "<u8"), ("dst", "<u8"), ("cout", "<i4"), ("cin", "<i4"),
                                           ("ks", "<i4"), ("mode", "<i4")])
         cum = np.zeros(len(live) + 1, dtype=np.int64)
         tiles = []
-        for i, (e, w) in enumerate(live):
+        for i, (e, w, _) in enumerate(live):
             ks = w.shape[2] if w.dim() == 3 else 1
             desc[i] = (w.data_ptr(), e[3].data_ptr(), w.shape[0], w.shape[1], ks, e[4])
             cum[i + 1] = cum[i] + w.numel()
@@ -214,8 +216,7 @@ def _refresh_all(device):
             rc = lib().ssamd_weight_prep(_ptr(_wtable["desc"]), _ptr(_wtable["cum"]), _wtable["n"], _wtable["total"],
                                          _stream())
         _check(rc, "ssamd_weight_prep")
-    for e, w in live:
-        owner = e[2]()
+    for e, w, owner in live:
         e[0], e[1] = owner._version, _wgen
 
 
