@@ -45,6 +45,23 @@ static __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
                         ^ (uint32_t)(seed >> 32));
   return (h >> 8) * (1.0f / 16777216.0f);
 }
+// Keep-scales of the N consecutive elements idx0 .. idx0+N-1, bit-identical to N drop_scale calls:
+// the seed half of the hash depends only on idx >> 32, which a chunk starting at a multiple of N
+// (N | 2^32) shares, so it is computed once per chunk; the uniform test is an integer compare
+// (u = (h >> 8) / 2^24 >= p  <=>  (h >> 8) >= ceil(p * 2^24), exact in fp32).
+template <int N>
+static __device__ __forceinline__ void drop_scales(uint64_t seed, uint64_t idx0, float p, float* ks) {
+  if (p <= 0.f) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) ks[i] = 1.f;
+    return;
+  }
+  const float keep = 1.f / (1.f - p);
+  const uint32_t S = hash_u32((uint32_t)seed ^ (uint32_t)(idx0 >> 32) * 0x9E3779B9U) ^ (uint32_t)(seed >> 32);
+  const uint32_t thr = (uint32_t)ceilf(p * 16777216.0f);
+#pragma unroll
+  for (int i = 0; i < N; ++i) ks[i] = (hash_u32(((uint32_t)idx0 + (uint32_t)i) ^ S) >> 8) >= thr ? keep : 0.f;
+}
 // keep-scale for element idx: 0 (dropped) or 1/(1-p)
 static __device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, float p) {
   if (p <= 0.f) return 1.f;

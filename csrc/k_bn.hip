@@ -140,11 +140,13 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
   for (long r = (long)blockIdx.x * m.rows_iter + ro; r < R; r += (long)gridDim.x * m.rows_iter) {
     float v[8];
     load8(h + r * C + c0, v);
+    float ks[8];
+    drop_scales<8>(seed, (uint64_t)(r * C + c0), p, ks);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float z = v[i] * sc[i] + sh[i];
       z = act_fwd(act_tanh, z);
-      v[i] = z * drop_scale(seed, (uint64_t)(r * C + c0 + i), p);
+      v[i] = z * ks[i];
     }
     if constexpr (OUT_F32) {
       float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + r * C + c0);
@@ -195,9 +197,11 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restric
       float hv[8], g[8];
       load8(h + off, hv);
       load_dy<DY_F32>(dy, off, g);
+      float ks[8];
+      drop_scales<8>(seed, (uint64_t)off, p, ks);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
+        float dz = g[i] * ks[i];
         if (act_tanh) dz *= act_grad(act_tanh, hv[i] * sc[i] + sh[i]);
         a[i] += dz;
         b[i] += dz * (hv[i] - mu[i]) * rs[i];
@@ -270,9 +274,11 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
     load8(h + off, hv);
     load_dy<DY_F32>(dy, off, g);
     short8 o;
+    float ks[8];
+    drop_scales<8>(seed, (uint64_t)off, p, ks);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float dz = g[i] * drop_scale(seed, (uint64_t)(off + i), p);
+      float dz = g[i] * ks[i];
       if (act_tanh) dz *= act_grad(act_tanh, hv[i] * sc[i] + sh[i]);
       o[i] = (short)f2bf(k1[i] * dz + k2[i] * hv[i] + k3[i]);
     }

@@ -1110,11 +1110,12 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
           const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
           const long ro = (long)m * 256 + n;
           *reinterpret_cast<short8*>(Y + ro) = v;  // a (the pre-LN GEMM output: the backward reads it)
-          float hv[8], sum = 0.f;
+          float hv[8], sum = 0.f, k1[8], k2[8];
+          drop_scales<8>(ex.seed, (uint64_t)ro, ex.pre_p, k1);
+          drop_scales<8>(ex.seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)ro, ex.post_p, k2);
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            hv[q] = bf2f((bf16_t)v[q]);
-            if (ex.pre_p > 0.f) hv[q] *= drop_scale(ex.seed, (uint64_t)ro + q, ex.pre_p);
+            hv[q] = bf2f((bf16_t)v[q]) * k1[q];
             hv[q] += bf2f((bf16_t)rr[it][q]);
             sum += hv[q];
           }
@@ -1131,7 +1132,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             float y = (hv[q] - mu) * rs * lw[q] + lb[q];
-            if (ex.post_p > 0.f) y *= drop_scale(ex.seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)ro + q, ex.post_p);
+            y *= k2[q];
             y = G[q] * y + Bt[q];
             o8[q] = (short)f2bf(rv[it] ? y : 0.f);
           }

@@ -92,8 +92,10 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
     float h[EPL];
     load_row<EPL>(a + row * C + c0, h);
     if (pre_p > 0.f) {
+      float ks[EPL];
+      drop_scales<EPL>(seed, (uint64_t)row * C + c0, pre_p, ks);
 #pragma unroll
-      for (int i = 0; i < EPL; ++i) h[i] *= drop_scale(seed, (uint64_t)row * C + c0 + i, pre_p);
+      for (int i = 0; i < EPL; ++i) h[i] *= ks[i];
     }
     if (res) {
       float rv[EPL];
@@ -112,12 +114,13 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
       q += d * d;
     }
     const float rs = rsqrtf(wave_sum(q) * invC + eps);
-    float y[EPL];
+    float y[EPL], k2[EPL];
     const bool valid = t < len;
+    drop_scales<EPL>(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0, post_p, k2);
 #pragma unroll
     for (int i = 0; i < EPL; ++i) {
       float v = (h[i] - mu) * rs * wv[i] + bv[i];
-      if (post_p > 0.f) v *= drop_scale(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0 + i, post_p);
+      v *= k2[i];
       v = G[i] * v + Bt[i];
       y[i] = valid ? v : 0.f;
     }
@@ -181,11 +184,9 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     }
     float h[EPL], m1[EPL];
     load_row<EPL>(a + row * C + c0, h);
+    drop_scales<EPL>(seed, (uint64_t)row * C + c0, pre_p, m1);
 #pragma unroll
-    for (int i = 0; i < EPL; ++i) {
-      m1[i] = drop_scale(seed, (uint64_t)row * C + c0 + i, pre_p);
-      h[i] *= m1[i];
-    }
+    for (int i = 0; i < EPL; ++i) h[i] *= m1[i];
     if (res) {
       float rv[EPL];
       load_row<EPL>(res + row * C + c0, rv);
@@ -195,12 +196,13 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     float go[EPL];
     load_row<EPL>(dout + row * C + c0, go);
     const float mu = mean_in[row], rs = rstd_in[row];
-    float xh[EPL], dx[EPL];
+    float xh[EPL], dx[EPL], m2v[EPL];
     float sum1 = 0.f, sum2 = 0.f;
+    drop_scales<EPL>(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0, post_p, m2v);
 #pragma unroll
     for (int i = 0; i < EPL; ++i) {
       xh[i] = (h[i] - mu) * rs;
-      const float m2 = drop_scale(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0 + i, post_p);
+      const float m2 = m2v[i];
       const float y = xh[i] * wv[i] + bv[i];
       acc_s1[i] += go[i] * y * m2;
       acc_s2[i] += go[i];

@@ -24,7 +24,8 @@ import torch
 from . import gradslots
 from . import reference as ref
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libssamd_kernels.so")
+_LIB_PATH = os.environ.get("SSAMD_KERNEL_LIB") or os.path.join(  # override: A/B runs of another build
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libssamd_kernels.so")
 _lib = None
 _lock = threading.Lock()
 
