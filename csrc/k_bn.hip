@@ -20,7 +20,7 @@ constexpr int NT = 256;
 __device__ __forceinline__ float fast_tanh(float z) {
   // 1 - 2/(exp(2z)+1): one exp + one rcp; saturates correctly for |z| large
   const float e = __expf(2.f * z);
-  return 1.f - 2.f / (e + 1.f);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);  // v_rcp_f32: no IEEE division sequence
 }
 
 // act: 0 none, 1 tanh (PostNet), 2 ReLU (GST Conv2d stack)
@@ -66,6 +66,7 @@ __global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const long r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
   if (active) {
+#pragma unroll 4
     for (long r = r0 + ro; r < r1; r += m.rows_iter) {
       float v[8];
       load8(h + r * C + c8 * 8, v);
@@ -137,6 +138,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
   float sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { sc[i] = scale[c0 + i]; sh[i] = shift[c0 + i]; }
+#pragma unroll 2
   for (long r = (long)blockIdx.x * m.rows_iter + ro; r < R; r += (long)gridDim.x * m.rows_iter) {
     float v[8];
     load8(h + r * C + c0, v);
@@ -192,6 +194,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restric
     for (int i = 0; i < 8; ++i) {
       sc[i] = scale[c8 * 8 + i]; sh[i] = shift[c8 * 8 + i]; mu[i] = mean[c8 * 8 + i]; rs[i] = rstd[c8 * 8 + i];
     }
+#pragma unroll 2
     for (long r = r0 + ro; r < r1; r += m.rows_iter) {
       const long off = r * C + c8 * 8;
       float hv[8], g[8];
@@ -268,6 +271,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
       k3[i] = 0.f;
     }
   }
+#pragma unroll 2
   for (long r = (long)blockIdx.x * m.rows_iter + ro; r < R; r += (long)gridDim.x * m.rows_iter) {
     const long off = r * C + c0;
     float hv[8], g[8];
