@@ -53,16 +53,26 @@ __device__ __forceinline__ void store_row(bf16_t* p, const float* v) {
   }
 }
 
-template <int EPL>
+// LPR = lanes per row: 64 (one wave per row), or 32 for C = 256 (two rows per wave, 16-B accesses)
+template <int EPL, int LPR>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int EPL, int LPR>
 __global__ void __launch_bounds__(256) addln_fwd_kernel(
     const bf16_t* __restrict__ a, const bf16_t* __restrict__ res, const float* __restrict__ w,
     const float* __restrict__ bias, const float* __restrict__ fg, const float* __restrict__ fb,
     const float* __restrict__ s_g, const float* __restrict__ s_b, const int64_t* __restrict__ lens,
     const int64_t* __restrict__ cu, bf16_t* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out, int L, int C,
     float pre_p, float post_p, uint64_t seed, float eps) {
+  constexpr int RPW = 64 / LPR;  // rows a wave covers per iteration
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int c0 = lane * EPL;
+  const int sub = lane / LPR, rl = lane % LPR;
+  const int c0 = rl * EPL;
   const int len = lens ? (int)lens[b] : L;
   // packed variable-length rows (cu = row offsets): sequence b owns rows cu[b] .. cu[b]+len-1
   const long rowb = cu ? (long)cu[b] : (long)b * L;
@@ -85,9 +95,9 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
     }
   }
   const float invC = 1.f / C;
-  for (int r = 0; r < ROWS_PER_WAVE; ++r) {
-    const int t = blockIdx.x * ROWS_PER_BLOCK + r * WAVES + wave;
-    if (t >= Lb) break;
+  for (int r = 0; r < ROWS_PER_WAVE / RPW; ++r) {
+    const int t = blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub;
+    if (t >= Lb) continue;  // per-half guard (the row reductions stay inside a half)
     const long row = rowb + t;
     float h[EPL];
     load_row<EPL>(a + row * C + c0, h);
@@ -106,14 +116,14 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < EPL; ++i) s += h[i];
-    const float mu = wave_sum(s) * invC;
+    const float mu = row_sum<EPL, LPR>(s) * invC;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < EPL; ++i) {
       const float d = h[i] - mu;
       q += d * d;
     }
-    const float rs = rsqrtf(wave_sum(q) * invC + eps);
+    const float rs = rsqrtf(row_sum<EPL, LPR>(q) * invC + eps);
     float y[EPL], k2[EPL];
     const bool valid = t < len;
     drop_scales<EPL>(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0, post_p, k2);
@@ -125,7 +135,7 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
       y[i] = valid ? v : 0.f;
     }
     store_row<EPL>(out + row * C + c0, y);
-    if (lane == 0 && mean_out) {
+    if (rl == 0 && mean_out) {
       mean_out[row] = mu;
       rstd_out[row] = rs;
     }
@@ -138,7 +148,7 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
 //   part[blk][2C..3C) S1[b]     part[blk][3C..4C) S2[b]       (FiLM: S1 = sum_t dout*yd, S2 = sum_t dout)
 // (blk = b * gridDim.x + blockIdx.x) and the host finishes them with fixed-order column sums
 // (k_reduce.hip) -- no float atomics.
-template <int EPL>
+template <int EPL, int LPR>
 __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ a, const bf16_t* __restrict__ res,
     const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ fg,
@@ -146,10 +156,12 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ da_out,
     float* __restrict__ part, int film, int L, int C, float pre_p, float post_p, uint64_t seed) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES][C]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES * RPW][C]
+  constexpr int RPW = 64 / LPR;
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int c0 = lane * EPL;
+  const int sub = lane / LPR, rl = lane % LPR;
+  const int c0 = rl * EPL;
   const int len = lens ? (int)lens[b] : L;
   const long rowb = cu ? (long)cu[b] : (long)b * L;
   const int Lb = cu ? len : L;
@@ -170,9 +182,9 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     acc_w[i] = acc_b[i] = acc_s1[i] = acc_s2[i] = 0.f;
   }
   const float invC = 1.f / C;
-  for (int r = 0; r < ROWS_PER_WAVE; ++r) {
-    const int t = blockIdx.x * ROWS_PER_BLOCK + r * WAVES + wave;
-    if (t >= Lb) break;
+  for (int r = 0; r < ROWS_PER_WAVE / RPW; ++r) {
+    const int t = blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub;
+    if (t >= Lb) continue;
     const long row = rowb + t;
     float dh[EPL];
     if (t >= len) {  // masked row: zero gradient flows back
@@ -213,8 +225,8 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
       sum1 += dx[i];
       sum2 += dx[i] * xh[i];
     }
-    sum1 = wave_sum(sum1) * invC;
-    sum2 = wave_sum(sum2) * invC;
+    sum1 = row_sum<EPL, LPR>(sum1) * invC;
+    sum2 = row_sum<EPL, LPR>(sum2) * invC;
 #pragma unroll
     for (int i = 0; i < EPL; ++i) dh[i] = rs * (dx[i] - sum1 - xh[i] * sum2);
     store_row<EPL>(dh_out + row * C + c0, dh);
@@ -231,21 +243,26 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     if (k >= nk) break;
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < EPL; ++i) red[wave * C + c0 + i] = accs[k][i];
+    for (int i = 0; i < EPL; ++i) red[(wave * RPW + sub) * C + c0 + i] = accs[k][i];
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += 256)
-      pb[k * C + c] = (red[c] + red[C + c]) + (red[2 * C + c] + red[3 * C + c]);
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES * RPW; ++w) t += red[w * C + c];  // fixed order
+      pb[k * C + c] = t;
+    }
   }
 }
 
 }  // namespace
 
-#define DISPATCH_EPL(C, ...)                                   \
-  switch ((C) / 64) {                                          \
-    case 4: { constexpr int EPL = 4; __VA_ARGS__; break; }     \
-    case 8: { constexpr int EPL = 8; __VA_ARGS__; break; }     \
-    case 16: { constexpr int EPL = 16; __VA_ARGS__; break; }   \
-    default: return -1;                                        \
+// C = 256: half a wave per row with 8 channels (16 B) per lane; wider rows: one wave per row
+#define DISPATCH_EPL(C, ...)                                                       \
+  switch ((C) / 64) {                                                              \
+    case 4: { constexpr int EPL = 8, LPR = 32; __VA_ARGS__; break; }               \
+    case 8: { constexpr int EPL = 8, LPR = 64; __VA_ARGS__; break; }               \
+    case 16: { constexpr int EPL = 16, LPR = 64; __VA_ARGS__; break; }             \
+    default: return -1;                                                            \
   }
 
 SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w, const float* bias, const float* fg,
@@ -256,7 +273,7 @@ SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w
   if (C % 256 != 0 && C != 256 && C != 512 && C != 1024) return -1;
   if (B == 0 || L == 0) return 0;
   dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
-  DISPATCH_EPL(C, hipLaunchKernelGGL(addln_fwd_kernel<EPL>, grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
+  DISPATCH_EPL(C, hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR>), grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
                                      s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
   return (int)hipGetLastError();
 }
@@ -279,8 +296,8 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
   const int nk = film ? 4 : 2;
   if (ws_floats < ssamd_addln_bwd_ws(B, L, C, film)) return -3;
   dim3 grid(gx, B);
-  size_t lds = (size_t)WAVES * C * sizeof(float);
-  DISPATCH_EPL(C, hipLaunchKernelGGL(addln_bwd_kernel<EPL>, grid, dim3(256), lds, stream, dout, a, res, w, bias, fg,
+  size_t lds = (size_t)WAVES * 2 * C * sizeof(float);  // [WAVES * rows per wave][C]
+  DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR>), grid, dim3(256), lds, stream, dout, a, res, w, bias, fg,
                                      s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
                                      (uint64_t)seed));
   int rc = (int)hipGetLastError();
