@@ -61,7 +61,9 @@ class Encoder(nn.Module):
     def forward(self, texts, src_lens, style=None, compute_dtype=torch.float32):
         T = texts.shape[1]
         pe = positional_rows(self.position_enc, T, self.d_model, texts.device).to(compute_dtype)
-        x = ops.embed_add_pe(texts, self.src_word_emb.weight.to(compute_dtype), pe)
+        # the fp32 table itself: the HIP op reads its cached bf16 image and writes the gradient slot
+        tab = self.src_word_emb.weight if ops.use_hip(texts) else self.src_word_emb.weight.to(compute_dtype)
+        x = ops.embed_add_pe(texts, tab, pe)
         for layer in self.layer_stack:
             x = layer(x, src_lens, style)
         return x
@@ -193,7 +195,7 @@ class VarianceAdaptor(nn.Module):
         else:
             pred = _apply_control(pred, control)
             values = pred
-        x = ops.bucketize_embed_add(x, values, bins, table.weight.to(x.dtype))
+        x = ops.bucketize_embed_add(x, values, bins, table.weight if ops.use_hip(x) else table.weight.to(x.dtype))
         return pred, x
 
     def packable(self):

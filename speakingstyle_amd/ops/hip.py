@@ -828,7 +828,10 @@ class _EmbedFn(torch.autograd.Function):
         out_shape = (*((ids if mode == 0 else vals).shape), C)
         out = torch.empty(out_shape, device=table.device, dtype=torch.bfloat16)
         idx = torch.empty(rows, device=table.device, dtype=torch.int32)
-        tb = table.to(torch.bfloat16).contiguous()
+        # fp32 parameter: its cached bf16 image (refreshed with every other weight image after the
+        # optimizer step), and the gradient goes straight into the parameter's arena slot
+        tb = weight_fwd(table) if (isinstance(table, torch.nn.Parameter) and _eligible(table)) \
+            else table.to(torch.bfloat16).contiguous()
         ad = addend.to(torch.bfloat16).contiguous()
         rc = lib().ssamd_embed_fwd(mode, _ptr(ids), _ptr(vals), _ptr(bins), 0 if bins is None else bins.numel(),
                                    _ptr(tb), _ptr(ad), L, _ptr(out), _ptr(idx), rows, C, _stream())

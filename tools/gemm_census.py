@@ -25,6 +25,28 @@ FWD_VARIANTS = (-1, 0, 1, 2, 4, 5)
 WGRAD_VARIANTS = (-1, 0, 1, 2)
 
 
+_FLUSH = None
+
+
+def timeit_cold(fn, iters):
+    """Mean time of fn with the L2 / Infinity Cache flushed before every call (a 1 GiB write),
+    events around fn only: what a GEMM costs inside the step, where its operands come from HBM."""
+    global _FLUSH
+    if _FLUSH is None:
+        _FLUSH = torch.empty(256 << 20, device="cuda", dtype=torch.float32)
+    fn()
+    tot = 0.0
+    for _ in range(iters):
+        _FLUSH.zero_()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        tot += s.elapsed_time(e)
+    return tot / iters * 1000.0
+
+
 def timeit(fn, iters):
     for _ in range(2):
         fn()
@@ -132,6 +154,8 @@ def replay(k, n, iters):
     ts = {v: rec[f"v{v}_us"] for v in variants if rec.get(f"v{v}_us")}
     best = min(ts, key=ts.get)
     rec["auto_TF"] = round(flops / ts[-1] / 1e6, 1)
+    rec["cold_us"] = round(timeit_cold(fn, iters), 1)
+    rec["cold_TF"] = round(flops / rec["cold_us"] / 1e6, 1)
     rec["best"] = best
     rec["best_TF"] = round(flops / ts[best] / 1e6, 1)
     return rec
@@ -147,14 +171,16 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
     calls = record_step(args)
-    tot_auto = tot_best = 0.0
+    tot_auto = tot_best = tot_cold = 0.0
     for k, n in calls.items():
         rec = replay(k, n, args.iters)
         tot_auto += n * rec["v-1_us"]
         tot_best += n * rec[f"v{rec['best']}_us"]
+        tot_cold += n * rec["cold_us"]
         print(json.dumps(rec), flush=True)
     print(json.dumps({"summary": args.config, "distinct": len(calls), "calls": sum(calls.values()),
-                      "gemm_us_auto": round(tot_auto, 1), "gemm_us_best_variant": round(tot_best, 1)}), flush=True)
+                      "gemm_us_auto": round(tot_auto, 1), "gemm_us_best_variant": round(tot_best, 1),
+                      "gemm_us_cold": round(tot_cold, 1)}), flush=True)
 
 
 if __name__ == "__main__":
