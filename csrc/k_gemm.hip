@@ -81,6 +81,11 @@ struct EpiX {
   int Lseq, Mseq;
   float pre_p, post_p, eps;
   unsigned long long seed;
+  // ReLU bitmask (big64 LDS-staged epilogue, N % 8 == 0): mask_out[m][n/8] bit q = (y[m][n+q] > 0)
+  // written by a ReLU GEMM; mask_in multiplies the output by the stored bits instead of reading a
+  // bf16 aux operand (16x fewer bytes for the FFN hidden layer's dgrad)
+  unsigned char* mask_out;
+  const unsigned char* mask_in;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -1144,7 +1149,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         }
         return;
       }
-      const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f;
+      const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_in;
       for (int e = tid; e < BG * 32; e += NT3) {
         const int r = e >> 5, c = e & 31;
         const int m = m0 + r, n = n0 + c * 8;
@@ -1156,6 +1161,12 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
           valid = tt < (int)lens[bb];
         }
         const long off = (long)m * ldy + n;
+        if (ex.mask_out) {  // ReLU output > 0  <=>  its bf16 bits are a positive non-zero value
+          unsigned bits = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) bits |= (unsigned)((short)v[q] > 0) << q;
+          ex.mask_out[(long)m * (g.N >> 3) + (n >> 3)] = (unsigned char)bits;
+        }
         if (aux || resid || !valid || xon) {
           float f[8];
 #pragma unroll
@@ -1164,6 +1175,11 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             const short8 a = *reinterpret_cast<const short8*>(aux + off);
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)a[q]) > 0.f ? f[q] : 0.f;
+          }
+          if (ex.mask_in) {
+            const unsigned bits = ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = (bits >> q) & 1u ? f[q] : 0.f;
           }
           if (resid) {
             const short8 rr = *reinterpret_cast<const short8*>(resid + off);
@@ -2594,6 +2610,11 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   // N = 256 shape (k9 dgrad 219 -> 141 us), while N >= 768 keeps the 256x256 tile.
   if (g_gemm_variant < 0 && N >= 256 && N <= 256 && ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG) <= 64)
     variant = (Cin % BK == 0) ? 2 : 1;
+  if (ex.mask_out || ex.mask_in) {  // the bitmask lives in the big64 LDS-staged epilogue only
+    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act < 0 || ex.ln_out) return -3;
+    if (ex.mask_out && act != ACT_RELU) return -3;
+    variant = 4;
+  }
   const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f;
   if (xon) {  // only the big64 (LDS-staged bf16 epilogue) and ring kernels implement EpiX
     if (out_f32 || !reg || (N % 8) || (ldy % 8) || act < 0) return -3;
@@ -2763,6 +2784,18 @@ SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* 
   ex.scale = scale;
   ex.post_act = post_act;
   return conv_gemm_impl(X, W, bias, nullptr, resid, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, nullptr, ex, s);
+}
+
+// conv_gemm with a ReLU bitmask: mask_out (act must be ReLU) stores bit (y > 0) per output element,
+// mask_in zeroes the outputs whose bit is clear (the dgrad of a ReLU layer).  [M][N/8] bytes.
+SSAMD_API int ssamd_conv_gemm_mask(const bf16_t* X, const bf16_t* W, const float* bias, void* Y, int B, int L,
+                                   int Cin, int ks, int dil, int pad, int N, int act, const int* rinfo,
+                                   unsigned char* mask_out, const unsigned char* mask_in, hipStream_t s) {
+  EpiX ex{};
+  ex.scale = 1.f;
+  ex.mask_out = mask_out;
+  ex.mask_in = mask_in;
+  return conv_gemm_impl(X, W, bias, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, rinfo, ex, s);
 }
 
 // conv_gemm (N = 256, bf16 out a) + the fused residual/LayerNorm/dropout/FiLM/mask tail (EpiX.ln_*).

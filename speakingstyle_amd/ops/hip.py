@@ -304,6 +304,30 @@ def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, re
     return y
 
 
+_NO_RELU_MASK = os.environ.get("SSAMD_RELU_MASK", "1") == "0"  # A/B: the bf16 aux operand instead
+_SIGS["ssamd_conv_gemm_mask"] = [P, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P]
+
+
+def conv_gemm_mask_raw(x, wimg, bias, B, L, Cin, ks, pad, N, act, rinfo=None, mask_out=None, mask_in=None):
+    """conv_gemm with the ReLU bitmask epilogue (``ssamd_conv_gemm_mask``): ``mask_out`` (uint8
+    [B*L, N/8], act = ReLU) receives bit (y > 0) per element; ``mask_in`` zeroes the elements whose
+    bit is clear (the data gradient through that ReLU)."""
+    _need(x, torch.bfloat16, "conv_mask.x")
+    _need(wimg, torch.bfloat16, "conv_mask.w")
+    assert x.numel() == B * L * Cin and wimg.numel() == N * ks * Cin, "conv_mask: shape"
+    for m in (mask_out, mask_in):
+        if m is not None:
+            _need(m, torch.uint8, "conv_mask.mask")
+            assert m.numel() == B * L * N // 8, "conv_mask: mask shape"
+    if bias is not None:
+        _need(bias, torch.float32, "conv_mask.bias")
+    y = torch.empty(B, L, N, device=x.device, dtype=torch.bfloat16)
+    rc = lib().ssamd_conv_gemm_mask(_ptr(x), _ptr(wimg), _ptr(bias), _ptr(y), B, L, Cin, ks, 1, pad, N, act,
+                                    _rinfo_ptr(rinfo, B * L), _ptr(mask_out), _ptr(mask_in), _stream())
+    _check(rc, "ssamd_conv_gemm_mask")
+    return y
+
+
 class LNSpec:
     """A residual + LayerNorm (+ dropout, FiLM, row mask) tail that the producing GEMM runs in its
     epilogue (``ssamd_conv_gemm_ln``; d_model = 256: one 256x256 tile owns whole rows).  Built by
@@ -589,26 +613,38 @@ class _FFNFn(torch.autograd.Function):
         r1 = rinfo if k1 > 1 else None
         r2 = rinfo if k2 > 1 else None
         ctx.cu = (cu if k1 > 1 else None, cu if k2 > 1 else None)
-        h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1, rinfo=r1)
+        mask = None
+        if H >= 256 and H % 8 == 0 and not _NO_RELU_MASK and has("ssamd_conv_gemm_mask"):
+            # ReLU bitmask of h for the second conv's data gradient (M x H/8 bytes instead of h itself)
+            mask = torch.empty(B * L, H // 8, device=x.device, dtype=torch.uint8)
+            h = conv_gemm_mask_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, (k1 - 1) // 2, H, 1,
+                                   rinfo=r1, mask_out=mask)
+        else:
+            h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1,
+                              rinfo=r1)
         if ln is not None and C == 256:
             z = conv_gemm_ln_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, ln, rinfo=r2)
         else:
             z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0, rinfo=r2)
         ctx.rinfo = (r1, r2)
-        ctx.save_for_backward(xc, h, w1, w2)
+        ctx.save_for_backward(xc, h, w1, w2, mask)
         ctx.biases = (b1, b2)
         ctx.dims = (B, L, C, H, k1, k2)
         return z
 
     @staticmethod
     def backward(ctx, dz):
-        xc, h, w1, w2 = ctx.saved_tensors
+        xc, h, w1, w2, mask = ctx.saved_tensors
         B, L, C, H, k1, k2 = ctx.dims
         dz = dz.to(torch.bfloat16).contiguous()
         p1, p2 = (k1 - 1) // 2, (k2 - 1) // 2
         b1, b2 = ctx.biases
         r1, r2 = ctx.rinfo
-        dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
+        if mask is not None:
+            dh = conv_gemm_mask_raw(dz, weight_dgrad(w2), None, B, L, C, k2, (k2 - 1) - p2, H, 0, rinfo=r2,
+                                    mask_in=mask)
+        else:
+            dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
         dw2, db2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=gradslots.claim(w2),
                                   db=gradslots.claim(b2), rinfo=r2, cu=ctx.cu[1])
         dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1,

@@ -1017,3 +1017,23 @@ def test_attention_d32_nf_variants(nf, packed):
     o_ref.backward(g.float())
     assert _rel(o.float() * mask, o_ref * mask) < 2e-2
     assert _rel(gq.float() * mask, qr.grad * mask) < 2e-2
+
+
+def test_relu_bitmask_epilogue_gpu():
+    """ReLU GEMM writes bit (y > 0) per element; the dgrad GEMM with mask_in equals the bf16-aux path."""
+    torch.manual_seed(33)
+    B, L, C, H, ks = 3, 301, 256, 1024, 9
+    x = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(H, ks, C, device=DEV) / (ks * C) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(H, device=DEV) * 0.1
+    mask = torch.empty(B * L, H // 8, device=DEV, dtype=torch.uint8)
+    h = hip.conv_gemm_mask_raw(x, w, b, B, L, C, ks, 4, H, 1, mask_out=mask)
+    h_ref = hip.conv_gemm_raw(x, w, b, B, L, C, ks, 1, 4, H, 1)
+    assert torch.equal(h, h_ref)
+    bits = ((mask.view(B * L, H // 8, 1).int() >> torch.arange(8, device=DEV)) & 1).view(B, L, H).bool()
+    assert torch.equal(bits, h > 0)
+    dz = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
+    w2 = (torch.randn(H, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16)  # dgrad image [H][1][C]
+    d_mask = hip.conv_gemm_mask_raw(dz, w2, None, B, L, C, 1, 0, H, 0, mask_in=mask)
+    d_aux = hip.conv_gemm_raw(dz, w2, None, B, L, C, 1, 1, 0, H, 0, aux=h)
+    assert torch.equal(d_mask, d_aux)
