@@ -996,14 +996,23 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (g.K + 63) / 64;
+  // split-K (gridDim.y > 1): block y owns the k slabs [kt0, kt1) and writes its fp32 partial
+  // tile to slice y of the workspace (Yv), reduced afterwards in a fixed order (splitk_reduce)
+  const int nk_all = (g.K + 63) / 64;
+  int kt0 = 0, nk = nk_all;
+  if (gridDim.y > 1) {
+    const int per = (nk_all + gridDim.y - 1) / gridDim.y;
+    kt0 = blockIdx.y * per;
+    nk = min(nk_all, kt0 + per);
+    Yv = reinterpret_cast<float*>(Yv) + (long)blockIdx.y * g.M * ldy;
+  }
   // double buffer: stage kt+1 is DMA'd while stage kt is computed (one stage = 1024 MFMA cycles
   // per wave, far longer than an L2-warm LDS-DMA), one barrier per 64-wide k slab
-  stage(0, 0);
+  if (kt0 < nk) stage(kt0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
+  for (int kt = kt0; kt < nk; ++kt) {
+    const int buf = (kt - kt0) & 1;
     if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
     const char* As = smem + buf * STG64_BYTES;
     const char* Bs = As + BG * 64 * 2;
@@ -2448,6 +2457,63 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// Split-K finish: out[m][n] = epilogue( sum_s P[s][m][n] ) in a fixed slice order, with the
+// epi_store4 semantics (bias, activation, ReLU-aux mask, residual, row validity).  8 columns per
+// thread (two float4 per slice).
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ P, int S, long M, int N,
+                                                            const float* __restrict__ bias,
+                                                            const bf16_t* __restrict__ aux,
+                                                            const bf16_t* __restrict__ resid,
+                                                            const int64_t* __restrict__ lens, int L, int act,
+                                                            int out_f32, void* __restrict__ Y) {
+  const int n8 = N >> 3;
+  const long e = blockIdx.x * 256L + threadIdx.x;
+  if (e >= M * n8) return;
+  const long m = e / n8;
+  const int n = (int)(e - m * n8) * 8;
+  const long off = m * N + n;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int sl = 0; sl < S; ++sl) {
+    const float4* p = reinterpret_cast<const float4*>(P + (long)sl * M * N + off);
+    const float4 a = p[0], b = p[1];
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (bias) v[q] += bias[n + q];
+    if (act == ACT_RELU) v[q] = fmaxf(v[q], 0.f);
+    else if (act == ACT_LRELU) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+    else if (act == ACT_TANH) v[q] = tanhf(v[q]);
+  }
+  if (aux) {
+    const short8 x = *reinterpret_cast<const short8*>(aux + off);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
+  }
+  if (resid) {
+    const short8 x = *reinterpret_cast<const short8*>(resid + off);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += bf2f((bf16_t)x[q]);
+  }
+  if (lens) {
+    const long b = m / L;
+    if (m - b * L >= lens[b]) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = 0.f;
+    }
+  }
+  if (out_f32) {
+    float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(Y) + off);
+    o[0] = make_float4(v[0], v[1], v[2], v[3]);
+    o[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    short8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (short)f2bf(v[q]);
+    *reinterpret_cast<short8*>(reinterpret_cast<bf16_t*>(Y) + off) = o;
+  }
+}
+
 // Split-parallel slab reduction: block = 64 float4 columns x 4 split lanes; lane l sums the slabs
 // l, l+4, ... (4 independent float4 loads in flight per thread, every block of the grid busy even
 // for a single 256x256 weight), the 4 lane sums are combined in LDS in a fixed order -> the same
@@ -2567,6 +2633,11 @@ static int g_debug_nostore = 0;
 SSAMD_API void ssamd_gemm_debug_nostore(int v) { g_debug_nostore = v; }
 static int g_num_cus = 256;  // persistent grid size (MI355X: 256 CUs); set from the device at first use
 static int g_gemm_variant = -1;  // -1 auto, 0: register staging, 1: LDS-DMA 128x128, 2: LDS-DMA 3-stage ring 256x128
+static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 split-K + reduce)
+static int g_num_cus_gemm = 256;
+static void* g_splitk_ws = nullptr;
+static size_t g_splitk_bytes = 0;
+SSAMD_API void ssamd_gemm_set_splitk(int v) { g_splitk = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
 SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
@@ -2610,6 +2681,48 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   // N = 256 shape (k9 dgrad 219 -> 141 us), while N >= 768 keeps the 256x256 tile.
   if (g_gemm_variant < 0 && N >= 256 && N <= 256 && ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG) <= 64)
     variant = (Cin % BK == 0) ? 2 : 1;
+  // Split-K for few 256x256 tiles with a long K (encoder-sized M, k = 9 data gradients, K = 9216):
+  // S slices of the k range as extra blocks writing fp32 partials, one fixed-order reduce kernel
+  // applies the epilogue.  Measured (tools/exp_splitk.py) on the tile-poor shapes only.
+  {
+    const int tiles = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
+    const int nk64 = (g.K + 63) / 64;
+    const bool plain = !(ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.ln_out || ex.mask_out || ex.mask_in);
+    int S = 0;
+    if (g_splitk > 0) S = g_splitk;
+    else if (g_splitk < 0 && g_gemm_variant < 0 && tiles <= 128 && nk64 >= 16)
+      // as many slices as keep the split grid within ONE wave of blocks (a second partial wave
+      // costs more than it saves: M = 10800 / 43 tiles: S = 4 81 us, S = 6 111 us, unsplit 149 us)
+      S = min(min(8, g_num_cus_gemm / tiles), nk64 / 6);
+    if (S > 1 && plain && reg && N >= 256 && (N % 8) == 0 && ldy == N && act >= 0 && (ldy % 8) == 0) {
+      const size_t need = (size_t)S * g.M * N * sizeof(float);
+      if (need > g_splitk_bytes) {
+        if (g_splitk_ws) (void)hipFree(g_splitk_ws);
+        g_splitk_ws = nullptr;
+        g_splitk_bytes = 0;
+        if (hipMalloc(&g_splitk_ws, need) != hipSuccess) return -4;
+        g_splitk_bytes = need;
+      }
+      static bool sk_set = false;
+      if (!sk_set) {
+        allow_lds(conv_gemm_big64_kernel<true, true, false>, B64_LDS);
+        allow_lds(conv_gemm_big64_kernel<true, false, false>, B64_LDS);
+        allow_lds(conv_gemm_big64_kernel<true, true, true>, B64_LDS);
+        allow_lds(conv_gemm_big64_kernel<true, false, true>, B64_LDS);
+        sk_set = true;
+      }
+      const bool fastk = (Cin % 64) == 0;
+      auto kfn = g.rinfo ? (fastk ? conv_gemm_big64_kernel<true, true, true> : conv_gemm_big64_kernel<true, false, true>)
+                         : (fastk ? conv_gemm_big64_kernel<true, true, false> : conv_gemm_big64_kernel<true, false, false>);
+      hipLaunchKernelGGL(kfn, dim3(tiles, S), dim3(NT3), B64_LDS, s, X, W, nullptr, nullptr, nullptr, nullptr,
+                         g_splitk_ws, g, 0, N, EpiX{});
+      const long nthr = (long)g.M * (N / 8);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(nthr, 256)), dim3(256), 0, s,
+                         reinterpret_cast<const float*>(g_splitk_ws), S, (long)g.M, N, bias, aux, resid, lens, g.L,
+                         act, out_f32, Y);
+      return (int)hipGetLastError();
+    }
+  }
   if (ex.mask_out || ex.mask_in) {  // the bitmask lives in the big64 LDS-staged epilogue only
     if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act < 0 || ex.ln_out) return -3;
     if (ex.mask_out && act != ACT_RELU) return -3;

@@ -43,6 +43,7 @@ _SIGS = {
     "ssamd_attn_set_nf32": [I, I],
     "ssamd_wgrad_set_reduce": [I],
     "ssamd_wgrad_set_imm": [I],
+    "ssamd_gemm_set_splitk": [I],
     "ssamd_attn_set_fwd": [I, I],
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],

@@ -1037,3 +1037,36 @@ def test_relu_bitmask_epilogue_gpu():
     d_mask = hip.conv_gemm_mask_raw(dz, w2, None, B, L, C, 1, 0, H, 0, mask_in=mask)
     d_aux = hip.conv_gemm_raw(dz, w2, None, B, L, C, 1, 1, 0, H, 0, aux=h)
     assert torch.equal(d_mask, d_aux)
+
+
+@pytest.mark.parametrize("act,use_bias,use_res,packed", [(0, False, True, False), (1, True, False, False),
+                                                         (0, True, True, True)])
+def test_splitk_gemm_vs_reference(act, use_bias, use_res, packed):
+    """Split-K (few 256x256 tiles, long K) vs fp32 torch conv: bias / ReLU / residual epilogue in the
+    fixed-order reduce, packed rows included; forced S = 3 and the auto choice."""
+    from speakingstyle_amd.ops.packing import PackInfo
+
+    torch.manual_seed(34)
+    L, Cin, ks, N = 4000, 512, 9, 256
+    x = torch.randn(1, L, Cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, ks, Cin, device=DEV) / (ks * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV) if use_bias else None
+    r = torch.randn(1, L, N, device=DEV).to(torch.bfloat16) if use_res else None
+    ri, xs = None, [x.float()]
+    if packed:
+        lens = torch.tensor([1500, 2500], device=DEV)
+        ri = PackInfo.build(lens, 2500, L).rinfo
+        xs = [x[:, :1500].float(), x[:, 1500:].float()]
+    ys = [F.conv1d(t.transpose(1, 2), w.float().permute(0, 2, 1), b, padding=4).transpose(1, 2) for t in xs]
+    y_ref = torch.cat(ys, 1)
+    if act == 1:
+        y_ref = torch.relu(y_ref)
+    if r is not None:
+        y_ref = y_ref + r.float()
+    for S in (3, -1):
+        hip.lib().ssamd_gemm_set_splitk(S)
+        try:
+            y = hip.conv_gemm_raw(x, w, b, 1, L, Cin, ks, 1, 4, N, act, resid=r, rinfo=ri)
+        finally:
+            hip.lib().ssamd_gemm_set_splitk(-1)
+        assert _rel(y, y_ref) < 1e-2, S
