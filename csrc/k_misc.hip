@@ -983,3 +983,56 @@ SSAMD_API int ssamd_pad_colsum(const void* dout, int f32, const int64_t* lens, i
   if (rc) return rc;
   return ssamd_seg_colsum(ws, C, 1, chunks, C, dfill, 0, 0, C, nullptr, ws + (long)chunks * C, seg_colsum_ws(1, C), s);
 }
+
+// ----------------------------------------------------------------------------
+// FiLM parameter gradients of one LayerNorm site (reference model/blocks.py:43-62):
+//   d gamma = S1 * s_g,  d beta = S2 * s_b            (bf16 or fp32 [n])
+//   d s_g = sum(S1 * gamma),  d s_b = sum(S2 * beta)   (scalars, fixed-order block reduction)
+// S1 / S2 = per-(b, c) sums from the LayerNorm backward.  One block; written, not accumulated.
+// ----------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) film_grads_kernel(const float* __restrict__ S1, const float* __restrict__ S2,
+                                                         const float* __restrict__ g, const float* __restrict__ bt,
+                                                         const float* __restrict__ sg, const float* __restrict__ sb,
+                                                         int n, int out_f32, void* __restrict__ dg,
+                                                         void* __restrict__ dbt, float* __restrict__ dsg,
+                                                         float* __restrict__ dsb) {
+  __shared__ float red[2][256];
+  const float a = *sg, c = *sb;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float x1 = S1[i], x2 = S2[i];
+    if (out_f32) {
+      reinterpret_cast<float*>(dg)[i] = x1 * a;
+      reinterpret_cast<float*>(dbt)[i] = x2 * c;
+    } else {
+      reinterpret_cast<bf16_t*>(dg)[i] = f2bf(x1 * a);
+      reinterpret_cast<bf16_t*>(dbt)[i] = f2bf(x2 * c);
+    }
+    s1 += x1 * g[i];
+    s2 += x2 * bt[i];
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    dsg[0] = red[0][0];
+    dsb[0] = red[1][0];
+  }
+}
+}  // namespace
+
+SSAMD_API int ssamd_film_grads(const float* S1, const float* S2, const float* g, const float* bt, const float* sg,
+                               const float* sb, int n, int out_f32, void* dg, void* dbt, float* dsg, float* dsb,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(film_grads_kernel, dim3(1), dim3(256), 0, s, S1, S2, g, bt, sg, sb, n, out_f32, dg, dbt, dsg,
+                     dsb);
+  return (int)hipGetLastError();
+}

@@ -44,6 +44,7 @@ _SIGS = {
     "ssamd_wgrad_set_reduce": [I],
     "ssamd_wgrad_set_imm": [I],
     "ssamd_gemm_set_splitk": [I],
+    "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P],
     "ssamd_attn_set_fwd": [I, I],
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],
@@ -678,14 +679,33 @@ def get_seed() -> int:
     return _seed_counter[0]
 
 
+_F32_MEMO = {}
+
+
+def _f32_view(t):
+    """fp32 contiguous copy of a (small) FiLM vector, shared by every LayerNorm site that uses
+    the same tensor in this step (the 11 FiLM sites of a styled model read ONE gamma / beta)."""
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t.detach()
+    key = (t.data_ptr(), t._version, tuple(t.shape), t.dtype)
+    hit = _F32_MEMO.get(key)
+    if hit is not None and hit[0]() is t:
+        return hit[1]
+    if len(_F32_MEMO) > 64:
+        _F32_MEMO.clear()
+    v = t.detach().float().contiguous()
+    _F32_MEMO[key] = (weakref.ref(t), v)
+    return v
+
+
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox, fused=None):
         B, L, C = a.shape if geom is None else geom  # packed: (sequences, longest, C) over [1, R, C] rows
         ac = a.contiguous()
         rc_ = None if res is None else res.contiguous()
-        gf = None if g is None else g.detach().float().contiguous()
-        bf = None if bt is None else bt.detach().float().contiguous()
+        gf = None if g is None else _f32_view(g)
+        bf = None if bt is None else _f32_view(bt)
         if fused is not None:  # the producing GEMM already ran this LayerNorm in its epilogue
             out, mean, rstd = fused.out, fused.mean, fused.rstd
             gf, bf = fused.g, fused.bt
@@ -699,6 +719,7 @@ class _AddLNFn(torch.autograd.Function):
             _check(rc, "ssamd_addln_fwd")
         ctx.cu = cu
         ctx.mailbox = mailbox
+        ctx.film_scales = (sg, sb)  # the Parameters themselves: gradient-slot owners
         ctx.save_for_backward(ac, rc_, w, b, gf, bf, sg, sb, lens, mean, rstd)
         ctx.cfg = (B, L, C, pre_p, post_p, seed, res is not None, g is not None)
         ctx.gdtype = None if g is None else (g.dtype, bt.dtype)
@@ -730,11 +751,25 @@ class _AddLNFn(torch.autograd.Function):
             ctx.mailbox.put(d_res)
             d_res = None
         dg = dbt = dsg = dsb = None
-        if has_film:
+        if has_film and not has("ssamd_film_grads"):  # older kernel library (A/B runs)
             dg = (S1 * sg).to(ctx.gdtype[0])
             dbt = (S2 * sb).to(ctx.gdtype[1])
             dsg = (S1 * gf).sum().reshape(1)
             dsb = (S2 * bf).sum().reshape(1)
+        elif has_film:  # one kernel: d gamma, d beta and the two scale gradients (into their slots)
+            f32 = ctx.gdtype[0] == torch.float32
+            dg = torch.empty(S1.shape, device=S1.device, dtype=torch.float32 if f32 else torch.bfloat16)
+            dbt = torch.empty_like(dg)
+            dsg = gradslots.claim(ctx.film_scales[0])
+            dsb = gradslots.claim(ctx.film_scales[1])
+            if dsg is None:
+                dsg = torch.empty(1, device=S1.device, dtype=torch.float32)
+            if dsb is None:
+                dsb = torch.empty(1, device=S1.device, dtype=torch.float32)
+            rc = lib().ssamd_film_grads(_ptr(S1), _ptr(S2), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb), S1.numel(),
+                                        int(f32), _ptr(dg), _ptr(dbt), _ptr(dsg), _ptr(dsb), _stream())
+            _check(rc, "ssamd_film_grads")
+            dg, dbt = dg.to(ctx.gdtype[0]), dbt.to(ctx.gdtype[1])
         return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None, None
 
 

@@ -1028,7 +1028,11 @@ def test_relu_bitmask_epilogue_gpu():
     b = torch.randn(H, device=DEV) * 0.1
     mask = torch.empty(B * L, H // 8, device=DEV, dtype=torch.uint8)
     h = hip.conv_gemm_mask_raw(x, w, b, B, L, C, ks, 4, H, 1, mask_out=mask)
-    h_ref = hip.conv_gemm_raw(x, w, b, B, L, C, ks, 1, 4, H, 1)
+    hip.lib().ssamd_gemm_set_splitk(0)  # same (unsplit) kernel: bitwise comparable
+    try:
+        h_ref = hip.conv_gemm_raw(x, w, b, B, L, C, ks, 1, 4, H, 1)
+    finally:
+        hip.lib().ssamd_gemm_set_splitk(-1)
     assert torch.equal(h, h_ref)
     bits = ((mask.view(B * L, H // 8, 1).int() >> torch.arange(8, device=DEV)) & 1).view(B, L, H).bool()
     assert torch.equal(bits, h > 0)
