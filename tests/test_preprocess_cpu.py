@@ -94,6 +94,8 @@ def test_prepare_and_preprocess(corpus):
 
 def test_dataset_and_real_data_step(corpus):
     root, pf, p = corpus
+    if not (root / "pre" / "train.txt").exists():  # run alone / on another xdist worker than the preprocess test
+        test_prepare_and_preprocess(corpus)
     from speakingstyle_amd.config import load_configs, load_named
     from speakingstyle_amd.data.dataset import Dataset, to_device
     from speakingstyle_amd.models.fastspeech2 import FastSpeech2
