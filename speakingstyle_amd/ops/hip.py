@@ -44,6 +44,8 @@ _SIGS = {
     "ssamd_wgrad_set_reduce": [I],
     "ssamd_wgrad_set_imm": [I],
     "ssamd_gemm_set_splitk": [I],
+    "ssamd_gemm_set_prio": [I],
+    "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P],
     "ssamd_attn_set_fwd": [I, I],
     "ssamd_attn_set_kv_dma": [I],
