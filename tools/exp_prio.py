@@ -37,7 +37,7 @@ def main():
             for p in (0, 1, 0, 1):
                 setp(p)
                 t[p].append(timeit(fn, 10))
-            setp(0 if name == "fwd" else 1)
+            setp(-1 if name == "fwd" else 1)
             res[f"{name}_us"] = round(min(t[0]), 1)
             res[f"{name}_prio_us"] = round(min(t[1]), 1)
         print(json.dumps({"Cin": Cin, "ks": ks, "N": N, "packed": packed, **res}), flush=True)
