@@ -7,7 +7,7 @@ in-tree location the Python bindings load; the .so is git-ignored but travels
 to the GPU box with the repository snapshot).  ``csrc/host_*.cpp`` form the
 native host-runtime library ``libssamd_host.so`` (g++, no GPU code).
 
-Usage: python csrc/build.py [--jobs N] [--debug] [--clean]
+Usage: python csrc/build.py [--jobs N] [--debug] [--clean] [--sanitize]
 """
 import argparse
 import concurrent.futures as cf
@@ -68,14 +68,41 @@ def build(jobs=8, debug=False, clean=False, verbose=False):
     return KLIB
 
 
+# Host-only sanitizer builds (GPU sanitizers are not available on the target pool).
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+def build_sanitized(verbose=False):
+    """Build the host runtime + its self-test (csrc/selftest_host_collate.cpp) under
+    ASan+UBSan and under TSan into build/sanitize/; returns {name: executable}."""
+    out_dir = os.path.join(ROOT, "build", "sanitize")
+    os.makedirs(out_dir, exist_ok=True)
+    hsrcs = sorted(glob.glob(os.path.join(HERE, "host_*.cpp")))
+    test = os.path.join(HERE, "selftest_host_collate.cpp")
+    exes = {}
+    for name, flags in SANITIZERS.items():
+        exe = os.path.join(out_dir, f"selftest_host_{name}")
+        if _stale(exe, hsrcs + [test]):
+            _run(["g++", "-O1", "-g", "-std=c++17", "-pthread"] + flags + ["-o", exe, test] + hsrcs)
+        exes[name] = exe
+    if verbose:
+        print("built", " ".join(exes.values()))
+    return exes
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--sanitize", action="store_true",
+                    help="also build the host runtime self-test under ASan+UBSan and TSan (build/sanitize/)")
     a = ap.parse_args()
     try:
         build(a.jobs, a.debug, a.clean, verbose=True)
+        if a.sanitize:
+            build_sanitized(verbose=True)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

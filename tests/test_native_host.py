@@ -39,6 +39,27 @@ def test_pad_rows_too_long_raises():
         native.pad_rows([np.zeros((5, 3), np.float32)], max_rows=4)
 
 
+@pytest.mark.parametrize("san", ["asan", "tsan"])
+def test_host_runtime_under_sanitizers(san):
+    """csrc/host_collate.cpp under ASan+UBSan / TSan (host-only sanitizers; the GPU
+    sanitizers are unavailable on the target pool): the self-test must run clean."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not available")
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "csrc"))
+    import build
+
+    exe = build.build_sanitized()[san]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0", TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "selftest_host_collate ok" in r.stdout
+
+
 def test_tools_pad_uses_native():
     arrs = [np.arange(n, dtype=np.int64) + 1 for n in (3, 7, 1)]
     np.testing.assert_array_equal(tools.pad_1d(arrs), _np_pad(arrs))
