@@ -117,7 +117,7 @@ _PREPROCESS_DEFAULTS: Config = {
         "audio": {"sampling_rate": 22050, "max_wav_value": 32768.0},
         "stft": {"filter_length": 1024, "hop_length": 256, "win_length": 1024},
         "mel": {"n_mel_channels": 80, "mel_fmin": 0, "mel_fmax": 8000},
-        "pitch": {"feature": "phoneme_level", "normalization": True},
+        "pitch": {"feature": "phoneme_level", "normalization": True, "extractor": "dio"},
         "energy": {"feature": "phoneme_level", "normalization": True},
         "speaker_embedder": "none",
     },
@@ -150,6 +150,7 @@ def normalize_preprocess_config(cfg: Config | None) -> Config:
     out = _merge(_PREPROCESS_DEFAULTS, cfg)
     pp = out["preprocessing"]
     _check_enum(pp["pitch"]["feature"], ["phoneme_level", "frame_level"], "preprocessing.pitch.feature")
+    _check_enum(pp["pitch"].get("extractor", "dio"), ["dio", "yin"], "preprocessing.pitch.extractor")
     _check_enum(pp["energy"]["feature"], ["phoneme_level", "frame_level"], "preprocessing.energy.feature")
     return out
 

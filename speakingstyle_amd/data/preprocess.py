@@ -8,10 +8,12 @@ mel + energy (TacotronSTFT), optional phoneme-level averaging, outlier-robust
 z-normalisation, ``stats.json`` / ``speakers.json`` / ``train.txt`` / ``val.txt``.
 Output layout is the reference's.
 
-Offline-image substitutions: TextGrids are parsed here (no ``tgt``), F0 uses a
-vectorised YIN (cumulative-mean-normalised difference) tracker instead of
-pyworld's dio+stonemask -- same frame grid (hop) and 0 = unvoiced convention;
-parity with pyworld is unpinned (the library is not installable here).
+Offline-image substitutions: TextGrids are parsed here (no ``tgt``); F0 is
+pyworld's algorithm pair DIO + StoneMask re-implemented in the native host
+runtime (``csrc/host_f0.cpp``, ``utils/native.dio/stonemask``), same frame period
+(hop / sr) and 0 = unvoiced convention; numerical parity with pyworld itself is
+unpinned (the library is not installable here).  ``preprocessing.pitch.extractor:
+yin`` selects the vectorised YIN tracker below instead.
 Utterances are processed by a multiprocessing pool (the reference uses
 joblib+dask, ``preprocessor/bc_2013.py:62-73``).
 """
@@ -133,6 +135,21 @@ def yin_f0(wav: np.ndarray, sr: int, hop: int, fmin: float = 71.0, fmax: float =
     return (f0 * energy_gate).astype(np.float64)
 
 
+def extract_f0(wav: np.ndarray, sr: int, hop: int, method: str = "dio") -> np.ndarray:
+    """Frame F0 (Hz, 0 = unvoiced) on the hop grid.  ``dio``: DIO + StoneMask exactly as
+    the reference calls pyworld (``preprocessor/preprocessor.py:182-187``: float64 wav,
+    frame_period = hop / sr * 1000 ms, default floor/ceil 71/800 Hz)."""
+    if method == "dio":
+        from ..utils import native
+
+        x = wav.astype(np.float64)
+        f0, t = native.dio(x, sr, frame_period=hop / sr * 1000)
+        return native.stonemask(x, f0, t, sr)
+    if method == "yin":
+        return yin_f0(wav, sr, hop)
+    raise ValueError(f"unknown pitch extractor {method!r} (dio | yin)")
+
+
 def interpolate_unvoiced(pitch: np.ndarray) -> np.ndarray:
     nz = np.nonzero(pitch)[0]
     if len(nz) == 0:
@@ -195,6 +212,7 @@ class Preprocessor:
         self.energy_phoneme = pp["energy"]["feature"] == "phoneme_level"
         self.pitch_norm = pp["pitch"]["normalization"]
         self.energy_norm = pp["energy"]["normalization"]
+        self.f0_method = pp["pitch"].get("extractor", "dio")
         self.stft = TacotronSTFT(pp["stft"]["filter_length"], self.hop_length, pp["stft"]["win_length"],
                                  pp["mel"]["n_mel_channels"], self.sampling_rate, pp["mel"]["mel_fmin"],
                                  pp["mel"]["mel_fmax"])
@@ -212,7 +230,7 @@ class Preprocessor:
         wav = wav[int(self.sampling_rate * start): int(self.sampling_rate * end)].astype(np.float32)
         with open(lab_path, encoding="utf-8") as f:
             raw_text = f.readline().strip("\n")
-        pitch = yin_f0(wav, self.sampling_rate, self.hop_length)
+        pitch = extract_f0(wav, self.sampling_rate, self.hop_length, self.f0_method)
         mel, energy = get_mel_from_wav(np.clip(wav, -1, 1), self.stft)
         T = sum(duration)
         pitch, mel, energy = pitch[:T], mel[:, :T], energy[:T]
