@@ -40,7 +40,21 @@ struct ConvGeom {
   const int64_t* cu;
   int nseq;
   int prio;  // 1: the second half of an 8-wave block runs at s_setprio 1 (experiment knob)
+  // 256x256 tile order: ngrp > 1 splits the N tiles into ngrp groups, group-major, so that each
+  // XCD's contiguous range of remapped ids covers nN / ngrp N tiles of more M tiles (its B slice
+  // stays L2-resident instead of the whole weight image streaming through every XCD's L2)
+  int ngrp;
 };
+
+// (tm, tn) of remapped block id T (bijective over nM * nN; ngrp must divide nN)
+__device__ __forceinline__ int2 tile_of(int T, int nM, int nN, int ngrp) {
+  if (ngrp > 1) {
+    const int per = nN / ngrp, gs = nM * per;
+    const int grp = T / gs, r = T - grp * gs;
+    return make_int2(r / per, grp * per + r % per);
+  }
+  return make_int2(T / nN, T % nN);
+}
 
 // (position, bound) of row m for the conv zero-padding test
 __device__ __forceinline__ int2 row_pos(const ConvGeom& g, int m) {
@@ -762,8 +776,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BG - 1) / BG;
   const int nM = (g.M + BG - 1) / BG;
-  const int wg = xcd_remap(blockIdx.x, nN * nM);
-  const int tn = wg % nN, tm = wg / nN;
+  const int2 tmn = tile_of(xcd_remap(blockIdx.x, nN * nM), nM, nN, g.ngrp);
+  const int tm = tmn.x, tn = tmn.y;
   const int m0 = tm * BG, n0 = tn * BG;
   // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -911,8 +925,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BG - 1) / BG;
   const int nM = (g.M + BG - 1) / BG;
-  const int wg = xcd_remap(blockIdx.x, nN * nM);
-  const int tn = wg % nN, tm = wg / nN;
+  const int2 tmn = tile_of(xcd_remap(blockIdx.x, nN * nM), nM, nN, g.ngrp);
+  const int tm = tmn.x, tn = tmn.y;
   const int m0 = tm * BG, n0 = tn * BG;
   // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2642,6 +2656,8 @@ static int g_gemm_variant = -1;  // -1 auto, 0: register staging, 1: LDS-DMA 128
 // N >= 1024 convs only
 static int g_gemm_prio = -1, g_wgrad_prio = 1;  // forward -1: auto (on for wide k > 1 convs only)
 SSAMD_API void ssamd_gemm_set_prio(int v) { g_gemm_prio = v; }
+static int g_gemm_ngrp = 1;  // 256x256 tile order: N-tile groups (tile_of); experiment knob
+SSAMD_API void ssamd_gemm_set_ngrp(int v) { g_gemm_ngrp = v; }
 SSAMD_API void ssamd_wgrad_set_prio(int v) { g_wgrad_prio = v; }
 static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 split-K + reduce)
 static int g_num_cus_gemm = 256;
@@ -2660,6 +2676,8 @@ static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N
   g.cu = nullptr;
   g.nseq = 0;
   g.prio = g_gemm_prio < 0 ? (N >= 1024 && ks > 1) : g_gemm_prio;
+  const int nN = (N + 255) / 256;
+  g.ngrp = (g_gemm_ngrp > 1 && nN % g_gemm_ngrp == 0) ? g_gemm_ngrp : 1;
   return g;
 }
 

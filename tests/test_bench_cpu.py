@@ -75,3 +75,15 @@ def test_world_size_mismatch_is_an_error():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--synth-steps", "0"] + ARGS, cwd=ROOT,
                        env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True, timeout=600)
     assert r.returncode != 0 and "3 ranks were requested" in r.stderr
+
+
+def test_slurm_job_script_syntax():
+    """scripts/train_job.sh (the reference's scripts/train_job.sh counterpart): valid bash,
+    one torchrun rank per GPU, RCCL env set; a full 2-rank CPU run of it is in docs (slow)."""
+    import subprocess
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts", "train_job.sh")
+    subprocess.run(["bash", "-n", path], check=True)
+    text = open(path).read()
+    assert "torch.distributed.run" in text and "--nproc-per-node" in text
+    assert "HSA_ENABLE_IPC_MODE_LEGACY=0" in text and "#SBATCH --gres=gpu:8" in text
