@@ -368,6 +368,11 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
+// buffer-descriptor LDS-DMA (16 B per lane, lane-linear destination): an out-of-range voffset lands zeros
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, int voff, int soff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff,
+                                           0, 0);
+}
 
 template <bool OUT_F32>
 __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
@@ -914,7 +919,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
 constexpr int STG64_BYTES = 2 * BG * 64 * 2;  // 64 KiB
 constexpr int B64_LDS = 256 * 528;          // 2 stages (128 KiB) or the padded bf16 epilogue tile (132 KiB)
 
-template <bool OUT_F32, bool FASTK, bool PACKED>
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
@@ -965,11 +970,41 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     b_ok[i] = n < g.N;
     brow_ptr[i] = W + (long)(b_ok[i] ? n : 0) * g.K + achunk[i] * 8;  // same row -> same chunk swizzle
   }
+  // BUF (FASTK only): LDS-DMA through buffer descriptors -- A over X rows [-pad, M), B over the weight
+  // image -- with loop-invariant 32-bit per-lane offsets: the k slab's tap shift is one scalar added
+  // per A row (plus the validity select), the B slab offset a scalar soffset; out of range = zeros
+  constexpr int kOOB = (int)0x80000000;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X - (long)g.pad * g.Cin), 0, BUF ? (g.M + g.pad) * g.Cin * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, BUF ? g.N * g.K * 2 : 0,
+                                                                      0x00020000);
+  int avo[4], bvo[4];
+  if constexpr (BUF) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      avo[i] = a_ok[i] ? ((a_m[i] + g.pad) * g.Cin + achunk[i] * 8) * 2 : kOOB;
+      const int row = (i * 8 + wave) * 8 + (lane >> 3);
+      bvo[i] = b_ok[i] ? ((n0 + row) * g.K + achunk[i] * 8) * 2 : kOOB;
+    }
+  }
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * STG64_BYTES;
     char* Bs = As + BG * 64 * 2;
     const int k0 = kt * 64;
-    if constexpr (FASTK) {  // Cin % 64 == 0: the 64-wide k slab sits in one tap
+    if constexpr (BUF) {
+      const int tap = k0 / g.Cin;
+      const int cin0 = k0 - tap * g.Cin;
+      const int shift = tap * g.dil - g.pad;
+      const int aoff = (shift * g.Cin + cin0) * 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ts = a_t[i] + shift;
+        const bool ok = (unsigned)ts < (unsigned)a_lim[i];
+        buf_lds16(rA, ok ? avo[i] + aoff : kOOB, 0, As + (i * 8 + wave) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf_lds16(rB, bvo[i], k0 * 2, Bs + (i * 8 + wave) * 1024);
+    } else if constexpr (FASTK) {  // Cin % 64 == 0: the 64-wide k slab sits in one tap
       const int tap = k0 / g.Cin;
       const int cin0 = k0 - tap * g.Cin;
       const int shift = tap * g.dil - g.pad;
@@ -2015,7 +2050,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big_kernel(const bf16_t* __
 
 constexpr int WB64_STAGE = 2 * 64 * 512;  // 64 KiB: dY [64][256] + X [64][256]
 
-template <bool PACKED, bool IMM>
+template <bool PACKED, bool IMM, bool BUF>
 __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* __restrict__ X,
                                                                 const bf16_t* __restrict__ dY,
                                                                 float* __restrict__ slabs,
@@ -2071,19 +2106,71 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
     const int m = r_begin + row;
     if constexpr (!PACKED) t_cur[i] = m % g.L;
   }
+  // BUF: the rinfo rows through a descriptor bounded at r_end (past it: (0, 0) = every tap invalid),
+  // no exec-masked load blocks
+  const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)g.rinfo, 0, (BUF && PACKED) ? r_end * 8 : 0, 0x00020000);
   auto load_ri = [&](int r0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + drow[i];
-      ri_nxt[i] = m < r_end ? g.rinfo[m] : make_int2(0, 0);
+      if constexpr (BUF) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rR, m * 8, 0, 0);
+        ri_nxt[i] = make_int2((int)v[0], (int)v[1]);
+      } else {
+        ri_nxt[i] = m < r_end ? g.rinfo[m] : make_int2(0, 0);
+      }
     }
   };
   if constexpr (PACKED) load_ri(r_begin);
+  // BUF: LDS-DMA through buffer descriptors -- dY over the rows of this split (a row past r_end or a
+  // column past N is out of range and lands as zeros), X over rows [-pad, M) -- with loop-invariant
+  // 32-bit per-lane offsets plus one 32-bit add per row and step: no 64-bit address math, no
+  // exec-masked address blocks and no zero-chunk selects in the stage issue (out-of-range = zeros)
+  const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dY + (long)r_begin * g.N), 0, BUF ? (r_end - r_begin) * g.N * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X - (long)g.pad * g.Cin), 0, BUF ? (g.M + g.pad) * g.Cin * 2 : 0, 0x00020000);
+  int yvo[4], xvo[4];
+  constexpr int kOOB = (int)0x80000000;
+  const bool x_always = g.ks == 1 && g.pad == 0;  // Linear / k = 1: every X row of a valid dY row is valid
+  if constexpr (BUF) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      yvo[i] = yok[i] ? (drow[i] * g.N + (int)(ysrc[i] - dY)) * 2 : kOOB;
+      xvo[i] = xkok[i] ? ((drow[i] + xshift[i] + g.pad) * g.Cin + xcin[i]) * 2 : kOOB;
+    }
+  }
   // LDS: dY images of the two stages at 0 / 32 KiB, X images at 64 / 96 KiB, so that every
   // fragment read is a loop-invariant per-lane base + an immediate (stage, k-half, +4 rows)
   auto stage = [&](int r0, int buf) {
     char* Ys = smem + buf * 32768;
     char* Xs = smem + 65536 + buf * 32768;
+    if constexpr (BUF) {
+      const int dy_off = (r0 - r_begin) * g.N * 2, x_off = r0 * g.Cin * 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf_lds16(rY, yvo[i] + dy_off, 0, Ys + (i * 8 + wave) * 1024);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool ok = true;
+        if (!x_always) {
+          int ts, lim;
+          if constexpr (PACKED) {
+            ts = ri_nxt[i].x + xshift[i];
+            lim = ri_nxt[i].y;
+          } else {
+            ts = t_cur[i] + xshift[i];
+            lim = g.L;
+            int t = t_cur[i] + 64;
+            while (t >= g.L) t -= g.L;
+            t_cur[i] = t;
+          }
+          ok = (unsigned)ts < (unsigned)lim;
+        }
+        buf_lds16(rX, ok ? xvo[i] + x_off : kOOB, 0, Xs + (i * 8 + wave) * 1024);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + drow[i];
@@ -2668,6 +2755,13 @@ SSAMD_API void ssamd_gemm_set_splitk(int v) { g_splitk = v; }
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
 SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
 
+static int g_gemm_buf = 1;  // big64 (FASTK) LDS-DMA through buffer descriptors (0: flat global_load_lds)
+SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
+// every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
+static bool big64_buf_ok(const ConvGeom& g) {
+  return g_gemm_buf != 0 && (long)(g.M + g.pad) * g.Cin * 2 < (1L << 31) && (long)g.N * g.K * 2 + 512 < (1L << 31);
+}
+
 static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N) {
   ConvGeom g;
   g.B = B; g.L = L; g.Cin = Cin; g.ks = ks; g.dil = dil; g.pad = pad;
@@ -2738,11 +2832,16 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
         allow_lds(conv_gemm_big64_kernel<true, false, false>, B64_LDS);
         allow_lds(conv_gemm_big64_kernel<true, true, true>, B64_LDS);
         allow_lds(conv_gemm_big64_kernel<true, false, true>, B64_LDS);
+        allow_lds(conv_gemm_big64_kernel<true, true, false, true>, B64_LDS);
+        allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
         sk_set = true;
       }
       const bool fastk = (Cin % 64) == 0;
-      auto kfn = g.rinfo ? (fastk ? conv_gemm_big64_kernel<true, true, true> : conv_gemm_big64_kernel<true, false, true>)
-                         : (fastk ? conv_gemm_big64_kernel<true, true, false> : conv_gemm_big64_kernel<true, false, false>);
+      const bool bf = fastk && big64_buf_ok(g);
+      auto kfn = g.rinfo ? (bf ? conv_gemm_big64_kernel<true, true, true, true>
+                               : fastk ? conv_gemm_big64_kernel<true, true, true> : conv_gemm_big64_kernel<true, false, true>)
+                         : (bf ? conv_gemm_big64_kernel<true, true, false, true>
+                               : fastk ? conv_gemm_big64_kernel<true, true, false> : conv_gemm_big64_kernel<true, false, false>);
       hipLaunchKernelGGL(kfn, dim3(tiles, S), dim3(NT3), B64_LDS, s, X, W, nullptr, nullptr, nullptr, nullptr,
                          g_splitk_ws, g, 0, N, EpiX{});
       const long nthr = (long)g.M * (N / 8);
@@ -2841,6 +2940,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<true, false, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -2848,13 +2951,18 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     const size_t LB = B64_LDS;
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
-      auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true> : conv_gemm_big64_kernel<F32, FK, false>; \
+      auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
       hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
+    const bool bf = fastk && big64_buf_ok(g);
     if (out_f32) {
-      if (fastk) B64_LAUNCH(true, true); else B64_LAUNCH(true, false);
+      if (bf) { constexpr bool BF = true; B64_LAUNCH(true, true); }
+      else if (fastk) { constexpr bool BF = false; B64_LAUNCH(true, true); }
+      else { constexpr bool BF = false; B64_LAUNCH(true, false); }
     } else {
-      if (fastk) B64_LAUNCH(false, true); else B64_LAUNCH(false, false);
+      if (bf) { constexpr bool BF = true; B64_LAUNCH(false, true); }
+      else if (fastk) { constexpr bool BF = false; B64_LAUNCH(false, true); }
+      else { constexpr bool BF = false; B64_LAUNCH(false, false); }
     }
 #undef B64_LAUNCH
   } else if (reg && variant >= 2) {
@@ -2966,6 +3074,8 @@ SSAMD_API int ssamd_conv_gemm_ln(const bf16_t* X, const bf16_t* W, const float* 
 
 static int g_wgrad_imm = -1;  // -1 auto, 0 / 1: force the big64 wgrad read schedule
 SSAMD_API void ssamd_wgrad_set_imm(int v) { g_wgrad_imm = v; }
+static int g_wgrad_buf = 1;  // big64 wgrad LDS-DMA through buffer descriptors (0: flat global_load_lds)
+SSAMD_API void ssamd_wgrad_set_buf(int v) { g_wgrad_buf = v; }
 static int g_wgrad_reduce_old = 0;  // 1: the pre-split-parallel reduction kernels (A/B measurement)
 SSAMD_API void ssamd_wgrad_set_reduce(int old) { g_wgrad_reduce_old = old; }
 
@@ -3027,10 +3137,14 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
   if (big && g_wgrad_variant != 2) {
     static bool b64_set = false;
     if (!b64_set) {
-      allow_lds(conv_wgrad_big64_kernel<false, false>, 160 * 1024);
-      allow_lds(conv_wgrad_big64_kernel<true, false>, 160 * 1024);
-      allow_lds(conv_wgrad_big64_kernel<false, true>, 160 * 1024);
-      allow_lds(conv_wgrad_big64_kernel<true, true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<false, false, false>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true, false, false>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<false, true, false>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true, true, false>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<false, false, true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true, false, true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<false, true, true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true, true, true>, 160 * 1024);
       b64_set = true;
     }
     const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
@@ -3049,8 +3163,13 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     // immediate-offset fragment reads: measured faster on packed rows (the decoder FFN), the
     // single-wait schedule on plain rows (tools/exp_packed_wgrad.py); g_wgrad_imm overrides
     const bool imm = g_wgrad_imm < 0 ? packed : g_wgrad_imm != 0;
-    auto wb = packed ? (imm ? conv_wgrad_big64_kernel<true, true> : conv_wgrad_big64_kernel<true, false>)
-                     : (imm ? conv_wgrad_big64_kernel<false, true> : conv_wgrad_big64_kernel<false, false>);
+    // buffer-descriptor DMA needs every byte offset in 31 bits (out-of-range marker 0x80000000)
+    const bool bufok = g_wgrad_buf != 0 && (long)(g.M + pad) * Cin * 2 < (1L << 31) &&
+                       (long)rows_per_split * N * 2 < (1L << 31);
+    auto wb = bufok ? (packed ? (imm ? conv_wgrad_big64_kernel<true, true, true> : conv_wgrad_big64_kernel<true, false, true>)
+                              : (imm ? conv_wgrad_big64_kernel<false, true, true> : conv_wgrad_big64_kernel<false, false, true>))
+                    : (packed ? (imm ? conv_wgrad_big64_kernel<true, true, false> : conv_wgrad_big64_kernel<true, false, false>)
+                              : (imm ? conv_wgrad_big64_kernel<false, true, false> : conv_wgrad_big64_kernel<false, false, false>));
     hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);
     launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);

@@ -46,6 +46,8 @@ _SIGS = {
     "ssamd_gemm_set_splitk": [I],
     "ssamd_gemm_set_prio": [I],
     "ssamd_gemm_set_ngrp": [I],
+    "ssamd_wgrad_set_buf": [I],
+    "ssamd_gemm_set_buf": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P],
     "ssamd_attn_set_fwd": [I, I],
