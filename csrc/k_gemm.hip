@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
 constexpr int BM3 = 256, NT3 = 512, NSTAGE = 3;
 constexpr int STAGE_BYTES = (BM3 + BN) * BK * 2;  // 48 KiB
 
-template <bool OUT_F32, bool FASTK, bool PACKED>
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                 const float* __restrict__ bias,
                                                                 const bf16_t* __restrict__ aux,
@@ -566,11 +566,41 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
     b_ok[i] = n < g.N;
     brow_ptr[i] = W + (long)(b_ok[i] ? n : 0) * g.K + bch * 8;
   }
+  // BUF (FASTK only): LDS-DMA through buffer descriptors, as in conv_gemm_big64_kernel
+  constexpr int kOOB = (int)0x80000000;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X - (long)g.pad * g.Cin), 0, BUF ? (g.M + g.pad) * g.Cin * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, BUF ? g.N * g.K * 2 : 0,
+                                                                      0x00020000);
+  int avo[4], bvo[2];
+  if constexpr (BUF) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) avo[i] = a_ok[i] ? ((a_m[i] + g.pad) * g.Cin + achunk[i] * 8) * 2 : kOOB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (i * 8 + wave) * 8 + (lane >> 3);
+      const int bch = (lane & 7) ^ ((row >> 1) & 7);
+      bvo[i] = b_ok[i] ? ((n0 + row) * g.K + bch * 8) * 2 : kOOB;
+    }
+  }
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * STAGE_BYTES;
     char* Bs = As + BM3 * BK * 2;
     const int k0 = kt * BK;
-    if constexpr (FASTK) {
+    if constexpr (BUF) {
+      const int tap = k0 / g.Cin;
+      const int cin0 = k0 - tap * g.Cin;
+      const int shift = tap * g.dil - g.pad;
+      const int aoff = (shift * g.Cin + cin0) * 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ts = a_t[i] + shift;
+        const bool ok = (unsigned)ts < (unsigned)a_lim[i];
+        buf_lds16(rA, ok ? avo[i] + aoff : kOOB, 0, As + (i * 8 + wave) * 8 * 128);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) buf_lds16(rB, bvo[i], k0 * 2, Bs + (i * 8 + wave) * 8 * 128);
+    } else if constexpr (FASTK) {
       // Cin % 64 == 0: the whole 64-wide k slab sits in one tap -> wave-uniform shift / offset
       const int tap = k0 / g.Cin;
       const int cin0 = k0 - tap * g.Cin;
@@ -2976,6 +3006,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_ring_kernel<false, true, true>, NSTAGE * STAGE_BYTES);
       allow_lds(conv_gemm_ring_kernel<true, false, true>, NSTAGE * STAGE_BYTES);
       allow_lds(conv_gemm_ring_kernel<false, false, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<true, true, false, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, true, false, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<true, true, true, true>, NSTAGE * STAGE_BYTES);
+      allow_lds(conv_gemm_ring_kernel<false, true, true, true>, NSTAGE * STAGE_BYTES);
       ring_set = true;
     }
     const int nwg3 = ((g.M + BM3 - 1) / BM3) * ((N + BN - 1) / BN);
@@ -2983,13 +3017,18 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     const size_t L3 = NSTAGE * STAGE_BYTES;
 #define RING_LAUNCH(F32, FK)                                                                        \
     do {                                                                                            \
-      auto kfn = g.rinfo ? conv_gemm_ring_kernel<F32, FK, true> : conv_gemm_ring_kernel<F32, FK, false>; \
+      auto kfn = g.rinfo ? conv_gemm_ring_kernel<F32, FK, true, BF> : conv_gemm_ring_kernel<F32, FK, false, BF>; \
       hipLaunchKernelGGL(kfn, dim3(nwg3), dim3(NT3), L3, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
+    const bool bf = fastk && big64_buf_ok(g);
     if (out_f32) {
-      if (fastk) RING_LAUNCH(true, true); else RING_LAUNCH(true, false);
+      if (bf) { constexpr bool BF = true; RING_LAUNCH(true, true); }
+      else if (fastk) { constexpr bool BF = false; RING_LAUNCH(true, true); }
+      else { constexpr bool BF = false; RING_LAUNCH(true, false); }
     } else {
-      if (fastk) RING_LAUNCH(false, true); else RING_LAUNCH(false, false);
+      if (bf) { constexpr bool BF = true; RING_LAUNCH(false, true); }
+      else if (fastk) { constexpr bool BF = false; RING_LAUNCH(false, true); }
+      else { constexpr bool BF = false; RING_LAUNCH(false, false); }
     }
 #undef RING_LAUNCH
   } else if (reg && variant == 1) {

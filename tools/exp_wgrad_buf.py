@@ -81,7 +81,36 @@ def main_fwd():
               flush=True)
 
 
+def main_ring():
+    """256x128 ring kernel (forced variant 2) on the encoder / predictor / mel-head shapes."""
+    dev = "cuda"
+    setb = hip.lib().ssamd_gemm_set_buf
+    hip.lib().ssamd_gemm_set_variant(2)
+    for Cin, ks, N, B, L in ((256, 3, 256, 200, 90), (256, 1, 80, 1, 108000), (1024, 1, 256, 200, 90),
+                             (256, 1, 256, 200, 90), (256, 9, 1024, 200, 90)):
+        Mx = B * L
+        x = torch.randn(1, Mx, Cin, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, ks, Cin, device=dev) / (ks * Cin) ** 0.5).to(torch.bfloat16)
+        bias = torch.randn(N, device=dev)
+        pad = (ks - 1) // 2
+        f = lambda: hip.conv_gemm_raw(x, w, bias, B, L, Cin, ks, 1, pad, N, 1)  # noqa: E731
+        setb(0)
+        ref = f().clone()
+        setb(1)
+        same = torch.equal(f(), ref)
+        t = {0: [], 1: []}
+        for b in (0, 1, 0, 1, 0, 1):
+            setb(b)
+            t[b].append(timeit(f, 10))
+        setb(1)
+        print(json.dumps({"kind": "ring", "M": Mx, "Cin": Cin, "ks": ks, "N": N, "bitwise_equal": same,
+                          "flat_us": round(min(t[0]), 1), "buf_us": round(min(t[1]), 1)}), flush=True)
+    hip.lib().ssamd_gemm_set_variant(-1)
+
+
 if __name__ == "__main__":
+    if os.environ.get("RING", "1") == "1":
+        main_ring()
     if os.environ.get("FWD", "1") == "1":
         main_fwd()
     main()
