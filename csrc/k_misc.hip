@@ -279,6 +279,17 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g,
   if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// one Adam element update (shared by adam_kernel and adam_img_kernel: same expression tree, so the
+// same FMA contraction and bitwise-identical results on either path)
+__device__ __forceinline__ float adam_upd(float pk, float gk, float& mk, float& vk, float coef, float wd, float b1,
+                                          float b2, float step, float bc2_sqrt, float eps) {
+#pragma clang fp contract(off)  // explicit fmaf only: no context-dependent contraction between the kernels
+  gk = fmaf(gk, coef, wd * pk);
+  mk = fmaf(b1, mk, (1.f - b1) * gk);
+  vk = fmaf(b2, vk, ((1.f - b2) * gk) * gk);
+  return fmaf(-step, mk / (sqrtf(vk) / bc2_sqrt + eps), pk);
+}
+
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n,
                                                    const float* __restrict__ ss, float clip, float lr, float b1,
@@ -301,19 +312,14 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const 
     float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
     float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float gk = ga[k] * coef + wd * pa[k];
-      ma[k] = b1 * ma[k] + (1.f - b1) * gk;
-      va[k] = b2 * va[k] + (1.f - b2) * gk * gk;
-      pa[k] -= step * ma[k] / (sqrtf(va[k]) / bc2_sqrt + eps);
-    }
+    for (int k = 0; k < 4; ++k) pa[k] = adam_upd(pa[k], ga[k], ma[k], va[k], coef, wd, b1, b2, step, bc2_sqrt, eps);
     p4[i] = pp; m4[i] = mm; v4[i] = vv;
   }
   for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gk = g[i] * coef + wd * p[i];
-    m[i] = b1 * m[i] + (1.f - b1) * gk;
-    v[i] = b2 * v[i] + (1.f - b2) * gk * gk;
-    p[i] -= step * m[i] / (sqrtf(v[i]) / bc2_sqrt + eps);
+    float mk = m[i], vk = v[i];
+    p[i] = adam_upd(p[i], g[i], mk, vk, coef, wd, b1, b2, step, bc2_sqrt, eps);
+    m[i] = mk;
+    v[i] = vk;
   }
 }
 
@@ -563,6 +569,112 @@ __global__ void __launch_bounds__(256) weight_prep_tiled_kernel(const WDesc* __r
   }
 }
 }  // namespace
+
+// ----------------------------------------------------------------------------
+// Clip + Adam that also writes the bf16 operand images (replaces adam_kernel + weight_prep after
+// every step).  Blocks [0, ntiles): one 64 (cout) x 64 (j = cin*ks + tap) tile of an image-bearing
+// weight -- p / g / m / v read coalesced along j, updated exactly as adam_kernel, the new fp32 tile
+// staged in LDS and written as the forward image [cout][tap][cin] and/or the dgrad image
+// [cin][ks-1-tap][cout] (same layouts and rounding as weight_prep_tiled_kernel).  Blocks past
+// ntiles: the remaining arena elements (biases, norms, embeddings), listed as ranges.
+// ----------------------------------------------------------------------------
+struct AdamImg {
+  long off;       // arena element offset of the weight [cout][cin][ks]
+  bf16_t* fwd;    // forward image or null
+  bf16_t* dgrad;  // dgrad image or null
+  int cout, cin, ks, pad_;
+};
+
+namespace {
+
+__global__ void __launch_bounds__(256) adam_img_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       const float* __restrict__ ss, float clip, float lr, float b1,
+                                                       float b2, float eps, float wd, float bc1, float bc2_sqrt,
+                                                       float* __restrict__ norm_out, long long* __restrict__ skipped,
+                                                       const AdamImg* __restrict__ wt, const int4* __restrict__ tiles,
+                                                       int ntiles, const long* __restrict__ rcum,
+                                                       const long* __restrict__ rstart, int nr, long rtotal) {
+  const float norm = sqrtf(*ss);
+  if (!isfinite(norm)) {  // skipped step: parameters and their images stay as they are
+    if (blockIdx.x == 0 && threadIdx.x == 0) { *norm_out = norm; *skipped += 1; }
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *norm_out = norm;
+  const float coef = clip > 0.f ? fminf(1.f, clip / (norm + 1e-6f)) : 1.f;
+  const float step = lr / bc1;
+  if ((int)blockIdx.x < ntiles) {
+    __shared__ float t[64][65];
+    const int4 tl = tiles[blockIdx.x];
+    const AdamImg d = wt[tl.x];
+    const int co0 = tl.y, j0 = tl.z;
+    const int K = d.cin * d.ks;
+    for (int e = threadIdx.x; e < 4096; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      const int co = co0 + r, j = j0 + c;
+      float nv = 0.f;
+      if (co < d.cout && j < K) {
+        const long i = d.off + (long)co * K + j;
+        float mk = m[i], vk = v[i];
+        nv = adam_upd(p[i], g[i], mk, vk, coef, wd, b1, b2, step, bc2_sqrt, eps);
+        p[i] = nv;
+        m[i] = mk;
+        v[i] = vk;
+      }
+      t[r][c] = nv;
+    }
+    __syncthreads();
+    if (d.dgrad) {  // [cin][ks - 1 - tap][cout]: consecutive threads -> consecutive cout
+      for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int jr = e >> 6, c = e & 63;
+        const int co = co0 + c, j = j0 + jr;
+        if (co >= d.cout || j >= K) continue;
+        const int ci = j / d.ks, tap = j - ci * d.ks;
+        d.dgrad[((long)ci * d.ks + (d.ks - 1 - tap)) * d.cout + co] = f2bf(t[c][jr]);
+      }
+    }
+    if (d.fwd) {  // [cout][tap][cin]
+      for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        const int co = co0 + r, j = j0 + c;
+        if (co >= d.cout || j >= K) continue;
+        const int ci = j / d.ks, tap = j - ci * d.ks;
+        d.fwd[(long)co * K + (long)tap * d.cin + ci] = f2bf(t[r][c]);
+      }
+    }
+    return;
+  }
+  // remaining elements: rest index e -> range r (rcum[r] <= e < rcum[r+1]) -> arena rstart[r] + e - rcum[r]
+  const long nthr = (long)(gridDim.x - ntiles) * blockDim.x;
+  for (long e = (long)(blockIdx.x - ntiles) * blockDim.x + threadIdx.x; e < rtotal; e += nthr) {
+    int lo = 0, hi = nr;
+    while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (rcum[mid] <= e) lo = mid; else hi = mid; }
+    const long i = rstart[lo] + (e - rcum[lo]);
+    float mk = m[i], vk = v[i];
+    p[i] = adam_upd(p[i], g[i], mk, vk, coef, wd, b1, b2, step, bc2_sqrt, eps);
+    m[i] = mk;
+    v[i] = vk;
+  }
+}
+}  // namespace
+
+// clip + Adam + image refresh (see adam_img_kernel); ws as ssamd_clip_adam
+SSAMD_API int ssamd_clip_adam_img(float* p, const float* g, float* m, float* v, long n, float* ws, float clip, float lr,
+                                  float b1, float b2, float eps, float wd, int step, float* norm_out,
+                                  long long* skipped, const void* wtab, const void* tiles, int ntiles,
+                                  const long* rcum, const long* rstart, int nr, long rtotal, hipStream_t s) {
+  const int nblk = grid_for(n, 16);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, s, g, n, ws + 1);
+  ssamd_small_sum(ws + 1, nblk, 1, ws, s);
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2 = 1.f - powf(b2, (float)step);
+  const int rblocks = rtotal > 0 ? (int)std::min<long>((long)cdiv(rtotal, 256L * 4), 2048L) : 0;
+  if (ntiles + rblocks == 0) return 0;
+  hipLaunchKernelGGL(adam_img_kernel, dim3(ntiles + rblocks), dim3(256), 0, s, p, g, m, v, ws, clip, lr, b1, b2, eps,
+                     wd, bc1, sqrtf(bc2), norm_out, skipped, reinterpret_cast<const AdamImg*>(wtab),
+                     reinterpret_cast<const int4*>(tiles), ntiles, rcum, rstart, nr, rtotal);
+  return (int)hipGetLastError();
+}
 
 SSAMD_API int ssamd_weight_prep_tiled(const void* table, const void* tiles, int ntiles, hipStream_t s) {
   if (ntiles == 0) return 0;

@@ -74,6 +74,7 @@ _SIGS = {
     "ssamd_clip_adam_ws": [L_],
     "ssamd_l1pair_bwd": [P, P, P, P, I, I, I, I, P, P, P, P, P],
     "ssamd_clip_adam": [P, P, P, P, L_, P, F, F, F, F, F, F, I, P, P, P],
+    "ssamd_clip_adam_img": [P, P, P, P, L_, P, F, F, F, F, F, F, I, P, P, P, P, I, P, P, I, L_, P],
     "ssamd_attn_fwd": [P, P, P, P, P, I, I, I, I, F, P],
     "ssamd_attn_bwd": [P, P, P, P, P, P, P, P, L_, I, I, I, I, F, P],
     "ssamd_relu_mask": [P, P, P, L_, P],
@@ -175,6 +176,7 @@ def _need(t, dtype, name):
 _wcache = {}          # key -> [version, generation, weakref(param), image, mode, src_ptr]
 _wgen = 0
 _wtable = {"n": -1}   # device descriptor table for the batched refresh
+_wepoch = 0           # bumped whenever the set of cached images changes (fused Adam plan key)
 
 
 def bump_weight_generation():
@@ -195,6 +197,7 @@ def _refresh_all(device):
         if owner is None or w.data_ptr() != e[5]:
             del _wcache[k]
             _wtable["n"] = -1
+            _bump_epoch()
         elif w.device == device and _eligible(w):
             live.append((e, w, owner))  # strong ref: the owner cannot die before its image is stamped
     if _wtable.get("n") != len(live) or _wtable.get("dev") != device:
@@ -245,7 +248,13 @@ def _cached(param: torch.Tensor, kind: str, mode: int, make, src: Optional[torch
     _wcache[key] = [param._version, _wgen, weakref.ref(param), img, mode, src.data_ptr(), tuple(src.shape),
                     src.detach()]
     _wtable["n"] = -1  # entry set changed: rebuild the descriptor table on the next refresh
+    _bump_epoch()
     return img
+
+
+def _bump_epoch():
+    global _wepoch
+    _wepoch += 1
 
 
 def weight_fwd(w: torch.Tensor, owner: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -1101,7 +1110,78 @@ def masked_l1_pair(mel_p, post_p, mel_t, mel_valid, count):
 _adam_ws = {}
 
 
-def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped):
+_adam_plan = {}
+
+
+def _adam_image_plan(p: torch.Tensor):
+    """Fused clip+Adam+image plan for the arena ``p``: the cached weight images whose source lies
+    in the arena (grouped per weight: forward and/or dgrad image), their 64x64 tiles, and the
+    arena ranges NOT covered by an image-bearing weight (updated element-wise).  Rebuilt when
+    the image set changes (``_wepoch``)."""
+    key = (p.data_ptr(), p.numel())
+    plan = _adam_plan.get(key)
+    if plan is not None and plan["epoch"] == _wepoch:
+        return plan
+    import numpy as np
+
+    base, n = p.data_ptr(), p.numel()
+    weights = {}  # src ptr -> [off, cout, cin, ks, fwd_dst, dgrad_dst, entries]
+    for k, e in list(_wcache.items()):
+        owner, w = e[2](), e[7]
+        if owner is None or w.data_ptr() != e[5] or w.device != p.device or not _eligible(w):
+            continue
+        sp = w.data_ptr()
+        if not (base <= sp and sp + w.numel() * 4 <= base + n * 4):
+            continue
+        ks = w.shape[2] if w.dim() == 3 else 1
+        rec = weights.setdefault(sp, [(sp - base) // 4, w.shape[0], w.shape[1], ks, 0, 0, []])
+        rec[4 + e[4]] = e[3].data_ptr()
+        rec[6].append(k)
+    recs = sorted(weights.values(), key=lambda r: r[0])
+    # an element must be updated exactly once: weights whose ranges overlap another image source
+    # (e.g. a fused view and one of its members) stay on the element-wise path + lazy refresh
+    span = [(r[0], r[0] + r[1] * r[2] * r[3]) for r in recs]
+    clash = [any(j != i and span[j][0] < b and a < span[j][1] for j in range(len(span))) for i, (a, b) in
+             enumerate(span)]
+    recs = [r for r, c in zip(recs, clash) if not c]
+    desc = np.zeros(len(recs), dtype=[("off", "<i8"), ("fwd", "<u8"), ("dgrad", "<u8"), ("cout", "<i4"),
+                                      ("cin", "<i4"), ("ks", "<i4"), ("pad", "<i4")])
+    tiles, covered = [], []
+    for i, (off, cout, cin, ks, fwd, dgr, _) in enumerate(recs):
+        desc[i] = (off, fwd, dgr, cout, cin, ks, 0)
+        K = cin * ks
+        covered.append((off, off + cout * K))
+        for co0 in range(0, cout, 64):
+            for j0 in range(0, K, 64):
+                tiles.append((i, co0, j0, 0))
+    rest, cur = [], 0
+    for a, b in covered:  # sorted, disjoint (distinct parameters)
+        if a > cur:
+            rest.append((cur, a))
+        cur = max(cur, b)
+    if cur < n:
+        rest.append((cur, n))
+    rstart = np.array([a for a, _ in rest] or [0], dtype=np.int64)
+    rcum = np.zeros(len(rest) + 1, dtype=np.int64)
+    rcum[1:] = np.cumsum([b - a for a, b in rest]) if rest else 0
+    dev = p.device
+    tiles = np.asarray(tiles, dtype=np.int32).reshape(-1, 4)
+    plan = {
+        "epoch": _wepoch,
+        "desc": torch.from_numpy(desc.view(np.uint8).copy()).to(dev) if len(recs) else None,
+        "tiles": torch.from_numpy(tiles).to(dev) if len(tiles) else None, "ntiles": len(tiles),
+        "rcum": torch.from_numpy(rcum).to(dev), "rstart": torch.from_numpy(rstart).to(dev),
+        "nr": len(rest), "rtotal": int(rcum[-1]),
+        "keys": [k for r in recs for k in r[6]],
+    }
+    _adam_plan[key] = plan
+    return plan
+
+
+def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped, images=True):
+    """Global-norm clip + Adam over the flat arena (no host sync).  ``images``: the same launch
+    rewrites the bf16 operand images of every cached weight inside the arena (no separate
+    ``weight_prep`` refresh before the next forward); the caller still bumps the generation."""
     for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v")):
         _need(t, torch.float32, "adam." + nm)
     assert p.numel() == g.numel() == m.numel() == v.numel()
@@ -1109,10 +1189,30 @@ def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped
     ws = _adam_ws.get(p.device)
     if ws is None or ws.numel() < n_ws:  # [global sum of squares, per-block partials]
         ws = _adam_ws[p.device] = torch.zeros(n_ws, device=p.device, dtype=torch.float32)
+    if images and has("ssamd_clip_adam_img"):
+        plan = _adam_image_plan(p)
+        rc = lib().ssamd_clip_adam_img(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(ws), float(clip),
+                                       float(lr), float(betas[0]), float(betas[1]), float(eps), float(wd), int(step),
+                                       _ptr(norm_out), _ptr(skipped), _ptr(plan["desc"]), _ptr(plan["tiles"]),
+                                       plan["ntiles"], _ptr(plan["rcum"]), _ptr(plan["rstart"]), plan["nr"],
+                                       plan["rtotal"], _stream())
+        _check(rc, "ssamd_clip_adam_img")
+        return plan["keys"]
     rc = lib().ssamd_clip_adam(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(ws), float(clip), float(lr),
                                float(betas[0]), float(betas[1]), float(eps), float(wd), int(step), _ptr(norm_out),
                                _ptr(skipped), _stream())
     _check(rc, "ssamd_clip_adam")
+    return []
+
+
+def stamp_images(keys):
+    """Mark the given cached images current (their fused-Adam rewrite is already queued)."""
+    for k in keys:
+        e = _wcache.get(k)
+        if e is not None:
+            owner = e[2]()
+            if owner is not None:
+                e[0], e[1] = owner._version, _wgen
 
 
 # ------------------------------------------------------------------------ BatchNorm (+tanh, dropout)

@@ -224,9 +224,11 @@ def fused_adam_step(opt: ScheduledOptim, lr: float):
     if a.data.is_cuda:
         from ..ops import hip
 
-        hip.clip_adam_step(a.data, a.grad, opt.exp_avg, opt.exp_avg_sq, lr, opt.betas, opt.eps, opt.weight_decay,
-                           opt.step_count, opt.grad_clip, opt.last_grad_norm, opt.skipped_steps)
+        fresh = hip.clip_adam_step(a.data, a.grad, opt.exp_avg, opt.exp_avg_sq, lr, opt.betas, opt.eps,
+                                   opt.weight_decay, opt.step_count, opt.grad_clip, opt.last_grad_norm,
+                                   opt.skipped_steps)
         hip.bump_weight_generation()  # raw-pointer writes: torch version counters do not move
+        hip.stamp_images(fresh)  # images rewritten by the same launch: no weight_prep refresh
         return
     g = a.grad
     norm = torch.linalg.vector_norm(g)

@@ -1074,3 +1074,55 @@ def test_splitk_gemm_vs_reference(act, use_bias, use_res, packed):
         finally:
             hip.lib().ssamd_gemm_set_splitk(-1)
         assert _rel(y, y_ref) < 1e-2, S
+
+
+@pytest.mark.gpu
+def test_fused_adam_images_match_two_kernel_path():
+    """clip+Adam that rewrites the bf16 images in the same launch (ssamd_clip_adam_img): parameters
+    and Adam moments bitwise equal to adam_kernel, every cached image equal to a fresh cast of its
+    updated weight, and no weight_prep refresh needed before the next forward."""
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+    from speakingstyle_amd.models.loss import FastSpeech2Loss
+    from speakingstyle_amd.ops import hip
+    from speakingstyle_amd.train.optim import ScheduledOptim
+
+    pp, mc, tc = load_named("LJSpeech")
+    mc["transformer"]["encoder_layer"] = mc["transformer"]["decoder_layer"] = 2
+    b = SyntheticBatches(4, device=DEV, seed=5, phone_counts=[30, 41, 17, 25]).make_batch()
+    lossf = FastSpeech2Loss(pp, tc)
+    states = []
+    for images in (False, True):
+        torch.manual_seed(3)
+        m = FastSpeech2(pp, mc).to(DEV).set_compute_dtype(torch.bfloat16)
+        opt = ScheduledOptim(m, tc, mc, 0)
+        m.train()
+        for it in range(2):
+            hip.set_seed(1234567 + it)  # same dropout masks in both runs
+            opt.zero_grad()
+            lo = lossf(b, m(*b[2:]), m.film_scalars())
+            lo[0].backward()
+            opt.arena.finalize_grads()
+            opt.step_count += 1
+            a = opt.arena
+            fresh = hip.clip_adam_step(a.data, a.grad, opt.exp_avg, opt.exp_avg_sq, 1e-2, opt.betas, opt.eps,
+                                       opt.weight_decay, opt.step_count, 1.0, opt.last_grad_norm, opt.skipped_steps,
+                                       images=images)
+            hip.bump_weight_generation()
+            hip.stamp_images(fresh)
+        torch.cuda.synchronize()
+        if images:
+            assert len(fresh) > 10  # the model's conv / linear images are covered
+            for k in fresh:  # stamped images == fresh casts of the updated weights
+                e = hip._wcache[k]
+                src = e[7]
+                if src.dim() == 2:
+                    want = src.to(torch.bfloat16) if e[4] == 0 else src.t().to(torch.bfloat16)
+                else:
+                    want = (src.permute(0, 2, 1) if e[4] == 0 else src.flip(2).permute(1, 2, 0)).to(torch.bfloat16)
+                assert torch.equal(e[3], want.contiguous()), k
+        states.append((opt.arena.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone()))
+        del m, opt
+    for x, y in zip(*states):
+        assert torch.equal(x, y)
