@@ -2850,11 +2850,15 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     if (S > 1 && plain && reg && N >= 256 && (N % 8) == 0 && ldy == N && act >= 0 && (ldy % 8) == 0) {
       const size_t need = (size_t)S * g.M * N * sizeof(float);
       if (need > g_splitk_bytes) {
+        // S * tiles <= 256 CUs bounds every split-K workspace by 256 tiles x 256 KiB = 64 MiB: allocate
+        // that once (the first split-K call, a warm-up step) -- a regrow would hipFree, a device-wide
+        // synchronisation in the middle of a training step
+        const size_t want = need > ((size_t)64 << 20) ? need : ((size_t)64 << 20);
         if (g_splitk_ws) (void)hipFree(g_splitk_ws);
         g_splitk_ws = nullptr;
         g_splitk_bytes = 0;
-        if (hipMalloc(&g_splitk_ws, need) != hipSuccess) return -4;
-        g_splitk_bytes = need;
+        if (hipMalloc(&g_splitk_ws, want) != hipSuccess) return -4;
+        g_splitk_bytes = want;
       }
       static bool sk_set = false;
       if (!sk_set) {

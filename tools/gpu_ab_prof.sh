@@ -24,7 +24,7 @@ def short(n):
 def load(v, last=3):  # per-kernel time over the LAST `last` steps (Adam-delimited): steady state only
     f = glob.glob(f"gpurun_out/abprof/{v}/**/*kernel_trace.csv", recursive=True)[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"] or "adam_img_kernel" in r["Kernel_Name"]]
     out = defaultdict(lambda: [0, 0.0])
     for r in rows[ends[-last - 1] + 1: ends[-1] + 1]:
         k = out[short(r["Kernel_Name"])]

@@ -1,0 +1,40 @@
+"""Host-side (Python) cost of a training step: cProfile over N steady-state Trainer steps (GPU box).
+Usage: python tools/host_profile.py [config] [steps]"""
+import cProfile
+import io
+import os
+import pstats
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from speakingstyle_amd.config import load_named  # noqa: E402
+from speakingstyle_amd.data.synthetic import SyntheticBatches  # noqa: E402
+from speakingstyle_amd.models.fastspeech2 import FastSpeech2  # noqa: E402
+from speakingstyle_amd.train.trainer import Trainer  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "LJSpeech"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+pp, mc, tc = load_named(cfg)
+torch.manual_seed(0)
+model = FastSpeech2(pp, mc).to("cuda").set_compute_dtype(torch.bfloat16)
+tr = Trainer(model, (pp, mc, tc), seed=1)
+gen = SyntheticBatches(int(tc["optimizer"]["batch_size"]), device="cuda", max_seq_len=mc["max_seq_len"], seed=5)
+b = gen.make_batch()
+for _ in range(3):
+    tr.train_step(b)
+torch.cuda.synchronize()
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(n):
+    tr.train_step(b)
+pr.disable()
+torch.cuda.synchronize()
+s = io.StringIO()
+ps = pstats.Stats(pr, stream=s).sort_stats("tottime")
+ps.print_stats(35)
+print(s.getvalue())
+s = io.StringIO()
+pstats.Stats(pr, stream=s).sort_stats("cumulative").print_stats(45)
+print(s.getvalue())

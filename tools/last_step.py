@@ -18,7 +18,7 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    ends = [i for i, r in enumerate(rows) if re.search(r"adam(_img)?_kernel", r["Kernel_Name"])]
     a, b = ends[-2] + 1, ends[-1] + 1
     step = rows[a:b]
     agg = defaultdict(lambda: [0, 0.0])

@@ -4,6 +4,7 @@
 usage: prof_summary.py <run_kernel_stats.csv> [<run_kernel_trace.csv>]
 """
 import csv
+import re
 import sys
 
 
@@ -44,7 +45,7 @@ def main():
         for g, n in gaps[:8]:
             print(f"  gap {g / 1e6:8.3f} ms before {n[:80]}")
         # steady-state window: between the last two optimizer (adam) launches = one training step
-        adam = [i for i, e in enumerate(ev) if "adam_kernel" in e[2]]
+        adam = [i for i, e in enumerate(ev) if re.search(r"adam(_img)?_kernel", e[2])]
         if len(adam) >= 2:
             i0, i1 = adam[-2], adam[-1]
             win = ev[i0 + 1:i1 + 1]
