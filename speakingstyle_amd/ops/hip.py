@@ -1183,6 +1183,8 @@ def _adam_image_plan(p: torch.Tensor):
         "rcum": torch.from_numpy(rcum).to(dev), "rstart": torch.from_numpy(rstart).to(dev),
         "nr": len(rest), "rtotal": int(rcum[-1]),
         "keys": [k for r in recs for k in r[6]],
+        # the cache entry lists themselves (an entry replaced in _wcache bumps _wepoch -> new plan)
+        "entries": [_wcache[k] for r in recs for k in r[6]],
     }
     _adam_plan[key] = plan
     _adam_plan_builds[0] += 1
@@ -1208,7 +1210,7 @@ def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped
                                        plan["ntiles"], _ptr(plan["rcum"]), _ptr(plan["rstart"]), plan["nr"],
                                        plan["rtotal"], _stream())
         _check(rc, "ssamd_clip_adam_img")
-        return plan["keys"]
+        return plan["entries"]
     rc = lib().ssamd_clip_adam(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(ws), float(clip), float(lr),
                                float(betas[0]), float(betas[1]), float(eps), float(wd), int(step), _ptr(norm_out),
                                _ptr(skipped), _stream())
@@ -1216,14 +1218,13 @@ def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped
     return []
 
 
-def stamp_images(keys):
-    """Mark the given cached images current (their fused-Adam rewrite is already queued)."""
-    for k in keys:
-        e = _wcache.get(k)
-        if e is not None:
-            owner = e[2]()
-            if owner is not None:
-                e[0], e[1] = owner._version, _wgen
+def stamp_images(entries):
+    """Mark the given cached image entries current (their fused-Adam rewrite is already queued)."""
+    g = _wgen
+    for e in entries:
+        owner = e[2]()
+        if owner is not None:
+            e[0], e[1] = owner._version, g
 
 
 # ------------------------------------------------------------------------ BatchNorm (+tanh, dropout)

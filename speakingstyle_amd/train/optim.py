@@ -112,9 +112,10 @@ class FlatArena:
 
     def finalize_grads(self):
         """After backward: every produced gradient lives in the arena."""
+        sp = self._slot_ptr
         for i, p in enumerate(self.params):
             g = p.grad
-            if g is not None and g.data_ptr() != self._slot_ptr[id(p)]:
+            if g is not None and g.data_ptr() != sp[id(p)]:
                 self.ensure_slot(p, i)
 
     def rebind_grads(self):

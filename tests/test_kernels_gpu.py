@@ -1114,14 +1114,13 @@ def test_fused_adam_images_match_two_kernel_path():
         torch.cuda.synchronize()
         if images:
             assert len(fresh) > 10  # the model's conv / linear images are covered
-            for k in fresh:  # stamped images == fresh casts of the updated weights
-                e = hip._wcache[k]
+            for e in fresh:  # stamped images == fresh casts of the updated weights
                 src = e[7]
                 if src.dim() == 2:
                     want = src.to(torch.bfloat16) if e[4] == 0 else src.t().to(torch.bfloat16)
                 else:
                     want = (src.permute(0, 2, 1) if e[4] == 0 else src.flip(2).permute(1, 2, 0)).to(torch.bfloat16)
-                assert torch.equal(e[3], want.contiguous()), k
+                assert torch.equal(e[3], want.contiguous()), tuple(src.shape)
         states.append((opt.arena.data.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone()))
         del m, opt
     for x, y in zip(*states):
