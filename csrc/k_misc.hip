@@ -457,6 +457,46 @@ SSAMD_API int ssamd_l1pair_bwd(const float* p1, const float* p2, const float* tg
   return (int)hipGetLastError();
 }
 
+namespace {
+// FastSpeech2 loss finalize (one block): the mel valid-element count (fixed-order sum of
+// min(len, M) x C, or the external global count), the five loss terms and their total in the
+// reference order mel + post + dur + pitch + energy (model/loss.py:91-93).
+// out: [total, mel, post, pitch, energy, dur];  cnt_out[0] = the mel count (backward divisor)
+__global__ void __launch_bounds__(256) fs2_loss_final_kernel(const float* __restrict__ l1sums,
+                                                             const float* __restrict__ var3,
+                                                             const int64_t* __restrict__ lens, int B, int M, int C,
+                                                             const float* __restrict__ ext, float* __restrict__ out,
+                                                             float* __restrict__ cnt_out) {
+  __shared__ float red[256];
+  float c = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) c += (float)(lens[b] < M ? lens[b] : M);
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float cnt = ext ? ext[0] : red[0] * (float)C;
+    const float inv = 1.f / fmaxf(cnt, 1.f);
+    const float mel = l1sums[0] * inv, post = l1sums[1] * inv;
+    out[1] = mel;
+    out[2] = post;
+    out[3] = var3[0];
+    out[4] = var3[1];
+    out[5] = var3[2];
+    out[0] = (((mel + post) + var3[2]) + var3[0]) + var3[1];
+    cnt_out[0] = cnt;
+  }
+}
+}  // namespace
+
+SSAMD_API int ssamd_fs2_loss_final(const float* l1sums, const float* var3, const int64_t* lens, int B, int M, int C,
+                                   const float* ext, float* out, float* cnt_out, hipStream_t s) {
+  hipLaunchKernelGGL(fs2_loss_final_kernel, dim3(1), dim3(256), 0, s, l1sums, var3, lens, B, M, C, ext, out, cnt_out);
+  return (int)hipGetLastError();
+}
+
 SSAMD_API long ssamd_clip_adam_ws(long n) { return 1L + grid_for(n, 16); }
 
 // ws: ssamd_clip_adam_ws(n) floats (ws[0] = global sum of squares, ws[1..] = block partials)

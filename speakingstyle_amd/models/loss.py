@@ -51,17 +51,19 @@ class FastSpeech2Loss(nn.Module):
             # GPU: two fused deterministic kernel pairs (L1 mel/postnet, MSE pitch/energy/duration)
             from ..ops import hip
 
-            mel_valid = ~mel_masks
+            # one autograd node: both fused kernel pairs + a finalize kernel that counts the valid mel
+            # elements from the lengths (mel_masks = t >= min(len, M)) and forms the total
             if global_counts is not None:
                 c_mel = global_counts[0]
                 gc = global_counts[[1 if phon_p else 2, 1 if phon_e else 2, 1]]
             else:
-                c_mel = (mel_valid.sum() * n_mel).float()
-                gc = None  # the kernel counts the unmasked elements itself
-            mel_l, post_l = hip.masked_l1_pair(mel_p, post_p, mel_t, mel_valid, c_mel)
-            pitch_l, energy_l, dur_l = hip.variance_losses(
-                p_p, p_t, src_masks if phon_p else mel_masks, e_p, e_t, src_masks if phon_e else mel_masks,
-                logd_p, d_t, src_masks, gc)
+                c_mel, gc = None, None  # the kernels count the unmasked elements themselves
+            total, mel_l, post_l, pitch_l, energy_l, dur_l = hip.fs2_losses(
+                mel_p, post_p, mel_t, inputs[7], p_p, p_t, src_masks if phon_p else mel_masks, e_p, e_t,
+                src_masks if phon_e else mel_masks, logd_p, d_t, src_masks, mel_count=c_mel, var_counts=gc)
+            if named_param is not None and self.lambda_f > 0:
+                total = total + self.lambda_f * torch.sum(torch.square(named_param))
+            return total, mel_l, post_l, pitch_l, energy_l, dur_l, self.lambda_f
         else:
             src_valid = ~src_masks
             mel_valid = ~mel_masks

@@ -1110,6 +1110,74 @@ def variance_losses(p_pred, p_t, p_mask, e_pred, e_t, e_mask, logd, d_t, src_mas
                             logd.float(), d_t.to(torch.int64), src_mask, counts)
 
 
+_SIGS["ssamd_fs2_loss_final"] = [P, P, P, I, I, I, P, P, P, P]
+
+
+class _FS2LossFn(torch.autograd.Function):
+    """All five FastSpeech2 loss terms and their total in ONE autograd node: masked L1 of mel and
+    postnet (``l1pair``), masked MSE of pitch / energy / log-duration (``var_loss``), and a one-block
+    finalize kernel (mel count from the lengths, divisions, total in the reference's order) --
+    instead of ~15 small torch ops (masks, counts, casts, divisions, adds) on the host-paced loss
+    path.  Backward: per-term scale = g_term + g_total, then the two fused gradient kernels."""
+
+    @staticmethod
+    def forward(ctx, mel_p, post_p, mel_t, lens, mel_count, pp, pt, pm, ep, et, em, ld, dt, dm, var_counts):
+        B, M, C = mel_p.shape
+        Mt = mel_t.shape[1]
+        p1c, p2c, tc = mel_p.float().contiguous(), post_p.float().contiguous(), mel_t.float().contiguous()
+        lens = lens.contiguous()
+        dev = mel_p.device
+        sums = torch.empty(2, device=dev, dtype=torch.float32)
+        ws = _workspace(dev, int(lib().ssamd_l1pair_ws(B, M, C)))
+        rc = lib().ssamd_l1pair_fwd(_ptr(p1c), _ptr(p2c), _ptr(tc), _ptr(lens), B, M, Mt, C, _ptr(sums), _ptr(ws),
+                                    ws.numel(), _stream())
+        _check(rc, "ssamd_l1pair_fwd")
+        pp, pt, ep, et, ld, dt = [t.contiguous() for t in (pp, pt, ep, et, ld, dt)]
+        pm, em, dm = pm.contiguous(), em.contiguous(), dm.contiguous()
+        var3 = torch.empty(3, device=dev, dtype=torch.float32)
+        vcnt = torch.empty(3, device=dev, dtype=torch.float32)
+        vws = _workspace(dev, int(lib().ssamd_var_loss_ws()))  # stream-ordered after l1pair: reuse is safe
+        ext = None if var_counts is None else var_counts.float().contiguous()
+        rc = lib().ssamd_var_loss_fwd(_vterm(pp, pt, pm), _vterm(ep, et, em), _vterm(ld, dt, dm), B, _ptr(ext),
+                                      _ptr(var3), _ptr(vcnt), _ptr(vws), _stream())
+        _check(rc, "ssamd_var_loss_fwd")
+        out = torch.empty(6, device=dev, dtype=torch.float32)
+        mcnt = torch.empty(1, device=dev, dtype=torch.float32)
+        mext = None if mel_count is None else mel_count.float().reshape(1).contiguous()
+        rc = lib().ssamd_fs2_loss_final(_ptr(sums), _ptr(var3), _ptr(lens), B, M, C, _ptr(mext), _ptr(out),
+                                        _ptr(mcnt), _stream())
+        _check(rc, "ssamd_fs2_loss_final")
+        ctx.save_for_backward(p1c, p2c, tc, lens, mcnt, pp, pt, pm, ep, et, em, ld, dt, dm, vcnt)
+        return out[0], out[1], out[2], out[3], out[4], out[5]
+
+    @staticmethod
+    def backward(ctx, g_tot, g_mel, g_post, g_pitch, g_energy, g_dur):
+        p1c, p2c, tc, lens, mcnt, pp, pt, pm, ep, et, em, ld, dt, dm, vcnt = ctx.saved_tensors
+        B, M, C = p1c.shape
+        gs = (torch.stack([g_mel, g_post, g_pitch, g_energy, g_dur]).float() + g_tot.float()).contiguous()
+        d1 = torch.empty_like(p1c)
+        d2 = torch.empty_like(p2c)
+        rc = lib().ssamd_l1pair_bwd(_ptr(p1c), _ptr(p2c), _ptr(tc), _ptr(lens), B, M, tc.shape[1], C, _ptr(gs),
+                                    _ptr(mcnt), _ptr(d1), _ptr(d2), _stream())
+        _check(rc, "ssamd_l1pair_bwd")
+        gp, ge, gd = [torch.empty_like(x) if x.shape[1] == m.shape[1] else torch.zeros_like(x)
+                      for x, m in ((pp, pm), (ep, em), (ld, dm))]
+        rc = lib().ssamd_var_loss_bwd(_vterm(pp, pt, pm, gp), _vterm(ep, et, em, ge), _vterm(ld, dt, dm, gd),
+                                      pm.shape[0], ctypes.c_void_p(gs.data_ptr() + 2 * 4), _ptr(vcnt), _stream())
+        _check(rc, "ssamd_var_loss_bwd")
+        return d1, d2, None, None, None, gp, None, None, ge, None, None, gd, None, None, None
+
+
+def fs2_losses(mel_p, post_p, mel_t, mel_lens, p_pred, p_t, p_mask, e_pred, e_t, e_mask, logd, d_t, src_mask,
+               mel_count=None, var_counts=None):
+    """-> (total, mel, postnet, pitch, energy, duration) losses; ``mel_lens`` (int64 [B], may exceed
+    the truncated length M) replaces the mel pad mask; masks are the reference's (True = padded);
+    ``mel_count`` / ``var_counts``: optional all-reduced global divisors (data parallelism)."""
+    return _FS2LossFn.apply(mel_p, post_p, mel_t, mel_lens.to(torch.int64), mel_count, p_pred.float(), p_t.float(),
+                            p_mask, e_pred.float(), e_t.float(), e_mask, logd.float(), d_t.to(torch.int64),
+                            src_mask, var_counts)
+
+
 def masked_l1_pair(mel_p, post_p, mel_t, mel_valid, count):
     lens = mel_valid.sum(1).to(torch.int64).contiguous()
     return _L1PairFn.apply(mel_p, post_p, mel_t, lens, count)
