@@ -22,6 +22,7 @@ layout with autograd (vocoder training is not a headline config).
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -67,6 +68,18 @@ def _w(conv):
     return conv.weight
 
 
+def _wn(conv):
+    """Differentiable effective weight ``g * v / ||v||`` of a weight-normed conv (torch recomputes
+    ``conv.weight`` in a forward pre-hook, which the channel-last training path does not run)."""
+    if hasattr(conv, "weight_g") and hasattr(conv, "weight_v"):
+        return torch._weight_norm(conv.weight_v, conv.weight_g, 0)
+    return conv.weight
+
+
+# generator training on the HIP implicit-GEMM convs (channel-last); 0: torch / MIOpen NCL convs
+_HIP_TRAIN = os.environ.get("SSAMD_HIFIGAN_HIP_TRAIN", "1") != "0"
+
+
 class ResBlock1(nn.Module):
     def __init__(self, channels, kernel_size=3, dilation=(1, 3, 5)):
         super().__init__()
@@ -85,6 +98,16 @@ class ResBlock1(nn.Module):
         for c1, c2 in zip(self.convs1, self.convs2):
             xt = c2(F.leaky_relu(c1(F.leaky_relu(x, LRELU_SLOPE)), LRELU_SLOPE))
             x = xt + x
+        return x
+
+    def forward_cl_train(self, x):
+        """Channel-last training path [B, T, C] bf16 on the HIP convs (autograd): lrelu -> dilated
+        conv -> lrelu -> conv -> + x per layer; the conv weights are the weight-normed tensors."""
+        k = self.kernel_size
+        for c1, c2, d in zip(self.convs1, self.convs2, self.dilation):
+            t = ops.conv1d(F.leaky_relu(x, LRELU_SLOPE), _wn(c1), c1.bias, get_padding(k, d), d, None)
+            t = ops.conv1d(F.leaky_relu(t, LRELU_SLOPE), _wn(c2), c2.bias, get_padding(k, 1), 1, None)
+            x = t + x
         return x
 
     def fusable(self, channels: int) -> bool:
@@ -161,6 +184,8 @@ class Generator(nn.Module):
 
     # ------------------------------------------------------------------ training (NCL)
     def forward(self, x):
+        if _HIP_TRAIN and x.is_cuda and ops.use_hip(x) and self._hip_train_ok():
+            return self._forward_hip_train(x)
         x = self.conv_pre(x)
         for i in range(self.num_upsamples):
             x = self.ups[i](F.leaky_relu(x, LRELU_SLOPE))
@@ -171,6 +196,41 @@ class Generator(nn.Module):
             x = xs / self.num_kernels
         x = self.conv_post(F.leaky_relu(x))  # default slope 0.01 (reference quirk, D16 preserved)
         return torch.tanh(x)
+
+    def _hip_train_ok(self) -> bool:
+        ok = self.conv_pre.in_channels % 8 == 0 and self.conv_pre.out_channels % 8 == 0
+        for up in self.ups:
+            K, s, pad = up.kernel_size[0], up.stride[0], up.padding[0]
+            ok = ok and up.out_channels % 8 == 0 and K == s + 2 * pad and 0 <= pad <= s
+        return ok
+
+    def _forward_hip_train(self, x):
+        """Generator forward for training on the HIP implicit-GEMM convs (channel-last bf16
+        activations, fp32 weight-normed weights, autograd through ``ops.conv1d``): each upsampler
+        is the 3-tap conv of ``convT_as_conv3`` (differentiable weight rearrangement) whose
+        [B, T, s*Cout] output reshapes to the interleaved [B, T*s, Cout]; LeakyReLU / residual /
+        MRF mean are torch elementwise ops; conv_post (one output channel, not MFMA-shaped) is a
+        torch conv on the fp32 activation.  Same function as ``forward`` (reference
+        ``hifigan/models.py:124-165``), returns [B, 1, T*hop] fp32."""
+        B = x.shape[0]
+        h = x.transpose(1, 2).to(torch.bfloat16).contiguous()
+        h = ops.conv1d(h, _wn(self.conv_pre), self.conv_pre.bias, 3, 1, None)
+        nk = self.num_kernels
+        for i in range(self.num_upsamples):
+            up = self.ups[i]
+            s = up.stride[0]
+            wu = convT_as_conv3(_wn(up).float(), s, up.padding[0])
+            bt = None if up.bias is None else up.bias.float().repeat(s)
+            T = h.shape[1]
+            h = ops.conv1d(F.leaky_relu(h, LRELU_SLOPE), wu, bt, 1, 1, None).reshape(B, T * s, -1)
+            xs = None
+            for j in range(nk):
+                r = self.resblocks[i * nk + j].forward_cl_train(h)
+                xs = r if xs is None else xs + r
+            h = xs / nk
+        z = F.conv1d(F.leaky_relu(h.float(), 0.01).transpose(1, 2), _wn(self.conv_post), self.conv_post.bias,
+                     padding=3)
+        return torch.tanh(z)
 
     # ------------------------------------------------------------------ inference (channel-last, HIP)
     @torch.no_grad()
