@@ -25,6 +25,8 @@ b = gen.make_batch()
 for _ in range(3):
     tr.train_step(b)
 torch.cuda.synchronize()
+if os.environ.get("SAME_THREAD_BWD", "1") == "1":  # backward on this thread so cProfile sees it
+    torch.autograd.set_multithreading_enabled(False)
 pr = cProfile.Profile()
 pr.enable()
 for _ in range(n):
