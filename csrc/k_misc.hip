@@ -1140,7 +1140,11 @@ SSAMD_API int ssamd_pad_colsum(const void* dout, int f32, const int64_t* lens, i
 // FiLM parameter gradients of one LayerNorm site (reference model/blocks.py:43-62):
 //   d gamma = S1 * s_g,  d beta = S2 * s_b            (bf16 or fp32 [n])
 //   d s_g = sum(S1 * gamma),  d s_b = sum(S2 * beta)   (scalars, fixed-order block reduction)
-// S1 / S2 = per-(b, c) sums from the LayerNorm backward.  One block; written, not accumulated.
+// S1 / S2 = per-(b, c) sums from the LayerNorm backward.  One block.  accum != 0: d gamma / d beta
+// are added to (running sums over the sites that share gamma / beta, in backward order on one
+// stream: deterministic) instead of one gradient per site summed by autograd.  l2_sg / l2_sb (optional):
+// this site's entries of the FiLM L2 term's gradient (ops/hip.py film_scalars_cat), folded into the
+// scalar gradients so each scalar gets ONE gradient, written straight into its arena slot.
 // ----------------------------------------------------------------------------
 namespace {
 __global__ void __launch_bounds__(256) film_grads_kernel(const float* __restrict__ S1, const float* __restrict__ S2,
@@ -1148,18 +1152,23 @@ __global__ void __launch_bounds__(256) film_grads_kernel(const float* __restrict
                                                          const float* __restrict__ sg, const float* __restrict__ sb,
                                                          int n, int out_f32, void* __restrict__ dg,
                                                          void* __restrict__ dbt, float* __restrict__ dsg,
-                                                         float* __restrict__ dsb) {
+                                                         float* __restrict__ dsb, const float* __restrict__ l2_sg,
+                                                         const float* __restrict__ l2_sb, int accum) {
   __shared__ float red[2][256];
   const float a = *sg, c = *sb;
   float s1 = 0.f, s2 = 0.f;
   for (int i = threadIdx.x; i < n; i += 256) {
     const float x1 = S1[i], x2 = S2[i];
     if (out_f32) {
-      reinterpret_cast<float*>(dg)[i] = x1 * a;
-      reinterpret_cast<float*>(dbt)[i] = x2 * c;
-    } else {
-      reinterpret_cast<bf16_t*>(dg)[i] = f2bf(x1 * a);
-      reinterpret_cast<bf16_t*>(dbt)[i] = f2bf(x2 * c);
+      float* pg = reinterpret_cast<float*>(dg) + i;
+      float* pb = reinterpret_cast<float*>(dbt) + i;
+      *pg = accum ? *pg + x1 * a : x1 * a;
+      *pb = accum ? *pb + x2 * c : x2 * c;
+    } else {  // accumulate rounds like autograd's bf16 add of per-site gradients (fp32 add, one rounding)
+      bf16_t* pg = reinterpret_cast<bf16_t*>(dg) + i;
+      bf16_t* pb = reinterpret_cast<bf16_t*>(dbt) + i;
+      *pg = f2bf(accum ? bf2f(*pg) + x1 * a : x1 * a);
+      *pb = f2bf(accum ? bf2f(*pb) + x2 * c : x2 * c);
     }
     s1 += x1 * g[i];
     s2 += x2 * bt[i];
@@ -1174,17 +1183,17 @@ __global__ void __launch_bounds__(256) film_grads_kernel(const float* __restrict
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    dsg[0] = red[0][0];
-    dsb[0] = red[1][0];
+  if (threadIdx.x == 0) {  // + the FiLM L2 term's gradient of this site's scalars, when folded in
+    dsg[0] = l2_sg ? red[0][0] + l2_sg[0] : red[0][0];
+    dsb[0] = l2_sb ? red[1][0] + l2_sb[0] : red[1][0];
   }
 }
 }  // namespace
 
 SSAMD_API int ssamd_film_grads(const float* S1, const float* S2, const float* g, const float* bt, const float* sg,
                                const float* sb, int n, int out_f32, void* dg, void* dbt, float* dsg, float* dsb,
-                               hipStream_t s) {
+                               const float* l2_sg, const float* l2_sb, int accum, hipStream_t s) {
   hipLaunchKernelGGL(film_grads_kernel, dim3(1), dim3(256), 0, s, S1, S2, g, bt, sg, sb, n, out_f32, dg, dbt, dsg,
-                     dsb);
+                     dsb, l2_sg, l2_sb, accum);
   return (int)hipGetLastError();
 }

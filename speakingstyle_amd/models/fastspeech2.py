@@ -316,11 +316,21 @@ class FastSpeech2(nn.Module):
     def film_scalars(self):
         """Stacked s_gamma/s_beta parameters (reference ``utils/model.py:53-59``).  The parameter
         list is collected once (named_parameters() walks the whole module tree every call)."""
+        ps = self._film_param_list()
+        if not ps:
+            return None
+        if ops.use_hip(ps[0]):
+            from ..ops import hip
+
+            return hip.film_scalars_cat(ps)  # L2 gradient folded into the sites' FiLM kernels
+        return torch.cat(ps)
+
+    def _film_param_list(self):
         ps = self.__dict__.get("_film_ps")
         if ps is None:
             ps = [p for n, p in self.named_parameters() if ("s_gamma" in n or "s_beta" in n)]
             self.__dict__["_film_ps"] = ps
-        return torch.cat(ps) if ps else None
+        return ps
 
     def compute_style(self, mels, mel_lens, max_mel_len, batch, device, style_weights=None):
         enc = self.style_encoder()
@@ -334,7 +344,10 @@ class FastSpeech2(nn.Module):
             return (z, z)
         else:
             g, b = enc(mels.to(self.compute_dtype), mel_lens, max_mel_len)
-        return (g.to(self.compute_dtype), b.to(self.compute_dtype))
+        g, b = g.to(self.compute_dtype), b.to(self.compute_dtype)
+        if ops.use_hip(g):  # fresh per forward: its LayerNorm sites may share one gradient buffer (_FilmAcc)
+            g._ssamd_film_acc = b._ssamd_film_acc = True
+        return (g, b)
 
     # ------------------------------------------------------------------ forward
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None, max_mel_len=None,
@@ -344,6 +357,12 @@ class FastSpeech2(nn.Module):
         batch's mel lengths, provided by the data pipeline) enables the packed decoder in training."""
         dev = texts.device
         cd = self.compute_dtype
+        if torch.is_grad_enabled() and ops.use_hip(texts):
+            ps = self._film_param_list()
+            if ps:  # the FiLM-L2 holder exists before the sites' forward (same hook pattern every step)
+                from ..ops import gradslots
+
+                gradslots.film_holder_for(ps)
         if mel_lens_host is None and mel_lens is not None:
             mel_lens_host = getattr(mel_lens, "host_lengths", None)
         if mels is not None and max_mel_len is None:

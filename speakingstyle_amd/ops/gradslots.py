@@ -29,6 +29,60 @@ import torch
 
 _slots = {}      # id(p) -> (weakref(p), arena, offset)
 _claimed = set()
+_film_holders = {}  # tuple(id(p) of the FiLM scalars) -> FilmL2Holder
+_film_of = {}       # id(scalar) -> FilmL2Holder
+
+
+class FilmL2Holder:
+    """Rendezvous between the concat of the FiLM scalars (s_gamma / s_beta of every LayerNorm
+    site, fed to the ``lambda_f * sum(s^2)`` loss term) and the LayerNorm sites that own them.
+
+    Each scalar has two gradient sources: the L2 term and its site.  Left to autograd that is a
+    fresh gradient + an add + a copy into the arena slot per scalar (~80 tiny kernels for the 26
+    scalars of a styled model).  Instead the concat's backward -- which runs first: it was recorded
+    after the whole model forward -- parks the L2 gradient here and returns None, and each site's
+    FiLM-gradient kernel adds its two entries while writing the scalar gradients straight into
+    their slots.  Should a site run first (any other order), the concat returns plain gradients."""
+
+    def __init__(self, params):
+        self.index = {id(p): i for i, p in enumerate(params)}
+        self.grad = None            # fp32 [n] L2-term gradient of this step, or None
+        self.sites_started = False
+        self.pending = set()        # ids of the scalars a site used in this step's forward
+
+    def reset(self):
+        self.grad = None
+        self.sites_started = False
+
+    def register_site(self, p):
+        """Forward of a LayerNorm site using scalar ``p`` (grad enabled): its backward will fold the
+        L2 entry in.  Scalars no site used (pitch / energy predictors run without style) get their
+        L2 gradient from the concat as usual."""
+        if id(p) in self.index:
+            self.pending.add(id(p))
+
+    def entry(self, p):
+        """This step's L2 gradient entry of scalar ``p`` (a [1] view), or None."""
+        self.sites_started = True
+        if self.grad is None or p is None:
+            return None
+        i = self.index.get(id(p))
+        return None if i is None else self.grad[i:i + 1]
+
+
+def film_holder_for(params) -> FilmL2Holder:
+    key = tuple(id(p) for p in params)
+    h = _film_holders.get(key)
+    if h is None:
+        h = FilmL2Holder(params)
+        _film_holders[key] = h
+        for p in params:
+            _film_of[id(p)] = h
+    return h
+
+
+def film_holder(p) -> Optional[FilmL2Holder]:
+    return None if p is None else _film_of.get(id(p))
 
 
 def register(p: torch.nn.Parameter, arena, offset: int):
@@ -41,6 +95,9 @@ def unregister(p: torch.nn.Parameter):
 
 def reset():
     _claimed.clear()
+    for h in _film_holders.values():  # no L2 gradient / site registration survives into the next step
+        h.reset()
+        h.pending.clear()
 
 
 def _entry(p):

@@ -49,7 +49,7 @@ _SIGS = {
     "ssamd_wgrad_set_buf": [I],
     "ssamd_gemm_set_buf": [I],
     "ssamd_wgrad_set_prio": [I],
-    "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P],
+    "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],
     "ssamd_attn_set_fwd": [I, I],
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],
@@ -720,6 +720,67 @@ def _f32_view(t):
     return v
 
 
+class _FilmAcc:
+    """Running d gamma / d beta of the LayerNorm sites sharing one FiLM (gamma, beta) pair -- used
+    for the model's style tensors (fresh per forward, marked ``_ssamd_film_acc``), never for a
+    tensor reused across graphs (a leaf fed to several forwards gets per-site gradients).  The
+    first site to run backward returns the buffer (a view in gamma's shape/dtype: autograd keeps it
+    as-is in the producer's input buffer), the later sites add into it in place and return None.
+    The producer of gamma / beta runs only after every site reachable in this backward, so it reads
+    the complete sum -- one gradient instead of one per site plus an autograd add per extra site."""
+
+    __slots__ = ("ref", "buf")
+
+    def __init__(self, g):
+        self.ref = weakref.ref(g)
+        self.buf = None
+
+
+_FILM_ACC = {}
+
+
+def _film_acc(g):
+    key = (g.data_ptr(), g._version, tuple(g.shape), g.dtype)
+    acc = _FILM_ACC.get(key)
+    if acc is None or acc.ref() is not g:
+        if len(_FILM_ACC) > 64:
+            _FILM_ACC.clear()
+        acc = _FilmAcc(g)
+        _FILM_ACC[key] = acc
+    return acc
+
+
+class _FilmCatFn(torch.autograd.Function):
+    """torch.cat of the FiLM scalars whose backward parks the L2 term's gradient in the
+    gradslots.FilmL2Holder (folded in by the sites' film_grads kernels) instead of returning it."""
+
+    @staticmethod
+    def forward(ctx, holder, *ps):
+        holder.reset()
+        ctx.holder = holder
+        ctx.ids = [id(p) for p in ps]
+        return torch.cat([p.detach().reshape(-1) for p in ps])
+
+    @staticmethod
+    def backward(ctx, g):
+        h = ctx.holder
+        pend, h.pending = h.pending, set()
+        if h.sites_started or not pend:  # a site already ran / none will: plain per-scalar gradients
+            return (None, *[g[i:i + 1] for i in range(g.numel())])
+        h.grad = g.float().contiguous()  # the sites in ``pend`` fold their entries in
+        return (None, *[None if k in pend else g[i:i + 1] for i, k in enumerate(ctx.ids)])
+
+
+def film_scalars_cat(ps):
+    """Concat of the FiLM scalar parameters (``[1]`` each) for the ``lambda_f`` L2 loss term."""
+    if not ps:
+        return None
+    if not (torch.is_grad_enabled() and ps[0].is_cuda and all(p.numel() == 1 for p in ps)
+            and any(p.requires_grad for p in ps)):
+        return torch.cat(ps)
+    return _FilmCatFn.apply(gradslots.film_holder_for(ps), *ps)
+
+
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox, fused=None):
@@ -742,6 +803,16 @@ class _AddLNFn(torch.autograd.Function):
         ctx.cu = cu
         ctx.mailbox = mailbox
         ctx.film_scales = (sg, sb)  # the Parameters themselves: gradient-slot owners
+        for k, p in ((6, sg), (7, sb)):
+            hold = gradslots.film_holder(p) if ctx.needs_input_grad[k] else None
+            if hold is not None:
+                hold.register_site(p)
+        ctx.acc = None
+        if (g is not None and bt is not None and getattr(g, "_ssamd_film_acc", False)
+                and g.dtype == bt.dtype and g.dtype in (torch.float32, torch.bfloat16)
+                and g.shape == bt.shape and g.numel() == B * C):
+            ctx.acc = _film_acc(g)
+            ctx.gshape = g.shape
         ctx.save_for_backward(ac, rc_, w, b, gf, bf, sg, sb, lens, mean, rstd)
         ctx.cfg = (B, L, C, pre_p, post_p, seed, res is not None, g is not None)
         ctx.gdtype = None if g is None else (g.dtype, bt.dtype)
@@ -780,18 +851,36 @@ class _AddLNFn(torch.autograd.Function):
             dsb = (S2 * bf).sum().reshape(1)
         elif has_film:  # one kernel: d gamma, d beta and the two scale gradients (into their slots)
             f32 = ctx.gdtype[0] == torch.float32
-            dg = torch.empty(S1.shape, device=S1.device, dtype=torch.float32 if f32 else torch.bfloat16)
-            dbt = torch.empty_like(dg)
-            dsg = gradslots.claim(ctx.film_scales[0])
-            dsb = gradslots.claim(ctx.film_scales[1])
+            acc = ctx.acc if (ctx.needs_input_grad[4] and ctx.needs_input_grad[5]) else None
+            first = False
+            if acc is not None:  # sites sharing gamma / beta: one running sum (see _FilmAcc)
+                first = acc.buf is None
+                if first:
+                    acc.buf = torch.empty((2,) + tuple(S1.shape), device=S1.device, dtype=ctx.gdtype[0])
+                dg, dbt = acc.buf[0], acc.buf[1]
+                f32 = ctx.gdtype[0] == torch.float32
+            else:
+                dg = torch.empty(S1.shape, device=S1.device, dtype=torch.float32 if f32 else torch.bfloat16)
+                dbt = torch.empty_like(dg)
+            ps_g, ps_b = ctx.film_scales
+            hold = gradslots.film_holder(ps_g) or gradslots.film_holder(ps_b)
+            l2g = l2b = None
+            if hold is not None:
+                l2g, l2b = hold.entry(ps_g), hold.entry(ps_b)
+            dsg = gradslots.claim(ps_g)
+            dsb = gradslots.claim(ps_b)
             if dsg is None:
                 dsg = torch.empty(1, device=S1.device, dtype=torch.float32)
             if dsb is None:
                 dsb = torch.empty(1, device=S1.device, dtype=torch.float32)
             rc = lib().ssamd_film_grads(_ptr(S1), _ptr(S2), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb), S1.numel(),
-                                        int(f32), _ptr(dg), _ptr(dbt), _ptr(dsg), _ptr(dsb), _stream())
+                                        int(f32), _ptr(dg), _ptr(dbt), _ptr(dsg), _ptr(dsb),
+                                        _ptr(l2g), _ptr(l2b), int(acc is not None and not first), _stream())
             _check(rc, "ssamd_film_grads")
-            dg, dbt = dg.to(ctx.gdtype[0]), dbt.to(ctx.gdtype[1])
+            if acc is not None:
+                dg, dbt = (dg.view(ctx.gshape), dbt.view(ctx.gshape)) if first else (None, None)
+            else:
+                dg, dbt = dg.to(ctx.gdtype[0]), dbt.to(ctx.gdtype[1])
         return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None, None
 
 

@@ -381,6 +381,61 @@ def test_model_step_hip_vs_reference(cfg):
     assert not bad, bad[:10]
 
 
+@pytest.mark.gpu
+def test_film_l2_folded_into_site_gradients():
+    """FiLM scalars with a dominant L2 term (lambda_f = 5): the concat's backward parks the L2
+    gradient and each LayerNorm site's film_grads kernel folds it in, writing every scalar gradient
+    straight into its arena slot (no copy); gamma / beta gradients of the sites are summed in one
+    running buffer.  Scalar and style-encoder gradients vs the torch fp32 model."""
+    import copy
+
+    from speakingstyle_amd import ops
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+    from speakingstyle_amd.models.loss import FastSpeech2Loss
+    from speakingstyle_amd.train.optim import FlatArena
+
+    pp, mc, tc = load_named("BC2013")
+    tc["loss"]["lambda_f"] = 5.0
+    torch.manual_seed(3)
+    m = FastSpeech2(pp, mc).to(DEV).eval()
+    with torch.no_grad():  # distinct, non-trivial scalars so each L2 entry lands on its own site
+        for i, (n, p) in enumerate((n, p) for n, p in m.named_parameters() if p.numel() == 1):
+            p.fill_(0.2 + 0.05 * i if "s_gamma" in n else -0.1 - 0.03 * i)
+    mr = copy.deepcopy(m)
+    m.set_compute_dtype(torch.bfloat16)
+    arena = FlatArena(list(reversed(list(m.parameters()))), groups=m.fused_param_groups())
+    b = SyntheticBatches(4, device=DEV, seed=5, phone_counts=[30, 45, 52, 25]).make_batch()
+    lossf = FastSpeech2Loss(pp, tc)
+    lo = lossf(b, m(*b[2:]), m.film_scalars())
+    lo[0].backward()
+    names = {id(p): n for n, p in m.named_parameters()}
+    copied = [names[id(p)] for p in arena.params if p.grad is not None and p.grad.data_ptr() != arena._slot_ptr[id(p)]]
+    arena.finalize_grads()
+    # pitch / energy predictors run without style (no site): their scalars only have the L2 gradient
+    sited = [n for n in copied if ("s_gamma" in n or "s_beta" in n)
+             and "pitch_predictor" not in n and "energy_predictor" not in n]
+    assert not sited, copied
+    ops.set_backend("reference")
+    try:
+        lr_ = lossf(b, mr(*b[2:]), mr.film_scalars())
+        lr_[0].backward()
+    finally:
+        ops.set_backend(None)
+    gr = dict(mr.named_parameters())
+    bad = []
+    for n, p in m.named_parameters():
+        if p.numel() == 1 and gr[n].grad is not None:
+            assert p.grad is not None, n
+            if abs(p.grad.item() - gr[n].grad.item()) > 0.05 * abs(gr[n].grad.item()) + 1e-3:
+                bad.append((n, p.grad.item(), gr[n].grad.item()))
+        elif n.startswith("reference_encoder") and gr[n].grad is not None and gr[n].grad.norm() > 1e-6:
+            if _rel(p.grad, gr[n].grad) > 0.15:
+                bad.append((n, _rel(p.grad, gr[n].grad)))
+    assert not bad, bad[:10]
+
+
 @pytest.mark.parametrize("C,act,training,out_f32", [(512, True, True, False), (80, False, True, True), (512, True, False, False)])
 def test_bn_act(C, act, training, out_f32):
     torch.manual_seed(10)
