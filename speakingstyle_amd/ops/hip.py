@@ -469,13 +469,15 @@ def colsum_raw(dy, N, db=None):
     return db
 
 
-def relu_mask_(dy, y):
-    """dy *= (y > 0) in place (bf16)."""
+def relu_mask_(dy, y, out=None):
+    """out = dy * (y > 0) (bf16); in place into dy when ``out`` is None."""
     _need(dy, torch.bfloat16, "relu_mask.dy")
     _need(y, torch.bfloat16, "relu_mask.y")
-    rc = lib().ssamd_relu_mask(_ptr(dy), _ptr(y), _ptr(dy), dy.numel(), _stream())
+    assert dy.is_contiguous() and y.is_contiguous() and y.numel() == dy.numel()
+    out = dy if out is None else out
+    rc = lib().ssamd_relu_mask(_ptr(dy), _ptr(y), _ptr(out), dy.numel(), _stream())
     _check(rc, "ssamd_relu_mask")
-    return dy
+    return out
 
 
 # ------------------------------------------------------------------------ conv / linear
@@ -505,7 +507,7 @@ class _ConvFn(torch.autograd.Function):
         B, L, Cin, ks, dil, pad, N = ctx.geom
         dy = dy.to(torch.bfloat16).contiguous()
         if ctx.act == "relu":
-            dy = relu_mask_(dy.clone(), y)
+            dy = relu_mask_(dy, y, out=torch.empty_like(dy))  # out of place: dy may be shared
         elif ctx.act is not None:
             raise NotImplementedError("backward for activation " + str(ctx.act))
         dx = dw = db = None
