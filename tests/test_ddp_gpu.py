@@ -44,17 +44,21 @@ def _capture(tr):
     return grads
 
 
-def test_rccl_bucket_path_single_rank():
+@pytest.mark.parametrize("name", ["LJSpeech", "BC2013"])
+def test_rccl_bucket_path_single_rank(name):
+    """BC2013 adds the FiLM sites: scalar gradients folded with the L2 term into their slots and the
+    shared style gamma/beta buffer must keep the per-parameter hook counts stable across steps."""
     import torch.distributed as dist
 
     from speakingstyle_amd.config import load_named
     from speakingstyle_amd.data.synthetic import SyntheticBatches
     from speakingstyle_amd.parallel import ddp
 
-    pp, mc, tc = load_named("LJSpeech")
+    pp, mc, tc = load_named(name)
     mc["transformer"]["encoder_layer"] = mc["transformer"]["decoder_layer"] = 2
     cfg = (pp, mc, tc)
-    batches = [SyntheticBatches(8, device="cuda", seed=3 + i).make_batch() for i in range(3)]
+    fl = pp["preprocessing"]["pitch"]["feature"] == "frame_level"
+    batches = [SyntheticBatches(8, device="cuda", seed=3 + i, frame_level=fl).make_batch() for i in range(3)]
 
     ref = _trainer(cfg)
     g_ref = _capture(ref)
