@@ -345,7 +345,7 @@ class FastSpeech2(nn.Module):
         else:
             g, b = enc(mels.to(self.compute_dtype), mel_lens, max_mel_len)
         g, b = g.to(self.compute_dtype), b.to(self.compute_dtype)
-        if ops.use_hip(g):  # fresh per forward: its LayerNorm sites may share one gradient buffer (_FilmAcc)
+        if ops.use_hip(g):  # fresh per forward, read only by FiLM LayerNorm sites: one shared gradient buffer (_FilmAcc)
             g._ssamd_film_acc = b._ssamd_film_acc = True
         return (g, b)
 

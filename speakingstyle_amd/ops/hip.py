@@ -729,7 +729,10 @@ class _FilmAcc:
     first site to run backward returns the buffer (a view in gamma's shape/dtype: autograd keeps it
     as-is in the producer's input buffer), the later sites add into it in place and return None.
     The producer of gamma / beta runs only after every site reachable in this backward, so it reads
-    the complete sum -- one gradient instead of one per site plus an autograd add per extra site."""
+    the complete sum -- one gradient instead of one per site plus an autograd add per extra site.
+    Contract: a marked tensor is consumed ONLY by FiLM LayerNorm sites (true for the model's style
+    gamma / beta); another consumer's gradient could be added out of place before the later sites
+    add theirs into the buffer."""
 
     __slots__ = ("ref", "buf")
 
