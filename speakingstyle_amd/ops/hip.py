@@ -123,7 +123,9 @@ def has(name: str) -> bool:
 
 
 def _ptr(t: Optional[torch.Tensor]):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """Device address as a plain int: every entry point has ``argtypes`` (_SIGS), so ctypes converts
+    it to a pointer itself -- no c_void_p object per operand (~3k per training step)."""
+    return None if t is None else t.data_ptr()
 
 
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
@@ -134,8 +136,8 @@ def _stream():
     """Current HIP stream handle.  The raw getter skips building a torch Stream object (and its
     device-guard calls) for every launch: ~10 us of host time per op on the hot path."""
     if _raw_stream is not None and _cur_dev is not None:
-        return ctypes.c_void_p(_raw_stream(_cur_dev()))
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return _raw_stream(_cur_dev())
+    return torch.cuda.current_stream().cuda_stream
 
 
 def _check(rc, name):
