@@ -21,6 +21,7 @@
 // register staging (one barrier per K-step), XOR-swizzled LDS images (conflict-free
 // ds_read_b128 / tr reads), XCD-aware bijective block remap so that the 8 blocks
 // that share an A panel run on one XCD's L2.
+#include <mutex>
 #include "common.h"
 #include <type_traits>
 
@@ -2778,8 +2779,37 @@ SSAMD_API void ssamd_gemm_set_ngrp(int v) { g_gemm_ngrp = v; }
 SSAMD_API void ssamd_wgrad_set_prio(int v) { g_wgrad_prio = v; }
 static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 split-K + reduce)
 static int g_num_cus_gemm = 256;
-static void* g_splitk_ws = nullptr;
-static size_t g_splitk_bytes = 0;
+// Split-K fp32 partials: one workspace per (device, stream).  A process-global buffer would hand a
+// foreign-device pointer to a second GPU and let GEMMs on two streams race on the same partials.
+struct SplitKWs { int dev; hipStream_t s; void* p; size_t bytes; };
+static SplitKWs g_splitk_ws[32];
+static int g_splitk_nws = 0;
+static std::mutex g_splitk_mu;
+// Workspace of >= need bytes for (current device, s), or nullptr.  Sized once to 64 MiB (S * tiles <=
+// 256 CUs bounds every split-K workspace by 256 tiles x 256 KiB): a regrow would hipFree, a device-wide
+// synchronisation in the middle of a training step.
+static void* splitk_workspace(hipStream_t s, size_t need) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_splitk_mu);
+  SplitKWs* e = nullptr;
+  for (int i = 0; i < g_splitk_nws; ++i)
+    if (g_splitk_ws[i].dev == dev && g_splitk_ws[i].s == s) e = &g_splitk_ws[i];
+  if (!e) {
+    if (g_splitk_nws == 32) return nullptr;
+    e = &g_splitk_ws[g_splitk_nws++];
+    *e = SplitKWs{dev, s, nullptr, 0};
+  }
+  if (need > e->bytes) {
+    const size_t want = need > ((size_t)64 << 20) ? need : ((size_t)64 << 20);
+    if (e->p) (void)hipFree(e->p);
+    e->p = nullptr;
+    e->bytes = 0;
+    if (hipMalloc(&e->p, want) != hipSuccess) return nullptr;
+    e->bytes = want;
+  }
+  return e->p;
+}
 SSAMD_API void ssamd_gemm_set_splitk(int v) { g_splitk = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
@@ -2848,18 +2878,8 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       // costs more than it saves: M = 10800 / 43 tiles: S = 4 81 us, S = 6 111 us, unsplit 149 us)
       S = min(min(8, g_num_cus_gemm / tiles), nk64 / 6);
     if (S > 1 && plain && reg && N >= 256 && (N % 8) == 0 && ldy == N && act >= 0 && (ldy % 8) == 0) {
-      const size_t need = (size_t)S * g.M * N * sizeof(float);
-      if (need > g_splitk_bytes) {
-        // S * tiles <= 256 CUs bounds every split-K workspace by 256 tiles x 256 KiB = 64 MiB: allocate
-        // that once (the first split-K call, a warm-up step) -- a regrow would hipFree, a device-wide
-        // synchronisation in the middle of a training step
-        const size_t want = need > ((size_t)64 << 20) ? need : ((size_t)64 << 20);
-        if (g_splitk_ws) (void)hipFree(g_splitk_ws);
-        g_splitk_ws = nullptr;
-        g_splitk_bytes = 0;
-        if (hipMalloc(&g_splitk_ws, want) != hipSuccess) return -4;
-        g_splitk_bytes = want;
-      }
+      void* ws = splitk_workspace(s, (size_t)S * g.M * N * sizeof(float));
+      if (!ws) return -4;
       static bool sk_set = false;
       if (!sk_set) {
         allow_lds(conv_gemm_big64_kernel<true, true, false>, B64_LDS);
@@ -2877,10 +2897,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
                          : (bf ? conv_gemm_big64_kernel<true, true, false, true>
                                : fastk ? conv_gemm_big64_kernel<true, true, false> : conv_gemm_big64_kernel<true, false, false>);
       hipLaunchKernelGGL(kfn, dim3(tiles, S), dim3(NT3), B64_LDS, s, X, W, nullptr, nullptr, nullptr, nullptr,
-                         g_splitk_ws, g, 0, N, EpiX{});
+                         ws, g, 0, N, EpiX{});
       const long nthr = (long)g.M * (N / 8);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(nthr, 256)), dim3(256), 0, s,
-                         reinterpret_cast<const float*>(g_splitk_ws), S, (long)g.M, N, bias, aux, resid, lens, g.L,
+                         reinterpret_cast<const float*>(ws), S, (long)g.M, N, bias, aux, resid, lens, g.L,
                          act, out_f32, Y);
       return (int)hipGetLastError();
     }

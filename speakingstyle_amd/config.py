@@ -91,15 +91,20 @@ _TRAIN_DEFAULTS: Config = {
     },
     "step": {"total_step": 900000, "log_step": 100, "synth_step": 1000, "val_step": 1000, "save_step": 10000},
     "mi355x": {
-        "dtype": "bf16",          # activation / GEMM operand dtype on GPU
+        # activation / GEMM operand dtype on the GPU: bf16 (HIP kernels, fp32 master weights + Adam
+        # state) or fp32 (torch reference ops in fp32 -- a numerics oracle, not a fast path)
+        "dtype": "bf16",
         "bucket_mb": 32,          # DDP gradient bucket size (fp32 MiB)
         "seed": 1234,
         "num_workers": 4,
-        "frames_per_gpu": None,   # optional frame budget per rank (overrides batch_size)
+        # per-rank frame budget: each GPU trains on its own batch of <= this many PADDED mel frames
+        # (data/dataset.py FrameBudgetSampler) instead of batch_size / world utterances of a global batch
+        "frames_per_gpu": None,
+        "max_batch_per_gpu": None,  # optional utterance cap of a frame-budget batch
         "phase_timing": False,    # per-phase host / device step timing (Perf/phase_* TB scalars)
         "preempt_check_steps": 10,  # DP: steps between cross-rank SIGTERM agreements
-        "nan_guard": True,        # skip the optimizer step if the loss is non-finite
-        "hip_kernels": True,      # False => torch reference ops even on GPU (debug only)
+        "hip_kernels": True,      # False => torch reference ops even on GPU (debug / A-B only)
+        # (non-finite steps are always skipped on the device by the fused clip+Adam kernel: no knob)
     },
 }
 
@@ -186,6 +191,12 @@ def normalize_train_config(cfg: Config | None) -> Config:
     out["loss"] = loss
     if out["optimizer"]["grad_acc_step"] < 1:
         raise ConfigError("optimizer.grad_acc_step must be >= 1")
+    mi = out["mi355x"]
+    _check_enum(mi["dtype"], ["bf16", "fp32"], "mi355x.dtype")
+    if mi.get("frames_per_gpu") is not None and int(mi["frames_per_gpu"]) <= 0:
+        raise ConfigError("mi355x.frames_per_gpu must be a positive frame count (or null)")
+    if "nan_guard" in mi:  # removed knob: the device-side non-finite skip is unconditional
+        mi.pop("nan_guard")
     return out
 
 

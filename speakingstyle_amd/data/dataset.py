@@ -117,11 +117,24 @@ class Dataset(_TorchDataset):
             self._tlens = np.array([len(text_to_sequence(t, self.cleaners)) for t in self.text], dtype=np.int64)
         return self._tlens
 
+    def mel_lengths(self) -> np.ndarray:
+        """Mel frames per utterance, read from the ``.npy`` headers only (memory-mapped, no data
+        pages touched); cached.  Sizes the frame-budget batches (``FrameBudgetSampler``)."""
+        if getattr(self, "_mlens", None) is None:
+            out = np.empty(len(self.text), dtype=np.int64)
+            for i, (spk, base) in enumerate(zip(self.speaker, self.basename)):
+                path = os.path.join(self.preprocessed_path, "mel", f"{spk}-mel-{base}.npy")
+                out[i] = np.load(path, mmap_mode="r").shape[0]
+            self._mlens = out
+        return self._mlens
+
     def collate_local(self, data):
         """Collate for ``ShardedGroupSampler``: ``data`` is this rank's rows of one global
         group, already in the global (length-sorted) batch order; split it back into
-        the per-batch shards."""
+        the per-batch shards.  ``FrameBudgetSampler`` items are one batch each."""
         sizes = self._local_sizes
+        if sizes is None:
+            return [self.reprocess(data, list(range(len(data))))]
         out, o = [], 0
         for n in sizes:
             if n:
@@ -149,6 +162,11 @@ class ShardedGroupSampler:
         self.rank, self.world = int(rank), int(world)
         self.seed, self.epoch, self.start = int(seed), int(epoch), int(start)
         self.drop_last = drop_last
+        if self.bs < self.world:
+            # some rank would get an empty shard of every batch, skip its train steps and leave the
+            # others waiting in the next collective until the timeout
+            raise ValueError(f"batch_size={self.bs} < world size {self.world}: every rank needs at least one "
+                             "utterance per batch (raise batch_size or set mi355x.frames_per_gpu)")
         self.tlens = dataset.text_lengths()
         dataset._local_sizes = [len(range(self.rank, self.bs, self.world))] * self.group
 
@@ -168,6 +186,75 @@ class ShardedGroupSampler:
             for k in range(self.group):
                 local.extend(idx[k * self.bs:(k + 1) * self.bs][self.rank::self.world].tolist())
             yield local
+
+
+class FrameBudgetSampler:
+    """Per-GPU frame budget (``mi355x.frames_per_gpu``): every rank gets a batch whose PADDED mel
+    frame count ``n * max(len)`` stays within ``budget`` -- the batch shape is sized for the GPU's
+    memory instead of a global utterance count split ``world`` ways.
+
+    Every rank computes the same plan from ``seed + epoch`` and the utterance lengths (no
+    communication): the shuffled corpus is cut into pools of ``pool`` utterances, each pool is
+    sorted by mel length (descending) and cut greedily into budget-sized batches, and consecutive
+    runs of ``world`` batches form one global step -- rank ``r`` takes the ``r``-th.  All ranks
+    therefore run the same number of steps, with similar lengths (neighbours in the sorted pool).
+    The loss divides by the all-reduced valid counts, so the DP=N gradient equals the single-process
+    gradient of the union of the N batches.  ``max_batch`` optionally caps the utterance count.
+
+    Items are one batch each; ``start`` = global steps already consumed (resumable)."""
+
+    def __init__(self, dataset: "Dataset", budget: int, rank: int = 0, world: int = 1, seed: int = 1234,
+                 epoch: int = 0, start: int = 0, pool: int = 4096, max_seq_len: int = 1000,
+                 max_batch: Optional[int] = None, mel_lens: Optional[np.ndarray] = None):
+        self.ds = dataset
+        self.budget = int(budget)
+        self.rank, self.world = int(rank), int(world)
+        self.seed, self.epoch, self.start = int(seed), int(epoch), int(start)
+        self.pool = int(pool)
+        self.max_batch = max_batch
+        lens = dataset.mel_lengths() if mel_lens is None else np.asarray(mel_lens)
+        self.lens = np.minimum(lens, max_seq_len)
+        if self.budget < int(self.lens.max(initial=1)):
+            raise ValueError(f"frames_per_gpu={self.budget} is smaller than the longest utterance "
+                             f"({int(self.lens.max())} frames after the max_seq_len cap)")
+        if dataset is not None:
+            dataset._local_sizes = None
+        self._plan_epoch = None
+
+    def plan(self):
+        """[global step][rank] -> utterance indices of this epoch."""
+        if self._plan_epoch == self.epoch:
+            return self._plan
+        g = torch.Generator().manual_seed(self.seed + self.epoch)
+        perm = torch.randperm(len(self.lens), generator=g).numpy()
+        batches = []
+        for p0 in range(0, len(perm), self.pool):
+            idx = perm[p0:p0 + self.pool]
+            idx = idx[np.argsort(-self.lens[idx], kind="stable")]
+            cur = []
+            for i in idx.tolist():
+                longest = self.lens[cur[0]] if cur else self.lens[i]
+                full = (len(cur) + 1) * longest > self.budget or (self.max_batch and len(cur) >= self.max_batch)
+                if cur and full:
+                    batches.append(cur)
+                    cur = []
+                cur.append(i)
+            if cur:
+                batches.append(cur)
+        n = len(batches) // self.world  # the tail that cannot give every rank a batch is dropped
+        steps = [batches[k * self.world:(k + 1) * self.world] for k in range(n)]
+        # shuffle the global steps (pool-internal order would run long batches first every pool)
+        order = torch.randperm(len(steps), generator=g).numpy() if steps else []
+        self._plan = [steps[k] for k in order]
+        self._plan_epoch = self.epoch
+        return self._plan
+
+    def __len__(self):
+        return max(0, len(self.plan()) - self.start)
+
+    def __iter__(self):
+        for step in self.plan()[self.start:]:
+            yield step[self.rank]
 
 
 class TextDataset(_TorchDataset):

@@ -11,6 +11,13 @@ length and split into batches, which bounds the padding per batch.
 
 Batches are the reference's 12-tuple with tensors already
 on ``device`` (no host->device copies in the timed loop).
+
+Frame budget (``frames_per_batch``, the ``mi355x.frames_per_gpu`` knob): instead
+of a fixed utterance count, a pool of utterances is sorted by mel length and cut
+into batches whose PADDED frame count ``n * max(len)`` stays within the budget
+(the PostNet runs on the padded layout, so that is the memory-relevant size);
+the utterance count per batch then varies with the lengths.  ``n_speakers > 1``
+draws speaker ids uniformly (multi-speaker configs, e.g. LibriTTS's 904).
 """
 from __future__ import annotations
 
@@ -42,8 +49,13 @@ def ljspeech_phone_counts(path: str = _LJ_META) -> Optional[np.ndarray]:
 class SyntheticBatches:
     def __init__(self, batch_size: int, device="cpu", n_mel: int = 80, n_speakers: int = 1, max_seq_len: int = 1000,
                  pitch_range=(-2.9, 11.4), energy_range=(-1.4, 8.2), frame_level: bool = False, group_size: int = 4,
-                 seed: int = 1234, frames_per_phone: float = 8.1, vocab: int = 360, phone_counts=None):
+                 seed: int = 1234, frames_per_phone: float = 8.1, vocab: int = 360, phone_counts=None,
+                 frames_per_batch: Optional[int] = None):
         self.B = batch_size
+        self.frame_budget = int(frames_per_batch) if frames_per_batch else None
+        if self.frame_budget is not None and self.frame_budget < max_seq_len:
+            raise ValueError(f"frames_per_batch={self.frame_budget} cannot hold one utterance of up to "
+                             f"max_seq_len={max_seq_len} frames")
         self.device = torch.device(device)
         self.n_mel = n_mel
         self.n_speakers = n_speakers
@@ -75,12 +87,34 @@ class SyntheticBatches:
         return d
 
     def _refill(self):
+        if self.frame_budget is not None:
+            return self._refill_budget()
         n = self.B * self.group
         Ts = self.rng.choice(self.phone_counts, size=n)
         order = np.argsort(-Ts, kind="stable")
         for c in range(self.group):
             idx = order[c * self.B:(c + 1) * self.B]
             self._queue.append({"T": Ts[idx], "d": [self._durations(int(t)) for t in Ts[idx]]})
+        perm = self.rng.permutation(len(self._queue))
+        self._queue = [self._queue[i] for i in perm]
+
+    def _refill_budget(self):
+        """~``group`` budget-sized batches: a pool sorted by mel length (descending), cut greedily so
+        that ``count * longest <= frame_budget``."""
+        est = max(1, int(self.frame_budget / (self.fpp * float(np.mean(self.phone_counts)))))
+        Ts = self.rng.choice(self.phone_counts, size=est * self.group)
+        ds = [self._durations(int(t)) for t in Ts]
+        lens = np.array([min(int(d.sum()), self.max_seq_len) for d in ds])
+        order = np.argsort(-lens, kind="stable")
+        cur = []
+        for i in order:
+            longest = lens[cur[0]] if cur else lens[i]
+            if cur and (len(cur) + 1) * longest > self.frame_budget:
+                self._queue.append({"T": Ts[cur], "d": [ds[j] for j in cur]})
+                cur = []
+            cur.append(int(i))
+        if cur:
+            self._queue.append({"T": Ts[cur], "d": [ds[j] for j in cur]})
         perm = self.rng.permutation(len(self._queue))
         self._queue = [self._queue[i] for i in perm]
 
@@ -92,8 +126,8 @@ class SyntheticBatches:
     # ----------------------------------------------------------------- device side
     def make_batch(self, plan=None):
         plan = plan or self.next_plan()
-        B = self.B
         Ts = plan["T"].astype(np.int64)
+        B = len(Ts)
         ds = plan["d"]
         T = int(Ts.max())
         mel_lens = np.array([int(d.sum()) for d in ds], dtype=np.int64)

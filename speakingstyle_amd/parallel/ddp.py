@@ -19,7 +19,11 @@ Design (MI355X-first):
   graph), a parameter is final when its count is reached; a bucket is ready when
   all its counted parameters are final, and ready buckets are launched strictly
   in bucket-index order (bucket i only after 0..i-1), so every rank issues the
-  identical collective sequence regardless of hook timing.  With the ``nccl``
+  identical collective sequence regardless of hook timing.  Later steps are
+  checked against the calibration: a parameter accumulating MORE often than
+  calibrated raises in its hook (its bucket may already be on the wire -- adding
+  into it would race the all-reduce); fewer accumulations only hold the bucket
+  back to ``finish()`` (counted in ``mismatched_steps``).  With the ``nccl``
   backend (= RCCL on ROCm) the collective runs on RCCL's internal stream after
   an event wait on the compute stream, so it overlaps the rest of backward.
   ``finish()`` makes the compute stream wait for all buckets before the fused
@@ -171,10 +175,11 @@ class GradBuckets:
         self.launch_order: List[int] = []  # bucket indices in issue order (current step)
         self.last_launch_order: List[int] = []
         self.enabled = True
+        self.mismatched_steps = 0  # calibrated steps whose hook counts fell short (buckets launched at finish)
         self._handles = []
         if self.active:
-            for p in arena.params:
-                self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
+            for i, p in enumerate(arena.params):
+                self._handles.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
 
     # ------------------------------------------------------------------ internals
     def _launch(self, bi):
@@ -198,13 +203,32 @@ class GradBuckets:
                 if c > 0:
                     self.pending[self.bucket_of[i]] += 1
 
-    def _hook(self, p):
-        i = self.param_index[id(p)]
-        self.fired[i] += 1
+    def _make_hook(self, i):
+        """Per-parameter hook with its arena index bound (no dict lookup on the backward path)."""
+        def hook(p):
+            self._hook(p, i)
+        return hook
+
+    def _hook(self, p, i=None):
+        if i is None:
+            i = self.param_index[id(p)]
+        f = self.fired[i] + 1
+        self.fired[i] = f
         if not self.enabled:
             return
         self.arena.ensure_slot(p, i)  # gradients from plain-torch ops: into the bucket
-        if self.counts is None or self.fired[i] != self.counts[i]:
+        counts = self.counts
+        if counts is None:
+            return
+        c = counts[i]
+        if f != c:
+            if f > c:
+                # the bucket may already be on the wire: a further accumulation into its slot would
+                # race the all-reduce and silently desynchronise the replicas
+                raise RuntimeError(
+                    f"GradBuckets: parameter {i} accumulated {f} times this backward but {c} times in the "
+                    "calibration step (the graph changed after calibration); refusing to add into a "
+                    "gradient bucket that may already be in flight")
             return
         bi = self.bucket_of[i]
         self.pending[bi] -= 1
@@ -232,6 +256,10 @@ class GradBuckets:
             return
         if self.counts is None:
             self._calibrate()
+        elif self.fired != self.counts:
+            # fewer accumulations than calibrated (over-counts raise in the hook): the affected buckets
+            # were held back and go out below, still in index order on every rank -- correct, no overlap
+            self.mismatched_steps += 1
         for bi in range(self.next_launch, len(self.buckets)):
             self._launch(bi)
         for w in self.works:

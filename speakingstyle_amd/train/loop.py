@@ -35,28 +35,45 @@ from .trainer import Trainer
 def _batches(configs, device, rank, world, synthetic: bool, seed: int, pos=None):
     """Yields (epoch, group_index, [batches]); one item = one global group of
     ``group`` length-sorted batches, this rank's shard of each.  ``pos`` =
-    (epoch, groups consumed) resumes the data order exactly where a checkpoint left it."""
+    (epoch, groups consumed) resumes the data order exactly where a checkpoint left it.
+
+    Batch semantics (``mi355x.frames_per_gpu``):
+    * unset (reference ``train.py:27-45``): ``optimizer.batch_size`` is the GLOBAL batch, split
+      over the ranks (each gets ``batch_size / world`` utterances of every sorted batch);
+    * set: every rank gets its own batch of up to ``frames_per_gpu`` padded mel frames
+      (``FrameBudgetSampler``), so the per-GPU shape is sized for HBM and the global batch grows
+      with the world size; one item = one global step."""
     preprocess_config, model_config, train_config = configs
     bs = int(train_config["optimizer"]["batch_size"])
+    mi = train_config.get("mi355x", {}) or {}
+    budget = mi.get("frames_per_gpu")
+    max_len = int(model_config["max_seq_len"])
     if synthetic:
+        if not budget and bs < world:
+            raise ValueError(f"batch_size={bs} < world size {world}: set mi355x.frames_per_gpu or a larger batch")
         per_rank = max(1, bs // world)
-        gen = SyntheticBatches(per_rank, device=device, max_seq_len=model_config["max_seq_len"], seed=seed + rank,
-                               n_speakers=_n_speakers(preprocess_config),
+        gen = SyntheticBatches(per_rank, device=device, max_seq_len=max_len, seed=seed + rank,
+                               n_speakers=_n_speakers(preprocess_config), frames_per_batch=budget or None,
                                frame_level=preprocess_config["preprocessing"]["pitch"]["feature"] == "frame_level")
         gi = 0
         while True:
             yield 0, gi, [gen.make_batch()]
             gi += 1
-    from ..data.dataset import ShardedGroupSampler
+    from ..data.dataset import FrameBudgetSampler, ShardedGroupSampler
 
     dataset = Dataset("train.txt", preprocess_config, train_config, sort=True, drop_last=True)
     group = 4
-    assert bs * group < len(dataset), "batch_size * group_size must be < dataset size"
+    if not budget:
+        assert bs * group < len(dataset), "batch_size * group_size must be < dataset size"
     epoch, start = pos if pos else (0, 0)
     while True:
-        sampler = ShardedGroupSampler(dataset, bs, group, rank, world, seed=seed, epoch=epoch, start=start)
+        if budget:
+            sampler = FrameBudgetSampler(dataset, int(budget), rank, world, seed=seed, epoch=epoch, start=start,
+                                         max_seq_len=max_len, max_batch=mi.get("max_batch_per_gpu"))
+        else:
+            sampler = ShardedGroupSampler(dataset, bs, group, rank, world, seed=seed, epoch=epoch, start=start)
         loader = DataLoader(dataset, batch_sampler=sampler, collate_fn=dataset.collate_local,
-                            num_workers=int(train_config.get("mi355x", {}).get("num_workers", 4)),
+                            num_workers=int(mi.get("num_workers", 4)),
                             pin_memory=torch.cuda.is_available())
         for gi, batchs in enumerate(loader, start=start):
             yield epoch, gi, [to_device(b, device) for b in batchs]
@@ -91,9 +108,13 @@ def train(args, configs):
     restore = int(args.restore_step or 0)
     if getattr(args, "auto_resume", False) and not restore:
         restore = mutil.latest_step(train_config)
-    model, _opt_unused = None, None
+    mi = train_config.get("mi355x", {}) or {}
+    if cuda and (not mi.get("hip_kernels", True) or mi.get("dtype", "bf16") == "fp32"):
+        from .. import ops
+
+        ops.set_backend("reference")  # torch ops on the GPU (fp32 oracle runs / A-B debugging)
     model = mutil.FastSpeech2(preprocess_config, model_config).to(device)
-    model.set_compute_dtype(torch.bfloat16 if cuda else torch.float32)
+    model.set_compute_dtype(torch.bfloat16 if (cuda and mi.get("dtype", "bf16") == "bf16") else torch.float32)
     ckpt = None
     if restore:
         ckpt = mutil.load_checkpoint(mutil.ckpt_file(train_config, restore))
@@ -157,6 +178,7 @@ def train(args, configs):
         return bool(t.item() > 0)
 
     step = restore + 1
+    bs_global = int(train_config["optimizer"]["batch_size"])
     t_last = time.perf_counter()
     synthetic = getattr(args, "synthetic", False) or not os.path.exists(
         os.path.join(preprocess_config["path"]["preprocessed_path"], "train.txt"))
@@ -171,6 +193,11 @@ def train(args, configs):
                 if fail_at and step == fail_at:
                     raise RuntimeError(f"fault injection at step {step}")
                 losses, output, lr = trainer.train_step(batch)
+                if step == restore + 1:  # per-rank batch shape of the first step (DP batch semantics)
+                    budget = (train_config.get("mi355x") or {}).get("frames_per_gpu")
+                    rule = f"frames_per_gpu={budget}" if budget else f"batch_size/world={bs_global}/{world}"
+                    print(f"[rank {rank}] first batch: {len(batch[0])} utterances, {len(batch[0]) * int(batch[8])} "
+                          f"padded mel frames ({rule})", flush=True)
                 # position AFTER this batch: the next run starts at the following batch
                 pos = (epoch, gi + 1, 0) if k + 1 == len(batchs) else (epoch, gi, k + 1)
                 if step % log_step == 0:

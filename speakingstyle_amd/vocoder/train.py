@@ -123,7 +123,9 @@ def train(a):
 
     gen.train(); mpd.train(); msd.train()
     try:
-        for epoch in range(max(0, last_epoch + 1), a.training_epochs):
+        # the checkpoint's epoch is the one it was written in: resume INSIDE it (reference
+        # ``hifigan/train.py:105``), so the ExponentialLR decay stays aligned with an uninterrupted run
+        for epoch in range(max(0, last_epoch), a.training_epochs):
             t_ep = time.time()
             if sampler is not None:
                 sampler.set_epoch(epoch)

@@ -138,3 +138,74 @@ def test_slot_path_buckets_dp2():
         with torch.no_grad():
             arena.data.add_(arena.grad, alpha=-0.1)
         arena.zero_grad()
+
+
+class Toy2(Toy):
+    """``use_shared=False`` drops ``shared`` from the graph (it accumulates once per backward in the
+    calibration step)."""
+
+    def forward(self, x, use_shared=True):
+        h = SlotMatmul.apply(x, self.shared) if use_shared else x
+        for w in self.w:
+            h = torch.tanh(SlotMatmul.apply(h, w))
+        return (h ** 2).mean() + self.plain.sum()
+
+
+def _worker_changed(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from speakingstyle_amd.parallel import ddp
+
+    ddp.init_distributed("gloo")
+    model = Toy2()
+    arena = _arena(model)
+    gb = ddp.GradBuckets(arena, bucket_mb=16 * 16 * 4 * 1.5 / 2 ** 20)
+    out = {}
+    # step 0 calibrates; step 1 leaves `shared` out (fewer accumulations: its bucket is held back to
+    # finish(), still correct)
+    for step, use in ((0, True), (1, False)):
+        model(_data(rank, step), use).backward()
+        gb.finish()
+        out[step] = arena.grad.clone().numpy()
+        arena.zero_grad()
+    out["mismatched"] = gb.mismatched_steps
+    # step 2 runs a second backward before finish(): every parameter accumulates twice, into buckets
+    # the first backward already put on the wire -> must raise instead of corrupting them
+    model(_data(rank, 2)).backward()
+    try:
+        model(_data(rank, 3)).backward()
+        out["raised"] = None
+    except RuntimeError as e:
+        out["raised"] = str(e)
+    q.put((rank, out))
+    torch.distributed.destroy_process_group()
+
+
+def test_graph_change_after_calibration_dp2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_changed, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, o = q.get(timeout=300)
+        res[r] = o
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert res[r]["mismatched"] == 1
+        assert res[r]["raised"] is not None and "calibration" in res[r]["raised"]
+    model = Toy2()
+    arena = _arena(model)
+    for step, use in ((0, True), (1, False)):
+        for r in range(world):
+            model(_data(r, step), use).backward()
+        arena.finalize_grads()
+        torch.testing.assert_close(torch.from_numpy(res[0][step]), arena.grad, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(torch.from_numpy(res[1][step]), arena.grad, rtol=1e-5, atol=1e-6)
+        arena.zero_grad()
