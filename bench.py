@@ -41,6 +41,10 @@ BASELINE_FRAMES_PER_S = 2.5e4  # derived GTX-1080Ti lower bound (tr
 BASELINE_RTF = 1.33  # batch-1 E2E synthesis on the authors' GPU node (notebooks/control.ipynb:778)
 
 
+def _num(x):
+    return int(x) if float(x).is_integer() else round(float(x), 1)
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -57,6 +61,10 @@ def parse(argv=None):
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--tiny", action="store_true", help="plumbing-size model (CPU launcher tests only)")
     ap.add_argument("--phase-times", action="store_true", help="per-phase host/device ms of the timed steps")
+    ap.add_argument("--frames-per-gpu", type=int, default=None,
+                    help="per-GPU padded mel-frame budget per step (mi355x.frames_per_gpu) instead of --batch")
+    ap.add_argument("--force-buckets", action="store_true",
+                    help="1 GPU: run the DP gradient path (1-rank RCCL group, hooks, bucket all-reduces)")
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
                     help="default: nccl (RCCL) on GPUs; gloo rehearses the multi-rank path on fewer GPUs")
     return ap.parse_args(argv)
@@ -112,10 +120,14 @@ def run(args):
         "data": "synthetic (LJSpeech-shaped lengths, random-init weights)",
         "config": {
             "model": f"FastSpeech2 ({args.config} model.yaml)" + (" tiny" if args.tiny else ""),
-            "global_batch": tr["batch"] * world,
+            "global_batch": _num(tr["utts_per_step"] * world),
             "seq_len": "T~LJSpeech phonemes, M<=1000 mel frames",
             "parallelism": f"dp{world}",
         },
+        "batch_per_gpu": tr["batch"] if not tr["frames_per_gpu"] else None,
+        "frames_per_gpu": tr["frames_per_gpu"],
+        "utterances_per_gpu_step": round(tr["utts_per_step"], 1),
+        "n_speakers": tr["n_speakers"],
         "world_size_seen": seen,
         "comm_backend": comm,
         "grad_buckets": tr["buckets"],

@@ -950,7 +950,17 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __r
 constexpr int STG64_BYTES = 2 * BG * 64 * 2;  // 64 KiB
 constexpr int B64_LDS = 256 * 528;          // 2 stages (128 KiB) or the padded bf16 epilogue tile (132 KiB)
 
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false>
+// Scheduling fence for the ping-pong main loop: keeps the compiler from moving LDS reads / DMA issues
+// (memory clobber) or MFMAs (sched_barrier) across the block barrier that separates two phases.
+__device__ __forceinline__ void pp_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool PP = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
@@ -968,7 +978,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 128 (m) x 64 (n)
   const float invCin = 1.f / (float)g.Cin;
-  if (g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (!PP && g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   // DMA: a wave instruction fills 8 rows x 128 B; A and B: 256 rows = 32 instructions = 4 per wave
   int a_lim[4], a_t[4], a_m[4], achunk[4];
@@ -1018,6 +1028,26 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       bvo[i] = b_ok[i] ? ((n0 + row) * g.K + achunk[i] * 8) * 2 : kOOB;
     }
   }
+  // BUF: the A (X rows) and B (weight) halves of a stage, issued separately by the ping-pong loop
+  auto stage_a = [&](int kt, int buf) {
+    char* As = smem + buf * STG64_BYTES;
+    const int k0 = kt * 64;
+    const int tap = k0 / g.Cin;
+    const int cin0 = k0 - tap * g.Cin;
+    const int shift = tap * g.dil - g.pad;
+    const int aoff = (shift * g.Cin + cin0) * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ts = a_t[i] + shift;
+      const bool ok = (unsigned)ts < (unsigned)a_lim[i];
+      buf_lds16(rA, ok ? avo[i] + aoff : kOOB, 0, As + (i * 8 + wave) * 1024);
+    }
+  };
+  auto stage_b = [&](int kt, int buf) {
+    char* Bs = smem + buf * STG64_BYTES + BG * 64 * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) buf_lds16(rB, bvo[i], kt * 128, Bs + (i * 8 + wave) * 1024);
+  };
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * STG64_BYTES;
     char* Bs = As + BG * 64 * 2;
@@ -1088,6 +1118,81 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     nk = min(nk_all, kt0 + per);
     Yv = reinterpret_cast<float*>(Yv) + (long)blockIdx.y * g.M * ldy;
   }
+  if constexpr (PP) {
+    // Ping-pong schedule (two wave groups = the two 128-row halves, one wave of each per SIMD):
+    // every 64-wide k slab is 4 phases, one 64x32 quadrant of the wave's 128x64 output each
+    // (16 MFMAs).  A phase is  [LDS fragment reads (+ DMA issue)] barrier [MFMAs] barrier, and
+    // group 1 runs one barrier behind group 0, so on every SIMD one wave reads LDS while the other
+    // issues MFMAs.  Stage t+1 is DMA'd in phases 0 / 1 of slab t (into the buffer slab t-1 used:
+    // its last reads were >= 2 barriers earlier) and retired by every wave before the barrier that
+    // ends phase 3 of slab t (group 0 after its MFMAs, group 1 after its empty read phase), so the
+    // first read of slab t+1 comes one phase after the wait that retires it.
+    const int ntile = nk - kt0;
+    if (ntile > 0) stage(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    if (wm == 1) pp_barrier();
+    const int c0 = lane >> 4, r16 = lane & 15;
+    short8 ra[2][4], rb0[2][2], rb1[2][2];
+    auto mma = [&](short8 (&a)[2][4], short8 (&b)[2][2], int i0, int j0) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kk][j], a[kk][i], acc[i0 + i][j0 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    for (int t = 0; t < ntile; ++t) {
+      const int buf = t & 1;
+      const char* As = smem + buf * STG64_BYTES;
+      const char* Bs = As + BG * 64 * 2;
+      const bool more = t + 1 < ntile;
+      // phase 0: rows 0-63 of the wave's half, columns 0-31
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          rb0[kk][j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + j * 16 + r16, kk * 4 + c0));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ra[kk][i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + i * 16 + r16, kk * 4 + c0));
+      }
+      if (more) stage_a(kt0 + t + 1, buf ^ 1);
+      pp_barrier();
+      mma(ra, rb0, 0, 0);
+      pp_barrier();
+      // phase 1: rows 0-63, columns 32-63
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          rb1[kk][j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + 32 + j * 16 + r16, kk * 4 + c0));
+      if (more) stage_b(kt0 + t + 1, buf ^ 1);
+      pp_barrier();
+      mma(ra, rb1, 0, 2);
+      pp_barrier();
+      // phase 2: rows 64-127, columns 32-63
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ra[kk][i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + 64 + i * 16 + r16, kk * 4 + c0));
+      pp_barrier();
+      mma(ra, rb1, 4, 2);
+      pp_barrier();
+      // phase 3: rows 64-127, columns 0-31 (fragments already in registers)
+      if (wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+      mma(ra, rb0, 4, 0);
+      if (wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+    }
+    if (wm == 0) pp_barrier();
+    // (every wave is past its last LDS read here: the epilogue may reuse the stage buffers)
+  } else {
   // double buffer: stage kt+1 is DMA'd while stage kt is computed (one stage = 1024 MFMA cycles
   // per wave, far longer than an L2-warm LDS-DMA), one barrier per 64-wide k slab
   if (kt0 < nk) stage(kt0, 0);
@@ -1113,6 +1218,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  }
   }
   if constexpr (!OUT_F32) {
     if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
@@ -2817,6 +2923,8 @@ SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 static int g_gemm_buf = 1;  // big64 (FASTK) LDS-DMA through buffer descriptors (0: flat global_load_lds)
 SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
+static int g_gemm_pp = 0;  // big64 (buffer-descriptor path): 1 = ping-pong main loop
+SSAMD_API void ssamd_gemm_set_pp(int v) { g_gemm_pp = v; }
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
 static bool big64_buf_ok(const ConvGeom& g) {
   return g_gemm_buf != 0 && (long)(g.M + g.pad) * g.Cin * 2 < (1L << 31) && (long)g.N * g.K * 2 + 512 < (1L << 31);
@@ -2896,6 +3004,8 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
                                : fastk ? conv_gemm_big64_kernel<true, true, true> : conv_gemm_big64_kernel<true, false, true>)
                          : (bf ? conv_gemm_big64_kernel<true, true, false, true>
                                : fastk ? conv_gemm_big64_kernel<true, true, false> : conv_gemm_big64_kernel<true, false, false>);
+      if (bf && g_gemm_pp)
+        kfn = g.rinfo ? conv_gemm_big64_kernel<true, true, true, true, true> : conv_gemm_big64_kernel<true, true, false, true, true>;
       hipLaunchKernelGGL(kfn, dim3(tiles, S), dim3(NT3), B64_LDS, s, X, W, nullptr, nullptr, nullptr, nullptr,
                          ws, g, 0, N, EpiX{});
       const long nthr = (long)g.M * (N / 8);
@@ -2998,6 +3108,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, false, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, false, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, true, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -3006,6 +3120,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
+      if constexpr (BF) {                                                                                \
+        if (g_gemm_pp) kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF, true>                    \
+                                     : conv_gemm_big64_kernel<F32, FK, false, BF, true>;                  \
+      }                                                                                                  \
       hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
     const bool bf = fastk && big64_buf_ok(g);

@@ -115,12 +115,24 @@ def train_phase(args, rank, world, device):
     trainer = Trainer(model, (pp, mc, tc), seed=1234)
     trainer.timer.enabled = bool(getattr(args, "phase_times", False)) or trainer.timer.enabled
 
-    gen = SyntheticBatches(batch, device=device, max_seq_len=mc["max_seq_len"], seed=1000 + rank,
+    if getattr(args, "force_buckets", False) and world == 1 and cuda:
+        # the multi-GPU gradient path on one GPU: a 1-rank RCCL group, per-parameter hooks and bucket
+        # all-reduces run exactly as under DP (identity reductions) -- measures their host cost
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_free_port()}")
+        trainer.buckets = ddp.GradBuckets(trainer.opt.arena, trainer.buckets_mb, force=True)
+    n_spk = n_speakers_of(pp) if mc.get("multi_speaker") else 1
+    budget = getattr(args, "frames_per_gpu", None)
+    gen = SyntheticBatches(batch, device=device, max_seq_len=mc["max_seq_len"], seed=1000 + rank, n_speakers=n_spk,
+                           frames_per_batch=budget,
                            frame_level=pp["preprocessing"]["pitch"]["feature"] == "frame_level")
     pool = []
     for _ in range(args.pool):
         b = gen.make_batch()
         pool.append((b, gen.last_valid_frames))
+    utts = [len(e[0][0]) for e in pool]
     # largest padded batch first: the first warm-up step sizes the allocator for all others
     pool.sort(key=lambda e: -(len(e[0][0]) * e[0][8]))
 
@@ -134,7 +146,7 @@ def train_phase(args, rank, world, device):
         return frames
 
     # at least one untimed step under DP: the gradient-bucket calibration pass (ddp.GradBuckets)
-    warm = max(args.warmup, 1 if world > 1 else 0)
+    warm = max(args.warmup, 1 if (world > 1 or trainer.buckets.active) else 0)
     for i in range(warm):
         step(i)
     trainer.timer.summary()  # drop the warm-up phases
@@ -154,7 +166,10 @@ def train_phase(args, rank, world, device):
     info = {
         "phases": phases,
         "elapsed": elapsed, "frames": frames_all, "batch": batch, "warmup": warm,
-        "buckets": len(trainer.buckets.buckets), "overlap": trainer.buckets.calibrated() if world > 1 else None,
+        "utts_per_step": sum(utts[(warm + i) % len(pool)] for i in range(args.steps)) / max(1, args.steps),
+        "frames_per_gpu": budget, "n_speakers": n_spk,
+        "buckets": len(trainer.buckets.buckets),
+        "overlap": trainer.buckets.calibrated() if (world > 1 or trainer.buckets.active) else None,
         "skipped_steps": int(trainer.opt.skipped_steps),
     }
     del trainer, model, pool
@@ -227,6 +242,17 @@ def synth_phase(args, rank, world, device):
     if cuda:
         torch.cuda.empty_cache()
     return info
+
+
+def n_speakers_of(pp) -> int:
+    """Speaker count of the config's ``speakers.json`` (LibriTTS: 904), 1 when absent."""
+    p = os.path.join(ROOT, pp["path"]["preprocessed_path"]) if not os.path.isabs(
+        pp["path"]["preprocessed_path"]) else pp["path"]["preprocessed_path"]
+    f = os.path.join(p, "speakers.json")
+    if os.path.exists(f):
+        with open(f) as fh:
+            return max(1, len(json.load(fh)))
+    return 1
 
 
 def report(rec: dict):

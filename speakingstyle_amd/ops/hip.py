@@ -48,6 +48,7 @@ _SIGS = {
     "ssamd_gemm_set_ngrp": [I],
     "ssamd_wgrad_set_buf": [I],
     "ssamd_gemm_set_buf": [I],
+    "ssamd_gemm_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],
     "ssamd_attn_set_fwd": [I, I],
@@ -1756,6 +1757,7 @@ def predictor_head(h, w, b, lengths):
     """[B, L, C] -> [B, L] fp32 = h @ w^T + b, 0 at padded rows (lengths may be None)."""
     C = h.shape[-1]
     if C not in (64, 128, 256, 512) or w.shape[0] != 1:
+        _torch_fallback(f"predictor_head(C={C}, out={w.shape[0]})")  # raises unless explicitly allowed
         out = ref.linear(h, w, b).float().squeeze(-1)
         return out if lengths is None else out.masked_fill(ref.lengths_to_mask(lengths, out.shape[1]), 0.0)
     lens = None if lengths is None else lengths.to(torch.int64).contiguous()

@@ -39,6 +39,7 @@ class Trainer:
         self.grad_acc = int(train_config["optimizer"]["grad_acc_step"])
         self.world = ddp.world_size()
         bm = bucket_mb if bucket_mb is not None else train_config.get("mi355x", {}).get("bucket_mb", 32)
+        self.buckets_mb = bm
         self.buckets = ddp.GradBuckets(self.opt.arena, bm)
         self.n_mel = preprocess_config["preprocessing"]["mel"]["n_mel_channels"]
         self.max_seq_len = model_config["max_seq_len"]

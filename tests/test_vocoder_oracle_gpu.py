@@ -1,0 +1,125 @@
+"""fp32 oracles for the synthesis (RTF) path on the GPU.
+
+The vocoder's HIP inference path (``Generator._infer_hip``: channel-last bf16, fused ResBlock
+layers, 3-tap ConvT GEMMs, fused conv_post/int16) and its HIP training path
+(``_forward_hip_train``) share the implicit-GEMM conv kernels, so comparing one against the other
+cannot catch a bug they share.  Here the oracle is the plain-PyTorch fp32 NCL forward (reference
+``hifigan/models.py:149-165``) with the op backend forced to ``reference`` and the kernel library
+made unreachable: the oracle provably runs no ``ssamd_`` kernel.
+
+The end-to-end test runs FastSpeech2 (BC2013: FiLM reference encoder on a reference mel) + HiFi-GAN
+to int16 samples on a bench-style synthetic batch -- durations, pitch and energy teacher-forced
+from the batch so that both paths regulate to identical lengths and buckets -- HIP bf16 vs fp32."""
+import contextlib
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp(min=1e-12)).item()
+
+
+@contextlib.contextmanager
+def torch_fp32_only():
+    """Force the torch reference ops and make the HIP kernel library unreachable."""
+    from speakingstyle_amd import ops
+    from speakingstyle_amd.models import hifigan as H
+    from speakingstyle_amd.ops import hip
+
+    saved = (hip.lib, H._HIP_TRAIN, ops._FORCED)
+
+    def _no_kernels(*a, **k):
+        raise AssertionError("an ssamd_ kernel was reached inside the fp32 oracle")
+
+    hip.lib = _no_kernels
+    H._HIP_TRAIN = False
+    ops.set_backend("reference")
+    try:
+        yield
+    finally:
+        hip.lib = saved[0]
+        H._HIP_TRAIN = saved[1]
+        ops.set_backend(saved[2])
+
+
+def _generator(seed):
+    from speakingstyle_amd.models import hifigan as H
+
+    torch.manual_seed(seed)
+    return H.Generator(H.default_config()).eval().fold_weight_norm().to(DEV)
+
+
+def test_oracle_reaches_no_kernel():
+    g = _generator(1)
+    mel = torch.randn(1, 80, 8, device=DEV)
+    with torch_fp32_only(), torch.no_grad():
+        g(mel)  # would raise inside if any op dispatched to the kernel library
+    from speakingstyle_amd.ops import hip
+
+    with torch_fp32_only():
+        with pytest.raises(AssertionError):
+            hip.lib()
+
+
+@pytest.mark.parametrize("B,T", [(2, 24), (3, 130)])
+def test_hifigan_hip_paths_vs_fp32_oracle(B, T):
+    """Both HIP generator paths (RTF inference and training forward) vs the fp32 NCL oracle."""
+    g = _generator(13 + T)
+    mel = torch.randn(B, 80, T, device=DEV) * 2 - 5
+    with torch_fp32_only(), torch.no_grad():
+        ref_w = g(mel).squeeze(1)
+    with torch.no_grad():
+        w_inf = g.infer(mel.transpose(1, 2).contiguous().to(torch.bfloat16)).float()
+        pcm = g.infer(mel.transpose(1, 2).contiguous().to(torch.bfloat16), int16_scale=32768.0)
+        w_tr = g._forward_hip_train(mel).squeeze(1).float()
+    assert w_inf.shape == ref_w.shape == (B, T * 256)
+    # bf16 operands with fp32 accumulation through ~20 conv layers: a few % relative L2
+    assert _rel(w_inf, ref_w) < 5e-2
+    assert _rel(w_tr, ref_w) < 5e-2
+    assert pcm.dtype == torch.int16
+    assert _rel(pcm.float() / 32768.0, ref_w) < 5e-2
+
+
+def test_bc2013_fs2_vocoder_int16_e2e_vs_fp32_oracle():
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+
+    pp, mc, tc = load_named("BC2013")
+    torch.manual_seed(0)
+    model = FastSpeech2(pp, mc).to(DEV).eval()
+    model.requires_grad_(False)
+    voc = _generator(5)
+    b = SyntheticBatches(4, device=DEV, seed=7).make_batch()
+    # (speakers, texts, src_lens, max_src, ref mels, mel_lens, max_mel, pitch, energy, durations)
+    args = b[2:12]
+    mx = 32768.0
+
+    with torch.no_grad():
+        model.set_compute_dtype(torch.bfloat16)
+        out = model(*args)
+        mel_hip, len_hip = out[1], out[9]
+        pcm_hip = voc.infer(mel_hip.to(torch.bfloat16).contiguous(), int16_scale=mx)
+    with torch_fp32_only(), torch.no_grad():
+        model.set_compute_dtype(torch.float32)
+        out_r = model(*args)
+        mel_ref, len_ref = out_r[1], out_r[9]
+        wav_ref = voc(mel_ref.transpose(1, 2)).squeeze(1)
+        pcm_ref = (wav_ref * mx).clamp(-32768, 32767).to(torch.int16)
+    assert torch.equal(len_hip.cpu(), len_ref.cpu())
+    assert pcm_hip.shape == pcm_ref.shape
+    # compare the valid samples of every utterance
+    hop = 256
+    errs = []
+    for i, n in enumerate(len_ref.tolist()):
+        a = pcm_hip[i, : n * hop].float()
+        r = pcm_ref[i, : n * hop].float()
+        errs.append(_rel(a, r))
+    assert _rel(mel_hip, mel_ref) < 3e-2
+    assert max(errs) < 8e-2, errs
