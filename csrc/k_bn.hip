@@ -16,6 +16,7 @@
 namespace {
 
 constexpr int NT = 256;
+constexpr int BN_U = 4;  // rows per thread and load batch in the streaming kernels
 
 __device__ __forceinline__ float fast_tanh(float z) {
   // 1 - 2/(exp(2z)+1): one exp + one rcp; saturates correctly for |z| large
@@ -66,12 +67,23 @@ __global__ void __launch_bounds__(NT) bn_stats_kernel(const bf16_t* __restrict__
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const long r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
   if (active) {
-#pragma unroll 4
-    for (long r = r0 + ro; r < r1; r += m.rows_iter) {
-      float v[8];
-      load8(h + r * C + c8 * 8, v);
+    for (long rb = r0 + ro; rb < r1; rb += BN_U * m.rows_iter) {
+      short8 x[BN_U];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { s[i] += v[i]; q[i] += v[i] * v[i]; }
+      for (int u = 0; u < BN_U; ++u) {
+        const long r = rb + u * m.rows_iter;
+        if (r < r1) x[u] = *reinterpret_cast<const short8*>(h + r * C + c8 * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        if (rb + u * m.rows_iter >= r1) break;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float v = bf2f((bf16_t)x[u][i]);
+          s[i] += v;
+          q[i] += v * v;
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -138,27 +150,38 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const bf16_t* __restrict__
   float sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { sc[i] = scale[c0 + i]; sh[i] = shift[c0 + i]; }
-#pragma unroll 2
-  for (long r = (long)blockIdx.x * m.rows_iter + ro; r < R; r += (long)gridDim.x * m.rows_iter) {
-    float v[8];
-    load8(h + r * C + c0, v);
-    float ks[8];
-    drop_scales<8>(seed, (uint64_t)(r * C + c0), p, ks);
+  // BN_U rows per thread and batch, every load of a batch issued before any use (memory-level
+  // parallelism: the per-row loop kept ~2 loads in flight per thread)
+  const long stride = (long)gridDim.x * m.rows_iter;
+  for (long r0 = (long)blockIdx.x * m.rows_iter + ro; r0 < R; r0 += BN_U * stride) {
+    short8 x[BN_U];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float z = v[i] * sc[i] + sh[i];
-      z = act_fwd(act_tanh, z);
-      v[i] = z * ks[i];
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = r0 + u * stride;
+      if (r < R) x[u] = *reinterpret_cast<const short8*>(h + r * C + c0);
     }
-    if constexpr (OUT_F32) {
-      float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + r * C + c0);
-      o[0] = make_float4(v[0], v[1], v[2], v[3]);
-      o[1] = make_float4(v[4], v[5], v[6], v[7]);
-    } else {
-      short8 o;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(v[i]);
-      *reinterpret_cast<short8*>(reinterpret_cast<bf16_t*>(out) + r * C + c0) = o;
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = r0 + u * stride;
+      if (r >= R) break;
+      float v[8], ks[8];
+      drop_scales<8>(seed, (uint64_t)(r * C + c0), p, ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float z = bf2f((bf16_t)x[u][i]) * sc[i] + sh[i];
+        z = act_fwd(act_tanh, z);
+        v[i] = z * ks[i];
+      }
+      if constexpr (OUT_F32) {
+        float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + r * C + c0);
+        o[0] = make_float4(v[0], v[1], v[2], v[3]);
+        o[1] = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        short8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(v[i]);
+        *reinterpret_cast<short8*>(reinterpret_cast<bf16_t*>(out) + r * C + c0) = o;
+      }
     }
   }
 }
@@ -194,20 +217,30 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restric
     for (int i = 0; i < 8; ++i) {
       sc[i] = scale[c8 * 8 + i]; sh[i] = shift[c8 * 8 + i]; mu[i] = mean[c8 * 8 + i]; rs[i] = rstd[c8 * 8 + i];
     }
-#pragma unroll 2
-    for (long r = r0 + ro; r < r1; r += m.rows_iter) {
-      const long off = r * C + c8 * 8;
-      float hv[8], g[8];
-      load8(h + off, hv);
-      load_dy<DY_F32>(dy, off, g);
-      float ks[8];
-      drop_scales<8>(seed, (uint64_t)off, p, ks);
+    for (long rb = r0 + ro; rb < r1; rb += BN_U * m.rows_iter) {
+      float hv[BN_U][8], g[BN_U][8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float dz = g[i] * ks[i];
-        if (act_tanh) dz *= act_grad(act_tanh, hv[i] * sc[i] + sh[i]);
-        a[i] += dz;
-        b[i] += dz * (hv[i] - mu[i]) * rs[i];
+      for (int u = 0; u < BN_U; ++u) {
+        const long r = rb + u * m.rows_iter;
+        if (r < r1) {
+          load8(h + r * C + c8 * 8, hv[u]);
+          load_dy<DY_F32>(dy, r * C + c8 * 8, g[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long r = rb + u * m.rows_iter;
+        if (r >= r1) break;
+        const long off = r * C + c8 * 8;
+        float ks[8];
+        drop_scales<8>(seed, (uint64_t)off, p, ks);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float dz = g[u][i] * ks[i];
+          if (act_tanh) dz *= act_grad(act_tanh, hv[u][i] * sc[i] + sh[i]);
+          a[i] += dz;
+          b[i] += dz * (hv[u][i] - mu[i]) * rs[i];
+        }
       }
     }
 #pragma unroll
@@ -271,22 +304,33 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
       k3[i] = 0.f;
     }
   }
-#pragma unroll 2
-  for (long r = (long)blockIdx.x * m.rows_iter + ro; r < R; r += (long)gridDim.x * m.rows_iter) {
-    const long off = r * C + c0;
-    float hv[8], g[8];
-    load8(h + off, hv);
-    load_dy<DY_F32>(dy, off, g);
-    short8 o;
-    float ks[8];
-    drop_scales<8>(seed, (uint64_t)off, p, ks);
+  const long stride = (long)gridDim.x * m.rows_iter;
+  for (long r0 = (long)blockIdx.x * m.rows_iter + ro; r0 < R; r0 += BN_U * stride) {
+    float hv[BN_U][8], g[BN_U][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float dz = g[i] * ks[i];
-      if (act_tanh) dz *= act_grad(act_tanh, hv[i] * sc[i] + sh[i]);
-      o[i] = (short)f2bf(k1[i] * dz + k2[i] * hv[i] + k3[i]);
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = r0 + u * stride;
+      if (r < R) {
+        load8(h + r * C + c0, hv[u]);
+        load_dy<DY_F32>(dy, r * C + c0, g[u]);
+      }
     }
-    *reinterpret_cast<short8*>(dh + off) = o;
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long r = r0 + u * stride;
+      if (r >= R) break;
+      const long off = r * C + c0;
+      short8 o;
+      float ks[8];
+      drop_scales<8>(seed, (uint64_t)off, p, ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float dz = g[u][i] * ks[i];
+        if (act_tanh) dz *= act_grad(act_tanh, hv[u][i] * sc[i] + sh[i]);
+        o[i] = (short)f2bf(k1[i] * dz + k2[i] * hv[u][i] + k3[i]);
+      }
+      *reinterpret_cast<short8*>(dh + off) = o;
+    }
   }
 }
 

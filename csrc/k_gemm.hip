@@ -960,7 +960,7 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool PP = false>
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
@@ -978,7 +978,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 128 (m) x 64 (n)
   const float invCin = 1.f / (float)g.Cin;
-  if (!PP && g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   // DMA: a wave instruction fills 8 rows x 128 B; A and B: 256 rows = 32 instructions = 4 per wave
   int a_lim[4], a_t[4], a_m[4], achunk[4];
@@ -1028,26 +1028,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       bvo[i] = b_ok[i] ? ((n0 + row) * g.K + achunk[i] * 8) * 2 : kOOB;
     }
   }
-  // BUF: the A (X rows) and B (weight) halves of a stage, issued separately by the ping-pong loop
-  auto stage_a = [&](int kt, int buf) {
-    char* As = smem + buf * STG64_BYTES;
-    const int k0 = kt * 64;
-    const int tap = k0 / g.Cin;
-    const int cin0 = k0 - tap * g.Cin;
-    const int shift = tap * g.dil - g.pad;
-    const int aoff = (shift * g.Cin + cin0) * 2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ts = a_t[i] + shift;
-      const bool ok = (unsigned)ts < (unsigned)a_lim[i];
-      buf_lds16(rA, ok ? avo[i] + aoff : kOOB, 0, As + (i * 8 + wave) * 1024);
-    }
-  };
-  auto stage_b = [&](int kt, int buf) {
-    char* Bs = smem + buf * STG64_BYTES + BG * 64 * 2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) buf_lds16(rB, bvo[i], kt * 128, Bs + (i * 8 + wave) * 1024);
-  };
   auto stage = [&](int kt, int buf) {
     char* As = smem + buf * STG64_BYTES;
     char* Bs = As + BG * 64 * 2;
@@ -1118,81 +1098,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     nk = min(nk_all, kt0 + per);
     Yv = reinterpret_cast<float*>(Yv) + (long)blockIdx.y * g.M * ldy;
   }
-  if constexpr (PP) {
-    // Ping-pong schedule (two wave groups = the two 128-row halves, one wave of each per SIMD):
-    // every 64-wide k slab is 4 phases, one 64x32 quadrant of the wave's 128x64 output each
-    // (16 MFMAs).  A phase is  [LDS fragment reads (+ DMA issue)] barrier [MFMAs] barrier, and
-    // group 1 runs one barrier behind group 0, so on every SIMD one wave reads LDS while the other
-    // issues MFMAs.  Stage t+1 is DMA'd in phases 0 / 1 of slab t (into the buffer slab t-1 used:
-    // its last reads were >= 2 barriers earlier) and retired by every wave before the barrier that
-    // ends phase 3 of slab t (group 0 after its MFMAs, group 1 after its empty read phase), so the
-    // first read of slab t+1 comes one phase after the wait that retires it.
-    const int ntile = nk - kt0;
-    if (ntile > 0) stage(kt0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
-    if (wm == 1) pp_barrier();
-    const int c0 = lane >> 4, r16 = lane & 15;
-    short8 ra[2][4], rb0[2][2], rb1[2][2];
-    auto mma = [&](short8 (&a)[2][4], short8 (&b)[2][2], int i0, int j0) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[kk][j], a[kk][i], acc[i0 + i][j0 + j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    for (int t = 0; t < ntile; ++t) {
-      const int buf = t & 1;
-      const char* As = smem + buf * STG64_BYTES;
-      const char* Bs = As + BG * 64 * 2;
-      const bool more = t + 1 < ntile;
-      // phase 0: rows 0-63 of the wave's half, columns 0-31
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          rb0[kk][j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + j * 16 + r16, kk * 4 + c0));
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          ra[kk][i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + i * 16 + r16, kk * 4 + c0));
-      }
-      if (more) stage_a(kt0 + t + 1, buf ^ 1);
-      pp_barrier();
-      mma(ra, rb0, 0, 0);
-      pp_barrier();
-      // phase 1: rows 0-63, columns 32-63
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          rb1[kk][j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + 32 + j * 16 + r16, kk * 4 + c0));
-      if (more) stage_b(kt0 + t + 1, buf ^ 1);
-      pp_barrier();
-      mma(ra, rb1, 0, 2);
-      pp_barrier();
-      // phase 2: rows 64-127, columns 32-63
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          ra[kk][i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + 64 + i * 16 + r16, kk * 4 + c0));
-      pp_barrier();
-      mma(ra, rb1, 4, 2);
-      pp_barrier();
-      // phase 3: rows 64-127, columns 0-31 (fragments already in registers)
-      if (wm == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      pp_barrier();
-      mma(ra, rb0, 4, 0);
-      if (wm == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      pp_barrier();
-    }
-    if (wm == 0) pp_barrier();
-    // (every wave is past its last LDS read here: the epilogue may reuse the stage buffers)
-  } else {
   // double buffer: stage kt+1 is DMA'd while stage kt is computed (one stage = 1024 MFMA cycles
   // per wave, far longer than an L2-warm LDS-DMA), one barrier per 64-wide k slab
   if (kt0 < nk) stage(kt0, 0);
@@ -1218,7 +1123,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-  }
   }
   if constexpr (!OUT_F32) {
     if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
@@ -2187,7 +2091,18 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big_kernel(const bf16_t* __
 
 constexpr int WB64_STAGE = 2 * 64 * 512;  // 64 KiB: dY [64][256] + X [64][256]
 
-template <bool PACKED, bool IMM, bool BUF>
+// lgkmcnt(0) that the fragments depend on (the inline-asm LDS reads are invisible to the compiler's
+// waitcnt pass, so the MFMAs consuming them must not be scheduled above the wait)
+__device__ __forceinline__ void lgkm_tie(short8 (&a)[2][4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]), "+v"(a[1][1]),
+                 "+v"(a[1][2]), "+v"(a[1][3]));
+}
+__device__ __forceinline__ void lgkm_tie(short8 (&b)[2][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]));
+}
+
+template <bool PACKED, bool IMM, bool BUF, bool PP = false>
 __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* __restrict__ X,
                                                                 const bf16_t* __restrict__ dY,
                                                                 float* __restrict__ slabs,
@@ -2208,7 +2123,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave >> 2, wk = wave & 3;
   const float invCin = 1.f / (float)g.Cin;
-  if (g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (!PP && g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   float4v acc[8][4];
 #pragma unroll
@@ -2280,6 +2195,36 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
   }
   // LDS: dY images of the two stages at 0 / 32 KiB, X images at 64 / 96 KiB, so that every
   // fragment read is a loop-invariant per-lane base + an immediate (stage, k-half, +4 rows)
+  // BUF: the dY and X halves of a stage, issued separately by the ping-pong loop
+  auto stage_y = [&](int r0, int buf) {
+    char* Ys = smem + buf * 32768;
+    const int dy_off = (r0 - r_begin) * g.N * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) buf_lds16(rY, yvo[i] + dy_off, 0, Ys + (i * 8 + wave) * 1024);
+  };
+  auto stage_x = [&](int r0, int buf) {
+    char* Xs = smem + 65536 + buf * 32768;
+    const int x_off = r0 * g.Cin * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool ok = true;
+      if (!x_always) {
+        int ts, lim;
+        if constexpr (PACKED) {
+          ts = ri_nxt[i].x + xshift[i];
+          lim = ri_nxt[i].y;
+        } else {
+          ts = t_cur[i] + xshift[i];
+          lim = g.L;
+          int t = t_cur[i] + 64;
+          while (t >= g.L) t -= g.L;
+          t_cur[i] = t;
+        }
+        ok = (unsigned)ts < (unsigned)lim;
+      }
+      buf_lds16(rX, ok ? xvo[i] + x_off : kOOB, 0, Xs + (i * 8 + wave) * 1024);
+    }
+  };
   auto stage = [&](int r0, int buf) {
     char* Ys = smem + buf * 32768;
     char* Xs = smem + 65536 + buf * 32768;
@@ -2341,6 +2286,109 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
   if (nsteps > 0) stage(r_begin, 0);
   if constexpr (PACKED) load_ri(r_begin + 64);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (PP) {
+    // Ping-pong schedule (see conv_gemm_big64_kernel): the two wave groups are the two 128-row halves
+    // of the dW tile (one wave of each per SIMD), 4 phases per 64-row step, one 64 (n) x 32 (k)
+    // quadrant of the wave's 128 x 64 each; group 1 runs one barrier behind group 0.  Step st+1 is
+    // DMA'd in phases 0 (dY) / 1 (X, then the rinfo rows of step st+2) of step st and retired before
+    // the barrier that ends phase 3; the bias column sums read the dY image in the (otherwise
+    // empty) phase-3 read slot.
+    if constexpr (PACKED) {  // retired by the vmcnt(0) above (see the end of the step loop)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(ri_nxt[i].x), "+v"(ri_nxt[i].y));
+    }
+    pp_barrier();
+    if (wn == 1) pp_barrier();
+    const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    short8 fa[2][4], fb0[2][2], fb1[2][2];
+    auto mma = [&](short8 (&a)[2][4], short8 (&b)[2][2], int i0, int j0) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j], acc[i0 + i][j0 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto rd = [&](const char* base, int rbase, int cb) {
+      const short4v v0 = ds_read_tr_asm(base + swz_tr512(rbase, cb));
+      const short4v v1 = ds_read_tr_asm(base + swz_tr512(rbase + 4, cb));
+      return (short8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    };
+    for (int st = 0; st < nsteps; ++st) {
+      const int buf = st & 1;
+      const char* Ys = smem + buf * 32768;
+      const char* Xs = smem + 65536 + buf * 32768;
+      const bool more = st + 1 < nsteps;
+      // phase 0: n rows 0-63 of the wave's half, k columns 0-31
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int rbase = kk * 32 + grp * 8 + q;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb0[kk][j] = rd(Xs, rbase, (wk * 64 + j * 16) / 4 + p);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[kk][i] = rd(Ys, rbase, (wn * 128 + i * 16) / 4 + p);
+      }
+      if (more) stage_y(r_begin + (st + 1) * 64, buf ^ 1);
+      pp_barrier();
+      lgkm_tie(fa);
+      lgkm_tie(fb0);
+      mma(fa, fb0, 0, 0);
+      pp_barrier();
+      // phase 1: n rows 0-63, k columns 32-63
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int rbase = kk * 32 + grp * 8 + q;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb1[kk][j] = rd(Xs, rbase, (wk * 64 + 32 + j * 16) / 4 + p);
+      }
+      if (more) {
+        stage_x(r_begin + (st + 1) * 64, buf ^ 1);
+        if constexpr (PACKED) load_ri(r_begin + (st + 2) * 64);
+      }
+      pp_barrier();
+      lgkm_tie(fb1);
+      mma(fa, fb1, 0, 2);
+      pp_barrier();
+      // phase 2: n rows 64-127, k columns 32-63
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int rbase = kk * 32 + grp * 8 + q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[kk][i] = rd(Ys, rbase, (wn * 128 + 64 + i * 16) / 4 + p);
+      }
+      pp_barrier();
+      lgkm_tie(fa);
+      mma(fa, fb1, 4, 2);
+      pp_barrier();
+      // phase 3: n rows 64-127, k columns 0-31 (fragments in registers); bias sums in the read slot
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = (tid >> 5) + 16 * j;
+          const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
+          const short8 v = *reinterpret_cast<const short8*>(Ys + row * 512 + ((bc16 ^ (f >> 1)) << 4));
+#pragma unroll
+          for (int t = 0; t < 8; ++t) bsum[t] += bf2f((bf16_t)v[t]);
+        }
+      }
+      if (wn == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+      mma(fa, fb0, 4, 0);
+      if (wn == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+      if constexpr (PACKED) {
+        // the rinfo rows of step st+2 are retired by the vmcnt(0) above; re-define them through an
+        // empty asm so the compiler's waitcnt pass (which cannot see that wait) does not make the
+        // next step's X stage wait for the dY DMA issued just before it
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(ri_nxt[i].x), "+v"(ri_nxt[i].y));
+      }
+    }
+    if (wn == 0) pp_barrier();
+  } else {
   __builtin_amdgcn_s_barrier();
   const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   typedef short v4s __attribute__((ext_vector_type(4)));
@@ -2446,6 +2494,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
+  }
   }
   if (do_bias) {
     float* red = reinterpret_cast<float*>(smem);  // [16][256]
@@ -2923,8 +2972,7 @@ SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 static int g_gemm_buf = 1;  // big64 (FASTK) LDS-DMA through buffer descriptors (0: flat global_load_lds)
 SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
-static int g_gemm_pp = 0;  // big64 (buffer-descriptor path): 1 = ping-pong main loop
-SSAMD_API void ssamd_gemm_set_pp(int v) { g_gemm_pp = v; }
+
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
 static bool big64_buf_ok(const ConvGeom& g) {
   return g_gemm_buf != 0 && (long)(g.M + g.pad) * g.Cin * 2 < (1L << 31) && (long)g.N * g.K * 2 + 512 < (1L << 31);
@@ -3004,8 +3052,6 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
                                : fastk ? conv_gemm_big64_kernel<true, true, true> : conv_gemm_big64_kernel<true, false, true>)
                          : (bf ? conv_gemm_big64_kernel<true, true, false, true>
                                : fastk ? conv_gemm_big64_kernel<true, true, false> : conv_gemm_big64_kernel<true, false, false>);
-      if (bf && g_gemm_pp)
-        kfn = g.rinfo ? conv_gemm_big64_kernel<true, true, true, true, true> : conv_gemm_big64_kernel<true, true, false, true, true>;
       hipLaunchKernelGGL(kfn, dim3(tiles, S), dim3(NT3), B64_LDS, s, X, W, nullptr, nullptr, nullptr, nullptr,
                          ws, g, 0, N, EpiX{});
       const long nthr = (long)g.M * (N / 8);
@@ -3108,10 +3154,6 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, false, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<true, true, false, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, false, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<true, true, true, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, true, true, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -3120,10 +3162,6 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
-      if constexpr (BF) {                                                                                \
-        if (g_gemm_pp) kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF, true>                    \
-                                     : conv_gemm_big64_kernel<F32, FK, false, BF, true>;                  \
-      }                                                                                                  \
       hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
     const bool bf = fastk && big64_buf_ok(g);
@@ -3257,6 +3295,10 @@ static int g_wgrad_imm = -1;  // -1 auto, 0 / 1: force the big64 wgrad read sche
 SSAMD_API void ssamd_wgrad_set_imm(int v) { g_wgrad_imm = v; }
 static int g_wgrad_buf = 1;  // big64 wgrad LDS-DMA through buffer descriptors (0: flat global_load_lds)
 SSAMD_API void ssamd_wgrad_set_buf(int v) { g_wgrad_buf = v; }
+// big64 wgrad (buffer-descriptor path) ping-pong main loop: -1 auto = on packed rows (decoder k9 wgrad
+// 646 -> 519 us vs 718 before, tools/exp_wgrad_pp.py), off on plain rows (PostNet k5 -14 %)
+static int g_wgrad_pp = -1;
+SSAMD_API void ssamd_wgrad_set_pp(int v) { g_wgrad_pp = v; }
 static int g_wgrad_reduce_old = 0;  // 1: the pre-split-parallel reduction kernels (A/B measurement)
 SSAMD_API void ssamd_wgrad_set_reduce(int old) { g_wgrad_reduce_old = old; }
 
@@ -3287,9 +3329,47 @@ static void launch_reduce(const float* ws, float* dW, const float* bws, float* d
                      ks, nb_main);
 }
 
+// Split-M count of the 256x256 weight-gradient kernel (one block per CU): the blocks run in
+// ceil(tiles * S / CUs) rounds of ceil(M / S / 64) row steps each, and every split adds a 256x256
+// fp32 slab to write and reduce (~8 % of a 64-row step per slab tile).  The old fixed target of 512
+// blocks left partial rounds (packed k9 wgrad: 36 tiles x 15 = 540 blocks = 2.1 rounds -> 3) and,
+// capped by the 128x128 kernels' split limit, single-tile weights ran on 64 CUs.
+static int g_cus_dev[64];
+static int device_cus() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!g_cus_dev[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    g_cus_dev[dev] = n;
+  }
+  return g_cus_dev[dev];
+}
+static int g_wgrad_blocks = 0;   // > 0: fixed split-M target (blocks per launch) instead of the cost model
+static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits) {
+  const int steps_all = (M + 63) / 64;
+  int smax = max_splits;
+  if (smax > steps_all / 4) smax = steps_all / 4 > 0 ? steps_all / 4 : 1;  // >= 4 row steps per split
+  if ((long)smax > ws_splits) smax = (int)ws_splits;
+  if (smax < 1) return (int)(ws_splits >= 1 ? 1 : 0);
+  if (g_wgrad_blocks > 0) {
+    const int sp = (g_wgrad_blocks + tiles - 1) / tiles;
+    return sp < smax ? sp : smax;
+  }
+  const int cus = device_cus();
+  int best = 1;
+  double best_c = 1e30;
+  for (int sp = 1; sp <= smax; ++sp) {
+    const long rounds = ((long)tiles * sp + cus - 1) / cus;
+    const long steps = (steps_all + sp - 1) / sp;
+    const double c = (double)rounds * (double)steps + 0.08 * (double)sp * tiles;
+    if (c < best_c - 1e-9) { best_c = c; best = sp; }
+  }
+  return best;
+}
+
 static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64), 0: 128x128, 1: 256x128 ring, 2: 256x256 BK=32 ring
-static int g_wgrad_blocks = 512;  // split-M target: blocks per launch
-SSAMD_API void ssamd_wgrad_set_blocks(int b) { g_wgrad_blocks = b > 0 ? b : 512; }
+SSAMD_API void ssamd_wgrad_set_blocks(int b) { g_wgrad_blocks = b > 0 ? b : 0; }
 SSAMD_API void ssamd_wgrad_set_variant(int v) { g_wgrad_variant = v; }
 
 SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, float* db,
@@ -3326,14 +3406,12 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
       allow_lds(conv_wgrad_big64_kernel<true, false, true>, 160 * 1024);
       allow_lds(conv_wgrad_big64_kernel<false, true, true>, 160 * 1024);
       allow_lds(conv_wgrad_big64_kernel<true, true, true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<false, false, true, true>, 160 * 1024);
+      allow_lds(conv_wgrad_big64_kernel<true, false, true, true>, 160 * 1024);
       b64_set = true;
     }
     const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
-    int splits = (g_wgrad_blocks + tiles - 1) / tiles;
-    const int max_by_rows = (g.M + 8 * 64 - 1) / (8 * 64);  // >= 8 steps per split
-    if (splits > max_by_rows) splits = max_by_rows;
-    if (splits > max_splits) splits = max_splits;
-    if ((long)splits * (slab + N) > ws_floats) splits = (int)(ws_floats / (slab + N));
+    int splits = choose_wgrad_splits(tiles, g.M, max_splits, ws_floats / (slab + N));
     if (splits < 1) return -3;
     int rows_per_split = (g.M + splits - 1) / splits;
     rows_per_split = (rows_per_split + 63) / 64 * 64;
@@ -3351,6 +3429,8 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
                               : (imm ? conv_wgrad_big64_kernel<false, true, true> : conv_wgrad_big64_kernel<false, false, true>))
                     : (packed ? (imm ? conv_wgrad_big64_kernel<true, true, false> : conv_wgrad_big64_kernel<true, false, false>)
                               : (imm ? conv_wgrad_big64_kernel<false, true, false> : conv_wgrad_big64_kernel<false, false, false>));
+    if (bufok && (g_wgrad_pp < 0 ? packed : g_wgrad_pp != 0))
+      wb = packed ? conv_wgrad_big64_kernel<true, false, true, true> : conv_wgrad_big64_kernel<false, false, true, true>;
     hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);
     launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);

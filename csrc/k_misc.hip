@@ -1147,43 +1147,79 @@ SSAMD_API int ssamd_pad_colsum(const void* dout, int f32, const int64_t* lens, i
 // scalar gradients so each scalar gets ONE gradient, written straight into its arena slot.
 // ----------------------------------------------------------------------------
 namespace {
-__global__ void __launch_bounds__(256) film_grads_kernel(const float* __restrict__ S1, const float* __restrict__ S2,
-                                                         const float* __restrict__ g, const float* __restrict__ bt,
-                                                         const float* __restrict__ sg, const float* __restrict__ sb,
-                                                         int n, int out_f32, void* __restrict__ dg,
-                                                         void* __restrict__ dbt, float* __restrict__ dsg,
-                                                         float* __restrict__ dsb, const float* __restrict__ l2_sg,
-                                                         const float* __restrict__ l2_sb, int accum) {
-  __shared__ float red[2][256];
+// One block of 1024 threads: every thread owns float4 groups i = 4*(tid + 1024*u), all U loads of an
+// outer iteration issued before any use (the per-element strided loop of one 256-thread block was a
+// chain of dependent memory round trips: ~80 us for n = 19200), fixed-order tree for the two scalars.
+constexpr int FG_T = 1024, FG_U = 4;
+__global__ void __launch_bounds__(FG_T) film_grads_kernel(const float* __restrict__ S1, const float* __restrict__ S2,
+                                                          const float* __restrict__ g, const float* __restrict__ bt,
+                                                          const float* __restrict__ sg, const float* __restrict__ sb,
+                                                          int n, int out_f32, void* __restrict__ dg,
+                                                          void* __restrict__ dbt, float* __restrict__ dsg,
+                                                          float* __restrict__ dsb, const float* __restrict__ l2_sg,
+                                                          const float* __restrict__ l2_sb, int accum) {
+  __shared__ float red[2][FG_T];
   const float a = *sg, c = *sb;
   float s1 = 0.f, s2 = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const float x1 = S1[i], x2 = S2[i];
-    if (out_f32) {
-      float* pg = reinterpret_cast<float*>(dg) + i;
-      float* pb = reinterpret_cast<float*>(dbt) + i;
-      *pg = accum ? *pg + x1 * a : x1 * a;
-      *pb = accum ? *pb + x2 * c : x2 * c;
-    } else {  // accumulate rounds like autograd's bf16 add of per-site gradients (fp32 add, one rounding)
-      bf16_t* pg = reinterpret_cast<bf16_t*>(dg) + i;
-      bf16_t* pb = reinterpret_cast<bf16_t*>(dbt) + i;
-      *pg = f2bf(accum ? bf2f(*pg) + x1 * a : x1 * a);
-      *pb = f2bf(accum ? bf2f(*pb) + x2 * c : x2 * c);
+  const int tid = threadIdx.x;
+  for (int base = 0; base < n; base += 4 * FG_T * FG_U) {
+    float4 x1[FG_U], x2[FG_U], gg[FG_U], bb[FG_U], o1[FG_U], o2[FG_U];
+#pragma unroll
+    for (int u = 0; u < FG_U; ++u) {
+      const int i = base + 4 * (tid + FG_T * u);
+      const bool ok = i < n;  // n % 4 == 0 (host check)
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      x1[u] = ok ? *reinterpret_cast<const float4*>(S1 + i) : z;
+      x2[u] = ok ? *reinterpret_cast<const float4*>(S2 + i) : z;
+      gg[u] = ok ? *reinterpret_cast<const float4*>(g + i) : z;
+      bb[u] = ok ? *reinterpret_cast<const float4*>(bt + i) : z;
+      o1[u] = z;
+      o2[u] = z;
+      if (ok && accum) {
+        if (out_f32) {
+          o1[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dg) + i);
+          o2[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dbt) + i);
+        } else {
+          const short4v p1 = *reinterpret_cast<const short4v*>(reinterpret_cast<const bf16_t*>(dg) + i);
+          const short4v p2 = *reinterpret_cast<const short4v*>(reinterpret_cast<const bf16_t*>(dbt) + i);
+          o1[u] = make_float4(bf2f((bf16_t)p1[0]), bf2f((bf16_t)p1[1]), bf2f((bf16_t)p1[2]), bf2f((bf16_t)p1[3]));
+          o2[u] = make_float4(bf2f((bf16_t)p2[0]), bf2f((bf16_t)p2[1]), bf2f((bf16_t)p2[2]), bf2f((bf16_t)p2[3]));
+        }
+      }
     }
-    s1 += x1 * g[i];
-    s2 += x2 * bt[i];
+#pragma unroll
+    for (int u = 0; u < FG_U; ++u) {
+      const int i = base + 4 * (tid + FG_T * u);
+      if (i >= n) continue;
+      // accumulate rounds like autograd's add of per-site gradients (fp32 add, one rounding)
+      const float4 r1 = make_float4(o1[u].x + x1[u].x * a, o1[u].y + x1[u].y * a, o1[u].z + x1[u].z * a,
+                                    o1[u].w + x1[u].w * a);
+      const float4 r2 = make_float4(o2[u].x + x2[u].x * c, o2[u].y + x2[u].y * c, o2[u].z + x2[u].z * c,
+                                    o2[u].w + x2[u].w * c);
+      if (out_f32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(dg) + i) = r1;
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(dbt) + i) = r2;
+      } else {
+        const short4v q1 = {(short)f2bf(r1.x), (short)f2bf(r1.y), (short)f2bf(r1.z), (short)f2bf(r1.w)};
+        const short4v q2 = {(short)f2bf(r2.x), (short)f2bf(r2.y), (short)f2bf(r2.z), (short)f2bf(r2.w)};
+        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(dg) + i) = q1;
+        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(dbt) + i) = q2;
+      }
+      s1 += x1[u].x * gg[u].x + x1[u].y * gg[u].y + x1[u].z * gg[u].z + x1[u].w * gg[u].w;
+      s2 += x2[u].x * bb[u].x + x2[u].y * bb[u].y + x2[u].z * bb[u].z + x2[u].w * bb[u].w;
+    }
   }
-  red[0][threadIdx.x] = s1;
-  red[1][threadIdx.x] = s2;
+  red[0][tid] = s1;
+  red[1][tid] = s2;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + w];
-      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+  for (int w = FG_T / 2; w > 0; w >>= 1) {
+    if (tid < w) {
+      red[0][tid] += red[0][tid + w];
+      red[1][tid] += red[1][tid + w];
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {  // + the FiLM L2 term's gradient of this site's scalars, when folded in
+  if (tid == 0) {  // + the FiLM L2 term's gradient of this site's scalars, when folded in
     dsg[0] = l2_sg ? red[0][0] + l2_sg[0] : red[0][0];
     dsb[0] = l2_sb ? red[1][0] + l2_sb[0] : red[1][0];
   }
@@ -1193,7 +1229,8 @@ __global__ void __launch_bounds__(256) film_grads_kernel(const float* __restrict
 SSAMD_API int ssamd_film_grads(const float* S1, const float* S2, const float* g, const float* bt, const float* sg,
                                const float* sb, int n, int out_f32, void* dg, void* dbt, float* dsg, float* dsb,
                                const float* l2_sg, const float* l2_sb, int accum, hipStream_t s) {
-  hipLaunchKernelGGL(film_grads_kernel, dim3(1), dim3(256), 0, s, S1, S2, g, bt, sg, sb, n, out_f32, dg, dbt, dsg,
+  if (n % 4) return -2;
+  hipLaunchKernelGGL(film_grads_kernel, dim3(1), dim3(FG_T), 0, s, S1, S2, g, bt, sg, sb, n, out_f32, dg, dbt, dsg,
                      dsb, l2_sg, l2_sb, accum);
   return (int)hipGetLastError();
 }

@@ -48,7 +48,7 @@ _SIGS = {
     "ssamd_gemm_set_ngrp": [I],
     "ssamd_wgrad_set_buf": [I],
     "ssamd_gemm_set_buf": [I],
-    "ssamd_gemm_set_pp": [I],
+    "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],
     "ssamd_attn_set_fwd": [I, I],
@@ -442,7 +442,9 @@ def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, 
         raise ValueError("wgrad: N must be a multiple of 8")
     K = ks * Cin
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    max_splits = max(1, min(64, (1536 + tiles - 1) // tiles))
+    max_splits = max(1, min(64, (1536 + tiles - 1) // tiles))  # 128x128 kernels
+    if N >= 256 and K >= 256:  # 256x256 kernel: up to one split per CU per output tile (C++ cost model)
+        max_splits = max(max_splits, min(256, 256 // max(1, ((N + 255) // 256) * ((K + 255) // 256)) * 2))
     ws = _workspace(x.device, max_splits * (N * K + N))
     if dW is None:
         dW = torch.empty(N, Cin, ks, device=x.device, dtype=torch.float32)

@@ -325,10 +325,10 @@ def test_attention(D, H):
     assert _rel(qh.grad, qr.grad) < 3e-2
 
 
-@pytest.mark.parametrize("cfg", ["BC2013", "BC2013_GST"])
+@pytest.mark.parametrize("cfg", ["LJSpeech", "LibriTTS", "BC2013", "BC2013_GST"])
 def test_model_step_hip_vs_reference(cfg):
-    """Full FastSpeech2 (BC2013 config: FiLM reference encoder, or the GST variant) forward+backward,
-    HIP vs torch fp32."""
+    """Full FastSpeech2 forward+backward, HIP bf16 vs torch fp32: LJSpeech (no style), LibriTTS
+    (multi-speaker: speaker-embedding add + its gradient), BC2013 (FiLM reference encoder), GST."""
     import copy
 
     from speakingstyle_amd import ops
@@ -346,7 +346,12 @@ def test_model_step_hip_vs_reference(cfg):
     from speakingstyle_amd.train.optim import FlatArena
 
     arena = FlatArena(list(reversed(list(m.parameters()))), groups=m.fused_param_groups())
-    b = SyntheticBatches(4, device=DEV, seed=11, phone_counts=[40, 55, 61, 20]).make_batch()
+    from speakingstyle_amd.benchmark import n_speakers_of
+
+    nspk = n_speakers_of(pp) if mc["multi_speaker"] else 1  # LibriTTS: 904 speaker ids (embedding add + bwd)
+    b = SyntheticBatches(4, device=DEV, seed=11, phone_counts=[40, 55, 61, 20], n_speakers=nspk).make_batch()
+    if nspk > 1:
+        assert len(set(b[2].tolist())) > 1
     lossf = FastSpeech2Loss(pp, tc)
     out = m(*b[2:])
     lo = lossf(b, out, m.film_scalars())
@@ -365,20 +370,33 @@ def test_model_step_hip_vs_reference(cfg):
     for a, c in zip(lo[:6], lr_[:6]):
         assert abs(a.item() - c.item()) <= 3e-2 * abs(c.item()) + 1e-3
     gr = dict(mr.named_parameters())
+    # bf16 error budget (measured, tools/grad_err_budget.py on MI355X): activations and operands are
+    # rounded to bf16 (u = 2^-8 = 0.39 %) at ~40 sites between the loss and the deepest weights, fp32
+    # accumulation; a weight gradient is a sum over ~10^4-10^5 rows, and where that sum cancels to a
+    # small fraction of its terms (bias and variance-predictor gradients, the embedding tables) the
+    # relative error grows by the cancellation ratio.  Measured per-tensor relative L2 error over the
+    # 4 configs: median 0.8-1.9 %, 90th percentile 3.0-6.1 %, max 8.1-12.5 % (LJSpeech energy-predictor
+    # biases).  The test bounds all three: median 3 %, p90 8 %, every tensor 15 %.
     # FiLM scale scalars: each gradient is one global sum over (batch, channel) that can cancel
     # down to a few % of its terms, so they get an absolute floor from the largest scalar gradient
     scal = max([gr[n].grad.abs().item() for n, p in m.named_parameters()
                 if p.numel() == 1 and gr[n].grad is not None] or [0.0])
-    bad = []
+    bad, errs = [], []
     for n, p in m.named_parameters():
         if p.grad is None or gr[n].grad is None:
             continue
         if p.numel() == 1:
             if abs(p.grad.item() - gr[n].grad.item()) > 0.15 * abs(gr[n].grad.item()) + 0.03 * scal:
                 bad.append((n, p.grad.item(), gr[n].grad.item()))
-        elif gr[n].grad.norm() > 1e-6 and _rel(p.grad, gr[n].grad) > 0.15:
-            bad.append((n, _rel(p.grad, gr[n].grad)))
+        elif gr[n].grad.norm() > 1e-6:
+            e = _rel(p.grad, gr[n].grad)
+            errs.append(e)
+            if e > 0.15:
+                bad.append((n, e))
     assert not bad, bad[:10]
+    errs.sort()
+    assert errs[len(errs) // 2] <= 0.03 and errs[int(0.9 * len(errs))] <= 0.08, (errs[len(errs) // 2],
+                                                                                errs[int(0.9 * len(errs))])
 
 
 @pytest.mark.gpu

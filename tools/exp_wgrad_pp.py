@@ -1,8 +1,8 @@
 #!/usr/bin/env python
-"""A/B of the ping-pong big64 GEMM main loop (ssamd_gemm_set_pp) against the double-buffered one on
-the training step's GEMM shapes: outputs must be bitwise equal (same per-accumulator k order), then
-time both (same process, alternating, warm).  Prints one JSON line per shape.
-Usage (GPU): python tools/exp_pp.py [--iters 20]"""
+"""A/B of the ping-pong wgrad main loop (ssamd_wgrad_set_pp) against the double-buffered one on the
+training step's weight-gradient shapes: dW / db must be bitwise equal (same per-accumulator row
+order), then time both (kernel + slab reduce, same process, alternating, warm).  JSON per shape.
+Usage (GPU): python tools/exp_wgrad_pp.py [--iters 20]"""
 import argparse
 import json
 import os
@@ -40,39 +40,39 @@ def main():
     M = int(lens.max())
     R = int(lens.sum())
     pk = ops.PackInfo.build(lens, M, R)
-    shapes = [  # name, Cin, N, ks, packed, rows (unpacked: B*L), act
-        ("dec ffn.w1 k9 256->1024 packed", 256, 1024, 9, True, R, 1),
-        ("dec ffn.w1 dgrad k9 1024->256 packed", 1024, 256, 9, True, R, 0),
-        ("dec ffn.w2 k1 1024->256", 1024, 256, 1, False, R, 0),
-        ("dec qkv 256->768", 256, 768, 1, False, R, 0),
-        ("dec fc 256->256", 256, 256, 1, False, R, 0),
-        ("postnet k5 512->512", 512, 512, 5, False, 140000, 0),
-        ("enc ffn.w1 k9 256->1024", 256, 1024, 9, False, 14000, 1),
+    shapes = [  # name, Cin, N, ks, packed, rows
+        ("dec ffn.w1 k9 256->1024 packed", 256, 1024, 9, True, R),
+        ("dec ffn.w2 k1 1024->256", 1024, 256, 1, False, R),
+        ("dec qkv 256->768", 256, 768, 1, False, R),
+        ("dec fc 256->256", 256, 256, 1, False, R),
+        ("postnet k5 512->512", 512, 512, 5, False, 140000),
+        ("postnet k5 80->512", 80, 512, 5, False, 140000),
+        ("enc ffn.w1 k9 256->1024", 256, 1024, 9, False, 14000),
     ]
-    for name, Cin, N, ks, packed, rows, act in shapes:
+    for name, Cin, N, ks, packed, rows in shapes:
         if packed:
-            Bq, L, rinfo = 1, rows, pk.rinfo
+            Bq, L, rinfo, cu = 1, rows, pk.rinfo, pk.cu
         else:
-            Bq, L, rinfo = 200, rows // 200, None
+            Bq, L, rinfo, cu = 200, rows // 200, None, None
         x = torch.randn(Bq, L, Cin, device=dev).to(torch.bfloat16)
-        w = (torch.randn(N, ks, Cin, device=dev) / (ks * Cin) ** 0.5).to(torch.bfloat16)
-        bias = torch.randn(N, device=dev)
+        dy = torch.randn(Bq, L, N, device=dev).to(torch.bfloat16)
         pad = (ks - 1) // 2
 
         def run():
-            return hip.conv_gemm_raw(x, w, bias, Bq, L, Cin, ks, 1, pad, N, act, rinfo=rinfo)
+            return hip.conv_wgrad_raw(x, dy, Bq, L, Cin, ks, 1, pad, N, with_bias=True, rinfo=rinfo, cu=cu)
 
-        hip.lib().ssamd_gemm_set_pp(0)
-        y0 = run()
-        hip.lib().ssamd_gemm_set_pp(1)
-        y1 = run()
-        same = bool(torch.equal(y0, y1))
+        hip.lib().ssamd_wgrad_set_pp(0)
+        w0, b0 = run()
+        w0, b0 = w0.clone(), b0.clone()
+        hip.lib().ssamd_wgrad_set_pp(1)
+        w1, b1 = run()
+        same = bool(torch.equal(w0, w1) and torch.equal(b0, b1))
         t = {0: [], 1: []}
         for rep in range(3):
             for v in (0, 1):
-                hip.lib().ssamd_gemm_set_pp(v)
+                hip.lib().ssamd_wgrad_set_pp(v)
                 t[v].append(timeit(run, a.iters))
-        hip.lib().ssamd_gemm_set_pp(0)
+        hip.lib().ssamd_wgrad_set_pp(0)
         flops = 2.0 * Bq * L * N * ks * Cin
         t0, t1 = min(t[0]), min(t[1])
         print(json.dumps({"shape": name, "rows": Bq * L, "bitwise_equal": same, "base_us": round(t0, 1),
