@@ -747,18 +747,11 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
 }
 
 
-// ----------------------------------------------------------------------------
-// 256x256 tile ("big"), BK = 32, 4-stage LDS-DMA ring (4 x 32 KiB), 8 waves (2 x 4 of
-// 128 x 64).  Twice the MACs per staged byte of the 256x128 ring: the 256x128 tile needs
-// ~48 B/clk/CU from L2 at MFMA rate, more than the ~29 B/clk/CU the L2 serves LDS-DMA at
-// (MI355X_MICROARCH.md, "gather into LDS"); this one needs ~32.  Rows are 64 B; the
-// 16-B chunk c of row r sits at c ^ (2 * ((r >> 3) & 1)), conflict-free for the
-// ds_read_b128 fragment reads (every lane group of 16 hits 16 distinct 16-B slots).
-// ----------------------------------------------------------------------------
-constexpr int BG = 256, BKG = 32, NSTG = 4;
-constexpr int STG_BYTES = 2 * BG * BKG * 2;  // 32 KiB
+// 256x256 tiles (big64 forward / data gradient, the weight gradient): 8 waves (2 x 4 of 128 x 64).
+// (A BK = 32 4-stage ring and a persistent variant of the forward kernel were measured and lost
+// in round 2: profiles/README.md; removed.)
+constexpr int BG = 256;
 
-__device__ __forceinline__ int swz64(int row, int c) { return row * 64 + ((c ^ (((row >> 3) & 1) << 1)) << 4); }
 
 template <bool OUT_F32>
 __device__ __forceinline__ void epi_store4(float (&v)[4], int m, int n, const float* __restrict__ bias,
@@ -798,152 +791,6 @@ __device__ __forceinline__ void epi_store4(float (&v)[4], int m, int n, const fl
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
     *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
-  }
-}
-
-template <bool OUT_F32, bool FASTK, bool PACKED>
-__global__ void __launch_bounds__(NT3, 1) conv_gemm_big_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
-                                                               const float* __restrict__ bias,
-                                                               const bf16_t* __restrict__ aux,
-                                                               const bf16_t* __restrict__ resid,
-                                                               const int64_t* __restrict__ lens, void* __restrict__ Yv,
-                                                               ConvGeom g, int act, int ldy) {
-  const void* const g_zero_chunk = zero_chunk_ptr();
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nN = (g.N + BG - 1) / BG;
-  const int nM = (g.M + BG - 1) / BG;
-  const int2 tmn = tile_of(xcd_remap(blockIdx.x, nN * nM), nM, nN, g.ngrp);
-  const int tm = tmn.x, tn = tmn.y;
-  const int m0 = tm * BG, n0 = tn * BG;
-  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 128 (m) x 64 (n)
-  const float invCin = 1.f / (float)g.Cin;
-
-  // DMA: a wave instruction fills 16 rows x 64 B; A and B: 256 rows = 16 instructions = 2 per wave
-  int a_lim[2], a_t[2], a_m[2], achunk[2];
-  const bf16_t* arow_ptr[2];
-  const bf16_t* brow_ptr[2];
-  bool a_ok[2], b_ok[2];
-  int2 rp[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (i * 8 + wave) * 16 + (lane >> 2);
-    achunk[i] = (lane & 3) ^ (((row >> 3) & 1) << 1);
-    a_m[i] = m0 + row;
-    a_ok[i] = a_m[i] < g.M;
-    if constexpr (PACKED) rp[i] = g.rinfo[a_ok[i] ? a_m[i] : 0];  // both loads issue back to back
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int mm = a_ok[i] ? a_m[i] : 0;
-    if constexpr (PACKED) {
-      a_t[i] = rp[i].x;
-      a_lim[i] = rp[i].y;
-    } else {
-      const int bb = mm / g.L;
-      a_t[i] = mm - bb * g.L;
-      a_lim[i] = g.L;
-    }
-    arow_ptr[i] = X + (long)mm * g.Cin + achunk[i] * 8;
-    const int row = (i * 8 + wave) * 16 + (lane >> 2);
-    const int n = n0 + row;
-    b_ok[i] = n < g.N;
-    brow_ptr[i] = W + (long)(b_ok[i] ? n : 0) * g.K + achunk[i] * 8;  // same row -> same chunk swizzle
-  }
-  auto stage = [&](int kt, int buf) {
-    char* As = smem + buf * STG_BYTES;
-    char* Bs = As + BG * BKG * 2;
-    const int k0 = kt * BKG;
-    if constexpr (FASTK) {  // Cin % 32 == 0: the 32-wide k slab sits in one tap
-      const int tap = k0 / g.Cin;
-      const int cin0 = k0 - tap * g.Cin;
-      const int shift = tap * g.dil - g.pad;
-      const long off = (long)shift * g.Cin + cin0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int ts = a_t[i] + shift;
-        const bool ok = a_ok[i] && (unsigned)ts < (unsigned)a_lim[i];
-        glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 1024);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        glds16(b_ok[i] ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk, Bs + (i * 8 + wave) * 1024);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int k = k0 + achunk[i] * 8;
-        const void* src = g_zero_chunk;
-        if (a_ok[i] && k < g.K) {
-          const int tap = (int)(((float)k + 0.5f) * invCin);
-          const int cin = k - tap * g.Cin;
-          const int sh = tap * g.dil - g.pad;
-          const int ts = a_t[i] + sh;
-          if (ts >= 0 && ts < a_lim[i]) src = arow_ptr[i] - achunk[i] * 8 + (long)sh * g.Cin + cin;
-        }
-        glds16(src, As + (i * 8 + wave) * 1024);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int k = k0 + achunk[i] * 8;
-        glds16((b_ok[i] && k < g.K) ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk,
-               Bs + (i * 8 + wave) * 1024);
-      }
-    }
-  };
-
-  float4v acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (g.K + BKG - 1) / BKG;
-  // prologue: stages 0..2 in flight, wait for stage 0 (4 DMA instructions per wave per stage)
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
-  if (nk > 2) stage(2, 2);
-  if (nk > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  const int c = lane >> 4;  // 16-B k chunk of the fragment (BK = 32: one k32 step per stage)
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & (NSTG - 1);
-    if (kt + 3 < nk) stage(kt + 3, (kt + 3) & (NSTG - 1));
-    const char* As = smem + buf * STG_BYTES;
-    const char* Bs = As + BG * BKG * 2;
-    short8 fa[8], fb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const short8*>(Bs + swz64(wn * 64 + j * 16 + (lane & 15), c));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const short8*>(As + swz64(wm * 128 + i * 16 + (lane & 15), c));
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    // retire stage kt+1 (keep kt+2, kt+3 in flight); the barrier frees buf for re-staging
-    if (kt + 3 < nk) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    else if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + (lane & 15);
-    if (m >= g.M) continue;
-    bool valid = true;
-    if (lens) {
-      const int bb = m / g.L, tt = m - bb * g.L;
-      valid = tt < (int)lens[bb];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= g.N) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      epi_store4<OUT_F32>(v, m, n, bias, aux, resid, valid, act, ldy, Yv);
-    }
   }
 }
 
@@ -1333,183 +1180,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 
 
 // ----------------------------------------------------------------------------
-// Persistent 256x256 / BK=64 GEMM: one block per CU walks its tiles (t = blockIdx + i*grid)
-// as ONE flat sequence of k-steps, so the first stage of the next tile is DMA'd while the
-// current tile's last stage is computed and its epilogue stored -- no exposed prologue or
-// epilogue per tile (that was ~40 % of a K = 256 tile's time).  Same LDS layout and
-// per-stage schedule as conv_gemm_big64_kernel.
-// ----------------------------------------------------------------------------
-template <bool OUT_F32, bool FASTK, bool PACKED>
-__global__ void __launch_bounds__(NT3, 1) conv_gemm_pers_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
-                                                                const float* __restrict__ bias,
-                                                                const bf16_t* __restrict__ aux,
-                                                                const bf16_t* __restrict__ resid,
-                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
-                                                                ConvGeom g, int act, int ldy) {
-  const void* const g_zero_chunk = zero_chunk_ptr();
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nN = (g.N + BG - 1) / BG;
-  const int nM = (g.M + BG - 1) / BG;
-  const int ntile = nN * nM;
-  const int G = gridDim.x;
-  const int my_tiles = ((int)blockIdx.x < ntile) ? (ntile - (int)blockIdx.x + G - 1) / G : 0;
-  const int nk = (g.K + 63) / 64;
-  const long total = (long)my_tiles * nk;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const float invCin = 1.f / (float)g.Cin;
-
-  // ---- stage-side per-lane state (the tile being DMA'd)
-  int a_lim[4], a_t[4], achunk[4];
-  const bf16_t* arow_ptr[4];
-  const bf16_t* brow_ptr[4];
-  bool a_ok[4], b_ok[4];
-  auto tile_coords = [&](int local, int& m0, int& n0) {
-    const int wg = xcd_remap((int)blockIdx.x + local * G, ntile);
-    m0 = (wg / nN) * BG;
-    n0 = (wg % nN) * BG;
-  };
-  auto setup = [&](int local) {
-    int m0, n0;
-    tile_coords(local, m0, n0);
-    int2 rp[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (i * 8 + wave) * 8 + (lane >> 3);
-      achunk[i] = (lane & 7) ^ ((row >> 1) & 7);
-      const int m = m0 + row;
-      a_ok[i] = m < g.M;
-      if constexpr (PACKED) rp[i] = g.rinfo[a_ok[i] ? m : 0];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (i * 8 + wave) * 8 + (lane >> 3);
-      const int mm = a_ok[i] ? m0 + row : 0;
-      if constexpr (PACKED) {
-        a_t[i] = rp[i].x;
-        a_lim[i] = rp[i].y;
-      } else {
-        const int bb = mm / g.L;
-        a_t[i] = mm - bb * g.L;
-        a_lim[i] = g.L;
-      }
-      arow_ptr[i] = X + (long)mm * g.Cin + achunk[i] * 8;
-      const int n = n0 + row;
-      b_ok[i] = n < g.N;
-      brow_ptr[i] = W + (long)(b_ok[i] ? n : 0) * g.K + achunk[i] * 8;
-    }
-  };
-  auto stage = [&](int kt, int buf) {
-    char* As = smem + buf * STG64_BYTES;
-    char* Bs = As + BG * 64 * 2;
-    const int k0 = kt * 64;
-    if constexpr (FASTK) {
-      const int tap = k0 / g.Cin;
-      const int cin0 = k0 - tap * g.Cin;
-      const int shift = tap * g.dil - g.pad;
-      const long off = (long)shift * g.Cin + cin0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ts = a_t[i] + shift;
-        const bool ok = a_ok[i] && (unsigned)ts < (unsigned)a_lim[i];
-        glds16(ok ? (const void*)(arow_ptr[i] + off) : (const void*)g_zero_chunk, As + (i * 8 + wave) * 1024);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        glds16(b_ok[i] ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk, Bs + (i * 8 + wave) * 1024);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + achunk[i] * 8;
-        const void* src = g_zero_chunk;
-        if (a_ok[i] && k < g.K) {
-          const int tap = (int)(((float)k + 0.5f) * invCin);
-          const int cin = k - tap * g.Cin;
-          const int sh = tap * g.dil - g.pad;
-          const int ts = a_t[i] + sh;
-          if (ts >= 0 && ts < a_lim[i]) src = arow_ptr[i] - achunk[i] * 8 + (long)sh * g.Cin + cin;
-        }
-        glds16(src, As + (i * 8 + wave) * 1024);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + achunk[i] * 8;
-        glds16((b_ok[i] && k < g.K) ? (const void*)(brow_ptr[i] + k0) : (const void*)g_zero_chunk,
-               Bs + (i * 8 + wave) * 1024);
-      }
-    }
-  };
-
-  float4v acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
-
-  if (total == 0) return;
-  setup(0);
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  int kt = 0, local = 0;  // compute-side position
-  for (long gs = 0; gs < total; ++gs) {
-    const int buf = (int)(gs & 1);
-    const bool last_k = kt + 1 == nk;
-    if (gs + 1 < total) {
-      if (last_k) {  // next tile: set up its pointers and start its first stage now
-        setup(local + 1);
-        stage(0, buf ^ 1);
-      } else {
-        stage(kt + 1, buf ^ 1);
-      }
-    }
-    const char* As = smem + buf * STG64_BYTES;
-    const char* Bs = As + BG * 64 * 2;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = kk * 4 + (lane >> 4);
-      short8 fa[8], fb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + j * 16 + (lane & 15), c));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + i * 16 + (lane & 15), c));
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    }
-    if (last_k) {  // epilogue of this tile overlaps the next tile's first DMA
-      int m0, n0;
-      tile_coords(local, m0, n0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = m0 + wm * 128 + i * 16 + (lane & 15);
-        bool valid = m < g.M;
-        if (valid && lens) {
-          const int bb = m / g.L, tt = m - bb * g.L;
-          valid = tt < (int)lens[bb];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-          if (m < g.M && n < g.N) {
-            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            epi_store4<OUT_F32>(v, m, n, bias, aux, resid, valid, act, ldy, Yv);
-          }
-          acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      kt = 0;
-      ++local;
-    } else {
-      ++kt;
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-}
-
-// ----------------------------------------------------------------------------
 // Weight gradient.  Tile: 128 (n = cout) x 128 (k = tap*Cin + cin), reduction over
 // rows m in steps of RB = 64.  LDS image per operand: [64 rows][128 cols] bf16,
 // 256-B rows, 8-B column chunks XOR-swizzled by f(row) = ((row&3) | ((row>>3)&1)<<2) << 2
@@ -1681,18 +1351,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(const bf16_t* __restr
 }
 
 
-// ----------------------------------------------------------------------------
-// Weight gradient, ring variant: 256 (n) x 128 (k) tile, 8 waves (4 x 2 of 64 x 64),
-// reduction over rows in RB = 64 row steps through a 3-stage LDS-DMA ring with a
-// counted vmcnt (the forward ring's schedule).  Stage = dY image [64][256] (512-B rows)
-// + X image [64][128] (256-B rows), both XOR-swizzled for ds_read_b64_tr_b16 (f(row) as
-// swz_tr; the 512-B rows span two bank rows, the same f keeps the 8 rows of a half-wave
-// on distinct 32-B slots).  Far fewer split-M slabs than the 128x128 kernels (a block
-// is one CU's worth of work), so the slab reduce is cheap.
-// PACKED: per-row sequence bounds come from an LDS copy of cu[] (advanced incrementally,
-// no per-row global table read in front of the DMA).
-// ----------------------------------------------------------------------------
-constexpr int WR_STAGE = RB * 512 + RB * 256;  // 48 KiB
+// LDS helpers of the 256x256 weight-gradient kernel (64-row dY / X images, 512-B rows)
 
 // ds_read_b64_tr_b16 as inline asm: the builtin carries no LDS alias information, so the
 // compiler's waitcnt pass drains EVERY in-flight LDS-DMA (vmcnt(0)) before it -- which
@@ -1714,379 +1373,6 @@ __device__ __forceinline__ void lgkm_wait_tie(short8 (&fa)[4], short8 (&fb)[4]) 
 __device__ __forceinline__ int swz_tr512(int row, int cc /*8-B chunk 0..63*/) {
   const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
   return row * 512 + ((cc ^ f) << 3);
-}
-
-template <bool PACKED>
-__global__ void __launch_bounds__(NT3, 1) conv_wgrad_ring_kernel(const bf16_t* __restrict__ X,
-                                                                 const bf16_t* __restrict__ dY,
-                                                                 float* __restrict__ slabs,
-                                                                 float* __restrict__ bias_slabs, ConvGeom g,
-                                                                 int rows_per_split) {
-  const void* const g_zero_chunk = zero_chunk_ptr();
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nN = (g.N + 255) / 256;
-  const int nK = (g.K + 127) / 128;
-  const int tiles = nN * nK;
-  // XCD-aware: the blocks of one split (which share the dY / X rows) land on one XCD
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = wg % tiles, split = wg / tiles;
-  const int tn = tile / nK, tk = tile % nK;
-  const int n0 = tn * 256, k0 = tk * 128;
-  const int r_begin = split * rows_per_split;
-  const int r_end = min(g.M, r_begin + rows_per_split);
-  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave >> 1, wk = wave & 1;
-  const float invCin = 1.f / (float)g.Cin;
-  int* cu_s = reinterpret_cast<int*>(smem + NSTAGE * WR_STAGE);
-  if constexpr (PACKED) {
-    for (int i = tid; i <= g.nseq; i += NT3) cu_s[i] = (int)g.cu[i];
-    __syncthreads();
-  }
-
-  float4v acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
-
-  // dY DMA: 4 wave-instructions (2 rows of 512 B each); X DMA: 2 wave-instructions (4 rows of 256 B)
-  int yrow[4];
-  const bf16_t* ysrc[4];
-  bool yok[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = 2 * (i * 8 + wave) + (lane >> 5);
-    yrow[i] = row;
-    const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
-    const int n = n0 + (((lane & 31) ^ (f >> 1)) << 3);
-    yok[i] = n < g.N;
-    ysrc[i] = dY + (yok[i] ? n : 0);
-  }
-  int xrow[2], xshift[2], xcin[2];
-  bool xkok[2];
-  int t_cur[2], s0[2], s1[2], sb[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 4 * (i * 8 + wave) + (lane >> 4);
-    xrow[i] = row;
-    const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
-    const int k = k0 + (((lane & 15) ^ (f >> 1)) << 3);
-    xkok[i] = k < g.K;
-    const int tap = xkok[i] ? (int)(((float)k + 0.5f) * invCin) : 0;
-    xcin[i] = k - tap * g.Cin;
-    xshift[i] = tap * g.dil - g.pad;
-    const int m = r_begin + row;
-    if constexpr (PACKED) {  // sequence of row m: largest b with cu[b] <= m
-      int lo = 0, hi = g.nseq;
-      while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cu_s[mid] <= m) lo = mid; else hi = mid; }
-      sb[i] = lo;
-      s0[i] = cu_s[lo];
-      s1[i] = cu_s[lo + 1];
-    } else {
-      t_cur[i] = m % g.L;
-    }
-  }
-  auto stage = [&](int r0, int buf) {
-    char* Ys = smem + buf * WR_STAGE;
-    char* Xs = Ys + RB * 512;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = r0 + yrow[i];
-      glds16((yok[i] && m < r_end) ? (const void*)(ysrc[i] + (long)m * g.N) : (const void*)g_zero_chunk,
-             Ys + (i * 8 + wave) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = r0 + xrow[i];
-      int ts, lim;
-      if constexpr (PACKED) {
-        while (m >= s1[i] && sb[i] + 1 < g.nseq) {  // rows only move forward: rare LDS step
-          ++sb[i];
-          s0[i] = s1[i];
-          s1[i] = cu_s[sb[i] + 1];
-        }
-        ts = m - s0[i] + xshift[i];
-        lim = s1[i] - s0[i];
-      } else {
-        ts = t_cur[i] + xshift[i];
-        lim = g.L;
-        int t = t_cur[i] + RB;
-        while (t >= g.L) t -= g.L;
-        t_cur[i] = t;
-      }
-      const bool ok = xkok[i] && m < r_end && ts >= 0 && ts < lim;
-      glds16(ok ? (const void*)(X + (long)(m + xshift[i]) * g.Cin + xcin[i]) : (const void*)g_zero_chunk,
-             Xs + (i * 8 + wave) * 1024);
-    }
-  };
-  const bool do_bias = bias_slabs != nullptr && tk == 0;
-  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int bc16 = tid & 31;
-
-  const int nsteps = (r_end - r_begin + RB - 1) / RB;
-  if (nsteps > 0) stage(r_begin, 0);
-  if (nsteps > 1) {
-    stage(r_begin + RB, 1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  int buf = 0;
-  for (int s = 0; s < nsteps; ++s) {
-    if (s + 2 < nsteps) stage(r_begin + (s + 2) * RB, (buf + 2) % NSTAGE);
-    const char* Ys = smem + buf * WR_STAGE;
-    const char* Xs = Ys + RB * 512;
-    if (do_bias) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = (tid >> 5) + 16 * j;
-        const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
-        const short8 v = *reinterpret_cast<const short8*>(Ys + row * 512 + ((bc16 ^ (f >> 1)) << 4));
-#pragma unroll
-        for (int t = 0; t < 8; ++t) bsum[t] += bf2f((bf16_t)v[t]);
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < RB / 32; ++kk) {
-      short8 fa[4], fb[4];
-      const int rbase = kk * 32 + grp * 8 + q;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ca = (wn * 64 + i * 16) / 4 + p;
-        const int cb = (wk * 64 + i * 16) / 4 + p;
-        short4v a0 = ds_read_tr_asm(Ys + swz_tr512(rbase, ca));
-        short4v a1 = ds_read_tr_asm(Ys + swz_tr512(rbase + 4, ca));
-        short4v b0 = ds_read_tr_asm(Xs + swz_tr(rbase, cb));
-        short4v b1 = ds_read_tr_asm(Xs + swz_tr(rbase + 4, cb));
-        fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        fb[i] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-      }
-      lgkm_wait_tie(fa, fb);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-    if (s + 2 < nsteps) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    buf = (buf + 1) % NSTAGE;
-  }
-  if (do_bias) {  // reduce the 16 row-groups sharing a column chunk: one partial per split
-    float* red = reinterpret_cast<float*>(smem);  // [16][256]
-#pragma unroll
-    for (int t = 0; t < 8; ++t) red[(tid >> 5) * 256 + bc16 * 8 + t] = bsum[t];
-    __syncthreads();
-    if (tid < 256 && n0 + tid < g.N) {
-      float t = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) t += red[j * 256 + tid];
-      bias_slabs[(long)split * g.N + n0 + tid] = t;
-    }
-  }
-  float* S = slabs + (long)split * g.N * g.K;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4 + r;
-        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
-        if (n < g.N && k < g.K) S[(long)n * g.K + k] = acc[i][j][r];
-      }
-}
-
-
-// ----------------------------------------------------------------------------
-// Weight gradient, 256 (n) x 256 (k) tile, 32-row steps through a 4-stage LDS-DMA ring
-// (4 x 32 KiB: dY image [32][256] + X image [32][256], 512-B rows, swz_tr512), 8 waves
-// (2 x 4 of 128 x 64), fragments via ds_read_b64_tr_b16 (asm, see ds_read_tr_asm).
-// Twice the MACs per staged byte of the 256x128 ring.
-// ----------------------------------------------------------------------------
-constexpr int WBR = 32;                     // rows per stage
-constexpr int WB_STAGE = 2 * WBR * 512;     // 32 KiB
-
-template <bool PACKED>
-__global__ void __launch_bounds__(NT3, 1) conv_wgrad_big_kernel(const bf16_t* __restrict__ X,
-                                                                const bf16_t* __restrict__ dY,
-                                                                float* __restrict__ slabs,
-                                                                float* __restrict__ bias_slabs, ConvGeom g,
-                                                                int rows_per_split) {
-  const void* const g_zero_chunk = zero_chunk_ptr();
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nN = (g.N + 255) / 256;
-  const int nK = (g.K + 255) / 256;
-  const int tiles = nN * nK;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = wg % tiles, split = wg / tiles;
-  const int tn = tile / nK, tk = tile % nK;
-  const int n0 = tn * 256, k0 = tk * 256;
-  const int r_begin = split * rows_per_split;
-  const int r_end = min(g.M, r_begin + rows_per_split);
-  // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave >> 2, wk = wave & 3;
-  const float invCin = 1.f / (float)g.Cin;
-  int* cu_s = reinterpret_cast<int*>(smem + NSTG * WB_STAGE);
-  if constexpr (PACKED) {
-    for (int i = tid; i <= g.nseq; i += NT3) cu_s[i] = (int)g.cu[i];
-    __syncthreads();
-  }
-
-  float4v acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
-
-  // DMA: a wave instruction = 2 rows of 512 B; each image 32 rows = 16 instructions = 2 per wave
-  int drow[2];
-  const bf16_t* ysrc[2];
-  bool yok[2];
-  int xshift[2], xcin[2];
-  bool xkok[2];
-  int t_cur[2], s0[2], s1[2], sb[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 2 * (i * 8 + wave) + (lane >> 5);
-    drow[i] = row;
-    const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
-    const int c16 = (lane & 31) ^ (f >> 1);
-    const int n = n0 + c16 * 8;
-    yok[i] = n < g.N;
-    ysrc[i] = dY + (yok[i] ? n : 0);
-    const int k = k0 + c16 * 8;
-    xkok[i] = k < g.K;
-    const int tap = xkok[i] ? (int)(((float)k + 0.5f) * invCin) : 0;
-    xcin[i] = k - tap * g.Cin;
-    xshift[i] = tap * g.dil - g.pad;
-    const int m = r_begin + row;
-    if constexpr (PACKED) {
-      int lo = 0, hi = g.nseq;
-      while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cu_s[mid] <= m) lo = mid; else hi = mid; }
-      sb[i] = lo;
-      s0[i] = cu_s[lo];
-      s1[i] = cu_s[lo + 1];
-    } else {
-      t_cur[i] = m % g.L;
-    }
-  }
-  auto stage = [&](int r0, int buf) {
-    char* Ys = smem + buf * WB_STAGE;
-    char* Xs = Ys + WBR * 512;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = r0 + drow[i];
-      glds16((yok[i] && m < r_end) ? (const void*)(ysrc[i] + (long)m * g.N) : (const void*)g_zero_chunk,
-             Ys + (i * 8 + wave) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = r0 + drow[i];
-      int ts, lim;
-      if constexpr (PACKED) {
-        while (m >= s1[i] && sb[i] + 1 < g.nseq) {
-          ++sb[i];
-          s0[i] = s1[i];
-          s1[i] = cu_s[sb[i] + 1];
-        }
-        ts = m - s0[i] + xshift[i];
-        lim = s1[i] - s0[i];
-      } else {
-        ts = t_cur[i] + xshift[i];
-        lim = g.L;
-        int t = t_cur[i] + WBR;
-        while (t >= g.L) t -= g.L;
-        t_cur[i] = t;
-      }
-      const bool ok = xkok[i] && m < r_end && ts >= 0 && ts < lim;
-      glds16(ok ? (const void*)(X + (long)(m + xshift[i]) * g.Cin + xcin[i]) : (const void*)g_zero_chunk,
-             Xs + (i * 8 + wave) * 1024);
-    }
-  };
-  const bool do_bias = bias_slabs != nullptr && tk == 0;
-  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int bc16 = tid & 31;
-
-  const int nsteps = (r_end - r_begin + WBR - 1) / WBR;
-  if (nsteps > 0) stage(r_begin, 0);
-  if (nsteps > 1) stage(r_begin + WBR, 1);
-  if (nsteps > 2) stage(r_begin + 2 * WBR, 2);
-  if (nsteps > 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (nsteps > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int rbase = grp * 8 + q;
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & (NSTG - 1);
-    if (s + 3 < nsteps) stage(r_begin + (s + 3) * WBR, (s + 3) & (NSTG - 1));
-    const char* Ys = smem + buf * WB_STAGE;
-    const char* Xs = Ys + WBR * 512;
-    if (do_bias) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = (tid >> 5) + 16 * j;
-        const int f = ((row & 3) | (((row >> 3) & 1) << 2)) << 2;
-        const short8 v = *reinterpret_cast<const short8*>(Ys + row * 512 + ((bc16 ^ (f >> 1)) << 4));
-#pragma unroll
-        for (int t = 0; t < 8; ++t) bsum[t] += bf2f((bf16_t)v[t]);
-      }
-    }
-    short8 fa[8], fb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cb = (wk * 64 + j * 16) / 4 + p;
-      short4v b0 = ds_read_tr_asm(Xs + swz_tr512(rbase, cb));
-      short4v b1 = ds_read_tr_asm(Xs + swz_tr512(rbase + 4, cb));
-      fb[j] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int ca = (wn * 128 + i * 16) / 4 + p;
-      short4v a0 = ds_read_tr_asm(Ys + swz_tr512(rbase, ca));
-      short4v a1 = ds_read_tr_asm(Ys + swz_tr512(rbase + 4, ca));
-      fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
-                   "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    if (s + 3 < nsteps) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    else if (s + 2 < nsteps) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  if (do_bias) {
-    float* red = reinterpret_cast<float*>(smem);  // [16][256]
-#pragma unroll
-    for (int t = 0; t < 8; ++t) red[(tid >> 5) * 256 + bc16 * 8 + t] = bsum[t];
-    __syncthreads();
-    if (tid < 256 && n0 + tid < g.N) {
-      float t = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) t += red[j * 256 + tid];
-      bias_slabs[(long)split * g.N + n0 + tid] = t;
-    }
-  }
-  float* S = slabs + (long)split * g.N * g.K;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
-        const int k = k0 + wk * 64 + j * 16 + (lane & 15);
-        if (n < g.N && k < g.K) S[(long)n * g.K + k] = acc[i][j][r];
-      }
 }
 
 constexpr int WB64_STAGE = 2 * 64 * 512;  // 64 KiB: dY [64][256] + X [64][256]
@@ -2713,40 +1999,6 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
       }
 }
 
-// dW[n][cin][tap] = sum_s slab[s][n][tap*Cin + cin]   (PyTorch Conv1d / Linear layout)
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slabs, float* __restrict__ dW,
-                                                           const float* __restrict__ bslabs, float* __restrict__ db,
-                                                           int splits, int N, int Cin, int ks) {
-  const long K = (long)Cin * ks;
-  const long total = (long)N * K;
-  if (bslabs) {
-    for (long n = blockIdx.x * (long)blockDim.x + threadIdx.x; n < N; n += (long)gridDim.x * blockDim.x) {
-      float s = 0.f;
-      for (int sp = 0; sp < splits; ++sp) s += bslabs[(long)sp * N + n];
-      db[n] = s;
-    }
-  }
-  // 4 consecutive k per thread (K % 4 == 0: Cin % 8 == 0), float4 slab reads
-  const long total4 = total / 4;
-  for (long e4 = blockIdx.x * (long)blockDim.x + threadIdx.x; e4 < total4; e4 += (long)gridDim.x * blockDim.x) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 8
-    for (int sp = 0; sp < splits; ++sp) {  // unrolled: 8 independent slab loads in flight
-      const float4 v = reinterpret_cast<const float4*>(slabs + (long)sp * total)[e4];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
-    const long e = e4 * 4;
-    const long n = e / K;
-    const int k = (int)(e - n * K);
-    const int tap = k / Cin, cin = k - tap * Cin;  // the 4 k share a tap (Cin % 4 == 0)
-    float* dst = dW + (n * Cin + cin) * ks + tap;
-    dst[0] = acc.x;
-    dst[ks] = acc.y;
-    dst[2 * ks] = acc.z;
-    dst[3 * ks] = acc.w;
-  }
-}
-
 // Split-K finish: out[m][n] = epilogue( sum_s P[s][m][n] ) in a fixed slice order, with the
 // epi_store4 semantics (bias, activation, ReLU-aux mask, residual, row validity).  8 columns per
 // thread (two float4 per slice).
@@ -2919,9 +2171,6 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
 }  // namespace
 
 static bool g_force_lds_epilogue = false;
-static int g_debug_nostore = 0;
-SSAMD_API void ssamd_gemm_debug_nostore(int v) { g_debug_nostore = v; }
-static int g_num_cus = 256;  // persistent grid size (MI355X: 256 CUs); set from the device at first use
 static int g_gemm_variant = -1;  // -1 auto, 0: register staging, 1: LDS-DMA 128x128, 2: LDS-DMA 3-stage ring 256x128
 // s_setprio 1 for waves 4-7 of the 8-wave big64 blocks (MI355X_MICROARCH "static priority for the
 // younger half"), measured per kernel (tools/exp_prio.py): weight gradients on packed rows -2..-4 %,
@@ -3076,70 +2325,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     if (xon || N != 256 || ldy != 256 || out_f32 || !reg || act != 0 || aux || resid || lens) return -3;
     variant = 4;
   }
-  if (g_debug_nostore && variant >= 3) act = -1;
-  if (reg && variant == 3 && N >= 256) {
-    static bool big_set = false;
-    if (!big_set) {
-      allow_lds(conv_gemm_big_kernel<true, true, false>, NSTG * STG_BYTES);
-      allow_lds(conv_gemm_big_kernel<false, true, false>, NSTG * STG_BYTES);
-      allow_lds(conv_gemm_big_kernel<true, false, false>, NSTG * STG_BYTES);
-      allow_lds(conv_gemm_big_kernel<false, false, false>, NSTG * STG_BYTES);
-      allow_lds(conv_gemm_big_kernel<true, true, true>, NSTG * STG_BYTES);
-      allow_lds(conv_gemm_big_kernel<false, true, true>, NSTG * STG_BYTES);
-      allow_lds(conv_gemm_big_kernel<true, false, true>, NSTG * STG_BYTES);
-      allow_lds(conv_gemm_big_kernel<false, false, true>, NSTG * STG_BYTES);
-      big_set = true;
-    }
-    const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
-    const bool fastk = (Cin % BKG) == 0;
-    const size_t LB = NSTG * STG_BYTES;
-#define BIG_LAUNCH(F32, FK)                                                                          \
-    do {                                                                                             \
-      auto kfn = g.rinfo ? conv_gemm_big_kernel<F32, FK, true> : conv_gemm_big_kernel<F32, FK, false>; \
-      hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy); \
-    } while (0)
-    if (out_f32) {
-      if (fastk) BIG_LAUNCH(true, true); else BIG_LAUNCH(true, false);
-    } else {
-      if (fastk) BIG_LAUNCH(false, true); else BIG_LAUNCH(false, false);
-    }
-#undef BIG_LAUNCH
-  } else if (reg && variant == 5 && N >= 256) {
-    static bool pers_set = false;
-    if (!pers_set) {
-      allow_lds(conv_gemm_pers_kernel<true, true, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_pers_kernel<false, true, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_pers_kernel<true, false, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_pers_kernel<false, false, false>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_pers_kernel<true, true, true>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_pers_kernel<false, true, true>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_pers_kernel<true, false, true>, 2 * STG64_BYTES);
-      allow_lds(conv_gemm_pers_kernel<false, false, true>, 2 * STG64_BYTES);
-      pers_set = true;
-    }
-    const int ntile = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
-    static const bool cus_once = [] {
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-        g_num_cus = n;
-      return true;
-    }();
-    (void)cus_once;
-    const int grid = ntile < g_num_cus ? ntile : g_num_cus;
-    const bool fastk = (Cin % 64) == 0;
-    const size_t LB = 2 * STG64_BYTES;
-#define PERS_LAUNCH(F32, FK)                                                                             \
-    do {                                                                                                 \
-      auto kfn = g.rinfo ? conv_gemm_pers_kernel<F32, FK, true> : conv_gemm_pers_kernel<F32, FK, false>;   \
-      hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy);     \
-    } while (0)
-    if (out_f32) {
-      if (fastk) PERS_LAUNCH(true, true); else PERS_LAUNCH(true, false);
-    } else {
-      if (fastk) PERS_LAUNCH(false, true); else PERS_LAUNCH(false, false);
-    }
-#undef PERS_LAUNCH
-  } else if (reg && variant == 4 && N >= 256) {
+  if (reg && variant == 4 && N >= 256) {
     static bool b64_set = false;
     if (!b64_set) {
       allow_lds(conv_gemm_big64_kernel<true, true, false>, B64_LDS);
@@ -3299,8 +2485,6 @@ SSAMD_API void ssamd_wgrad_set_buf(int v) { g_wgrad_buf = v; }
 // 646 -> 519 us vs 718 before, tools/exp_wgrad_pp.py), off on plain rows (PostNet k5 -14 %)
 static int g_wgrad_pp = -1;
 SSAMD_API void ssamd_wgrad_set_pp(int v) { g_wgrad_pp = v; }
-static int g_wgrad_reduce_old = 0;  // 1: the pre-split-parallel reduction kernels (A/B measurement)
-SSAMD_API void ssamd_wgrad_set_reduce(int old) { g_wgrad_reduce_old = old; }
 
 // Workspace: splits * N * ks*Cin floats.  Returns the number of splits used via *splits_used.
 // ws: splits*N*ks*Cin (+ splits*N when db != null) floats.  db (optional): fused bias gradient.
@@ -3308,14 +2492,6 @@ static void launch_reduce(const float* ws, float* dW, const float* bws, float* d
                           int blocks, hipStream_t s) {
   const int K = Cin * ks;
   (void)blocks;
-  if (g_wgrad_reduce_old) {
-    if (ks > 1 && (size_t)K * 4 <= 65536)  // transposed through LDS: contiguous dW rows
-      hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(N), dim3(256), (size_t)K * 4, s, ws, dW, bws, db, splits, N, Cin,
-                         ks);
-    else
-      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, dW, bws, db, splits, N, Cin, ks);
-    return;
-  }
   // many output rows of a k > 1 conv: one block per row keeps the dW stores contiguous; otherwise
   // (Linear / k = 1 weights, few rows) the split-parallel kernel keeps every CU busy
   if (ks > 1 && N >= 256 && (size_t)K * 4 <= 65536) {
@@ -3368,7 +2544,7 @@ static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits)
   return best;
 }
 
-static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64), 0: 128x128, 1: 256x128 ring, 2: 256x256 BK=32 ring
+static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64 when it applies), 0: force the 128x128 kernels
 SSAMD_API void ssamd_wgrad_set_blocks(int b) { g_wgrad_blocks = b > 0 ? b : 0; }
 SSAMD_API void ssamd_wgrad_set_variant(int v) { g_wgrad_variant = v; }
 
@@ -3388,14 +2564,11 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     return (int)hipGetLastError();
   }
   const bool packed = rinfo != nullptr;
-  bool ring = N >= 256 && (!packed || (cu != nullptr && nseq > 0 && nseq < 4096));
-  if (g_wgrad_variant == 0) ring = false;
-  // 256x256 ring when there are >= 2 output tiles (a single-tile problem -- e.g. 256x256 Linear -- needs so
-  // many split-M slabs that the 128x128 kernels win, measured); the 256x128 ring only when forced
-  const bool big = ring && g_wgrad_variant != 1 && N >= 256 && g.K >= 256 && (long)N * g.K >= 2L * 256 * 256 &&
-                   (!packed || nseq < 8192);
-  if (g_wgrad_variant < 0 && !big) ring = false;
-  if (big && g_wgrad_variant != 2) {
+  // 256x256 kernel (split-M slabs + fixed-order reduce) when there are >= 2 output tiles; variant 0
+  // forces the 128x128 kernels (the choice for single-tile and narrow problems)
+  const bool big = g_wgrad_variant != 0 && N >= 256 && g.K >= 256 && (long)N * g.K >= 2L * 256 * 256 &&
+                   (!packed || (cu != nullptr && nseq > 0 && nseq < 8192));
+  if (big) {
     static bool b64_set = false;
     if (!b64_set) {
       allow_lds(conv_wgrad_big64_kernel<false, false, false>, 160 * 1024);
@@ -3432,56 +2605,6 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
     if (bufok && (g_wgrad_pp < 0 ? packed : g_wgrad_pp != 0))
       wb = packed ? conv_wgrad_big64_kernel<true, false, true, true> : conv_wgrad_big64_kernel<false, false, true, true>;
     hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
-    const int blocks = (int)min((slab + 255) / 256, 8192L);
-    launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);
-    return (int)hipGetLastError();
-  }
-  if (big) {
-    static bool big_set = false;
-    if (!big_set) {
-      allow_lds(conv_wgrad_big_kernel<false>, NSTG * WB_STAGE + 32768);
-      allow_lds(conv_wgrad_big_kernel<true>, NSTG * WB_STAGE + 32768);
-      big_set = true;
-    }
-    const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
-    int splits = (512 + tiles - 1) / tiles;
-    const int max_by_rows = (g.M + 8 * WBR - 1) / (8 * WBR);  // >= 8 ring steps per split
-    if (splits > max_by_rows) splits = max_by_rows;
-    if (splits > max_splits) splits = max_splits;
-    if ((long)splits * (slab + N) > ws_floats) splits = (int)(ws_floats / (slab + N));
-    if (splits < 1) return -3;
-    int rows_per_split = (g.M + splits - 1) / splits;
-    rows_per_split = (rows_per_split + WBR - 1) / WBR * WBR;
-    splits = (g.M + rows_per_split - 1) / rows_per_split;
-    float* bws = db ? ws + (long)splits * slab : nullptr;
-    const size_t lds = NSTG * WB_STAGE + (packed ? (size_t)(nseq + 1) * 4 : 0);
-    auto wb = packed ? conv_wgrad_big_kernel<true> : conv_wgrad_big_kernel<false>;
-    hipLaunchKernelGGL(wb, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
-    const int blocks = (int)min((slab + 255) / 256, 8192L);
-    launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);
-    return (int)hipGetLastError();
-  }
-  if (ring) {
-    static bool ring_set = false;
-    if (!ring_set) {
-      allow_lds(conv_wgrad_ring_kernel<false>, NSTAGE * WR_STAGE + 16384);
-      allow_lds(conv_wgrad_ring_kernel<true>, NSTAGE * WR_STAGE + 16384);
-      ring_set = true;
-    }
-    const int tiles = ((N + 255) / 256) * ((g.K + 127) / 128);
-    int splits = (512 + tiles - 1) / tiles;
-    const int max_by_rows = (g.M + 4 * RB - 1) / (4 * RB);  // >= 4 ring steps per split
-    if (splits > max_by_rows) splits = max_by_rows;
-    if (splits > max_splits) splits = max_splits;
-    if ((long)splits * (slab + N) > ws_floats) splits = (int)(ws_floats / (slab + N));
-    if (splits < 1) return -3;
-    int rows_per_split = (g.M + splits - 1) / splits;
-    rows_per_split = (rows_per_split + RB - 1) / RB * RB;
-    splits = (g.M + rows_per_split - 1) / rows_per_split;
-    float* bws = db ? ws + (long)splits * slab : nullptr;
-    const size_t lds = NSTAGE * WR_STAGE + (packed ? (size_t)(nseq + 1) * 4 : 0);
-    auto wr = packed ? conv_wgrad_ring_kernel<true> : conv_wgrad_ring_kernel<false>;
-    hipLaunchKernelGGL(wr, dim3(tiles * splits), dim3(NT3), lds, s, X, dY, ws, bws, g, rows_per_split);
     const int blocks = (int)min((slab + 255) / 256, 8192L);
     launch_reduce(ws, dW, bws, db, splits, N, Cin, ks, blocks, s);
     return (int)hipGetLastError();

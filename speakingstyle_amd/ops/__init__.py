@@ -20,7 +20,6 @@ from . import reference as ref
 from .packing import PackInfo, pack as _pack, unpack as _unpack  # noqa: F401
 
 _FORCED = os.environ.get("SSAMD_BACKEND")  # "reference" | "hip" | None
-_NO_MAILBOX = os.environ.get("SSAMD_NO_MAILBOX") == "1"  # A/B switch for the residual-gradient fusion
 
 
 def set_backend(name: Optional[str]):
@@ -67,7 +66,7 @@ def ln_spec(residual, ln_w, ln_b, **kw):
 def residual_mailbox(x, weights=None):
     """A GradMailbox for a sub-layer whose input x is also its LayerNorm residual (HIP path
     only; None otherwise): the residual gradient is added inside the first GEMM's backward."""
-    if not use_hip(x) or x.dtype != torch.bfloat16 or not x.requires_grad or _NO_MAILBOX:
+    if not use_hip(x) or x.dtype != torch.bfloat16 or not x.requires_grad:
         return None
     hip = _hip()
     if weights is not None and hip.gradslots.fused_data(list(weights)) is None:

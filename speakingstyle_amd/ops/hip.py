@@ -41,7 +41,6 @@ _SIGS = {
     "ssamd_wgrad_set_variant": [I],
     "ssamd_attn_set_nf": [I, I],
     "ssamd_attn_set_nf32": [I, I],
-    "ssamd_wgrad_set_reduce": [I],
     "ssamd_wgrad_set_imm": [I],
     "ssamd_gemm_set_splitk": [I],
     "ssamd_gemm_set_prio": [I],
@@ -105,8 +104,6 @@ def lib():
                     if fn is not None:
                         fn.argtypes = args
                         fn.restype = _RESTYPES.get(name, I)
-                if os.environ.get("SSAMD_WGRAD_BLOCKS"):  # tuning knob: split-M target of the wgrad GEMMs
-                    handle.ssamd_wgrad_set_blocks(int(os.environ["SSAMD_WGRAD_BLOCKS"]))
                 _lib = handle
     return _lib
 
@@ -331,7 +328,6 @@ def conv_gemm_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, N, act=0, aux=None, re
     return y
 
 
-_NO_RELU_MASK = os.environ.get("SSAMD_RELU_MASK", "1") == "0"  # A/B: the bf16 aux operand instead
 _SIGS["ssamd_conv_gemm_mask"] = [P, P, P, P, I, I, I, I, I, I, I, I, P, P, P, P]
 
 
@@ -645,7 +641,7 @@ class _FFNFn(torch.autograd.Function):
         r2 = rinfo if k2 > 1 else None
         ctx.cu = (cu if k1 > 1 else None, cu if k2 > 1 else None)
         mask = None
-        if H >= 256 and H % 8 == 0 and not _NO_RELU_MASK and has("ssamd_conv_gemm_mask"):
+        if H >= 256 and H % 8 == 0 and has("ssamd_conv_gemm_mask"):
             # ReLU bitmask of h for the second conv's data gradient (M x H/8 bytes instead of h itself)
             mask = torch.empty(B * L, H // 8, device=x.device, dtype=torch.uint8)
             h = conv_gemm_mask_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, (k1 - 1) // 2, H, 1,
@@ -1286,7 +1282,6 @@ _adam_ws = {}
 
 
 _adam_plan = {}
-_ADAM_IMAGES = os.environ.get("SSAMD_ADAM_IMAGES", "1") != "0"  # 0: adam_kernel + lazy weight_prep (A/B)
 _adam_plan_builds = [0]  # diagnostics: plan (re)builds
 
 
@@ -1369,7 +1364,7 @@ def clip_adam_step(p, g, m, v, lr, betas, eps, wd, step, clip, norm_out, skipped
     ws = _adam_ws.get(p.device)
     if ws is None or ws.numel() < n_ws:  # [global sum of squares, per-block partials]
         ws = _adam_ws[p.device] = torch.zeros(n_ws, device=p.device, dtype=torch.float32)
-    if images and _ADAM_IMAGES and has("ssamd_clip_adam_img"):
+    if images and has("ssamd_clip_adam_img"):
         plan = _adam_image_plan(p)
         rc = lib().ssamd_clip_adam_img(_ptr(p), _ptr(g), _ptr(m), _ptr(v), p.numel(), _ptr(ws), float(clip),
                                        float(lr), float(betas[0]), float(betas[1]), float(eps), float(wd), int(step),
