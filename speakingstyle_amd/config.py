@@ -51,6 +51,9 @@ _MODEL_DEFAULTS: Config = {
     # the reference (config/BC2013/model.yaml:33-39); we implement it.
     "gst": None,
     "multi_speaker": False,
+    # condition on preprocessing.speaker_embedder vectors through a learned projection (not in the
+    # reference model: its checkpoints lack the projection, so this is opt-in)
+    "speaker_embed_proj": False,
     "max_seq_len": 1000,
     "vocoder": {"model": "HiFi-GAN", "speaker": "LJSpeech"},
 }

@@ -292,10 +292,12 @@ class FastSpeech2(nn.Module):
             self.speaker_emb = nn.Embedding(_n_speakers(preprocess_config), d)
         # external speaker embeddings (reference ``synthesize.py:268-277``: ``{spk}-spker_embed.npy`` under
         # ``preprocessed_path/spker_embed`` when ``preprocessing.speaker_embedder != 'none'``).  The
-        # reference loads them and drops them; here they condition the model: a per-speaker table
-        # (non-persistent buffer, looked up by speaker id in training and synthesis alike) projected
-        # to the encoder width and added next to the speaker-id embedding.
-        table = _spker_table(preprocess_config) if model_config["multi_speaker"] else None
+        # reference loads them and drops them, and so does this model unless ``speaker_embed_proj: true``
+        # is set in model.yaml (opt-in: it adds a trainable projection the reference checkpoints lack).
+        # With it, a per-speaker table (non-persistent buffer, looked up by speaker id in training and
+        # synthesis alike) is projected to the encoder width and added next to the speaker-id embedding.
+        use_table = model_config["multi_speaker"] and bool(model_config.get("speaker_embed_proj", False))
+        table = _spker_table(preprocess_config) if use_table else None
         self.spker_embed_proj = None
         if table is not None:
             self.register_buffer("spker_table", table, persistent=False)

@@ -1,6 +1,8 @@
 """External speaker embeddings (reference ``synthesize.py:268-277``): with
-``preprocessing.speaker_embedder != 'none'`` the per-speaker ``spker_embed/{spk}-spker_embed.npy``
-vectors are loaded into a table and condition the encoder output next to the speaker-id embedding."""
+``preprocessing.speaker_embedder != 'none'`` AND the opt-in ``speaker_embed_proj: true`` the per-speaker
+``spker_embed/{spk}-spker_embed.npy`` vectors are loaded into a table and condition the encoder output
+next to the speaker-id embedding; without the flag the model keeps the reference layout (the
+reference loads the vectors and drops them)."""
 import json
 import os
 
@@ -8,7 +10,7 @@ import numpy as np
 import torch
 
 
-def _cfg(tmp_path, embedder):
+def _cfg(tmp_path, embedder, proj=True):
     from speakingstyle_amd.config import load_named
 
     pp, mc, tc = load_named("LJSpeech")
@@ -22,6 +24,7 @@ def _cfg(tmp_path, embedder):
     pp["path"]["preprocessed_path"] = str(root)
     pp["preprocessing"]["speaker_embedder"] = embedder
     mc["multi_speaker"] = True
+    mc["speaker_embed_proj"] = proj
     mc["transformer"].update(encoder_layer=1, decoder_layer=1, conv_filter_size=64, encoder_hidden=32,
                              decoder_hidden=32, encoder_head=2, decoder_head=2)
     mc["variance_predictor"]["filter_size"] = 32
@@ -59,5 +62,14 @@ def test_no_embedder_keeps_reference_layout(tmp_path):
     from speakingstyle_amd.models.fastspeech2 import FastSpeech2
 
     pp, mc, tc = _cfg(tmp_path, "none")
+    m = FastSpeech2(pp, mc)
+    assert m.spker_embed_proj is None and not any("spker" in k for k in m.state_dict())
+
+
+def test_embedder_without_opt_in_keeps_reference_layout(tmp_path):
+    """speaker_embedder alone (reference configs): no projection, reference state-dict keys."""
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+
+    pp, mc, tc = _cfg(tmp_path, "DeepSpeaker", proj=False)
     m = FastSpeech2(pp, mc)
     assert m.spker_embed_proj is None and not any("spker" in k for k in m.state_dict())
