@@ -19,13 +19,17 @@ Adam state, synthetic LJSpeech-shaped data (phoneme counts drawn from the real
 LJSpeech metadata, ~8.1 frames per phoneme, groups of 4 batches sorted by text
 length exactly like the reference loader), random-init weights.  Scaling is
 weak: every rank runs ``--batch`` utterances (default: the config's
-``optimizer.batch_size`` = 200), global batch N*200.  (``train.py`` instead
-splits ``batch_size`` across ranks -- the reference semantics of a global batch.)
+``optimizer.batch_size`` = 200), global batch N*200; ``--frames-per-gpu F`` sizes
+each rank's batch by a padded-frame budget instead (``mi355x.frames_per_gpu``, the
+same per-GPU batch semantics ``train.py`` uses when that key is set; without it
+``train.py`` splits ``batch_size`` across ranks -- the reference's global batch).
 
 Synthesis (``synth_rtf`` field, BASELINE's second metric): text ids -> int16 wav
-through FastSpeech2 + style encoder (``--synth-config``, default BC2013 = FiLM
-reference encoder on a reference mel) + HiFi-GAN V1, batch 256 per GPU,
-independent shards per rank; RTF = max-over-ranks wall / total audio seconds.
+through FastSpeech2 + style encoder (``--synth-config``, default BC2013_GST = the
+GST reference encoder + style-token attention on a reference mel, BASELINE #5) +
+HiFi-GAN V1, batch 256 per GPU, independent shards per rank; RTF = max-over-ranks
+wall / total audio seconds.  ``synth.rtf_also`` repeats it with ``--synth-also``
+(default BC2013: the reference's FiLM reference encoder).
 See ``speakingstyle_amd/benchmark.py`` for the duration-injection detail.
 """
 from __future__ import annotations
@@ -54,7 +58,10 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (default: config batch_size)")
     ap.add_argument("--pool", type=int, default=8, help="distinct synthetic batches cycled through")
     ap.add_argument("--backend", default=None, choices=[None, "hip", "reference"])
-    ap.add_argument("--synth-config", default="BC2013")
+    ap.add_argument("--synth-config", default="BC2013_GST",
+                    help="FS2 + style encoder of the synth_rtf line (BASELINE #5: FS2 + GST)")
+    ap.add_argument("--synth-also", default="BC2013",
+                    help="second synthesis config reported as synth.rtf_also ('' disables): the FiLM encoder")
     ap.add_argument("--synth-batch", type=int, default=256)
     ap.add_argument("--synth-steps", type=int, default=3, help="0 disables the synthesis phase")
     ap.add_argument("--synth-warmup", type=int, default=1)
@@ -103,6 +110,13 @@ def run(args):
 
     tr = B.train_phase(args, rank, world, device)
     sy = B.synth_phase(args, rank, world, device) if args.synth_steps > 0 else None
+    sy2 = None
+    if sy is not None and args.synth_also and args.synth_also != args.synth_config:
+        import copy
+
+        a2 = copy.copy(args)
+        a2.synth_config = args.synth_also
+        sy2 = B.synth_phase(a2, rank, world, device)
 
     value = tr["frames"] / tr["elapsed"]
     rec = {
@@ -151,6 +165,9 @@ def run(args):
                 "parallelism": f"dp{world} (independent shards)",
             },
         })
+        if sy2 is not None:
+            rec["synth"]["rtf_also"] = {"model": f"FastSpeech2 ({args.synth_also}) + HiFi-GAN V1", "rtf": sy2["rtf"],
+                                        "audio_seconds": round(sy2["audio_s"], 2)}
     if rank == 0:
         B.report(rec)
     if world > 1:
