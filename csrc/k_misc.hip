@@ -1063,6 +1063,32 @@ __global__ void __launch_bounds__(256) unpack_rows_kernel(const T* __restrict__ 
   }
 }
 
+// Between two packed layouts of the same sequences: output row i is (b, t) = divmod(dst_out[i], M_out);
+// it takes source row cu_src[b] + t when t < lens_src[b] (else 0), plus pe[t] when given.  8 channels
+// per thread (16-B bf16 / 2x16-B fp32 accesses).
+template <typename T>
+__global__ void __launch_bounds__(256) repack_rows_kernel(const T* __restrict__ src, const int64_t* __restrict__ cu_src,
+                                                          const int64_t* __restrict__ lens_src,
+                                                          const int64_t* __restrict__ dst_out, int M_out, long rows,
+                                                          int C, const bf16_t* __restrict__ pe, T* __restrict__ out) {
+  const int c8n = C / 8;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < rows * c8n; e += (long)gridDim.x * 256) {
+    const long i = e / c8n;
+    const int c0 = (int)(e - i * c8n) * 8;
+    const long d = dst_out[i];
+    const int b = (int)(d / M_out), t = (int)(d - (long)b * M_out);
+    const bool ok = t < lens_src[b];
+    const T* xs = src + (cu_src[b] + t) * C + c0;
+    T* o = out + i * C + c0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float v = ok ? ld_as_f<T>(xs + q) : 0.f;
+      if (pe) v += bf2f(pe[(long)t * C + c0 + q]);
+      st_from_f<T>(o + q, v);
+    }
+  }
+}
+
 // block = 64 columns x 4 row lanes over a 256-row chunk: coalesced 64-column row pieces, 64 rows
 // per thread, lanes combined in LDS in a fixed order
 template <typename T>
@@ -1098,6 +1124,21 @@ SSAMD_API int ssamd_pack_rows(const void* x, const int64_t* dst, const bf16_t* p
   else
     hipLaunchKernelGGL(pack_rows_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)x, dst, pe, M, R, C,
                        (bf16_t*)out);
+  return (int)hipGetLastError();
+}
+
+// f32: 1 = fp32 rows, 0 = bf16 rows; pe (bf16 [>= max t + 1, C]) optional
+SSAMD_API int ssamd_repack_rows(const void* src, const int64_t* cu_src, const int64_t* lens_src, const int64_t* dst_out,
+                                int M_out, long rows, int C, const bf16_t* pe, int f32, void* out, hipStream_t s) {
+  if (C % 8) return -1;
+  if (rows == 0) return 0;
+  const int g = grid_for(rows * (C / 8));
+  if (f32)
+    hipLaunchKernelGGL(repack_rows_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)src, cu_src, lens_src, dst_out,
+                       M_out, rows, C, pe, (float*)out);
+  else
+    hipLaunchKernelGGL(repack_rows_kernel<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)src, cu_src, lens_src,
+                       dst_out, M_out, rows, C, pe, (bf16_t*)out);
   return (int)hipGetLastError();
 }
 

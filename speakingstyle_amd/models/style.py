@@ -46,16 +46,16 @@ class ReferenceEncoder(nn.Module):
         self.feature_wise_affine = LinearNorm(d, 2 * d)
 
     def forward(self, mel, mel_lens, max_len=None):
+        host = getattr(mel_lens, "host_lengths", None)
+        M = mel.shape[1]
+        if (host is not None and not self.mean_over_valid and ops.use_hip(mel)
+                and (self.training or M <= self.max_seq_len)):
+            return self._forward_packed(mel, mel_lens, host)
         h = mel
-        M = h.shape[1]
         for seq in self.layer_stack:
             conv, ln = seq[0], seq[2]
             h = conv(h, act="relu")
             h = ops.add_layernorm(h, None, ln.weight, ln.bias, post_drop=self.dropout, training=self.training)
-        host = getattr(mel_lens, "host_lengths", None)
-        if (host is not None and not self.mean_over_valid and ops.use_hip(h)
-                and (self.training or M <= self.max_seq_len)):
-            return self._forward_packed(h, mel_lens, host)
         # pad frames are zeroed once after the whole conv stack (modules.py:370-371)
         h = h.masked_fill(ops.lengths_to_mask(mel_lens, M).unsqueeze(-1), 0.0)
         if (not self.training) and M > self.max_seq_len:
@@ -76,18 +76,37 @@ class ReferenceEncoder(nn.Module):
         gb = self.feature_wise_affine(pooled.to(h.dtype))
         return gb[:, : self.d_model], gb[:, self.d_model:]
 
-    def _forward_packed(self, h, mel_lens, host):
-        """FFT blocks over the valid frames only (``ops/packing.py``), same result as the padded
-        path: pad rows there are zeroed after every sublayer, so they contribute nothing to the
-        attention (masked keys), to the k=3 FFN convs (zero padding at sequence ends) or to the
-        mean, which still divides by the padded length (D8).  The host lengths size the packed
-        rows without a device sync."""
-        M = min(h.shape[1], self.max_seq_len)
-        if h.shape[1] != M:
-            h = h[:, :M].contiguous()
+    def halo(self) -> int:
+        """Frames past a sequence's end that the conv stack must still compute for its valid
+        outputs to equal the padded computation: the reference zeroes pads only AFTER the stack
+        (``model/modules.py:366-371``), so layer l sees the previous layers' non-zero values in the
+        first (k-1)/2 * (layers-1) pad frames."""
+        k = self.layer_stack[0][0].conv.kernel_size[0]
+        return (k - 1) // 2 * (len(self.layer_stack) - 1)
+
+    def _forward_packed(self, mel, mel_lens, host):
+        """Valid frames only (``ops/packing.py``), same result as the padded path.
+
+        * conv stack on rows packed with a halo of ``halo()`` pad frames per sequence (mel pad rows
+          are zero, as in the padded batch); the packed convs zero-pad past each packed length, which
+          is exactly where the padded path's inputs are zero or irrelevant to the valid outputs;
+        * the FFT blocks on the valid rows (repacked from the halo layout with the PE added): pad rows
+          there are zeroed after every sublayer, so they contribute nothing to the attention (masked
+          keys), to the k=3 FFN convs or to the mean, which still divides by the padded length (D8).
+        The host lengths size both packings without a device sync."""
+        Mf = mel.shape[1]
+        hl = self.halo()
+        R_h = int(sum(min(int(v) + hl, Mf) for v in host))
+        pk_h = ops.PackInfo.build((mel_lens.clamp(max=Mf) + hl).clamp(max=Mf), Mf, R_h)
+        h = ops.pack_rows(mel, pk_h)
+        for seq in self.layer_stack:
+            conv, ln = seq[0], seq[2]
+            h = ops.conv1d(h, conv.conv.weight, conv.conv.bias, conv.pad, conv.dil, "relu", pack=pk_h)
+            h = ops.add_layernorm(h, None, ln.weight, ln.bias, post_drop=self.dropout, training=self.training)
+        M = min(Mf, self.max_seq_len)
         R = int(sum(min(int(v), M) for v in host))
         pk = ops.PackInfo.build(mel_lens, M, R)
-        x = ops.pack_rows(h, pk, self.position_enc[0, :M])
+        x = ops.repack_rows(h, pk_h, pk, self.position_enc[0, :M])
         x = self.fftb_linear(x)
         for blk in self.fftb_stack:
             x = blk(x, pk.lens, None, pack=pk)

@@ -85,10 +85,24 @@ def linear_group(x, weights, biases, mailbox=None):
     return ref.linear(x, torch.cat(list(weights), 0), torch.cat(list(biases), 0))
 
 
-def conv1d(x, w, b=None, pad=0, dil=1, act=None):
+def conv1d(x, w, b=None, pad=0, dil=1, act=None, pack: Optional[PackInfo] = None):
+    """``pack``: x is packed ``[1, R, C]``; the conv zero-pads at every sequence end."""
     if use_hip(x):
-        return _hip().conv1d(x, w, b, pad, dil, act)
+        return _hip().conv1d(x, w, b, pad, dil, act, pack=pack)
+    if pack is not None:
+        return pack_rows(ref.conv1d(unpack_rows(x, pack), w, b, pad, dil, act), pack)
     return ref.conv1d(x, w, b, pad, dil, act)
+
+
+def repack_rows(x, src_pack: PackInfo, out_pack: PackInfo, pe=None):
+    """Rows of one packed layout -> another over the same sequences (+ ``pe[t]``); rows past the
+    source length are 0 (e.g. the halo-packed FiLM conv stack -> the FFT blocks' packed rows)."""
+    if use_hip(x):
+        return _hip().repack_rows(x, src_pack, out_pack, pe)
+    y = unpack_rows(x, src_pack)  # [B, M_src, C], 0 past each source length
+    if y.shape[1] < out_pack.M:
+        y = F.pad(y, (0, 0, 0, out_pack.M - y.shape[1]))
+    return pack_rows(y[:, : out_pack.M], out_pack, pe)
 
 
 def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None, mailbox=None, ln=None):

@@ -484,17 +484,23 @@ def relu_mask_(dy, y, out=None):
 # ------------------------------------------------------------------------ conv / linear
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, pad, dil, act, out_f32, ln=None):
+    def forward(ctx, x, w, b, pad, dil, act, out_f32, ln=None, pack=None):
+        """``pack``: x is packed [1, R, Cin]; the conv zero-pads at every sequence end (rinfo)."""
         B, L, Cin = x.shape
         ks = 1 if w.dim() == 2 else w.shape[2]
         N = w.shape[0]
         xc = x.contiguous()
         bf = None if b is None else b.detach().float().contiguous()
+        rinfo = pack.rinfo if (pack is not None and ks > 1) else None
+        if rinfo is not None:
+            assert B == 1 and L == pack.R, "packed conv: x must be [1, R, C]"
         if ln is not None:
-            assert act is None and not out_f32 and N == 256
+            assert act is None and not out_f32 and N == 256 and rinfo is None
             y = conv_gemm_ln_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, ln)
         else:
-            y = conv_gemm_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, N, _ACT[act], out_f32=out_f32)
+            y = conv_gemm_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, N, _ACT[act], out_f32=out_f32,
+                              rinfo=rinfo)
+        ctx.pack = pack if rinfo is not None else None
         ctx.geom = (B, L, Cin, ks, dil, pad, N)
         ctx.act = act
         ctx.has_b = b is not None
@@ -512,23 +518,26 @@ class _ConvFn(torch.autograd.Function):
         elif ctx.act is not None:
             raise NotImplementedError("backward for activation " + str(ctx.act))
         dx = dw = db = None
+        pk = ctx.pack
+        rinfo = None if pk is None else pk.rinfo
         if ctx.needs_input_grad[0]:
-            dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin)
+            dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin, rinfo=rinfo)
         want_b = ctx.has_b and ctx.needs_input_grad[2]
         sb = gradslots.claim(ctx.b) if want_b else None
         if ctx.needs_input_grad[1]:
             sw = gradslots.claim(w)
-            res = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b, dW=sw, db=sb)
+            res = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b, dW=sw, db=sb, rinfo=rinfo,
+                                 cu=None if pk is None else pk.cu)
             dw, db = res if want_b else (res, None)
             if w.dim() == 2:
                 dw = dw.view(N, Cin)
         elif want_b:
             db = colsum_raw(dy, N, sb)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
-def conv1d(x, w, b=None, pad=0, dil=1, act=None, out_f32=False):
-    return _ConvFn.apply(x, w, b, pad, dil, act, out_f32)
+def conv1d(x, w, b=None, pad=0, dil=1, act=None, out_f32=False, pack=None):
+    return _ConvFn.apply(x, w, b, pad, dil, act, out_f32, None, pack)
 
 
 def linear(x, w, b=None, act=None, out_f32=False, ln=None):
@@ -1916,6 +1925,46 @@ def _unpack_raw(x, pk, fill=None):
                                  _stream())
     _check(rc, "ssamd_unpack_rows")
     return out
+
+
+_SIGS.update({"ssamd_repack_rows": [P, P, P, P, I, L_, I, P, I, P, P]})
+
+
+def _repack_raw(x, src_pk, out_pk, pe=None):
+    """Rows of packed layout ``src_pk`` -> packed layout ``out_pk`` (same sequences; an output row
+    whose position is past the source length gets 0), + ``pe[t]``."""
+    f32 = x.dtype == torch.float32
+    xc = x.contiguous() if f32 else x.to(torch.bfloat16).contiguous()
+    C = xc.shape[-1]
+    assert xc.numel() == src_pk.R * C and src_pk.B == out_pk.B, "repack_rows: x must be [1, R_src, C]"
+    pec = None if pe is None else pe.to(torch.bfloat16).contiguous()
+    if pec is not None:
+        assert pec.shape[0] >= out_pk.M and pec.shape[-1] == C
+    out = torch.empty(1, out_pk.R, C, device=xc.device, dtype=xc.dtype)
+    rc = lib().ssamd_repack_rows(_ptr(xc), _ptr(src_pk.cu), _ptr(src_pk.lens), _ptr(out_pk.dst), out_pk.M, out_pk.R, C,
+                                 _ptr(pec), int(f32), _ptr(out), _stream())
+    _check(rc, "ssamd_repack_rows")
+    return out
+
+
+class _RepackRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, src_pk, out_pk, pe):
+        ctx.pks, ctx.dtype = (src_pk, out_pk), x.dtype
+        return _repack_raw(x, src_pk, out_pk, pe)
+
+    @staticmethod
+    def backward(ctx, g):
+        src_pk, out_pk = ctx.pks
+        gc = g.contiguous() if g.dtype == torch.float32 else g.to(torch.bfloat16).contiguous()
+        return _repack_raw(gc, out_pk, src_pk).to(ctx.dtype), None, None, None  # rows not gathered: 0
+
+
+def repack_rows(x, src_pk, out_pk, pe=None):
+    """[1, R_src, C] packed as ``src_pk`` -> [1, R_out, C] packed as ``out_pk`` (+ ``pe[t]``)."""
+    if x.shape[-1] % 8 or x.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"repack_rows: C={x.shape[-1]} dtype={x.dtype} not covered by the HIP kernel")
+    return _RepackRowsFn.apply(x, src_pk, out_pk, pe)
 
 
 class _PackRowsFn(torch.autograd.Function):
