@@ -70,6 +70,8 @@ def parse(argv=None):
     ap.add_argument("--phase-times", action="store_true", help="per-phase host/device ms of the timed steps")
     ap.add_argument("--frames-per-gpu", type=int, default=None,
                     help="per-GPU padded mel-frame budget per step (mi355x.frames_per_gpu) instead of --batch")
+    ap.add_argument("--no-side-wgrad", action="store_true",
+                    help="weight gradients on the main stream (A/B of the side-stream overlap)")
     ap.add_argument("--force-buckets", action="store_true",
                     help="1 GPU: run the DP gradient path (1-rank RCCL group, hooks, bucket all-reduces)")
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
@@ -100,6 +102,10 @@ def run(args):
 
     if args.backend:
         ops.set_backend(args.backend)
+    if args.no_side_wgrad and torch.cuda.is_available():
+        from speakingstyle_amd.ops import hip
+
+        hip.set_wgrad_stream(False)
     rank, world, local_rank = ddp.init_distributed(backend=args.dist_backend, expect_world=args.gpus)
     cuda = torch.cuda.is_available()
     device = torch.device("cuda", local_rank) if cuda else torch.device("cpu")

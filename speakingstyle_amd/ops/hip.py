@@ -287,11 +287,60 @@ _ws = {}
 
 
 def _workspace(device, nfloats: int) -> torch.Tensor:
-    cur = _ws.get(device)
+    """Scratch buffer of the current stream (the weight-gradient side stream has its own)."""
+    key = (device, _stream())
+    cur = _ws.get(key)
     if cur is None or cur.numel() < nfloats:
         cur = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
-        _ws[device] = cur
+        _ws[key] = cur
     return cur
+
+
+# ------------------------------------------------------------------------ weight-gradient side stream
+# The weight gradients of a layer feed only the optimizer (and the DDP buckets), never the rest of the
+# backward chain.  They run on a second HIP stream, so their GEMMs fill the CUs the data-gradient chain
+# leaves idle (partial last rounds of 256x256 tiles, the small encoder-sized kernels).  Only kernels
+# that write straight into claimed arena slots go there (nothing the main stream touches before the
+# join); their inputs are record_stream()-ed so the caching allocator cannot recycle them early.
+# join_side_streams() orders the current stream after everything queued (before the optimizer reads the
+# arena and before a gradient bucket is all-reduced).
+_side = {}
+_side_used = {}
+_SIDE_WGRAD = [True]
+
+
+def set_wgrad_stream(enabled: bool):
+    _SIDE_WGRAD[0] = bool(enabled)
+
+
+def _side_stream(device):
+    s = _side.get(device.index)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _side[device.index] = s
+    return s
+
+
+def wgrad_async(launch, inputs, slots_ok: bool):
+    """``launch()`` (weight-gradient kernels writing arena slots) on the side stream when possible."""
+    if not (_SIDE_WGRAD[0] and slots_ok):
+        return launch()
+    dev = inputs[0].device
+    side = _side_stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        out = launch()
+    for t in inputs:
+        t.record_stream(side)
+    _side_used[dev.index] = True
+    return out
+
+
+def join_side_streams():
+    for idx, used in _side_used.items():
+        if used:
+            torch.cuda.current_stream(idx).wait_stream(_side[idx])
+            _side_used[idx] = False
 
 
 # ------------------------------------------------------------------------ raw launchers
@@ -526,8 +575,9 @@ class _ConvFn(torch.autograd.Function):
         sb = gradslots.claim(ctx.b) if want_b else None
         if ctx.needs_input_grad[1]:
             sw = gradslots.claim(w)
-            res = conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b, dW=sw, db=sb, rinfo=rinfo,
-                                 cu=None if pk is None else pk.cu)
+            res = wgrad_async(lambda: conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b, dW=sw,
+                                                     db=sb, rinfo=rinfo, cu=None if pk is None else pk.cu),
+                              (xc, dy), sw is not None and (sb is not None or not want_b))
             dw, db = res if want_b else (res, None)
             if w.dim() == 2:
                 dw = dw.view(N, Cin)
@@ -614,8 +664,9 @@ class _GroupLinearFn(torch.autograd.Function):
         dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin,
                            resid=_resid_for(ctx.mailbox, xc))
         sw, sb = gradslots.claim_fused(ws), gradslots.claim_fused(bs)
-        dw, db = conv_wgrad_raw(xc, dy, B, L, Cin, 1, 1, 0, N, with_bias=True,
-                                dW=None if sw is None else sw.view(N, Cin, 1), db=sb)
+        dw, db = wgrad_async(lambda: conv_wgrad_raw(xc, dy, B, L, Cin, 1, 1, 0, N, with_bias=True,
+                                                    dW=None if sw is None else sw.view(N, Cin, 1), db=sb),
+                             (xc, dy), sw is not None and sb is not None)
         dw = dw.view(N, Cin)
         return (dx, None, None, None, None, *gradslots.split_rows(dw, ws), *gradslots.split_rows(db, bs))
 
@@ -681,12 +732,16 @@ class _FFNFn(torch.autograd.Function):
                                     mask_in=mask)
         else:
             dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
-        dw2, db2 = conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=gradslots.claim(w2),
-                                  db=gradslots.claim(b2), rinfo=r2, cu=ctx.cu[1])
+        s2w, s2b = gradslots.claim(w2), gradslots.claim(b2)
+        dw2, db2 = wgrad_async(lambda: conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=s2w, db=s2b,
+                                                      rinfo=r2, cu=ctx.cu[1]),
+                               (h, dz), s2w is not None and s2b is not None)
         dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1,
                            resid=_resid_for(ctx.mailbox, xc))
-        dw1, db1 = conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=gradslots.claim(w1),
-                                  db=gradslots.claim(b1), rinfo=r1, cu=ctx.cu[0])
+        s1w, s1b = gradslots.claim(w1), gradslots.claim(b1)
+        dw1, db1 = wgrad_async(lambda: conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=s1w,
+                                                      db=s1b, rinfo=r1, cu=ctx.cu[0]),
+                               (xc, dh), s1w is not None and s1b is not None)
         return dx, dw1, db1, dw2, db2, None, None, None
 
 

@@ -185,6 +185,10 @@ class GradBuckets:
     def _launch(self, bi):
         s, e, _ = self.buckets[bi]
         self.launch_order.append(bi)
+        if self.arena.grad.is_cuda:
+            from ..ops import hip
+
+            hip.join_side_streams()  # the bucket's weight gradients may still be on the side stream
         self.works[bi] = dist.all_reduce(self.arena.grad[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _launch_ready(self):

@@ -129,6 +129,10 @@ class Trainer:
         else:
             with self.buckets.no_sync():
                 (total / self.grad_acc).backward()
+        if self.opt.arena.data.is_cuda:
+            from ..ops import hip
+
+            hip.join_side_streams()  # weight gradients computed on the side stream
         self.opt.arena.finalize_grads()
         self.micro += 1
         hl = getattr(batch[7], "host_lengths", None)

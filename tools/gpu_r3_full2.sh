@@ -4,7 +4,7 @@ set -o pipefail
 R="$(cd "$(dirname "$0")/.." && pwd)"
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 600 python -u -m pytest tests/test_train_fidelity_gpu.py tests/test_train_gpu.py tests/test_vocoder_oracle_gpu.py -x -q -s --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu2.log 2>&1 || { tail -60 gpurun_out/pytest_gpu2.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -q -s --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu2.log 2>&1 || { tail -60 gpurun_out/pytest_gpu2.log; exit 1; }
 grep -E "loss hip|passed|failed" gpurun_out/pytest_gpu2.log
 for c in LJSpeech BC2013 BC2013_GST; do
   timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 3 --synth-steps 0 > gpurun_out/b_$c.log 2>&1 || { tail -20 gpurun_out/b_$c.log; exit 1; }
