@@ -29,6 +29,7 @@ import torch
 
 _slots = {}      # id(p) -> (weakref(p), arena, offset)
 _claimed = set()
+_single = {}     # id(p) -> True when the last backward ended with p.grad == its slot view (one contribution)
 _film_holders = {}  # tuple(id(p) of the FiLM scalars) -> FilmL2Holder
 _film_of = {}       # id(scalar) -> FilmL2Holder
 
@@ -151,6 +152,23 @@ def claim_fused(params: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
     arena, o, n = c
     rows = sum(p.shape[0] for p in params)
     return arena.grad[o:o + n].view(rows, *params[0].shape[1:])
+
+
+def single_contribution(p) -> bool:
+    """True when ``p``'s gradient was its slot view after the previous backward: autograd adopted the
+    slot without summing it with another contribution (a parameter used twice -- e.g. the mel_linear
+    bias, also the padded-frame fill -- gets an InputBuffer add on the main stream, which must not
+    read a slot a side-stream kernel is still writing).  Unknown (first step) counts as False."""
+    return p is not None and _single.get(id(p), False)
+
+
+def note_contributions(arena):
+    """After a backward (all streams joined): record which parameters ended with their slot view."""
+    sp = arena._slot_ptr
+    copied = getattr(arena, "copied_ids", ())
+    for p in arena.params:
+        g = p.grad
+        _single[id(p)] = g is not None and g.data_ptr() == sp[id(p)] and id(p) not in copied
 
 
 def split_rows(g: torch.Tensor, params: Sequence[torch.Tensor]) -> List[torch.Tensor]:

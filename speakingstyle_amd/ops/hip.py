@@ -321,9 +321,11 @@ def _side_stream(device):
     return s
 
 
-def wgrad_async(launch, inputs, slots_ok: bool):
-    """``launch()`` (weight-gradient kernels writing arena slots) on the side stream when possible."""
-    if not (_SIDE_WGRAD[0] and slots_ok):
+def wgrad_async(launch, inputs, slots_ok: bool, params=()):
+    """``launch()`` (weight-gradient kernels writing the arena slots of ``params``) on the side stream
+    when every slot was claimed and every parameter is known to receive that single gradient
+    (``gradslots.single_contribution``: autograd adopts the slot view without touching its data)."""
+    if not (_SIDE_WGRAD[0] and slots_ok and all(gradslots.single_contribution(p) for p in params)):
         return launch()
     dev = inputs[0].device
     side = _side_stream(dev)
@@ -577,7 +579,8 @@ class _ConvFn(torch.autograd.Function):
             sw = gradslots.claim(w)
             res = wgrad_async(lambda: conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b, dW=sw,
                                                      db=sb, rinfo=rinfo, cu=None if pk is None else pk.cu),
-                              (xc, dy), sw is not None and (sb is not None or not want_b))
+                              (xc, dy), sw is not None and (sb is not None or not want_b),
+                              (w, ctx.b) if want_b else (w,))
             dw, db = res if want_b else (res, None)
             if w.dim() == 2:
                 dw = dw.view(N, Cin)
@@ -666,7 +669,7 @@ class _GroupLinearFn(torch.autograd.Function):
         sw, sb = gradslots.claim_fused(ws), gradslots.claim_fused(bs)
         dw, db = wgrad_async(lambda: conv_wgrad_raw(xc, dy, B, L, Cin, 1, 1, 0, N, with_bias=True,
                                                     dW=None if sw is None else sw.view(N, Cin, 1), db=sb),
-                             (xc, dy), sw is not None and sb is not None)
+                             (xc, dy), sw is not None and sb is not None, tuple(ws) + tuple(bs))
         dw = dw.view(N, Cin)
         return (dx, None, None, None, None, *gradslots.split_rows(dw, ws), *gradslots.split_rows(db, bs))
 
@@ -735,13 +738,13 @@ class _FFNFn(torch.autograd.Function):
         s2w, s2b = gradslots.claim(w2), gradslots.claim(b2)
         dw2, db2 = wgrad_async(lambda: conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=s2w, db=s2b,
                                                       rinfo=r2, cu=ctx.cu[1]),
-                               (h, dz), s2w is not None and s2b is not None)
+                               (h, dz), s2w is not None and s2b is not None, (w2, b2))
         dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1,
                            resid=_resid_for(ctx.mailbox, xc))
         s1w, s1b = gradslots.claim(w1), gradslots.claim(b1)
         dw1, db1 = wgrad_async(lambda: conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=s1w,
                                                       db=s1b, rinfo=r1, cu=ctx.cu[0]),
-                               (xc, dh), s1w is not None and s1b is not None)
+                               (xc, dh), s1w is not None and s1b is not None, (w1, b1))
         return dx, dw1, db1, dw2, db2, None, None, None
 
 

@@ -72,6 +72,7 @@ class FlatArena:
         self.grad = torch.zeros(n, dtype=torch.float32, device=device)
         self._slot_ptr = {}
         self.copied = 0  # gradients that did not arrive in their slot (diagnostics)
+        self.copied_ids = set()  # this step's parameters whose gradient had to be copied into the slot
         for p, o in zip(self.params, offs):
             k = p.numel()
             self.data[o:o + k].copy_(p.detach().reshape(-1).float())
@@ -96,6 +97,7 @@ class FlatArena:
         self.grad.zero_()
         for p in self.params:
             p.grad = None
+        self.copied_ids.clear()
         gradslots.reset()
 
     def ensure_slot(self, p, i=None):
@@ -109,6 +111,7 @@ class FlatArena:
         slot.copy_(g)
         p.grad = slot
         self.copied += 1
+        self.copied_ids.add(id(p))
 
     def finalize_grads(self):
         """After backward: every produced gradient lives in the arena."""

@@ -130,9 +130,10 @@ class Trainer:
             with self.buckets.no_sync():
                 (total / self.grad_acc).backward()
         if self.opt.arena.data.is_cuda:
-            from ..ops import hip
+            from ..ops import gradslots, hip
 
             hip.join_side_streams()  # weight gradients computed on the side stream
+            gradslots.note_contributions(self.opt.arena)  # which parameters may use it next step
         self.opt.arena.finalize_grads()
         self.micro += 1
         hl = getattr(batch[7], "host_lengths", None)
