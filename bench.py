@@ -66,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--synth-steps", type=int, default=3, help="0 disables the synthesis phase")
     ap.add_argument("--synth-warmup", type=int, default=1)
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
+    ap.add_argument("--vocoder-buckets", type=int, default=8,
+                    help="max length buckets of the vocoder (1: vocode the padded batch)")
     ap.add_argument("--tiny", action="store_true", help="plumbing-size model (CPU launcher tests only)")
     ap.add_argument("--phase-times", action="store_true", help="per-phase host/device ms of the timed steps")
     ap.add_argument("--frames-per-gpu", type=int, default=None,
@@ -168,6 +170,7 @@ def run(args):
                 "batch_per_gpu": args.synth_batch, "steps": args.synth_steps, "warmup": args.synth_warmup,
                 "audio_seconds": round(sy["audio_s"], 2), "wall_s": round(sy["wall"], 4),
                 "mel_frames_per_utt": round(sy["frames_per_utt"], 1),
+                "vocoder_length_buckets": args.vocoder_buckets,
                 "parallelism": f"dp{world} (independent shards)",
             },
         })

@@ -25,7 +25,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, dest="synth_batch")
     ap.add_argument("--steps", type=int, default=3, dest="synth_steps")
     ap.add_argument("--warmup", type=int, default=1, dest="synth_warmup")
-    ap.add_argument("--config", default="BC2013", dest="synth_config")
+    ap.add_argument("--config", default="BC2013_GST", dest="synth_config")
+    ap.add_argument("--vocoder-buckets", type=int, default=8, help="1: vocode the padded batch")
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--tiny", action="store_true")
     return ap.parse_args()

@@ -214,12 +214,14 @@ def synth_phase(args, rank, world, device):
     def synth():
         out = model(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
         mel, mel_len = out[1], out[9]
+        lens = mel_len.cpu()  # host lengths: the vocoder runs length-bucketed (exact on valid samples)
         if cuda:  # int16 conversion fused into the vocoder's conv_post kernel
-            pcm = voc.infer(mel.to(torch.bfloat16).contiguous(), int16_scale=mx)
+            pcm = voc.infer(mel.to(torch.bfloat16).contiguous(), int16_scale=mx, lengths=lens.tolist(),
+                            max_buckets=args.vocoder_buckets)
         else:
             wav = voc(mel.transpose(1, 2)).squeeze(1)
             pcm = (wav.float() * mx).clamp(-32768, 32767).to(torch.int16)
-        return pcm, mel_len
+        return pcm, lens
 
     for _ in range(args.synth_warmup):
         synth()
@@ -230,7 +232,7 @@ def synth_phase(args, rank, world, device):
     samples = 0
     for _ in range(args.synth_steps):
         pcm, mel_len = synth()
-        samples += int(mel_len.sum().item()) * hop  # valid audio (the D2H of lengths is part of the pipeline)
+        samples += int(mel_len.sum()) * hop  # valid audio (the D2H of lengths is inside synth())
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)

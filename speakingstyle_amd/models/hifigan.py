@@ -233,10 +233,83 @@ class Generator(nn.Module):
         return torch.tanh(z)
 
     # ------------------------------------------------------------------ inference (channel-last, HIP)
+    def receptive_radius(self) -> int:
+        """Mel frames on each side that one output sample depends on (through every layer, with
+        the per-layer zero padding): walk the stack from conv_post back to conv_pre, adding each
+        MRF's widest branch (sum over its layers of the dilated + plain conv half-widths) at that
+        stage's rate and converting across each transposed conv (input index (o + pad - k) / s)."""
+        nk = self.num_kernels
+        r = (self.conv_post.kernel_size[0] - 1) // 2
+        for i in reversed(range(self.num_upsamples)):
+            blocks = [self.resblocks[i * nk + j] for j in range(nk)]
+            r += max(sum(d * (b.kernel_size - 1) // 2 + (b.kernel_size - 1) // 2 for d in b.dilation) for b in blocks)
+            up = self.ups[i]
+            s, K, pad = up.stride[0], up.kernel_size[0], up.padding[0]
+            r = -(-(r + max(pad, K - 1 - pad)) // s)
+        return r + (self.conv_pre.kernel_size[0] - 1) // 2
+
+    @staticmethod
+    def length_buckets(lengths, T: int, halo: int, max_buckets: int = 8, bucket_cost: int = 512):
+        """Split utterances (mel-frame ``lengths``, padded length ``T``) into at most ``max_buckets``
+        groups of consecutive sorted lengths, each vocoded at ``min(T, max_len + halo)`` frames.
+        Exact DP over the sorted lengths minimising sum(rows * frames) + ``bucket_cost`` per group
+        (a group's launches / tails cost about that many frame-rows).  Returns [(indices, T_b)]."""
+        import numpy as np
+
+        L = np.asarray(lengths, dtype=np.int64)
+        order = np.argsort(L, kind="stable")
+        Ls = L[order]
+        n = len(Ls)
+        width = np.minimum(T, Ls + halo).astype(np.float64)  # a group ending at sorted row i-1 runs at width[i-1]
+        ii = np.arange(n + 1)
+        best = np.full(n + 1, np.inf)
+        best[0] = 0.0
+        cut = np.zeros((max_buckets + 1, n + 1), dtype=np.int64)
+        table = [best]
+        for j in range(1, max_buckets + 1):
+            prev = table[-1]
+            # cand[i, p] = prev[p] + (i - p) * width[i - 1] + bucket_cost, for p < i
+            cand = prev[None, :] + (ii[:, None] - ii[None, :]) * np.concatenate([[0.0], width])[:, None] + bucket_cost
+            cand[np.triu_indices(n + 1)] = np.inf
+            cur = cand.min(axis=1)
+            cur[0] = 0.0
+            cut[j] = cand.argmin(axis=1)
+            table.append(cur)
+        j = int(np.argmin([t[n] for t in table[1:]])) + 1
+        groups, i = [], n
+        while i > 0:
+            p = int(cut[j, i])
+            groups.append((order[p:i], int(width[i - 1])))
+            i, j = p, j - 1
+        return groups[::-1]
+
     @torch.no_grad()
-    def infer(self, mel_cl: torch.Tensor, int16_scale=None) -> torch.Tensor:
+    def infer(self, mel_cl: torch.Tensor, int16_scale=None, lengths=None, max_buckets: int = 8,
+              bucket_cost: int = 512) -> torch.Tensor:
         """mel [B, T, n_mel] (channel-last) -> wav [B, T*hop] in [-1, 1] (or int16 samples
-        scaled by ``int16_scale``, fused into the conv_post kernel)."""
+        scaled by ``int16_scale``, fused into the conv_post kernel).
+
+        ``lengths`` (host mel-frame counts): vocode length-sorted groups, each truncated to
+        ``max_len + receptive_radius()`` frames, instead of the whole padded batch.  Exact for the
+        valid samples ``[0, lengths[b] * hop)``: their dependency cone never reaches the truncation
+        point (``tests/test_vocoder_buckets_cpu.py``); samples past a group's width are zero.  The
+        reference vocodes the padded batch and trims (``utils/model.py:97-115``)."""
+        if lengths is not None and mel_cl.shape[0] > 1:
+            B, T, _ = mel_cl.shape
+            groups = self.length_buckets([int(v) for v in lengths], T, self.receptive_radius(), max_buckets,
+                                         bucket_cost)
+            if len(groups) > 1 or groups[0][1] < T:
+                hop = 1
+                for u in self.h.upsample_rates:
+                    hop *= u
+                out = None
+                for idx, Tb in groups:
+                    sel = torch.as_tensor(idx, device=mel_cl.device)
+                    y = self.infer(mel_cl.index_select(0, sel)[:, :Tb].contiguous(), int16_scale)
+                    if out is None:
+                        out = y.new_zeros(B, T * hop)
+                    out[sel, : y.shape[1]] = y
+                return out
         if mel_cl.is_cuda and ops.use_hip(mel_cl):
             return self._infer_hip(mel_cl.to(torch.bfloat16).contiguous(), int16_scale)
         x = ops.conv1d(mel_cl, _w(self.conv_pre), self.conv_pre.bias, 3, 1, None)

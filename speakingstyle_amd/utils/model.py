@@ -142,7 +142,10 @@ def vocoder_infer(mels, vocoder, model_config, preprocess_config, lengths=None, 
     mx = preprocess_config["preprocessing"]["audio"]["max_wav_value"]
     if x.is_cuda:
         x = x.to(torch.bfloat16).contiguous()
-        wavs = vocoder.infer(x, int16_scale=mx).cpu().numpy()  # int16 written by the conv_post kernel
+        hop = preprocess_config["preprocessing"]["stft"]["hop_length"]
+        frames = None if lengths is None else [-(-int(n) // hop) for n in lengths]
+        # int16 written by the conv_post kernel; length-bucketed when the lengths are known
+        wavs = vocoder.infer(x, int16_scale=mx, lengths=frames).cpu().numpy()
     else:
         wavs = vocoder(x.transpose(1, 2).float()).squeeze(1)
         wavs = (wavs * mx).clamp(-32768, 32767).cpu().numpy().astype(np.int16)

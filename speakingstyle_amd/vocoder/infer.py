@@ -52,7 +52,8 @@ def vocode(g, h, mels: List[torch.Tensor], device, batch_size: int = 16) -> List
             batch[k, : mels[i].shape[-1]] = mels[i].t()
         x = batch.to(device)
         if x.is_cuda:
-            pcm = g.infer(x.to(torch.bfloat16).contiguous(), int16_scale=32768.0).cpu().numpy()
+            pcm = g.infer(x.to(torch.bfloat16).contiguous(), int16_scale=32768.0,
+                          lengths=[mels[i].shape[-1] for i in idx]).cpu().numpy()
         else:
             w = g(x.transpose(1, 2)).squeeze(1)
             pcm = (w * 32768.0).clamp(-32768, 32767).to(torch.int16).numpy()
