@@ -155,6 +155,7 @@ def run(args):
         "grad_buckets": tr["buckets"],
         "bucket_overlap": tr["overlap"],
         "skipped_steps": tr["skipped_steps"],
+        "host_enqueue_ms_per_step": round(tr["host_ms_per_step"], 3),
     }
     if tr.get("phases"):
         rec["phase_ms"] = {k: {"host": round(v["host_ms"], 3), "device": round(v["device_ms"], 3)}

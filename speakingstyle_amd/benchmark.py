@@ -155,8 +155,11 @@ def train_phase(args, rank, world, device):
     _sync(cuda)
     t0 = time.perf_counter()
     frames = 0
+    host = 0.0  # time inside train_step (enqueue): ~= elapsed when the step is host-bound
     for i in range(args.steps):
+        h0 = time.perf_counter()
         frames += step(warm + i)
+        host += time.perf_counter() - h0
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)
@@ -171,6 +174,7 @@ def train_phase(args, rank, world, device):
         "buckets": len(trainer.buckets.buckets),
         "overlap": trainer.buckets.calibrated() if (world > 1 or trainer.buckets.active) else None,
         "skipped_steps": int(trainer.opt.skipped_steps),
+        "host_ms_per_step": 1000.0 * host / max(1, args.steps),
     }
     del trainer, model, pool
     if cuda:
