@@ -1098,63 +1098,106 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         return;
       }
       const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_in;
-      for (int e = tid; e < BG * 32; e += NT3) {
-        const int r = e >> 5, c = e & 31;
-        const int m = m0 + r, n = n0 + c * 8;
-        if (m >= g.M || n >= g.N) continue;
-        short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
-        bool valid = true;
-        if (lens) {
-          const int bb = m / g.L, tt = m - bb * g.L;
-          valid = tt < (int)lens[bb];
+      // Thread (c = tid & 31, r0 = tid >> 5) owns the 16-B column chunk c of rows r0 + 16 it.  The
+      // global operands of EPG rows (aux / residual / accumulator segments, mask bytes, sequence
+      // lengths) are all loaded before any is used: one loop iteration per row would expose a full
+      // memory round trip per row (16 in a row per tile -- the K = 256 ReLU-mask data gradient
+      // spent most of its time there).  Same arithmetic, same order as the one-row form.
+      constexpr int EPI = BG * 32 / NT3;  // 16 rows per thread
+      constexpr int EPG = 8;              // rows per load batch (register budget: 3 x 8 x 16 B)
+      const int c = tid & 31, r0 = tid >> 5;
+      const int n = n0 + c * 8;
+      const bool col_ok = n < g.N;
+      const bool loads = aux || resid || ex.acc || ex.mask_in || lens;
+      if (!loads && !xon) {  // store-only epilogue (+ the ReLU bitmask): the plain row loop
+        for (int e = tid; e < BG * 32; e += NT3) {
+          const int r = e >> 5, cc = e & 31;
+          const int m = m0 + r, nn = n0 + cc * 8;
+          if (m >= g.M || nn >= g.N) continue;
+          const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + cc * 16);
+          if (ex.mask_out) {
+            unsigned bits = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) bits |= (unsigned)((short)v[q] > 0) << q;
+            ex.mask_out[(long)m * (g.N >> 3) + (nn >> 3)] = (unsigned char)bits;
+          }
+          *reinterpret_cast<short8*>(Y + (long)m * ldy + nn) = v;
         }
-        const long off = (long)m * ldy + n;
-        if (ex.mask_out) {  // ReLU output > 0  <=>  its bf16 bits are a positive non-zero value
-          unsigned bits = 0;
+        return;
+      }
 #pragma unroll
-          for (int q = 0; q < 8; ++q) bits |= (unsigned)((short)v[q] > 0) << q;
-          ex.mask_out[(long)m * (g.N >> 3) + (n >> 3)] = (unsigned char)bits;
+      for (int g0 = 0; g0 < EPI; g0 += EPG) {
+        short8 va[EPG], vr[EPG], vc[EPG];
+        unsigned mb[EPG];
+        bool vv[EPG];
+        if (loads) {
+#pragma unroll
+          for (int u = 0; u < EPG; ++u) {
+            const int m = m0 + r0 + 16 * (g0 + u);
+            const bool in = col_ok && m < g.M;
+            const long off = (long)m * ldy + n;
+            if (in && aux) va[u] = *reinterpret_cast<const short8*>(aux + off);
+            if (in && resid) vr[u] = *reinterpret_cast<const short8*>(resid + off);
+            if (in && ex.acc) vc[u] = *reinterpret_cast<const short8*>(ex.acc + off);
+            mb[u] = (in && ex.mask_in) ? (unsigned)ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : 0xffu;
+            vv[u] = true;
+            if (in && lens) {
+              const int bb = m / g.L, tt = m - bb * g.L;
+              vv[u] = tt < (int)lens[bb];
+            }
+          }
         }
-        if (aux || resid || !valid || xon) {
-          float f[8];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)v[q]);
-          if (aux) {
-            const short8 a = *reinterpret_cast<const short8*>(aux + off);
+        for (int u = 0; u < EPG; ++u) {
+          const int r = r0 + 16 * (g0 + u);
+          const int m = m0 + r;
+          if (m >= g.M || !col_ok) continue;
+          short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
+          const bool valid = loads ? vv[u] : true;
+          const long off = (long)m * ldy + n;
+          if (ex.mask_out) {  // ReLU output > 0  <=>  its bf16 bits are a positive non-zero value
+            unsigned bits = 0;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)a[q]) > 0.f ? f[q] : 0.f;
+            for (int q = 0; q < 8; ++q) bits |= (unsigned)((short)v[q] > 0) << q;
+            ex.mask_out[(long)m * (g.N >> 3) + (n >> 3)] = (unsigned char)bits;
           }
-          if (ex.mask_in) {
-            const unsigned bits = ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)];
+          if (aux || resid || !valid || xon) {
+            float f[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) f[q] = (bits >> q) & 1u ? f[q] : 0.f;
+            for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)v[q]);
+            if (aux) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] = bf2f((bf16_t)va[u][q]) > 0.f ? f[q] : 0.f;
+            }
+            if (ex.mask_in) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] = (mb[u] >> q) & 1u ? f[q] : 0.f;
+            }
+            if (resid) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)vr[u][q]);
+            }
+            if (ex.acc) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)vc[u][q]);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] = valid ? f[q] * ex.scale : 0.f;
+            if (ex.y2) {
+              short8 o2;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) o2[q] = (short)f2bf(f[q] > 0.f ? f[q] : 0.1f * f[q]);
+              *reinterpret_cast<short8*>(ex.y2 + off) = o2;
+            }
+            if (ex.post_act == ACT_LRELU) {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) f[q] = f[q] > 0.f ? f[q] : 0.1f * f[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = (short)f2bf(f[q]);
           }
-          if (resid) {
-            const short8 rr = *reinterpret_cast<const short8*>(resid + off);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)rr[q]);
-          }
-          if (ex.acc) {
-            const short8 aa = *reinterpret_cast<const short8*>(ex.acc + off);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)aa[q]);
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) f[q] = valid ? f[q] * ex.scale : 0.f;
-          if (ex.y2) {
-            short8 o2;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) o2[q] = (short)f2bf(f[q] > 0.f ? f[q] : 0.1f * f[q]);
-            *reinterpret_cast<short8*>(ex.y2 + off) = o2;
-          }
-          if (ex.post_act == ACT_LRELU) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) f[q] = f[q] > 0.f ? f[q] : 0.1f * f[q];
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = (short)f2bf(f[q]);
+          *reinterpret_cast<short8*>(Y + off) = v;
         }
-        *reinterpret_cast<short8*>(Y + off) = v;
       }
       return;
     }

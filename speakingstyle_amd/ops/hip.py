@@ -917,12 +917,7 @@ class _AddLNFn(torch.autograd.Function):
             ctx.mailbox.put(d_res)
             d_res = None
         dg = dbt = dsg = dsb = None
-        if has_film and not has("ssamd_film_grads"):  # older kernel library (A/B runs)
-            dg = (S1 * sg).to(ctx.gdtype[0])
-            dbt = (S2 * sb).to(ctx.gdtype[1])
-            dsg = (S1 * gf).sum().reshape(1)
-            dsb = (S2 * bf).sum().reshape(1)
-        elif has_film:  # one kernel: d gamma, d beta and the two scale gradients (into their slots)
+        if has_film:  # one kernel: d gamma, d beta and the two scale gradients (into their slots)
             f32 = ctx.gdtype[0] == torch.float32
             acc = ctx.acc if (ctx.needs_input_grad[4] and ctx.needs_input_grad[5]) else None
             first = False

@@ -1231,3 +1231,4 @@ def test_hifigan_generator_hip_training_vs_torch():
         if _rel(grads[n], p.grad) > 0.2:
             bad.append((n, _rel(grads[n], p.grad)))
     assert len(grads) > 50 and not bad, bad
+
