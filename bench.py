@@ -74,6 +74,8 @@ def parse(argv=None):
                     help="per-GPU padded mel-frame budget per step (mi355x.frames_per_gpu) instead of --batch")
     ap.add_argument("--no-side-wgrad", action="store_true",
                     help="weight gradients on the main stream (A/B of the side-stream overlap)")
+    ap.add_argument("--ctypes-bindings", action="store_true",
+                    help="launch kernels through ctypes instead of the generated native bindings (A/B)")
     ap.add_argument("--force-buckets", action="store_true",
                     help="1 GPU: run the DP gradient path (1-rank RCCL group, hooks, bucket all-reduces)")
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
@@ -104,6 +106,10 @@ def run(args):
 
     if args.backend:
         ops.set_backend(args.backend)
+    if args.ctypes_bindings:
+        from speakingstyle_amd.ops import hip
+
+        hip._USE_FAST[0] = False
     if args.no_side_wgrad and torch.cuda.is_available():
         from speakingstyle_amd.ops import hip
 

@@ -15,6 +15,7 @@ import glob
 import os
 import subprocess
 import sys
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -22,6 +23,7 @@ OUT_DIR = os.path.join(ROOT, "speakingstyle_amd", "_lib")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")
 KLIB = os.path.join(OUT_DIR, "libssamd_kernels.so")
 HLIB = os.path.join(OUT_DIR, "libssamd_host.so")
+FLIB = os.path.join(OUT_DIR, "ssamd_fast" + sysconfig.get_config_var("EXT_SUFFIX"))  # launch bindings
 ARCH = os.environ.get("SSAMD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -58,14 +60,37 @@ def build(jobs=8, debug=False, clean=False, verbose=False):
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
     if clean or _stale(KLIB, objs):
-        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", KLIB] + objs)
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-Wl,-soname,libssamd_kernels.so", "-o", KLIB] + objs)
+
+    build_fastcall(clean)
 
     hsrcs = sorted(glob.glob(os.path.join(HERE, "host_*.cpp")))
     if hsrcs and (clean or _stale(HLIB, hsrcs + headers)):
         _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", HLIB] + hsrcs)
     if verbose:
-        print("built", KLIB, HLIB if hsrcs else "")
+        print("built", KLIB, FLIB, HLIB if hsrcs else "")
     return KLIB
+
+
+def build_fastcall(clean=False):
+    """Native METH_FASTCALL launch bindings generated from hip._SIGS (csrc/gen_fastcall.py)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, HERE)
+    import gen_fastcall
+
+    src = gen_fastcall.generate(*gen_fastcall.signatures())
+    gen_dir = os.path.join(ROOT, "build", "gen")
+    os.makedirs(gen_dir, exist_ok=True)
+    cpp = os.path.join(gen_dir, "ssamd_fast.cpp")
+    old = open(cpp).read() if os.path.exists(cpp) else None
+    if old != src:
+        with open(cpp, "w") as f:
+            f.write(src)
+    if clean or _stale(FLIB, [cpp, KLIB]):
+        inc = sysconfig.get_paths()["include"]
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", inc, "-o", FLIB, cpp, "-L", OUT_DIR,
+              "-l:libssamd_kernels.so", "-Wl,-rpath,$ORIGIN"])
+    return FLIB
 
 
 # Host-only sanitizer builds (GPU sanitizers are not available on the target pool).

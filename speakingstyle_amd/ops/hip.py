@@ -13,6 +13,7 @@ once per optimizer step and cached on the parameter's version counter.
 from __future__ import annotations
 
 import ctypes
+import sysconfig
 import math
 import os
 import threading
@@ -89,6 +90,46 @@ _RESTYPES = {"ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws
              "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_}
 
 
+_FAST_PATH = os.path.join(os.path.dirname(_LIB_PATH),
+                          "ssamd_fast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+_USE_FAST = [True]  # bench.py --ctypes-bindings: A/B of the launch-binding host cost
+
+
+class _KernelLib:
+    """Kernel entry points: the generated METH_FASTCALL launch bindings (``csrc/gen_fastcall.py``,
+    ~0.35 us per call instead of ctypes' ~3.3 us) where they exist, the ctypes handle otherwise
+    (struct-by-value arguments).  Same library mapping, same ABI, same argument lists."""
+
+    def __init__(self, handle, fast):
+        self._handle = handle
+        self._fast = fast
+
+    def __getattr__(self, name):
+        f = getattr(self._fast, name, None) if self._fast is not None and name.startswith("ssamd_") else None
+        if f is None:
+            f = getattr(self._handle, name)
+        self.__dict__[name] = f
+        return f
+
+
+def _load_fast(handle):
+    if not _USE_FAST[0] or os.environ.get("SSAMD_KERNEL_LIB") or not os.path.exists(_FAST_PATH):
+        return None
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("ssamd_fast", _FAST_PATH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    # one mapping of the kernel library (one set of its globals: workspaces, LDS opt-ins, variant state)
+    mine = ctypes.cast(getattr(handle, mod.entry_name), ctypes.c_void_p).value
+    if mod._entry_addr() != mine:
+        import warnings
+
+        warnings.warn(f"{_FAST_PATH} resolved a different copy of the kernel library; using ctypes bindings")
+        return None
+    return mod
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -104,8 +145,13 @@ def lib():
                     if fn is not None:
                         fn.argtypes = args
                         fn.restype = _RESTYPES.get(name, I)
-                _lib = handle
+                _lib = _KernelLib(handle, _load_fast(handle))
     return _lib
+
+
+def fast_bindings() -> bool:
+    """True when the kernel launches go through the generated native bindings."""
+    return lib()._fast is not None
 
 
 def available() -> bool:

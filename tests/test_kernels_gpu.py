@@ -24,6 +24,7 @@ def _rel(a, b):
 @pytest.fixture(autouse=True, scope="module")
 def _lib_loaded():
     assert hip.available(), "kernel library must be built and loadable on the GPU box"
+    assert hip.fast_bindings(), "generated launch bindings (_lib/ssamd_fast*.so) must be loaded"
 
 
 @pytest.mark.parametrize("B,L,Cin,N,ks,act", [
