@@ -1275,3 +1275,32 @@ SSAMD_API int ssamd_film_grads(const float* S1, const float* S2, const float* g,
                      dsb, l2_sg, l2_sb, accum);
   return (int)hipGetLastError();
 }
+
+// Cross-stream ordering for the weight-gradient side stream: `waiter` waits for everything queued on
+// `signaler` so far.  One event record + one stream wait from a per-device ring of pre-created
+// timing-free events (a wait is bound to the record current at the time of the wait call, so a ring
+// slot can be re-recorded while earlier waits are pending); replaces torch's Stream.wait_stream (a
+// fresh Python Event object per call) on the per-layer backward path.
+#include <mutex>
+namespace {
+constexpr int SW_DEV = 16, SW_RING = 64;
+hipEvent_t g_sw_ev[SW_DEV][SW_RING];
+int g_sw_next[SW_DEV];
+bool g_sw_init[SW_DEV];
+std::mutex g_sw_mu;
+}  // namespace
+
+SSAMD_API int ssamd_stream_wait(hipStream_t waiter, hipStream_t signaler) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= SW_DEV) return -2;
+  std::lock_guard<std::mutex> lk(g_sw_mu);
+  if (!g_sw_init[dev]) {
+    for (int i = 0; i < SW_RING; ++i)
+      if (hipEventCreateWithFlags(&g_sw_ev[dev][i], hipEventDisableTiming) != hipSuccess) return -3;
+    g_sw_init[dev] = true;
+  }
+  hipEvent_t e = g_sw_ev[dev][g_sw_next[dev]];
+  g_sw_next[dev] = (g_sw_next[dev] + 1) % SW_RING;
+  if (hipEventRecord(e, signaler) != hipSuccess) return -4;
+  return hipStreamWaitEvent(waiter, e, 0) == hipSuccess ? 0 : -5;
+}

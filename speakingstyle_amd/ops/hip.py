@@ -83,6 +83,7 @@ _SIGS = {
     "ssamd_gemm_set_variant": [I],
     "ssamd_weight_prep": [P, P, I, L_, P],
     "ssamd_weight_prep_tiled": [P, P, I, P],
+    "ssamd_stream_wait": [P, P],
 }
 
 
@@ -176,9 +177,15 @@ _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _cur_dev = getattr(torch._C, "_cuda_getDevice", None)
 
 
+_stream_override = [None]  # raw handle of the weight-gradient side stream while its kernels are issued
+
+
 def _stream():
     """Current HIP stream handle.  The raw getter skips building a torch Stream object (and its
     device-guard calls) for every launch: ~10 us of host time per op on the hot path."""
+    o = _stream_override[0]
+    if o is not None:
+        return o
     if _raw_stream is not None and _cur_dev is not None:
         return _raw_stream(_cur_dev())
     return torch.cuda.current_stream().cuda_stream
@@ -333,11 +340,17 @@ _ws = {}
 
 
 def _workspace(device, nfloats: int) -> torch.Tensor:
-    """Scratch buffer of the current stream (the weight-gradient side stream has its own)."""
+    """Scratch buffer of the current stream (the weight-gradient side stream has its own, allocated
+    under that stream so the caching allocator orders its reuse after the side-stream kernels)."""
     key = (device, _stream())
     cur = _ws.get(key)
     if cur is None or cur.numel() < nfloats:
-        cur = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        side = _side_by_handle.get(key[1])
+        if side is not None:
+            with torch.cuda.stream(side):
+                cur = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
+        else:
+            cur = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=device)
         _ws[key] = cur
     return cur
 
@@ -352,6 +365,8 @@ def _workspace(device, nfloats: int) -> torch.Tensor:
 # arena and before a gradient bucket is all-reduced).
 _side = {}
 _side_used = {}
+_side_by_handle = {}  # raw handle -> torch Stream (workspace allocation under the side stream)
+_side_keep = {}       # device -> inputs of queued side-stream kernels, released at the join
 _SIDE_WGRAD = [True]
 
 
@@ -364,31 +379,49 @@ def _side_stream(device):
     if s is None:
         s = torch.cuda.Stream(device=device)
         _side[device.index] = s
+        _side_by_handle[s.cuda_stream] = s
     return s
 
 
 def wgrad_async(launch, inputs, slots_ok: bool, params=()):
     """``launch()`` (weight-gradient kernels writing the arena slots of ``params``) on the side stream
     when every slot was claimed and every parameter is known to receive that single gradient
-    (``gradslots.single_contribution``: autograd adopts the slot view without touching its data)."""
+    (``gradslots.single_contribution``: autograd adopts the slot view without touching its data).
+
+    Host-lean: one native event record + stream wait (``ssamd_stream_wait``), the launch issued with
+    the side stream's raw handle (``_stream_override``; ``launch`` allocates nothing but the side
+    stream's own workspace), and the inputs kept alive until ``join_side_streams`` instead of a
+    ``record_stream`` per tensor (after the join the current stream is ordered behind every
+    side-stream read, so the caching allocator may recycle them)."""
     if not (_SIDE_WGRAD[0] and slots_ok and all(gradslots.single_contribution(p) for p in params)):
         return launch()
     dev = inputs[0].device
-    side = _side_stream(dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(side):
+    sh = _side_stream(dev).cuda_stream
+    _check(lib().ssamd_stream_wait(sh, _stream()), "ssamd_stream_wait")
+    _stream_override[0] = sh
+    try:
         out = launch()
-    for t in inputs:
-        t.record_stream(side)
+    finally:
+        _stream_override[0] = None
+    keep = _side_keep.get(dev.index)
+    if keep is None:
+        keep = _side_keep[dev.index] = []
+    keep.extend(inputs)
     _side_used[dev.index] = True
+    if len(keep) > 4096:  # a caller that never joins (no optimizer step): bound the held references
+        join_side_streams()
     return out
 
 
 def join_side_streams():
     for idx, used in _side_used.items():
         if used:
-            torch.cuda.current_stream(idx).wait_stream(_side[idx])
+            with torch.cuda.device(idx):
+                _check(lib().ssamd_stream_wait(_stream(), _side[idx].cuda_stream), "ssamd_stream_wait")
             _side_used[idx] = False
+            keep = _side_keep.get(idx)
+            if keep:
+                keep.clear()
 
 
 # ------------------------------------------------------------------------ raw launchers
