@@ -318,9 +318,334 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Whole ResBlock1 in one kernel (reference hifigan/models.py:20-44, the three (c1_d, c2) layer
+// pairs, dilations d0 / d1 / d2):
+//
+//     x_{p+1} = x_p + conv2_p( lrelu( conv1_p,d_p( lrelu(x_p) ) + b1_p ) ) + b2_p      p = 0, 1, 2
+//     out = (acc_in + x_3) * out_scale  [-> lrelu]
+//
+// for the narrow stages (C = 32 at 256x the mel rate, C = 64 at 128x), where the per-layer kernel
+// above is bound by streaming the activation through HBM three times per ResBlock (read x + halo,
+// re-read x for the residual, write) at a low arithmetic intensity (C = 32: ~64 FLOP/B).  Here one
+// workgroup owns R0 = 16 * NB rows of the sequence, of which the middle BM = R0 - 2 * HT are output
+// rows (HT = (K-1)/2 * (d0 + d1 + d2 + 3): the summed halo of the six convs, recomputed by the
+// neighbouring tiles):
+//   * the residual stream x_p lives in fp32 REGISTERS in the MFMA accumulator layout (each lane owns
+//     the same (row, channel) elements in every conv2 epilogue), so it never round-trips through
+//     memory between layers and is not rounded to bf16 between them (the per-layer path rounds it
+//     three times);
+//   * two bf16 LDS tiles hold lrelu(x_p) (A) and lrelu(conv1 + b1) (T); rows are addressed in one
+//     absolute frame, so every conv is "16-row block b of the output reads rows 16b - h + tap*step of
+//     its input" and the valid region shrinks by h = step * (K-1)/2 per conv; rows outside it are
+//     don't-care values that no valid row reads (MG margin rows keep the reads in bounds);
+//   * each conv's whole weight image [C][K][C] sits in LDS (row pitch padded to 2 mod 4 16-B units:
+//     conflict-free B-fragment reads), so the MFMA loop has no barrier at all; the next conv's
+//     image is prefetched into registers during the current conv and written after its barrier;
+//   * rows outside [0, T) are zeroed in A and T (each reference conv zero-pads its own input).
+// HBM traffic per ResBlock: x (+ halo) once, acc_in once, out once -- 3x less than three layer
+// launches.  Validated against the fp32 torch ResBlock (tests/test_kernels_gpu.py).
+struct RFW {
+  const bf16_t* w[6];  // c1_0, c2_0, c1_1, c2_1, c1_2, c2_2: bf16 [C][K][C] forward images
+  const float* b[6];   // fp32 [C]
+  int d[3];
+};
+
+template <int C, int K>
+struct RF {
+  static constexpr int NW = 8;
+  static constexpr int NT = 64 * NW;
+  static constexpr int WC = C >= 64 ? 2 : 1;       // column groups
+  static constexpr int WR = NW / WC;               // row groups
+  static constexpr int H2 = (K - 1) / 2;
+  static constexpr int MG = MAXD * H2;             // margin rows: the widest conv's half window
+  static constexpr int NB = C == 32 ? 40 : 24;     // 16-row blocks per tile
+  static constexpr int R0 = NB * 16;
+  static constexpr int LDC = C + 16;               // bf16 pitch: 2 (mod 4) 16-B units (see RB)
+  static constexpr int ROWS = R0 + 2 * MG;
+  static constexpr int BUF = (ROWS * LDC * 2 + 15) / 16 * 16;
+  static constexpr int NS = C / 16;
+  static constexpr int NSW = NS / WC;
+  static constexpr int KC = C / 32;
+  static constexpr int WROW = K * C / 8;           // 16-B chunks per weight-image row
+  static constexpr int WP = (WROW + 2) * 16;       // padded row pitch (bytes): 2 (mod 4) units
+  static constexpr int WBYTES = C * WP;
+  static constexpr int WCH = C * WROW;             // 16-B chunks of one image
+  static constexpr int WIT = (WCH + NT - 1) / NT;
+  static constexpr int MAXRB = NB / WR;
+  static constexpr int OSP = C + 4;                // fp32 output tile pitch
+  static constexpr int LDS = 2 * BUF + WBYTES;
+  static_assert(NB % WR == 0, "row blocks split evenly over the row groups");
+  static_assert(LDS <= 160 * 1024, "fused resblock tile");
+  static_assert(R0 * OSP * 4 <= 2 * BUF, "output tile aliases the A / T tiles");
+};
+
+// acc[j][s] = conv over the wave's row blocks blk = wr + WR*j (all NB blocks of the tile are computed:
+// straight-line MFMA code; rows outside the conv's valid region are don't-care).
+template <int C, int K>
+__device__ __forceinline__ void conv_rf(const bf16_t* __restrict__ src, int step, const char* Ws, int wr, int wc,
+                                        int col, int quad, float4v (&acc)[RF<C, K>::MAXRB][RF<C, K>::NSW]) {
+  using R = RF<C, K>;
+#pragma unroll
+  for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+    for (int s = 0; s < R::NSW; ++s) acc[j][s] = float4v{0.f, 0.f, 0.f, 0.f};
+  const int h = step * R::H2;
+  const bf16_t* abase = src + (wr * 16 + col - h) * R::LDC + 8 * quad;
+  const char* bbase = Ws + ((wc * R::NSW) * 16 + col) * R::WP + 16 * quad;
+#pragma unroll
+  for (int tap = 0; tap < K; ++tap) {
+#pragma unroll
+    for (int kc = 0; kc < R::KC; ++kc) {
+      short8 bf[R::NSW], a[R::MAXRB];
+#pragma unroll
+      for (int s = 0; s < R::NSW; ++s)
+        bf[s] = *reinterpret_cast<const short8*>(bbase + s * 16 * R::WP + (tap * C + kc * 32) * 2);
+#pragma unroll
+      for (int j = 0; j < R::MAXRB; ++j)
+        a[j] = *reinterpret_cast<const short8*>(abase + (j * R::WR * 16 + tap * step) * R::LDC + kc * 32);
+#pragma unroll
+      for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+        for (int s = 0; s < R::NSW; ++s)
+          acc[j][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], bf[s], acc[j][s], 0, 0, 0);
+    }
+  }
+}
+
+template <int C, int K>
+__global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf16_t* __restrict__ x, RFW p,
+                                                                        const bf16_t* acc_in, bf16_t* out, int T,
+                                                                        int tiles, int HT, float slope,
+                                                                        float out_scale, int post_lrelu) {
+  using R = RF<C, K>;
+  constexpr int NT = R::NT;
+  constexpr int CH = C / 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(lds) + R::MG * R::LDC;           // absolute row r at As + r * LDC
+  bf16_t* Ts = reinterpret_cast<bf16_t*>(lds + R::BUF) + R::MG * R::LDC;
+  char* Ws = reinterpret_cast<char*>(lds + 2 * R::BUF);
+  float* Os = reinterpret_cast<float*>(lds);                               // final fp32 tile (aliases A / T)
+  const int BM = R::R0 - 2 * HT;
+  const int b = blockIdx.x / tiles, t0 = (blockIdx.x - b * tiles) * BM;
+  const int tb = t0 - HT;  // sequence position of absolute row 0
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave % R::WR, wc = wave / R::WR;
+  const int col = lane & 15, quad = lane >> 4;
+  const bf16_t* xb = x + (long)b * T * C;
+
+  short8 wreg[R::WIT];
+  auto wload = [&](const bf16_t* __restrict__ w) {
+#pragma unroll
+    for (int it = 0; it < R::WIT; ++it) {
+      const int q = tid + it * NT;
+      if (q < R::WCH) wreg[it] = *reinterpret_cast<const short8*>(w + q * 8);
+    }
+  };
+  auto wstore = [&]() {
+#pragma unroll
+    for (int it = 0; it < R::WIT; ++it) {
+      const int q = tid + it * NT;
+      if (q < R::WCH) {
+        const int n = q / R::WROW;
+        *reinterpret_cast<short8*>(Ws + n * R::WP + (q - n * R::WROW) * 16) = wreg[it];
+      }
+    }
+  };
+
+  // 1. raw x rows [0, R0) (zero outside [0, T)) -> A; first conv's weights -> W
+  {
+    constexpr int IT = (R::R0 * CH + NT - 1) / NT;
+    short8 v[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
+      const int t = tb + r;
+      if (r < R::R0 && t >= 0 && t < T) {
+        v[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[it][i] = 0;
+      }
+    }
+    wload(p.w[0]);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
+      if (r < R::R0) *reinterpret_cast<short8*>(As + r * R::LDC + c0) = v[it];
+    }
+    wstore();
+  }
+  __syncthreads();
+
+  // 2. residual registers X (fp32, accumulator layout) and A = lrelu(x) in place (each element is
+  //    read and rewritten by its owning lane only)
+  float4v X[R::MAXRB][R::NSW];
+#pragma unroll
+  for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+    for (int s = 0; s < R::NSW; ++s) {
+      const int ch = (wc * R::NSW + s) * 16 + col;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = (wr + R::WR * j) * 16 + 4 * quad + i;
+        const float v = bf2f(As[row * R::LDC + ch]);
+        X[j][s][i] = v;
+        As[row * R::LDC + ch] = f2bf(lrelu(v, slope));
+      }
+    }
+  __syncthreads();
+
+  float4v acc[R::MAXRB][R::NSW];
+#pragma unroll
+  for (int pp = 0; pp < 3; ++pp) {
+    const int d = p.d[pp];
+    // conv1 (dilation d) of lrelu(x_p) -> T = lrelu(. + b1), zero outside [0, T)
+    wload(p.w[2 * pp + 1]);  // in flight during the MFMAs
+    conv_rf<C, K>(As, d, Ws, wr, wc, col, quad, acc);
+    {
+      const float* b1 = p.b[2 * pp];
+#pragma unroll
+      for (int s = 0; s < R::NSW; ++s) {
+        const int ch = (wc * R::NSW + s) * 16 + col;
+        const float bias = b1[ch];
+#pragma unroll
+        for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = (wr + R::WR * j) * 16 + 4 * quad + i;
+            const int t = tb + row;
+            const float v = (t >= 0 && t < T) ? lrelu(acc[j][s][i] + bias, slope) : 0.f;
+            Ts[row * R::LDC + ch] = f2bf(v);
+          }
+      }
+    }
+    __syncthreads();  // T complete; everyone is done with conv1's weights and with A
+    wstore();
+    __syncthreads();
+    // conv2 (dilation 1) of T; X += . + b2; A = lrelu(X) for the next pair
+    if (pp < 2) wload(p.w[2 * pp + 2]);
+    conv_rf<C, K>(Ts, 1, Ws, wr, wc, col, quad, acc);
+    {
+      const float* b2 = p.b[2 * pp + 1];
+#pragma unroll
+      for (int s = 0; s < R::NSW; ++s) {
+        const int ch = (wc * R::NSW + s) * 16 + col;
+        const float bias = b2[ch];
+#pragma unroll
+        for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v = X[j][s][i] + (acc[j][s][i] + bias);
+            X[j][s][i] = v;
+            if (pp < 2) {
+              const int row = (wr + R::WR * j) * 16 + 4 * quad + i;
+              const int t = tb + row;
+              As[row * R::LDC + ch] = f2bf((t >= 0 && t < T) ? lrelu(v, slope) : 0.f);
+            }
+          }
+      }
+    }
+    __syncthreads();  // A complete; everyone is done with conv2's weights and with T
+    if (pp < 2) {
+      wstore();
+      __syncthreads();
+    }
+  }
+
+  // 3. X -> fp32 tile (aliases A / T), then coalesced: (acc_in +) X, * out_scale [, lrelu] -> out
+#pragma unroll
+  for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+    for (int s = 0; s < R::NSW; ++s) {
+      const int ch = (wc * R::NSW + s) * 16 + col;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Os[((wr + R::WR * j) * 16 + 4 * quad + i) * R::OSP + ch] = X[j][s][i];
+    }
+  __syncthreads();
+  {
+    constexpr int ITMAX = (R::R0 * CH + NT - 1) / NT;
+    bf16_t* ob = out + (long)b * T * C;
+    const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
+    short8 ar[ITMAX];
+#pragma unroll
+    for (int it = 0; it < ITMAX; ++it) {
+      const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+      const int t = t0 + j;
+      if (j < BM && t < T && ab) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
+    }
+#pragma unroll
+    for (int it = 0; it < ITMAX; ++it) {
+      const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+      const int t = t0 + j;
+      if (j >= BM || t >= T) continue;
+      const float* orow = Os + (HT + j) * R::OSP + c0;
+      const float4 o0 = *reinterpret_cast<const float4*>(orow);
+      const float4 o1 = *reinterpret_cast<const float4*>(orow + 4);
+      const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+      short8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float v = ov[i];
+        if (ab) v += bf2f((bf16_t)ar[it][i]);
+        v *= out_scale;
+        if (post_lrelu) v = lrelu(v, slope);
+        o[i] = (short)f2bf(v);
+      }
+      *reinterpret_cast<short8*>(ob + (long)t * C + c0) = o;
+    }
+  }
+}
+
+template <int C, int K>
+int launch_rf(const bf16_t* x, const RFW& p, const bf16_t* acc_in, bf16_t* out, int B, int T, float slope,
+              float out_scale, int post_lrelu, hipStream_t s) {
+  using R = RF<C, K>;
+  const int HT = R::H2 * (p.d[0] + p.d[1] + p.d[2] + 3);
+  const int BM = R::R0 - 2 * HT;
+  if (BM < 16) return -2;
+  static bool lds_set = false;
+  if (!lds_set) {
+    allow_lds(resblock_fused_kernel<C, K>, R::LDS);
+    lds_set = true;
+  }
+  const int tiles = (T + BM - 1) / BM;
+  hipLaunchKernelGGL((resblock_fused_kernel<C, K>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, p, acc_in,
+                     out, T, tiles, HT, slope, out_scale, post_lrelu);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 SSAMD_API void ssamd_resblock_debug(int v) { g_rb_debug = v; }
+
+// Whole ResBlock1 (see resblock_fused_kernel).  x / out / acc_in [B, T, C] bf16 (out must not alias x;
+// acc_in may alias out, or be null); w: 6 bf16 [C][K][C] images (c1_0, c2_0, c1_1, c2_1, c1_2, c2_2);
+// b: 6 fp32 [C]; dilations 1 <= d <= 5.  Returns -2 for a geometry without a fused instance
+// (ssamd_resblock_fusable).
+SSAMD_API int ssamd_resblock_fusable(int C, int K) {
+  return (C == 32 && (K == 3 || K == 7 || K == 11)) || (C == 64 && K == 3);
+}
+
+SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16_t* w1, const bf16_t* w2,
+                                   const bf16_t* w3, const bf16_t* w4, const bf16_t* w5, const float* b0,
+                                   const float* b1, const float* b2, const float* b3, const float* b4,
+                                   const float* b5, const bf16_t* acc_in, bf16_t* out, int B, int T, int C, int K,
+                                   int d0, int d1, int d2, float slope, float out_scale, int post_lrelu,
+                                   hipStream_t s) {
+  const int dd[3] = {d0, d1, d2};
+  for (int i = 0; i < 3; ++i)
+    if (dd[i] < 1 || dd[i] > MAXD) return -2;
+  if ((long)B * T == 0) return 0;
+  if (x == out) return -2;
+  RFW p = {{w0, w1, w2, w3, w4, w5}, {b0, b1, b2, b3, b4, b5}, {d0, d1, d2}};
+  if (C == 32 && K == 3) return launch_rf<32, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 32 && K == 7) return launch_rf<32, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 32 && K == 11) return launch_rf<32, 11>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 64 && K == 3) return launch_rf<64, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  return -2;
+}
 
 // x / out / acc_in [B, T, C] bf16 (acc_in may alias out, or be null); w1 / w2 bf16 [C][K][C] (the
 // implicit-GEMM forward image); b1 / b2 fp32 [C].  C in {32, 64, 128}, K in {3, 7, 11}, 1 <= d <= 5.

@@ -33,6 +33,8 @@ from torch.nn.utils import spectral_norm, weight_norm
 from .. import ops
 
 LRELU_SLOPE = 0.1
+# whole-ResBlock kernel for the narrow stages (False: one fused kernel per layer pair; A/B + tests)
+_WHOLE_BLOCK = [True]
 
 
 class AttrDict(dict):
@@ -131,6 +133,10 @@ class ResBlock1(nn.Module):
         n = len(self.convs1)
         if self.fused_ok(x):
             hip = ops._hip()
+            if _WHOLE_BLOCK[0] and n == 3 and hip.resblock_fusable(x.shape[-1], k):
+                # all three layers in one kernel: the residual stream stays in registers, no HBM round trips
+                return hip.resblock_fused(x, self.convs1, self.convs2, self.dilation, LRELU_SLOPE, acc=acc,
+                                          out_scale=out_scale, post_lrelu=post_lrelu)
             for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
                 last = i == n - 1
                 x = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE, acc=acc if last else None,

@@ -1795,6 +1795,43 @@ def resblock_layer(x, c1, c2, d, slope, acc=None, out_scale=1.0, post_lrelu=Fals
     return out
 
 
+_SIGS.update({"ssamd_resblock_fused": [P] * 15 + [I, I, I, I, I, I, I, F, F, I, P],
+              "ssamd_resblock_fusable": [I, I]})
+
+
+def resblock_fusable(C: int, K: int) -> bool:
+    """Geometry with a whole-ResBlock kernel instance (``ssamd_resblock_fused``)."""
+    return bool(lib().ssamd_resblock_fusable(int(C), int(K)))
+
+
+def resblock_fused(x, convs1, convs2, dilations, slope, acc=None, out_scale=1.0, post_lrelu=False):
+    """A whole HiFi-GAN ResBlock1 (three lrelu -> dilated conv -> lrelu -> conv -> + x layers) in ONE
+    kernel (csrc/k_vocoder.hip ``resblock_fused_kernel``): the residual stream stays in fp32 registers
+    across the three layers, the activations in LDS.  Channel-last bf16, no autograd; same output
+    contract as three ``resblock_layer`` calls."""
+    _need(x, torch.bfloat16, "resblock.x")
+    B, T, C = x.shape
+    K = convs1[0].weight.shape[2]
+    ws, bs = [], []
+    for c1, c2 in zip(convs1, convs2):
+        for c in (c1, c2):
+            assert tuple(c.weight.shape) == (C, C, K)
+            ws.append(weight_fwd(c.weight))
+            bs.append(c.bias.detach().float().contiguous())
+    if acc is not None:
+        _need(acc, torch.bfloat16, "resblock.acc")
+        assert acc.shape == x.shape and acc.data_ptr() != x.data_ptr(), "acc must be a separate [B, T, C] buffer"
+        out = acc
+    else:
+        out = torch.empty_like(x)
+    d0, d1, d2 = (int(v) for v in dilations)
+    rc = lib().ssamd_resblock_fused(_ptr(x), *[_ptr(w) for w in ws], *[_ptr(b) for b in bs], _ptr(acc), _ptr(out),
+                                    B, T, C, K, d0, d1, d2, float(slope), float(out_scale),
+                                    int(bool(post_lrelu)), _stream())
+    _check(rc, "ssamd_resblock_fused")
+    return out
+
+
 def conv1d_infer(x, w, b, pad, dil, act=None, resid=None, acc=None, scale=1.0, post_act=None, dual_lrelu=False,
                  wimg=None):
     """Inference conv (no autograd), channel-last bf16, everything in the GEMM epilogue:

@@ -941,6 +941,50 @@ def test_resblock_layer_fused(C, K, d, T):
         assert _rel(out, expect) < 1e-2
 
 
+@pytest.mark.parametrize("C,K,T", [(32, 3, 1500), (32, 7, 700), (32, 11, 1100), (32, 11, 9), (64, 3, 900),
+                                   (64, 3, 5)])
+def test_resblock_whole_block_fused(C, K, T):
+    """Whole ResBlock1 kernel (3 layer pairs, dilations 1/3/5, residual in fp32 registers) vs the fp32
+    torch ResBlock1 (reference hifigan/models.py:20-44), with the MRF accumulate / scale / post-lrelu
+    epilogue; several tiles per sequence (halo recompute at tile edges) and sequences shorter than one
+    tile's halo.  Also against the per-layer kernel path."""
+    from speakingstyle_amd.models import hifigan as H
+
+    torch.manual_seed(25)
+    B = 3
+    blk = H.ResBlock1(C, K, (1, 3, 5)).to(DEV)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.Conv1d):
+            if hasattr(m, "weight_g"):
+                torch.nn.utils.remove_weight_norm(m)
+            m.weight.data.normal_(0, 0.5 / math.sqrt(C * K))
+            m.weight.data = m.weight.data.to(torch.bfloat16).float()
+            m.bias.data.normal_(0, 0.1)
+    assert hip.resblock_fusable(C, K)
+    x = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    acc = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        yr = blk.forward(x.float().transpose(1, 2)).transpose(1, 2)  # fp32 NCL torch
+        y = hip.resblock_fused(x, blk.convs1, blk.convs2, blk.dilation, H.LRELU_SLOPE)
+        assert _rel(y, yr) < 1e-2
+        expect = F.leaky_relu((acc.float() + yr) * (1 / 3), H.LRELU_SLOPE)
+        acc2 = acc.clone()
+        out = hip.resblock_fused(x, blk.convs1, blk.convs2, blk.dilation, H.LRELU_SLOPE, acc=acc2, out_scale=1 / 3,
+                                 post_lrelu=True)
+        assert out.data_ptr() == acc2.data_ptr()
+        assert _rel(out, expect) < 1e-2
+        H._WHOLE_BLOCK[0] = False
+        try:
+            acc3 = acc.clone()
+            per_layer = blk.forward_cl(x, acc=acc3, out_scale=1 / 3, post_lrelu=True)
+        finally:
+            H._WHOLE_BLOCK[0] = True
+        assert _rel(per_layer, expect) < 1e-2
+        acc4 = acc.clone()
+        via_module = blk.forward_cl(x, acc=acc4, out_scale=1 / 3, post_lrelu=True)
+        assert torch.equal(via_module, out)
+
+
 def test_duration_round_seq_mean_add_rowvec():
     """K12 duration rounding (+ scalar / per-phoneme control), K16 mean pool, K1 per-utterance add."""
     from speakingstyle_amd import ops as O
