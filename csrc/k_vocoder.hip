@@ -353,13 +353,17 @@ struct RFW {
 
 template <int C, int K>
 struct RF {
+  // RING: the weights stream per (tap, 32-deep chunk) through a 3-slot LDS ring (one barrier per step)
+  // instead of a whole image per conv -- the wide / long-kernel instances, whose whole image would
+  // leave too few rows for the tile
+  static constexpr bool RING = C >= 128 || K > 3 && C >= 64;
   static constexpr int NW = 8;
   static constexpr int NT = 64 * NW;
   static constexpr int WC = C >= 64 ? 2 : 1;       // column groups
   static constexpr int WR = NW / WC;               // row groups
   static constexpr int H2 = (K - 1) / 2;
   static constexpr int MG = MAXD * H2;             // margin rows: the widest conv's half window
-  static constexpr int NB = C == 32 ? 40 : 24;     // 16-row blocks per tile
+  static constexpr int NB = C == 32 ? 40 : (C == 64 ? 24 : 12);  // 16-row blocks per tile
   static constexpr int R0 = NB * 16;
   static constexpr int LDC = C + 16;               // bf16 pitch: 2 (mod 4) 16-B units (see RB)
   static constexpr int ROWS = R0 + 2 * MG;
@@ -369,9 +373,10 @@ struct RF {
   static constexpr int KC = C / 32;
   static constexpr int WROW = K * C / 8;           // 16-B chunks per weight-image row
   static constexpr int WP = (WROW + 2) * 16;       // padded row pitch (bytes): 2 (mod 4) units
-  static constexpr int WBYTES = C * WP;
+  static constexpr int SLOT = C * 64;              // ring slot: [C][32] bf16
+  static constexpr int WBYTES = RING ? 3 * SLOT : C * WP;
   static constexpr int WCH = C * WROW;             // 16-B chunks of one image
-  static constexpr int WIT = (WCH + NT - 1) / NT;
+  static constexpr int WIT = RING ? 1 : (WCH + NT - 1) / NT;
   static constexpr int MAXRB = NB / WR;
   static constexpr int OSP = C + 4;                // fp32 output tile pitch
   static constexpr int LDS = 2 * BUF + WBYTES;
@@ -413,6 +418,75 @@ __device__ __forceinline__ void conv_rf(const bf16_t* __restrict__ src, int step
   }
 }
 
+// RING form of conv_rf: weight slices [C][32] (tap, chunk) DMA'd three steps ahead into a 3-slot ring
+// (same source-side chunk swizzle and pipeline as conv_tile), fragments of step+1 read while step's
+// MFMAs run, one barrier per step.
+template <int C, int K>
+__device__ __forceinline__ void stage_ring(const bf16_t* __restrict__ w, int step, char* slot, int tid, int wave) {
+  if (wave * 64 < C * 4) {  // wave-uniform: C*4 16-B chunks per slice
+    constexpr int KC = C / 32;
+    const int tap = step / KC, kc = step - tap * KC;
+    const int n = tid >> 2, p = tid & 3;
+    const int lc = p ^ (((n >> 2) & 1) << 1);
+    glds16(w + (n * K + tap) * C + kc * 32 + 8 * lc, slot + wave * 1024);
+  }
+}
+
+template <int C, int K>
+__device__ __forceinline__ void conv_rf_ring(const bf16_t* __restrict__ src, int step_d, const bf16_t* __restrict__ w,
+                                             char* ring, int tid, int wave, int wr, int wc, int col, int quad,
+                                             float4v (&acc)[RF<C, K>::MAXRB][RF<C, K>::NSW]) {
+  using R = RF<C, K>;
+  constexpr int STEPS = K * R::KC;
+  constexpr int SLOT = R::SLOT;
+#pragma unroll
+  for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+    for (int s = 0; s < R::NSW; ++s) acc[j][s] = float4v{0.f, 0.f, 0.f, 0.f};
+  stage_ring<C, K>(w, 0, ring, tid, wave);
+  if (STEPS > 1) stage_ring<C, K>(w, 1, ring + SLOT, tid, wave);
+  if (STEPS > 2) stage_ring<C, K>(w, 2, ring + 2 * SLOT, tid, wave);
+  if (STEPS > 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (STEPS > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int h = step_d * R::H2;
+  const bf16_t* abase = src + (wr * 16 + col - h) * R::LDC + 8 * quad;
+  int boff[R::NSW];
+#pragma unroll
+  for (int s = 0; s < R::NSW; ++s) {
+    const int n = (wc * R::NSW + s) * 16 + col;
+    boff[s] = n * 64 + ((quad ^ (((n >> 2) & 1) << 1)) << 4);
+  }
+  short8 a[2][R::MAXRB], bf[2][R::NSW];
+  auto load = [&](int st, int buf) {
+    const int tap = st / R::KC, kc = st - tap * R::KC;
+    const char* bs = ring + (st % 3) * SLOT;
+#pragma unroll
+    for (int s = 0; s < R::NSW; ++s) bf[buf][s] = *reinterpret_cast<const short8*>(bs + boff[s]);
+#pragma unroll
+    for (int j = 0; j < R::MAXRB; ++j)
+      a[buf][j] = *reinterpret_cast<const short8*>(abase + (j * R::WR * 16 + tap * step_d) * R::LDC + kc * 32);
+  };
+  load(0, 0);
+#pragma unroll
+  for (int st = 0; st < STEPS; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < STEPS) {
+      if (st + 2 < STEPS) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (st + 3 < STEPS) stage_ring<C, K>(w, st + 3, ring + (st % 3) * SLOT, tid, wave);
+      load(st + 1, cur ^ 1);
+    }
+#pragma unroll
+    for (int j = 0; j < R::MAXRB; ++j)
+#pragma unroll
+      for (int s = 0; s < R::NSW; ++s)
+        acc[j][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cur][j], bf[cur][s], acc[j][s], 0, 0, 0);
+  }
+}
+
 template <int C, int K>
 __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf16_t* __restrict__ x, RFW p,
                                                                         const bf16_t* acc_in, bf16_t* out, int T,
@@ -435,15 +509,18 @@ __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf
   const int col = lane & 15, quad = lane >> 4;
   const bf16_t* xb = x + (long)b * T * C;
 
-  short8 wreg[R::WIT];
-  auto wload = [&](const bf16_t* __restrict__ w) {
+  // Weight images go global -> registers -> LDS.  Two register sets: the load of conv c+2's image is
+  // issued at the start of conv c (two convs of latency cover), conv c+1's image is written to LDS
+  // after conv c's closing barrier.
+  short8 wr0[R::WIT], wr1[R::WIT];
+  auto wload = [&](short8 (&wreg)[R::WIT], const bf16_t* __restrict__ w) {
 #pragma unroll
     for (int it = 0; it < R::WIT; ++it) {
       const int q = tid + it * NT;
       if (q < R::WCH) wreg[it] = *reinterpret_cast<const short8*>(w + q * 8);
     }
   };
-  auto wstore = [&]() {
+  auto wstore = [&](const short8 (&wreg)[R::WIT]) {
 #pragma unroll
     for (int it = 0; it < R::WIT; ++it) {
       const int q = tid + it * NT;
@@ -454,10 +531,11 @@ __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf
     }
   };
 
-  // 1. raw x rows [0, R0) (zero outside [0, T)) -> A; first conv's weights -> W
+  // 1. raw x rows [0, R0) (zero outside [0, T)) -> A; conv 0's weights -> W, conv 1's in flight
   {
     constexpr int IT = (R::R0 * CH + NT - 1) / NT;
     short8 v[IT];
+    if constexpr (!R::RING) wload(wr0, p.w[0]);
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
@@ -469,13 +547,15 @@ __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf
         for (int i = 0; i < 8; ++i) v[it][i] = 0;
       }
     }
-    wload(p.w[0]);
+    if constexpr (!R::RING) {
+      wload(wr1, p.w[1]);
+      wstore(wr0);
+    }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
       if (r < R::R0) *reinterpret_cast<short8*>(As + r * R::LDC + c0) = v[it];
     }
-    wstore();
   }
   __syncthreads();
 
@@ -497,13 +577,22 @@ __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf
     }
   __syncthreads();
 
+  // the final epilogue's acc_in rows, loaded during the last conv
+  constexpr int ITMAX = (R::R0 * CH + NT - 1) / NT;
+  const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
+  short8 ar[ITMAX];
+
   float4v acc[R::MAXRB][R::NSW];
 #pragma unroll
   for (int pp = 0; pp < 3; ++pp) {
     const int d = p.d[pp];
-    // conv1 (dilation d) of lrelu(x_p) -> T = lrelu(. + b1), zero outside [0, T)
-    wload(p.w[2 * pp + 1]);  // in flight during the MFMAs
-    conv_rf<C, K>(As, d, Ws, wr, wc, col, quad, acc);
+    // conv 2pp = conv1 (dilation d) of lrelu(x_p) -> T = lrelu(. + b1), zero outside [0, T)
+    if constexpr (R::RING) {
+      conv_rf_ring<C, K>(As, d, p.w[2 * pp], Ws, tid, wave, wr, wc, col, quad, acc);
+    } else {
+      if (pp < 2) wload(wr0, p.w[2 * pp + 2]);  // in flight during two convs
+      conv_rf<C, K>(As, d, Ws, wr, wc, col, quad, acc);
+    }
     {
       const float* b1 = p.b[2 * pp];
 #pragma unroll
@@ -522,11 +611,23 @@ __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf
       }
     }
     __syncthreads();  // T complete; everyone is done with conv1's weights and with A
-    wstore();
-    __syncthreads();
-    // conv2 (dilation 1) of T; X += . + b2; A = lrelu(X) for the next pair
-    if (pp < 2) wload(p.w[2 * pp + 2]);
-    conv_rf<C, K>(Ts, 1, Ws, wr, wc, col, quad, acc);
+    if constexpr (!R::RING) {
+      wstore(wr1);  // conv 2pp+1's image
+      __syncthreads();
+    }
+    // conv 2pp+1 = conv2 (dilation 1) of T; X += . + b2; A = lrelu(X) for the next pair
+    if (pp < 2) {
+      if constexpr (!R::RING) wload(wr1, p.w[2 * pp + 3]);
+    } else if (ab && !R::RING) {  // (the ring's vmcnt waits would also wait for these)
+#pragma unroll
+      for (int it = 0; it < ITMAX; ++it) {
+        const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+        const int t = t0 + j;
+        if (j < BM && t < T) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
+      }
+    }
+    if constexpr (R::RING) conv_rf_ring<C, K>(Ts, 1, p.w[2 * pp + 1], Ws, tid, wave, wr, wc, col, quad, acc);
+    else conv_rf<C, K>(Ts, 1, Ws, wr, wc, col, quad, acc);
     {
       const float* b2 = p.b[2 * pp + 1];
 #pragma unroll
@@ -548,8 +649,8 @@ __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf
       }
     }
     __syncthreads();  // A complete; everyone is done with conv2's weights and with T
-    if (pp < 2) {
-      wstore();
+    if (pp < 2 && !R::RING) {
+      wstore(wr0);  // conv 2pp+2's image
       __syncthreads();
     }
   }
@@ -563,18 +664,19 @@ __global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf
 #pragma unroll
       for (int i = 0; i < 4; ++i) Os[((wr + R::WR * j) * 16 + 4 * quad + i) * R::OSP + ch] = X[j][s][i];
     }
+  if constexpr (R::RING) {
+    if (ab) {
+#pragma unroll
+      for (int it = 0; it < ITMAX; ++it) {
+        const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+        const int t = t0 + j;
+        if (j < BM && t < T) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
+      }
+    }
+  }
   __syncthreads();
   {
-    constexpr int ITMAX = (R::R0 * CH + NT - 1) / NT;
     bf16_t* ob = out + (long)b * T * C;
-    const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
-    short8 ar[ITMAX];
-#pragma unroll
-    for (int it = 0; it < ITMAX; ++it) {
-      const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
-      const int t = t0 + j;
-      if (j < BM && t < T && ab) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
-    }
 #pragma unroll
     for (int it = 0; it < ITMAX; ++it) {
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
@@ -625,7 +727,7 @@ SSAMD_API void ssamd_resblock_debug(int v) { g_rb_debug = v; }
 // b: 6 fp32 [C]; dilations 1 <= d <= 5.  Returns -2 for a geometry without a fused instance
 // (ssamd_resblock_fusable).
 SSAMD_API int ssamd_resblock_fusable(int C, int K) {
-  return (C == 32 && (K == 3 || K == 7 || K == 11)) || (C == 64 && K == 3);
+  return (C == 32 && (K == 3 || K == 7 || K == 11)) || (C == 64 && (K == 3 || K == 7)) || (C == 128 && K == 3);
 }
 
 SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16_t* w1, const bf16_t* w2,
@@ -644,6 +746,8 @@ SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16
   if (C == 32 && K == 7) return launch_rf<32, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
   if (C == 32 && K == 11) return launch_rf<32, 11>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
   if (C == 64 && K == 3) return launch_rf<64, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 64 && K == 7) return launch_rf<64, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 128 && K == 3) return launch_rf<128, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
   return -2;
 }
 

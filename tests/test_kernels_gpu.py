@@ -942,7 +942,7 @@ def test_resblock_layer_fused(C, K, d, T):
 
 
 @pytest.mark.parametrize("C,K,T", [(32, 3, 1500), (32, 7, 700), (32, 11, 1100), (32, 11, 9), (64, 3, 900),
-                                   (64, 3, 5)])
+                                   (64, 3, 5), (64, 7, 1000), (128, 3, 700), (128, 3, 40)])
 def test_resblock_whole_block_fused(C, K, T):
     """Whole ResBlock1 kernel (3 layer pairs, dilations 1/3/5, residual in fp32 registers) vs the fp32
     torch ResBlock1 (reference hifigan/models.py:20-44), with the MRF accumulate / scale / post-lrelu

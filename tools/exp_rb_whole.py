@@ -14,7 +14,8 @@ from speakingstyle_amd.ops import hip  # noqa: E402
 dev = "cuda"
 B, TM = 64, 680  # utterances x mel frames
 res = []
-for C, K, up in ((32, 3, 256), (32, 7, 256), (32, 11, 256), (64, 3, 128), (64, 7, 128), (64, 11, 128)):
+for C, K, up in ((32, 3, 256), (32, 7, 256), (32, 11, 256), (64, 3, 128), (64, 7, 128), (64, 11, 128), (128, 3, 64),
+                  (128, 7, 64)):
     blk = H.ResBlock1(C, K, (1, 3, 5)).to(dev)
     for m in blk.modules():
         if isinstance(m, torch.nn.Conv1d) and hasattr(m, "weight_g"):
