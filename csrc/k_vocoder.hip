@@ -28,6 +28,9 @@ constexpr int MAXD = 5;
 // (C = 128: 2 + 4 reads / 8 MFMAs, under the LDS array's 1 read per 16-cycle MFMA at 2 waves per
 // SIMD).  The output tile BM = 16 * RPW * WR - (K - 1) is chosen so that conv1's BM + K - 1 rows
 // fill the row blocks exactly (no straggler block on one wave).
+// (Measured and lost: C = 128 at one wave per SIMD with a 64 x 64 wave tile -- 8 fragment reads per 16
+// MFMAs instead of 6 per 8 -- K = 7 5.25 -> 5.85 ms, K = 3 3.47 -> 4.00 ms: the second wave per SIMD
+// hides more than the saved LDS reads.)
 template <int C, int K>
 struct RB {
   static constexpr int NW = C >= 128 ? 8 : 4;       // waves per block
@@ -79,17 +82,38 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
                                    (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
+// DMA pieces per thread and pipeline step (vmcnt bookkeeping of conv_tile)
+template <int C, int K>
+constexpr int rb_dps() {
+  return RB<C, K>::KC2 * (C * 4 > RB<C, K>::NT ? C * 4 / RB<C, K>::NT : 1);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
 template <int C, int K>
 __device__ __forceinline__ void stage_b(const bf16_t* __restrict__ w, int step, char* slot, int tid, int wave) {
   using R = RB<C, K>;
   constexpr int CHUNKS = C * 4;  // 16-B chunks per [C][32] sub-slice
+  constexpr int REP = CHUNKS > R::NT ? CHUNKS / R::NT : 1;
+  static_assert(CHUNKS <= R::NT || CHUNKS % R::NT == 0, "slice chunks over the block");
   if (wave * 64 < CHUNKS) {      // wave-uniform
     const int c0 = step * R::KC2, tap = c0 / R::KC, kc = c0 - tap * R::KC;
-    const int n = tid >> 2, p = tid & 3;
-    const int lc = p ^ (((n >> 2) & 1) << 1);  // logical chunk stored at physical chunk p (see conv_tile)
 #pragma unroll
-    for (int j = 0; j < R::KC2; ++j)
-      glds16(w + (n * K + tap) * C + (kc + j) * 32 + 8 * lc, slot + j * C * 64 + wave * 1024);
+    for (int q = 0; q < REP; ++q) {
+      const int t = tid + q * R::NT;
+      const int n = t >> 2, p = t & 3;
+      const int lc = p ^ (((n >> 2) & 1) << 1);  // logical chunk stored at physical chunk p (see conv_tile)
+#pragma unroll
+      for (int j = 0; j < R::KC2; ++j)
+        glds16(w + (n * K + tap) * C + (kc + j) * 32 + 8 * lc, slot + j * C * 64 + (wave + q * R::NW) * 1024);
+    }
   }
 }
 
@@ -112,11 +136,11 @@ __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int ro
   stage_b<C, K>(w, 0, bring, tid, wave);
   if (STEPS > 1) stage_b<C, K>(w, 1, bring + SLOT, tid, wave);
   if (STEPS > 2) stage_b<C, K>(w, 2, bring + 2 * SLOT, tid, wave);
-  // (vmcnt counts this thread's DMA pieces: KC2 per step)
-  if (STEPS > 2 && R::KC2 == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (STEPS > 2 || (STEPS > 1 && R::KC2 == 2)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if (STEPS > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (vmcnt counts this thread's DMA pieces: DPS per step)
+  constexpr int DPS = rb_dps<C, K>();
+  if constexpr (STEPS > 2) wait_vm<2 * DPS>();
+  else if constexpr (STEPS > 1) wait_vm<DPS>();
+  else wait_vm<0>();
   __builtin_amdgcn_s_barrier();
   const bf16_t* arow = src + (wr * 16 + col) * R::LDC + 8 * quad;  // row block wr + WR*r
   // B-fragment read offsets (bytes) within a slot, per 16-column sub-tile of this wave
@@ -145,9 +169,8 @@ __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int ro
   for (int step = 0; step < STEPS; ++step) {
     const int cur = step & 1;
     if (step + 1 < STEPS) {
-      if (step + 2 < STEPS && R::KC2 == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-      else if (step + 2 < STEPS) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (step + 2 < STEPS) wait_vm_lgkm0<DPS>();
+      else wait_vm_lgkm0<0>();
       __builtin_amdgcn_s_barrier();
       if (step + 3 < STEPS) stage_b<C, K>(w, step + 3, bring + (step % 3) * SLOT, tid, wave);
       load(step + 1, cur ^ 1);
@@ -363,7 +386,12 @@ struct RF {
   static constexpr int WR = NW / WC;               // row groups
   static constexpr int H2 = (K - 1) / 2;
   static constexpr int MG = MAXD * H2;             // margin rows: the widest conv's half window
-  static constexpr int NB = C == 32 ? 40 : (C == 64 ? 24 : 12);  // 16-row blocks per tile
+  // OCC: workgroups per CU.  C = 32 / K = 3 is latency-bound at one workgroup per CU (little MFMA work
+  // between the phase barriers and the HBM / L2 round trips), so it takes a smaller tile (9 % halo
+  // recompute) that lets two workgroups overlap each other's phases (1.41 -> 1.18 ms per ResBlock).
+  // (C = 64 / K = 3 measured: the 8-block tile at two per CU is 12 % slower than 24 blocks at one)
+  static constexpr int OCC = K == 3 && C == 32 ? 2 : 1;
+  static constexpr int NB = K == 3 && C == 32 ? 16 : C == 32 ? 40 : (C == 64 ? 24 : 12);
   static constexpr int R0 = NB * 16;
   static constexpr int LDC = C + 16;               // bf16 pitch: 2 (mod 4) 16-B units (see RB)
   static constexpr int ROWS = R0 + 2 * MG;
@@ -381,7 +409,7 @@ struct RF {
   static constexpr int OSP = C + 4;                // fp32 output tile pitch
   static constexpr int LDS = 2 * BUF + WBYTES;
   static_assert(NB % WR == 0, "row blocks split evenly over the row groups");
-  static_assert(LDS <= 160 * 1024, "fused resblock tile");
+  static_assert(LDS * OCC <= 160 * 1024, "fused resblock tile");
   static_assert(R0 * OSP * 4 <= 2 * BUF, "output tile aliases the A / T tiles");
 };
 
@@ -488,7 +516,7 @@ __device__ __forceinline__ void conv_rf_ring(const bf16_t* __restrict__ src, int
 }
 
 template <int C, int K>
-__global__ void __launch_bounds__((RF<C, K>::NT)) resblock_fused_kernel(const bf16_t* __restrict__ x, RFW p,
+__global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fused_kernel(const bf16_t* __restrict__ x, RFW p,
                                                                         const bf16_t* acc_in, bf16_t* out, int T,
                                                                         int tiles, int HT, float slope,
                                                                         float out_scale, int post_lrelu) {

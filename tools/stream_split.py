@@ -1,0 +1,63 @@
+#!/usr/bin/env python
+"""Per-stream view of the last training steps in a rocprofv3 kernel trace (weight gradients on the
+side stream): per step, the busy time of each stream, the time both run together, and how long the
+optimizer waited at the join for the side stream after the main stream's last backward kernel.
+
+Usage: python tools/stream_split.py <kernel_trace.csv> [--last 5]"""
+import argparse
+import csv
+import re
+from collections import defaultdict
+
+
+def union(iv):
+    tot, cur = 0, None
+    for s, e in sorted(iv):
+        if cur is None or s > cur[1]:
+            if cur:
+                tot += cur[1] - cur[0]
+            cur = [s, e]
+        else:
+            cur[1] = max(cur[1], e)
+    if cur:
+        tot += cur[1] - cur[0]
+    return tot
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--last", type=int, default=5)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    skey = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
+    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get(skey, "0")) for r in rows)
+    ends = [i for i, k in enumerate(ks) if re.search(r"adam(_img)?_kernel", k[2])]
+    steps = list(zip(ends[:-1], ends[1:]))[-a.last:]
+    print(f"stream key: {skey}")
+    for i0, i1 in steps:
+        t0, t1 = ks[i0][1], ks[i1][1]
+        seg = ks[i0 + 1:i1 + 1]
+        per = defaultdict(list)
+        for s, e, n, q in seg:
+            per[q].append((s, e))
+        main_q = ks[i1][3]
+        busy = {q: union(v) / 1e6 for q, v in per.items()}
+        allu = union([(s, e) for s, e, _, _ in seg]) / 1e6
+        both = sum(busy.values()) - allu
+        side = [q for q in per if q != main_q]
+        # the optimizer (adam) start vs the last main-stream kernel before it and the last side kernel
+        adam_s = ks[i1][0]
+        main_prev = max((e for s, e, n, q in seg[:-1] if q == main_q), default=t0)
+        side_last = max((e for s, e, n, q in seg if q in side), default=t0)
+        print(f"span {(t1 - t0) / 1e6:7.3f} ms  union {allu:7.3f}  overlap {both:6.3f}  "
+              + "  ".join(f"q{q}:{busy[q]:7.3f}({len(per[q])})" for q in sorted(per))
+              + f"  | main-idle-before-adam {(adam_s - main_prev) / 1e6:6.3f}  side-ends-before-adam {(adam_s - side_last) / 1e6:6.3f}")
+        # main-stream idle gaps inside the step (waiting for host or for the side stream)
+        mv = sorted(per[main_q])
+        gaps = [(mv[i + 1][0] - mv[i][1]) / 1e3 for i in range(len(mv) - 1)]
+        print(f"   main-stream gaps: total {sum(g for g in gaps if g > 0) / 1e3:.3f} ms, >20us: {sum(1 for g in gaps if g > 20)}")
+
+
+if __name__ == "__main__":
+    main()
