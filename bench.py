@@ -74,6 +74,8 @@ def parse(argv=None):
                     help="per-GPU padded mel-frame budget per step (mi355x.frames_per_gpu) instead of --batch")
     ap.add_argument("--no-side-wgrad", action="store_true",
                     help="weight gradients on the main stream (A/B of the side-stream overlap)")
+    ap.add_argument("--normal-priority", action="store_true",
+                    help="main chain on a normal-priority stream (A/B of Trainer.use_priority_stream)")
     ap.add_argument("--ctypes-bindings", action="store_true",
                     help="launch kernels through ctypes instead of the generated native bindings (A/B)")
     ap.add_argument("--force-buckets", action="store_true",

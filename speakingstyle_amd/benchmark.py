@@ -113,6 +113,8 @@ def train_phase(args, rank, world, device):
     model.set_compute_dtype(torch.bfloat16 if cuda else torch.float32)
     ddp.broadcast_module_state(model)
     trainer = Trainer(model, (pp, mc, tc), seed=1234)
+    # the step's main chain on a high-priority stream, weight gradients on the normal-priority side stream
+    trainer.use_priority_stream(cuda and not getattr(args, "normal_priority", False))
     trainer.timer.enabled = bool(getattr(args, "phase_times", False)) or trainer.timer.enabled
 
     if getattr(args, "force_buckets", False) and world == 1 and cuda:

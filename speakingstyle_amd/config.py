@@ -107,6 +107,9 @@ _TRAIN_DEFAULTS: Config = {
         "phase_timing": False,    # per-phase host / device step timing (Perf/phase_* TB scalars)
         "preempt_check_steps": 10,  # DP: steps between cross-rank SIGTERM agreements
         "hip_kernels": True,      # False => torch reference ops even on GPU (debug / A-B only)
+        # "high": the step's main chain on a high-priority HIP stream (weight gradients on a normal-
+        # priority side stream fill the idle CUs); "normal": one priority for both (A/B)
+        "stream_priority": "high",
         # (non-finite steps are always skipped on the device by the fused clip+Adam kernel: no knob)
     },
 }
@@ -196,6 +199,7 @@ def normalize_train_config(cfg: Config | None) -> Config:
         raise ConfigError("optimizer.grad_acc_step must be >= 1")
     mi = out["mi355x"]
     _check_enum(mi["dtype"], ["bf16", "fp32"], "mi355x.dtype")
+    _check_enum(mi.get("stream_priority", "high"), ["high", "normal"], "mi355x.stream_priority")
     if mi.get("frames_per_gpu") is not None and int(mi["frames_per_gpu"]) <= 0:
         raise ConfigError("mi355x.frames_per_gpu must be a positive frame count (or null)")
     if "nan_guard" in mi:  # removed knob: the device-side non-finite skip is unconditional

@@ -121,6 +121,7 @@ def train(args, configs):
         mutil.restore_model(model, ckpt, train_config.get("ignore_layers", []))
     ddp.broadcast_module_state(model)
     trainer = Trainer(model, configs, restore_step=restore, seed=seed)
+    trainer.use_priority_stream(cuda and (train_config.get("mi355x", {}) or {}).get("stream_priority", "high") == "high")
     if ckpt is not None and "optimizer" in ckpt:
         trainer.opt.load_state_dict(ckpt["optimizer"])
     if ckpt is not None and isinstance(ckpt.get("rng"), torch.Tensor) and not cuda:

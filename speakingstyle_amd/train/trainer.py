@@ -59,6 +59,22 @@ class Trainer:
         mi = train_config.get("mi355x", {}) or {}
         self.timer = PhaseTimer(bool(mi.get("phase_timing", False)) or os.environ.get("SSAMD_PHASE_TIMING") == "1")
 
+    def use_priority_stream(self, enabled: bool = True):
+        """Run the step's main chain on a HIGH-priority HIP stream (made the current stream of this
+        thread).  The weight gradients go to a normal-priority side stream (``ops/hip.py::wgrad_async``)
+        and only fill the CUs the data-gradient chain leaves idle; with both at one priority the
+        dispatcher splits CUs between them and the critical-path kernels run slower.  Call before the
+        first step; tensors made earlier on the old stream are synchronised once here."""
+        dev = self.opt.arena.data.device
+        if not (enabled and dev.type == "cuda"):
+            return None
+        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+        torch.cuda.synchronize(dev)
+        s = torch.cuda.Stream(device=dev, priority=hi)
+        torch.cuda.set_stream(s)
+        self.compute_stream = s
+        return s
+
     def take_frames(self) -> int:
         """Valid mel frames consumed since the last call, summed over ranks (host sync: log steps only)."""
         f = self.frames.clone() + self.frames_host
