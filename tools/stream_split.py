@@ -10,6 +10,12 @@ import re
 from collections import defaultdict
 
 
+def short(n):
+    n = n.replace("(anonymous namespace)::", "").replace("void ", "")
+    m = re.match(r"([\w:]+(?:<[^()]*?>)?)", n)
+    return (m.group(1) if m else n)[:48]
+
+
 def union(iv):
     tot, cur = 0, None
     for s, e in sorted(iv):
@@ -28,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, default=5)
+    ap.add_argument("--detail", action="store_true", help="per-stream top kernels and the kernels after main-stream gaps")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     skey = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
@@ -54,9 +61,22 @@ def main():
               + "  ".join(f"q{q}:{busy[q]:7.3f}({len(per[q])})" for q in sorted(per))
               + f"  | main-idle-before-adam {(adam_s - main_prev) / 1e6:6.3f}  side-ends-before-adam {(adam_s - side_last) / 1e6:6.3f}")
         # main-stream idle gaps inside the step (waiting for host or for the side stream)
-        mv = sorted(per[main_q])
-        gaps = [(mv[i + 1][0] - mv[i][1]) / 1e3 for i in range(len(mv) - 1)]
-        print(f"   main-stream gaps: total {sum(g for g in gaps if g > 0) / 1e3:.3f} ms, >20us: {sum(1 for g in gaps if g > 20)}")
+        mk = sorted((s, e, n) for s, e, n, q in seg if q == main_q)
+        gaps = [((mk[i + 1][0] - mk[i][1]) / 1e3, mk[i + 1][2]) for i in range(len(mk) - 1)]
+        print(f"   main-stream gaps: total {sum(g for g, _ in gaps if g > 0) / 1e3:.3f} ms, "
+              f">20us: {sum(1 for g, _ in gaps if g > 20)}")
+        if a.detail:
+            by = defaultdict(float)
+            for g, n in gaps:
+                if g > 0:
+                    by[short(n)] += g
+            print("   gap before (us): " + ", ".join(f"{k} {v:.0f}" for k, v in sorted(by.items(), key=lambda x: -x[1])[:8]))
+            for q in sorted(per):
+                tot = defaultdict(float)
+                for s_, e_, n, qq in seg:
+                    if qq == q:
+                        tot[short(n)] += (e_ - s_) / 1e3
+                print(f"   q{q} top: " + ", ".join(f"{k} {v:.0f}" for k, v in sorted(tot.items(), key=lambda x: -x[1])[:10]))
 
 
 if __name__ == "__main__":
