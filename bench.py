@@ -74,6 +74,8 @@ def parse(argv=None):
                     help="per-GPU padded mel-frame budget per step (mi355x.frames_per_gpu) instead of --batch")
     ap.add_argument("--no-side-wgrad", action="store_true",
                     help="weight gradients on the main stream (A/B of the side-stream overlap)")
+    ap.add_argument("--ln-reduce-main", action="store_true",
+                    help="LayerNorm weight-gradient reductions on the main stream (A/B of the side-stream move)")
     ap.add_argument("--normal-priority", action="store_true",
                     help="main chain on a normal-priority stream (A/B of Trainer.use_priority_stream)")
     ap.add_argument("--ctypes-bindings", action="store_true",
@@ -116,6 +118,10 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.set_wgrad_stream(False)
+    if args.ln_reduce_main and torch.cuda.is_available():
+        from speakingstyle_amd.ops import hip
+
+        hip._SIDE_LN[0] = False
     rank, world, local_rank = ddp.init_distributed(backend=args.dist_backend, expect_world=args.gpus)
     cuda = torch.cuda.is_available()
     device = torch.device("cuda", local_rank) if cuda else torch.device("cpu")

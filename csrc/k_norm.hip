@@ -303,10 +303,24 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   float* scratch = ws + nblk * nk * C;
-  // dw | db over every block, in block order
-  rc = ssamd_seg_colsum(ws, (long)nk * C, 1, (int)nblk, 2 * C, dw, 0, 0, C, db, scratch, seg_colsum_ws(1, 2 * C),
-                        stream);
-  if (rc || !film) return rc;
+  // dw | db over every block, in block order (dw == null: the caller reduces them later from ws with
+  // ssamd_addln_wb_reduce -- on the weight-gradient side stream, off the data-gradient chain)
+  if (dw) {
+    rc = ssamd_seg_colsum(ws, (long)nk * C, 1, (int)nblk, 2 * C, dw, 0, 0, C, db, scratch, seg_colsum_ws(1, 2 * C),
+                          stream);
+    if (rc) return rc;
+  }
+  if (!film) return 0;
   // S1[b] | S2[b] over the gx blocks of sequence b
   return ssamd_seg_colsum(ws + 2 * C, (long)nk * C, B, gx, 2 * C, S1, C, 0, C, S2, nullptr, 0, stream);
+}
+
+// LayerNorm weight / bias gradients from the partials ssamd_addln_bwd left in ws (called with dw = null).
+SSAMD_API int ssamd_addln_wb_reduce(const float* ws, int B, int L, int C, int film, float* dw, float* db,
+                                    float* scratch, hipStream_t stream) {
+  if (B == 0 || L == 0) return 0;
+  const long nblk = (long)cdiv(L, ROWS_PER_BLOCK) * B;
+  const int nk = film ? 4 : 2;
+  return ssamd_seg_colsum(ws, (long)nk * C, 1, (int)nblk, 2 * C, dw, 0, 0, C, db, scratch, seg_colsum_ws(1, 2 * C),
+                          stream);
 }

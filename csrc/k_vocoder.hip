@@ -413,6 +413,9 @@ struct RF {
   static_assert(R0 * OSP * 4 <= 2 * BUF, "output tile aliases the A / T tiles");
 };
 
+// (Measured and lost: the epilogue tiles written as conflict-free b32 channel pairs after a DPP swap
+// with the neighbour column's lane -- LDS conflicts 0.30 -> 0.16 but 6-10 % slower per ResBlock,
+// profiles/r3_v7_rb_pairs_lost.jsonl; the 16-bit scattered stores stay.)
 // acc[j][s] = conv over the wave's row blocks blk = wr + WR*j (all NB blocks of the tile are computed:
 // straight-line MFMA code; rows outside the conv's valid region are don't-care).
 template <int C, int K>

@@ -64,6 +64,7 @@ _SIGS = {
     "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
     "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P, L_, P],
     "ssamd_addln_bwd_ws": [I, I, I, I],
+    "ssamd_addln_wb_reduce": [P, I, I, I, I, P, P, P, P],
     "ssamd_lr_fwd": [P, P, P, P, P, P, I, I, I, I, P],
     "ssamd_lr_bwd": [P, P, P, P, P, I, I, I, I, P],
     "ssamd_pack_info": [P, I, I, P, P, P, P],
@@ -368,6 +369,7 @@ _side_used = {}
 _side_by_handle = {}  # raw handle -> torch Stream (workspace allocation under the side stream)
 _side_keep = {}       # device -> inputs of queued side-stream kernels, released at the join
 _SIDE_WGRAD = [True]
+_SIDE_LN = [True]  # LayerNorm weight-gradient reductions on the side stream too (A/B: bench --ln-reduce-main)
 
 
 def set_wgrad_stream(enabled: bool):
@@ -978,6 +980,7 @@ class _AddLNFn(torch.autograd.Function):
         dh = torch.empty_like(ac)
         da = torch.empty_like(ac) if pre_p > 0 else None
         dw, db = gradslots.claim(w), gradslots.claim(b)  # written (not accumulated) by the fixed-order reduce
+        in_slots = dw is not None and db is not None
         if dw is None:
             dw = torch.empty(C, device=ac.device, dtype=torch.float32)
         if db is None:
@@ -985,11 +988,24 @@ class _AddLNFn(torch.autograd.Function):
         S1 = torch.empty(B, C, device=ac.device, dtype=torch.float32) if has_film else None
         S2 = torch.empty_like(S1) if has_film else None
         nws = int(lib().ssamd_addln_bwd_ws(B, L, C, int(has_film)))
-        ws = _workspace(ac.device, nws)
+        # the dw / db column sums are weight gradients: reduced on the side stream from a partials buffer
+        # of their own (the shared workspace is reused by the next main-stream op) when both slots are
+        # in place and single-contribution, like wgrad_async's weight-gradient GEMMs
+        side = (_SIDE_WGRAD[0] and _SIDE_LN[0] and in_slots and ctx.needs_input_grad[2]
+                and gradslots.single_contribution(w) and gradslots.single_contribution(b))
+        ws = torch.empty(nws, device=ac.device, dtype=torch.float32) if side else _workspace(ac.device, nws)
         rc = lib().ssamd_addln_bwd(_ptr(dout), _ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(sg), _ptr(lens),
-                                   _ptr(ctx.cu), _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da), _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
+                                   _ptr(ctx.cu), _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da),
+                                   None if side else _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
                                    B, L, C, pre_p, post_p, seed, _ptr(ws), ws.numel(), _stream())
         _check(rc, "ssamd_addln_bwd")
+        if side:
+            scratch = ws[nws - 16 * 2 * C:]  # the tail of the buffer is the column-sum scratch
+
+            def _reduce():
+                _check(lib().ssamd_addln_wb_reduce(_ptr(ws), B, L, C, int(has_film), _ptr(dw), _ptr(db), _ptr(scratch),
+                                                   _stream()), "ssamd_addln_wb_reduce")
+            wgrad_async(_reduce, (ws,), True, (w, b))
         d_a = da if da is not None else dh
         d_res = dh if has_res else None
         if d_res is not None and ctx.mailbox is not None:  # the consumer GEMM adds it (GradMailbox)
