@@ -74,6 +74,8 @@ def parse(argv=None):
                     help="per-GPU padded mel-frame budget per step (mi355x.frames_per_gpu) instead of --batch")
     ap.add_argument("--no-side-wgrad", action="store_true",
                     help="weight gradients on the main stream (A/B of the side-stream overlap)")
+    ap.add_argument("--synth-serial", action="store_true",
+                    help="synthesis on one stream (A/B of the FS2 / vocoder two-stream pipeline)")
     ap.add_argument("--ln-reduce-main", action="store_true",
                     help="LayerNorm weight-gradient reductions on the main stream (A/B of the side-stream move)")
     ap.add_argument("--normal-priority", action="store_true",

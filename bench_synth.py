@@ -29,6 +29,7 @@ def parse():
     ap.add_argument("--vocoder-buckets", type=int, default=8, help="1: vocode the padded batch")
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--tiny", action="store_true")
+    ap.add_argument("--synth-serial", action="store_true", help="one stream (A/B of the two-stream pipeline)")
     return ap.parse_args()
 
 

@@ -216,14 +216,26 @@ def synth_phase(args, rank, world, device):
     speakers, texts, src_lens, max_src = b[2], b[3], b[4], b[5]
     ref_mels, ref_lens, ref_max = b[6], b[7], b[8]
 
+    # Two-stage pipeline: the vocoder of batch i runs on its own stream while FastSpeech2 of batch i+1
+    # runs on the main stream -- FastSpeech2's host syncs (predicted lengths) wait for the main stream
+    # only, so the GPU is not drained between batches.  Every batch still does its full FS2 + vocoder
+    # work; the RTF is wall time over all audio of the timed batches (--synth-serial: one stream, A/B).
+    voc_stream = torch.cuda.Stream(device=device) if (cuda and not getattr(args, "synth_serial", False)) else None
+
     @torch.no_grad()
     def synth():
         out = model(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
         mel, mel_len = out[1], out[9]
         lens = mel_len.cpu()  # host lengths: the vocoder runs length-bucketed (exact on valid samples)
         if cuda:  # int16 conversion fused into the vocoder's conv_post kernel
-            pcm = voc.infer(mel.to(torch.bfloat16).contiguous(), int16_scale=mx, lengths=lens.tolist(),
-                            max_buckets=args.vocoder_buckets)
+            mel_b = mel.to(torch.bfloat16).contiguous()
+            if voc_stream is not None:
+                voc_stream.wait_stream(torch.cuda.current_stream())
+                mel_b.record_stream(voc_stream)  # the main stream's allocator must not recycle it early
+                with torch.cuda.stream(voc_stream):
+                    pcm = voc.infer(mel_b, int16_scale=mx, lengths=lens.tolist(), max_buckets=args.vocoder_buckets)
+            else:
+                pcm = voc.infer(mel_b, int16_scale=mx, lengths=lens.tolist(), max_buckets=args.vocoder_buckets)
         else:
             wav = voc(mel.transpose(1, 2)).squeeze(1)
             pcm = (wav.float() * mx).clamp(-32768, 32767).to(torch.int16)
