@@ -85,10 +85,11 @@ _SIGS = {
     "ssamd_weight_prep": [P, P, I, L_, P],
     "ssamd_weight_prep_tiled": [P, P, I, P],
     "ssamd_stream_wait": [P, P],
+    "ssamd_stream_create_cumask": [ctypes.c_uint],
 }
 
 
-_RESTYPES = {"ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws": L_, "ssamd_embed_bwd_ws": L_,
+_RESTYPES = {"ssamd_stream_create_cumask": P, "ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws": L_, "ssamd_embed_bwd_ws": L_,
              "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_}
 
 
@@ -376,10 +377,20 @@ def set_wgrad_stream(enabled: bool):
     _SIDE_WGRAD[0] = bool(enabled)
 
 
+_SIDE_CU_MASK = [None]  # 32-bit CU pattern of the side stream (None: all CUs); bench --side-cu-mask
+
+
 def _side_stream(device):
     s = _side.get(device.index)
     if s is None:
-        s = torch.cuda.Stream(device=device)
+        if _SIDE_CU_MASK[0] is not None:
+            with torch.cuda.device(device):
+                ptr = lib().ssamd_stream_create_cumask(int(_SIDE_CU_MASK[0]) & 0xFFFFFFFF)
+            if not ptr:
+                raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+            s = torch.cuda.ExternalStream(ptr, device=device)
+        else:
+            s = torch.cuda.Stream(device=device)
         _side[device.index] = s
         _side_by_handle[s.cuda_stream] = s
     return s
@@ -394,7 +405,11 @@ def wgrad_async(launch, inputs, slots_ok: bool, params=()):
     the side stream's raw handle (``_stream_override``; ``launch`` allocates nothing but the side
     stream's own workspace), and the inputs kept alive until ``join_side_streams`` instead of a
     ``record_stream`` per tensor (after the join the current stream is ordered behind every
-    side-stream read, so the caching allocator may recycle them)."""
+    side-stream read, so the caching allocator may recycle them).  ``inputs`` must list EVERY device
+    tensor the launch reads, the packed-row tables included: one freed early could be handed out by
+    the main stream's allocator while the side-stream kernel is still pending.  (Measured and lost:
+    issuing each launch one weight-gradient call later, so the main stream's next kernels are queued
+    first -- neutral, profiles/r3_v8_wgrad_defer_ab.txt.)"""
     if not (_SIDE_WGRAD[0] and slots_ok and all(gradslots.single_contribution(p) for p in params)):
         return launch()
     dev = inputs[0].device
@@ -408,7 +423,7 @@ def wgrad_async(launch, inputs, slots_ok: bool, params=()):
     keep = _side_keep.get(dev.index)
     if keep is None:
         keep = _side_keep[dev.index] = []
-    keep.extend(inputs)
+    keep.extend(t for t in inputs if t is not None)
     _side_used[dev.index] = True
     if len(keep) > 4096:  # a caller that never joins (no optimizer step): bound the held references
         join_side_streams()
@@ -660,7 +675,8 @@ class _ConvFn(torch.autograd.Function):
             sw = gradslots.claim(w)
             res = wgrad_async(lambda: conv_wgrad_raw(xc, dy, B, L, Cin, ks, dil, pad, N, with_bias=want_b, dW=sw,
                                                      db=sb, rinfo=rinfo, cu=None if pk is None else pk.cu),
-                              (xc, dy), sw is not None and (sb is not None or not want_b),
+                              (xc, dy, rinfo, None if pk is None else pk.cu),
+                              sw is not None and (sb is not None or not want_b),
                               (w, ctx.b) if want_b else (w,))
             dw, db = res if want_b else (res, None)
             if w.dim() == 2:
@@ -817,15 +833,15 @@ class _FFNFn(torch.autograd.Function):
         else:
             dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
         s2w, s2b = gradslots.claim(w2), gradslots.claim(b2)
-        dw2, db2 = wgrad_async(lambda: conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=s2w, db=s2b,
-                                                      rinfo=r2, cu=ctx.cu[1]),
-                               (h, dz), s2w is not None and s2b is not None, (w2, b2))
+        dw2, db2 = wgrad_async(lambda: conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=s2w,
+                                                      db=s2b, rinfo=r2, cu=ctx.cu[1]),
+                               (h, dz, r2, ctx.cu[1]), s2w is not None and s2b is not None, (w2, b2))
         dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1,
                            resid=_resid_for(ctx.mailbox, xc))
         s1w, s1b = gradslots.claim(w1), gradslots.claim(b1)
         dw1, db1 = wgrad_async(lambda: conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=s1w,
                                                       db=s1b, rinfo=r1, cu=ctx.cu[0]),
-                               (xc, dh), s1w is not None and s1b is not None, (w1, b1))
+                               (xc, dh, r1, ctx.cu[0]), s1w is not None and s1b is not None, (w1, b1))
         return dx, dw1, db1, dw2, db2, None, None, None
 
 
@@ -1001,9 +1017,10 @@ class _AddLNFn(torch.autograd.Function):
         _check(rc, "ssamd_addln_bwd")
         if side:
             scratch = ws[nws - 16 * 2 * C:]  # the tail of the buffer is the column-sum scratch
+            p_dw, p_db = dw.data_ptr(), db.data_ptr()  # raw addresses: the closure holds no slot tensor
 
             def _reduce():
-                _check(lib().ssamd_addln_wb_reduce(_ptr(ws), B, L, C, int(has_film), _ptr(dw), _ptr(db), _ptr(scratch),
+                _check(lib().ssamd_addln_wb_reduce(_ptr(ws), B, L, C, int(has_film), p_dw, p_db, _ptr(scratch),
                                                    _stream()), "ssamd_addln_wb_reduce")
             wgrad_async(_reduce, (ws,), True, (w, b))
         d_a = da if da is not None else dh
