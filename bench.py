@@ -74,8 +74,6 @@ def parse(argv=None):
                     help="per-GPU padded mel-frame budget per step (mi355x.frames_per_gpu) instead of --batch")
     ap.add_argument("--no-side-wgrad", action="store_true",
                     help="weight gradients on the main stream (A/B of the side-stream overlap)")
-    ap.add_argument("--side-cu-mask", type=lambda v: int(v, 0), default=None,
-                    help="CU pattern of the weight-gradient side stream (e.g. 0x77777777: 3 of 4 CUs)")
     ap.add_argument("--synth-serial", action="store_true",
                     help="synthesis on one stream (A/B of the FS2 / vocoder two-stream pipeline)")
     ap.add_argument("--ln-reduce-main", action="store_true",
@@ -122,10 +120,6 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.set_wgrad_stream(False)
-    if args.side_cu_mask is not None and torch.cuda.is_available():
-        from speakingstyle_amd.ops import hip
-
-        hip._SIDE_CU_MASK[0] = args.side_cu_mask
     if args.ln_reduce_main and torch.cuda.is_available():
         from speakingstyle_amd.ops import hip
 

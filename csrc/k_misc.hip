@@ -1304,21 +1304,3 @@ SSAMD_API int ssamd_stream_wait(hipStream_t waiter, hipStream_t signaler) {
   if (hipEventRecord(e, signaler) != hipSuccess) return -4;
   return hipStreamWaitEvent(waiter, e, 0) == hipSuccess ? 0 : -5;
 }
-
-// A stream restricted to a subset of the device's CUs (hipExtStreamCreateWithCUMask): the weight-gradient
-// side stream can leave part of every XCD to the data-gradient chain, whose memory-bound kernels (BatchNorm /
-// LayerNorm backward) otherwise wait for CUs the side stream's GEMM blocks hold (their VGPRs fill the SIMDs).
-// `pattern` repeats over the 32-CU words of the mask (e.g. 0x77777777: 3 of every 4 CUs; CUs are numbered
-// round-robin over the XCDs, so every XCD keeps the same share).  Returns the stream handle (null on error).
-SSAMD_API void* ssamd_stream_create_cumask(unsigned pattern) {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return nullptr;
-  const int words = (n + 31) / 32;
-  uint32_t mask[64];
-  if (words > 64) return nullptr;
-  for (int i = 0; i < words; ++i) mask[i] = pattern;
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) return nullptr;
-  return (void*)s;
-}

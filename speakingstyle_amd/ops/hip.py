@@ -85,11 +85,10 @@ _SIGS = {
     "ssamd_weight_prep": [P, P, I, L_, P],
     "ssamd_weight_prep_tiled": [P, P, I, P],
     "ssamd_stream_wait": [P, P],
-    "ssamd_stream_create_cumask": [ctypes.c_uint],
 }
 
 
-_RESTYPES = {"ssamd_stream_create_cumask": P, "ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws": L_, "ssamd_embed_bwd_ws": L_,
+_RESTYPES = {"ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws": L_, "ssamd_embed_bwd_ws": L_,
              "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_}
 
 
@@ -377,20 +376,10 @@ def set_wgrad_stream(enabled: bool):
     _SIDE_WGRAD[0] = bool(enabled)
 
 
-_SIDE_CU_MASK = [None]  # 32-bit CU pattern of the side stream (None: all CUs); bench --side-cu-mask
-
-
 def _side_stream(device):
     s = _side.get(device.index)
     if s is None:
-        if _SIDE_CU_MASK[0] is not None:
-            with torch.cuda.device(device):
-                ptr = lib().ssamd_stream_create_cumask(int(_SIDE_CU_MASK[0]) & 0xFFFFFFFF)
-            if not ptr:
-                raise RuntimeError("hipExtStreamCreateWithCUMask failed")
-            s = torch.cuda.ExternalStream(ptr, device=device)
-        else:
-            s = torch.cuda.Stream(device=device)
+        s = torch.cuda.Stream(device=device)
         _side[device.index] = s
         _side_by_handle[s.cuda_stream] = s
     return s
