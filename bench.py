@@ -173,6 +173,10 @@ def run(args):
         "skipped_steps": tr["skipped_steps"],
         "host_enqueue_ms_per_step": round(tr["host_ms_per_step"], 3),
     }
+    if tr.get("host_lead_ms"):
+        rec["host_lead_ms"] = tr["host_lead_ms"]
+    if tr.get("host_tail_ms"):
+        rec["host_tail_ms"] = tr["host_tail_ms"]
     if tr.get("phases"):
         rec["phase_ms"] = {k: {"host": round(v["host_ms"], 3), "device": round(v["device_ms"], 3)}
                            for k, v in tr["phases"].items()}

@@ -155,13 +155,26 @@ def train_phase(args, rank, world, device):
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)
+    if trainer._host_tail is not None:
+        trainer._host_tail.clear()  # timed steps only
     t0 = time.perf_counter()
     frames = 0
     host = 0.0  # time inside train_step (enqueue): ~= elapsed when the step is host-bound
+    # SSAMD_HOST_LEAD=1: per step, how far the host's enqueue ran ahead of the GPU finishing the step
+    lead = cuda and os.environ.get("SSAMD_HOST_LEAD") == "1"
+    if lead:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        evs, hts = [], []
     for i in range(args.steps):
         h0 = time.perf_counter()
         frames += step(warm + i)
         host += time.perf_counter() - h0
+        if lead:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            evs.append(e)
+            hts.append(time.perf_counter() - t0)
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)
@@ -178,6 +191,12 @@ def train_phase(args, rank, world, device):
         "skipped_steps": int(trainer.opt.skipped_steps),
         "host_ms_per_step": 1000.0 * host / max(1, args.steps),
     }
+    if lead:
+        # GPU finish time of step i minus the host time its enqueue ended (both from t0; ev0 recorded ~t0)
+        info["host_lead_ms"] = [round(ev0.elapsed_time(e) - 1e3 * h, 2) for e, h in zip(evs, hts)]
+    tail = trainer.host_tail_summary()
+    if tail is not None:
+        info["host_tail_ms"] = tail
     del trainer, model, pool
     if cuda:
         torch.cuda.empty_cache()

@@ -110,6 +110,8 @@ _TRAIN_DEFAULTS: Config = {
         # "high": the step's main chain on a high-priority HIP stream (weight gradients on a normal-
         # priority side stream fill the idle CUs); "normal": one priority for both (A/B)
         "stream_priority": "high",
+        # run backward on the calling thread (no autograd device worker thread): less host time per step
+        "backward_same_thread": True,
         # (non-finite steps are always skipped on the device by the fused clip+Adam kernel: no knob)
     },
 }

@@ -419,7 +419,13 @@ def wgrad_async(launch, inputs, slots_ok: bool, params=()):
     return out
 
 
-def join_side_streams():
+def join_side_streams(defer_release=False):
+    """Make the current stream wait for the side-stream weight-gradient kernels.  The inputs those
+    kernels held are released here, or -- ``defer_release`` -- handed back to the caller: dropping a
+    few hundred tensors costs the host ~0.5 ms, which at the end of a backward is GPU idle time, so
+    the trainer drops them while the next step's forward keeps the GPU busy (their memory stays
+    reserved until then; safe either way, the join orders every later reuse after those kernels)."""
+    held = []
     for idx, used in _side_used.items():
         if used:
             with torch.cuda.device(idx):
@@ -427,7 +433,12 @@ def join_side_streams():
             _side_used[idx] = False
             keep = _side_keep.get(idx)
             if keep:
-                keep.clear()
+                if defer_release:
+                    held.append(keep)
+                    _side_keep[idx] = []
+                else:
+                    keep.clear()
+    return held
 
 
 # ------------------------------------------------------------------------ raw launchers

@@ -17,6 +17,7 @@ MI355X-specific structure:
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -56,7 +57,18 @@ class Trainer:
 
         from ..utils.timing import PhaseTimer
 
+        # SSAMD_HOST_TAIL=1: host timestamps of the step tail (backward return .. optimizer launch)
+        self._host_tail = [] if os.environ.get("SSAMD_HOST_TAIL") == "1" else None
+        self._defer_release = os.environ.get("SSAMD_DEFER_RELEASE", "1") == "1"
+        self._held = None
         mi = train_config.get("mi355x", {}) or {}
+        # backward on the calling thread instead of autograd's per-device worker thread: no thread
+        # hand-off per backward and less engine bookkeeping -- host enqueue per step 15.7 -> 12.1 ms
+        # (BC2013_GST), 18.6 -> 15.1 (BC2013), 12.2 -> 10.3 (LJSpeech); profiles/r3_v10_host_lead.txt
+        same = mi.get("backward_same_thread", True)
+        if os.environ.get("SSAMD_BWD_SAME_THREAD") in ("0", "1"):
+            same = os.environ["SSAMD_BWD_SAME_THREAD"] == "1"
+        torch.autograd.set_multithreading_enabled(not same)
         self.timer = PhaseTimer(bool(mi.get("phase_timing", False)) or os.environ.get("SSAMD_PHASE_TIMING") == "1")
 
     def use_priority_stream(self, enabled: bool = True):
@@ -130,6 +142,7 @@ class Trainer:
         last_micro = (self.micro + 1) % self.grad_acc == 0
         tm.phase("forward")
         output = self.model(*batch[2:])
+        self._held = None  # previous backward's side-stream inputs (see join_side_streams)
         if work is not None:
             work.wait()
         tm.phase("loss")
@@ -140,17 +153,28 @@ class Trainer:
             # the FiLM L2 term is identical on every rank: scale so the SUM all-reduce counts it once
             total = total - (1.0 - 1.0 / self.world) * self.loss_fn.lambda_f * torch.sum(torch.square(named))
         tm.phase("backward")
+        ht = self._host_tail
+        if ht is not None:
+            ht.append(("bwd_call", time.perf_counter()))
         if last_micro or self.world == 1:
             (total / self.grad_acc).backward()
         else:
             with self.buckets.no_sync():
                 (total / self.grad_acc).backward()
-        if self.opt.arena.data.is_cuda:
-            from ..ops import gradslots, hip
+        if ht is not None:
+            ht.append(("bwd_return", time.perf_counter()))
+        cuda = self.opt.arena.data.is_cuda
+        if cuda:
+            from ..ops import hip
 
-            hip.join_side_streams()  # weight gradients computed on the side stream
-            gradslots.note_contributions(self.opt.arena)  # which parameters may use it next step
+            # weight gradients computed on the side stream; their inputs are dropped during the
+            # next forward (host time here is GPU idle time)
+            self._held = hip.join_side_streams(defer_release=self._defer_release)
+        if ht is not None:
+            ht.append(("joined", time.perf_counter()))
         self.opt.arena.finalize_grads()
+        if ht is not None:
+            ht.append(("finalized", time.perf_counter()))
         self.micro += 1
         hl = getattr(batch[7], "host_lengths", None)
         if hl is not None:  # host copy from the loader: no device work
@@ -163,7 +187,32 @@ class Trainer:
             self.buckets.finish()
             tm.phase("optimizer")
             lr = self.opt.step_and_update_lr()
+            if ht is not None:
+                ht.append(("opt_launched", time.perf_counter()))
+        if cuda:
+            # host bookkeeping for the next step AFTER the optimizer launch: the GPU runs clip + Adam
+            # meanwhile instead of idling at the end of the step
+            from ..ops import gradslots
+
+            gradslots.note_contributions(self.opt.arena)  # which parameters may use their slot next step
+        if last_micro:
             self.opt.zero_grad()
             self.last_lr = lr
+        if ht is not None:
+            ht.append(("step_end", time.perf_counter()))
         tm.stop()
         return losses, output, lr
+
+    def host_tail_summary(self):
+        """Mean host ms between consecutive step-tail marks (SSAMD_HOST_TAIL=1), or None."""
+        ht = self._host_tail
+        if not ht:
+            return None
+        acc, n = {}, {}
+        for (a, ta), (b, tb) in zip(ht, ht[1:]):
+            if b == "bwd_call":
+                continue  # forward + loss of the next step
+            k = f"{a}->{b}"
+            acc[k] = acc.get(k, 0.0) + (tb - ta) * 1e3
+            n[k] = n.get(k, 0) + 1
+        return {k: round(acc[k] / n[k], 3) for k in acc}

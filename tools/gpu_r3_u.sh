@@ -10,7 +10,7 @@ for c in LJSpeech BC2013; do
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/u/$c" -o run -- python3 "$R/bench.py" --config $c --steps 4 --warmup 2 --synth-steps 0 > "$R/gpurun_out/u_$c.log" 2>&1 || { tail -20 "$R/gpurun_out/u_$c.log"; exit 1; }
   cd "$R"
   t=$(find gpurun_out/u/$c -name "*kernel_trace.csv" | head -1)
-  python tools/stream_split.py "$t" --last 4 > gpurun_out/u_split_$c.txt 2>&1 || { tail -20 gpurun_out/u_split_$c.txt; exit 1; }
+  python tools/stream_split.py "$t" --last 2 --detail > gpurun_out/u_split_$c.txt 2>&1 || { tail -20 gpurun_out/u_split_$c.txt; exit 1; }
   cat gpurun_out/u_split_$c.txt
   rm -rf gpurun_out/u/$c
 done

@@ -34,6 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--last", type=int, default=5)
+    ap.add_argument("--tail", type=int, default=0, help="print the last N kernels (both streams) before Adam")
     ap.add_argument("--detail", action="store_true", help="per-stream top kernels and the kernels after main-stream gaps")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
@@ -61,6 +62,9 @@ def main():
               + "  ".join(f"q{q}:{busy[q]:7.3f}({len(per[q])})" for q in sorted(per))
               + f"  | main-idle-before-adam {(adam_s - main_prev) / 1e6:6.3f}  side-ends-before-adam {(adam_s - side_last) / 1e6:6.3f}")
         # main-stream idle gaps inside the step (waiting for host or for the side stream)
+        if a.tail:
+            for s_, e_, n, q in seg[-a.tail:]:
+                print(f"   {(s_ - t0) / 1e3:9.1f} .. {(e_ - t0) / 1e3:9.1f} us  q{q}  {short(n)}")
         mk = sorted((s, e, n) for s, e, n, q in seg if q == main_q)
         gaps = [((mk[i + 1][0] - mk[i][1]) / 1e3, mk[i + 1][2]) for i in range(len(mk) - 1)]
         print(f"   main-stream gaps: total {sum(g for g, _ in gaps if g > 0) / 1e3:.3f} ms, "
