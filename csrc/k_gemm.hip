@@ -2565,6 +2565,9 @@ static int device_cus() {
   return g_cus_dev[dev];
 }
 static int g_wgrad_blocks = 0;   // > 0: fixed split-M target (blocks per launch) instead of the cost model
+// > 0: plan the split-M rounds for this many CUs instead of the device's (a weight gradient on the side
+// stream then leaves the other CUs to the data-gradient chain instead of holding every CU's LDS)
+static int g_wgrad_cus = 0;
 static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits) {
   const int steps_all = (M + 63) / 64;
   int smax = max_splits;
@@ -2575,7 +2578,7 @@ static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits)
     const int sp = (g_wgrad_blocks + tiles - 1) / tiles;
     return sp < smax ? sp : smax;
   }
-  const int cus = device_cus();
+  const int cus = g_wgrad_cus > 0 ? g_wgrad_cus : device_cus();
   int best = 1;
   double best_c = 1e30;
   for (int sp = 1; sp <= smax; ++sp) {
@@ -2589,6 +2592,7 @@ static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits)
 
 static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64 when it applies), 0: force the 128x128 kernels
 SSAMD_API void ssamd_wgrad_set_blocks(int b) { g_wgrad_blocks = b > 0 ? b : 0; }
+SSAMD_API void ssamd_wgrad_set_cus(int n) { g_wgrad_cus = n > 0 ? n : 0; }
 SSAMD_API void ssamd_wgrad_set_variant(int v) { g_wgrad_variant = v; }
 
 SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, float* db,

@@ -115,6 +115,10 @@ def train_phase(args, rank, world, device):
     trainer = Trainer(model, (pp, mc, tc), seed=1234)
     # the step's main chain on a high-priority stream, weight gradients on the normal-priority side stream
     trainer.use_priority_stream(cuda and not getattr(args, "normal_priority", False))
+    if cuda and os.environ.get("SSAMD_WGRAD_CUS"):  # experiment: weight-gradient split plan for fewer CUs
+        from .ops import hip
+
+        hip.lib().ssamd_wgrad_set_cus(int(os.environ["SSAMD_WGRAD_CUS"]))
     trainer.timer.enabled = bool(getattr(args, "phase_times", False)) or trainer.timer.enabled
 
     if getattr(args, "force_buckets", False) and world == 1 and cuda:

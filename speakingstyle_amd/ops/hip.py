@@ -55,6 +55,7 @@ _SIGS = {
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],
     "ssamd_wgrad_set_blocks": [I],
+    "ssamd_wgrad_set_cus": [I],
     "ssamd_head_fwd": [P, P, P, P, L_, I, I, P, P],
     "ssamd_head_bwd": [P, P, P, P, L_, I, I, P, P, P, P, L_, P],
     "ssamd_head_bwd_ws": [L_, I],
