@@ -71,12 +71,16 @@ class Trainer:
         torch.autograd.set_multithreading_enabled(not same)
         self.timer = PhaseTimer(bool(mi.get("phase_timing", False)) or os.environ.get("SSAMD_PHASE_TIMING") == "1")
 
-    def use_priority_stream(self, enabled: bool = True):
+    def use_priority_stream(self, enabled: bool = True, wgrad_cu_frac: float = 0.75):
         """Run the step's main chain on a HIGH-priority HIP stream (made the current stream of this
         thread).  The weight gradients go to a normal-priority side stream (``ops/hip.py::wgrad_async``)
         and only fill the CUs the data-gradient chain leaves idle; with both at one priority the
         dispatcher splits CUs between them and the critical-path kernels run slower.  Call before the
-        first step; tensors made earlier on the old stream are synchronised once here."""
+        first step; tensors made earlier on the old stream are synchronised once here.
+
+        The weight-gradient split plan is also sized for ``wgrad_cu_frac`` of the CUs: its 256x256
+        blocks hold a CU's whole LDS, so a plan for every CU locks the data-gradient GEMMs out of the
+        GPU until its blocks drain (LJSpeech +0.5 % at 3/4, ``profiles/r3_v10_wgrad_cus_ab.txt``)."""
         dev = self.opt.arena.data.device
         if not (enabled and dev.type == "cuda"):
             return None
@@ -85,6 +89,11 @@ class Trainer:
         s = torch.cuda.Stream(device=dev, priority=hi)
         torch.cuda.set_stream(s)
         self.compute_stream = s
+        if wgrad_cu_frac and wgrad_cu_frac < 1.0:
+            from ..ops import hip
+
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            hip.lib().ssamd_wgrad_set_cus(max(1, int(cus * wgrad_cu_frac)))
         return s
 
     def take_frames(self) -> int:
