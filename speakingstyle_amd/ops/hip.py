@@ -369,6 +369,9 @@ _side = {}
 _side_used = {}
 _side_by_handle = {}  # raw handle -> torch Stream (workspace allocation under the side stream)
 _side_keep = {}       # device -> inputs of queued side-stream kernels, released at the join
+# issue a layer's weight gradient (side stream) BEFORE its data gradient (main stream): the side stream
+# then waits only for the operands, not for the data-gradient GEMM too (A/B knob SSAMD_WGRAD_FIRST)
+_WGRAD_FIRST = [os.environ.get("SSAMD_WGRAD_FIRST", "0") == "1"]
 _SIDE_WGRAD = [True]
 _SIDE_LN = [True]  # LayerNorm weight-gradient reductions on the side stream too (A/B: bench --ln-reduce-main)
 
@@ -668,7 +671,8 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = db = None
         pk = ctx.pack
         rinfo = None if pk is None else pk.rinfo
-        if ctx.needs_input_grad[0]:
+        first = _WGRAD_FIRST[0]
+        if ctx.needs_input_grad[0] and not first:
             dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin, rinfo=rinfo)
         want_b = ctx.has_b and ctx.needs_input_grad[2]
         sb = gradslots.claim(ctx.b) if want_b else None
@@ -684,6 +688,8 @@ class _ConvFn(torch.autograd.Function):
                 dw = dw.view(N, Cin)
         elif want_b:
             db = colsum_raw(dy, N, sb)
+        if ctx.needs_input_grad[0] and first:
+            dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin, rinfo=rinfo)
         return dx, dw, db, None, None, None, None, None, None
 
 
@@ -762,12 +768,17 @@ class _GroupLinearFn(torch.autograd.Function):
         ws, bs = ctx.members
         B, L, Cin, N = ctx.dims
         dy = dy.to(torch.bfloat16).contiguous()
-        dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin,
-                           resid=_resid_for(ctx.mailbox, xc))
+        first = _WGRAD_FIRST[0]
+        if not first:
+            dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin,
+                               resid=_resid_for(ctx.mailbox, xc))
         sw, sb = gradslots.claim_fused(ws), gradslots.claim_fused(bs)
         dw, db = wgrad_async(lambda: conv_wgrad_raw(xc, dy, B, L, Cin, 1, 1, 0, N, with_bias=True,
                                                     dW=None if sw is None else sw.view(N, Cin, 1), db=sb),
                              (xc, dy), sw is not None and sb is not None, tuple(ws) + tuple(bs))
+        if first:
+            dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin,
+                               resid=_resid_for(ctx.mailbox, xc))
         dw = dw.view(N, Cin)
         return (dx, None, None, None, None, *gradslots.split_rows(dw, ws), *gradslots.split_rows(db, bs))
 
@@ -828,21 +839,36 @@ class _FFNFn(torch.autograd.Function):
         p1, p2 = (k1 - 1) // 2, (k2 - 1) // 2
         b1, b2 = ctx.biases
         r1, r2 = ctx.rinfo
+        first = _WGRAD_FIRST[0]
+
+        def _wgrad2():
+            s2w, s2b = gradslots.claim(w2), gradslots.claim(b2)
+            return wgrad_async(lambda: conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=s2w,
+                                                      db=s2b, rinfo=r2, cu=ctx.cu[1]),
+                               (h, dz, r2, ctx.cu[1]), s2w is not None and s2b is not None, (w2, b2))
+
+        if first:
+            dw2, db2 = _wgrad2()
         if mask is not None:
             dh = conv_gemm_mask_raw(dz, weight_dgrad(w2), None, B, L, C, k2, (k2 - 1) - p2, H, 0, rinfo=r2,
                                     mask_in=mask)
         else:
             dh = conv_gemm_raw(dz, weight_dgrad(w2), None, B, L, C, k2, 1, (k2 - 1) - p2, H, 0, aux=h, rinfo=r2)
-        s2w, s2b = gradslots.claim(w2), gradslots.claim(b2)
-        dw2, db2 = wgrad_async(lambda: conv_wgrad_raw(h, dz, B, L, H, k2, 1, p2, C, with_bias=True, dW=s2w,
-                                                      db=s2b, rinfo=r2, cu=ctx.cu[1]),
-                               (h, dz, r2, ctx.cu[1]), s2w is not None and s2b is not None, (w2, b2))
-        dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1,
-                           resid=_resid_for(ctx.mailbox, xc))
-        s1w, s1b = gradslots.claim(w1), gradslots.claim(b1)
-        dw1, db1 = wgrad_async(lambda: conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=s1w,
+        if not first:
+            dw2, db2 = _wgrad2()
+
+        def _wgrad1():
+            s1w, s1b = gradslots.claim(w1), gradslots.claim(b1)
+            return wgrad_async(lambda: conv_wgrad_raw(xc, dh, B, L, C, k1, 1, p1, H, with_bias=True, dW=s1w,
                                                       db=s1b, rinfo=r1, cu=ctx.cu[0]),
                                (xc, dh, r1, ctx.cu[0]), s1w is not None and s1b is not None, (w1, b1))
+
+        if first:
+            dw1, db1 = _wgrad1()
+        dx = conv_gemm_raw(dh, weight_dgrad(w1), None, B, L, H, k1, 1, (k1 - 1) - p1, C, 0, rinfo=r1,
+                           resid=_resid_for(ctx.mailbox, xc))
+        if not first:
+            dw1, db1 = _wgrad1()
         return dx, dw1, db1, dw2, db2, None, None, None
 
 
