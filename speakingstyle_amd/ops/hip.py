@@ -371,7 +371,17 @@ _side_by_handle = {}  # raw handle -> torch Stream (workspace allocation under t
 _side_keep = {}       # device -> inputs of queued side-stream kernels, released at the join
 # issue a layer's weight gradient (side stream) BEFORE its data gradient (main stream): the side stream
 # then waits only for the operands, not for the data-gradient GEMM too (A/B knob SSAMD_WGRAD_FIRST)
-_WGRAD_FIRST = [os.environ.get("SSAMD_WGRAD_FIRST", "0") == "1"]
+# (A/B knob SSAMD_WGRAD_FIRST = 0 / 1 / auto).  Measured (profiles/r3_v10_wgrad_first_ab.txt): +0.8 %
+# BC2013 and +1.5 % GST (M ~ 40-50k-row layers whose data-gradient GEMMs leave CUs idle in their
+# last wave), -0.7 % LJSpeech (~110k rows); "auto": first only below _WGRAD_FIRST_ROWS rows (default off
+# until measured).
+_WGRAD_FIRST = [{"0": 0, "1": 1}.get(os.environ.get("SSAMD_WGRAD_FIRST", "0"), 2)]
+_WGRAD_FIRST_ROWS = int(os.environ.get("SSAMD_WGRAD_FIRST_ROWS", 80000))
+
+
+def _wgrad_first(rows: int) -> bool:
+    m = _WGRAD_FIRST[0]
+    return m == 1 or (m == 2 and rows < _WGRAD_FIRST_ROWS)
 _SIDE_WGRAD = [True]
 _SIDE_LN = [True]  # LayerNorm weight-gradient reductions on the side stream too (A/B: bench --ln-reduce-main)
 
@@ -671,7 +681,7 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = db = None
         pk = ctx.pack
         rinfo = None if pk is None else pk.rinfo
-        first = _WGRAD_FIRST[0]
+        first = _wgrad_first(B * L)
         if ctx.needs_input_grad[0] and not first:
             dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin, rinfo=rinfo)
         want_b = ctx.has_b and ctx.needs_input_grad[2]
@@ -768,7 +778,7 @@ class _GroupLinearFn(torch.autograd.Function):
         ws, bs = ctx.members
         B, L, Cin, N = ctx.dims
         dy = dy.to(torch.bfloat16).contiguous()
-        first = _WGRAD_FIRST[0]
+        first = _wgrad_first(B * L)
         if not first:
             dx = conv_gemm_raw(dy, weight_dgrad(wf, owner=ws[0]), None, B, L, N, 1, 1, 0, Cin,
                                resid=_resid_for(ctx.mailbox, xc))
@@ -839,7 +849,7 @@ class _FFNFn(torch.autograd.Function):
         p1, p2 = (k1 - 1) // 2, (k2 - 1) // 2
         b1, b2 = ctx.biases
         r1, r2 = ctx.rinfo
-        first = _WGRAD_FIRST[0]
+        first = _wgrad_first(B * L)
 
         def _wgrad2():
             s2w, s2b = gradslots.claim(w2), gradslots.claim(b2)
