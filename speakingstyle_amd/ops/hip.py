@@ -382,6 +382,8 @@ _WGRAD_FIRST_ROWS = int(os.environ.get("SSAMD_WGRAD_FIRST_ROWS", 80000))
 def _wgrad_first(rows: int) -> bool:
     m = _WGRAD_FIRST[0]
     return m == 1 or (m == 2 and rows < _WGRAD_FIRST_ROWS)
+
+
 _SIDE_WGRAD = [True]
 _SIDE_LN = [True]  # LayerNorm weight-gradient reductions on the side stream too (A/B: bench --ln-reduce-main)
 
