@@ -373,9 +373,9 @@ _side_keep = {}       # device -> inputs of queued side-stream kernels, released
 # then waits only for the operands, not for the data-gradient GEMM too (A/B knob SSAMD_WGRAD_FIRST)
 # (A/B knob SSAMD_WGRAD_FIRST = 0 / 1 / auto).  Measured (profiles/r3_v10_wgrad_first_ab.txt): +0.8 %
 # BC2013 and +1.5 % GST (M ~ 40-50k-row layers whose data-gradient GEMMs leave CUs idle in their
-# last wave), -0.7 % LJSpeech (~110k rows); "auto": first only below _WGRAD_FIRST_ROWS rows (default off
-# until measured).
-_WGRAD_FIRST = [{"0": 0, "1": 1}.get(os.environ.get("SSAMD_WGRAD_FIRST", "0"), 2)]
+# last wave), -0.7 % LJSpeech (~110k rows); "auto" (default): first only below _WGRAD_FIRST_ROWS rows --
+# +0.6 % LJSpeech, +0.7 % BC2013, +1.2 % GST vs off, two repetitions each.
+_WGRAD_FIRST = [{"0": 0, "1": 1}.get(os.environ.get("SSAMD_WGRAD_FIRST", "auto"), 2)]
 _WGRAD_FIRST_ROWS = int(os.environ.get("SSAMD_WGRAD_FIRST_ROWS", 80000))
 
 
