@@ -231,6 +231,10 @@ class VarianceAdaptor(nn.Module):
 
 def _bins(lo, hi, n_bins, quant):
     if quant == "log":
+        if not lo > 0:
+            raise ValueError(
+                f"log pitch/energy quantization needs positive feature stats (min={lo}); z-score normalised "
+                "features (preprocessing.*.normalization: True) only work with linear quantization")
         return torch.exp(torch.linspace(math.log(lo), math.log(hi), n_bins - 1))
     return torch.linspace(lo, hi, n_bins - 1)
 
@@ -240,8 +244,13 @@ def _load_stats(preprocess_config):
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f)
-    # normalised features without stats: z-scores in a generous range
-    return {"pitch": [-4.0, 12.0, 0.0, 1.0], "energy": [-2.0, 10.0, 0.0, 1.0]}
+    # no stats.json (synthetic runs / fresh configs): a generous range in the features' own units --
+    # z-scores when normalised, Hz and STFT-magnitude energy otherwise (positive: log bins work)
+    pp = preprocess_config["preprocessing"]
+    norm_p = pp["pitch"].get("normalization", True)
+    norm_e = pp["energy"].get("normalization", True)
+    return {"pitch": [-4.0, 12.0, 0.0, 1.0] if norm_p else [40.0, 900.0, 0.0, 1.0],
+            "energy": [-2.0, 10.0, 0.0, 1.0] if norm_e else [0.01, 400.0, 0.0, 1.0]}
 
 
 def _spker_table(preprocess_config):

@@ -68,8 +68,7 @@ def main(argv=None):
         ds = TextDataset(args.source, pp, tc)
         batchs = list(DataLoader(ds, batch_size=args.batch_size, collate_fn=ds.collate_fn))
     else:
-        lex_path = pp["path"]["lexicon_path"]
-        lexicon = g2p.read_lexicon(lex_path) if os.path.exists(lex_path) else {}
+        lexicon = g2p.load_lexicon(pp["path"]["lexicon_path"], pp["preprocessing"]["text"].get("language", "en"))
         batch, phones, use_ref = single_batch(args.text, pp, args.speaker_id, args.ref_audio, lexicon)
         batchs = [batch]
         if any(v is not None for v in (args.word_pitch, args.word_energy, args.word_duration)):

@@ -13,7 +13,8 @@ ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 def stft_block():
     return {"filter_length": 1024, "hop_length": 256, "win_length": 1024}
 
-def preprocess(name, lang="en", cleaners=("english_cleaners",), pitch="phoneme_level", energy="phoneme_level"):
+def preprocess(name, lang="en", cleaners=("english_cleaners",), pitch="phoneme_level", energy="phoneme_level",
+               norm=True):
     return {
         "dataset": name,
         "path": {
@@ -28,8 +29,8 @@ def preprocess(name, lang="en", cleaners=("english_cleaners",), pitch="phoneme_l
             "audio": {"sampling_rate": 22050, "max_wav_value": 32768.0},
             "stft": stft_block(),
             "mel": {"n_mel_channels": 80, "mel_fmin": 0, "mel_fmax": 8000},
-            "pitch": {"feature": pitch, "normalization": True},
-            "energy": {"feature": energy, "normalization": True},
+            "pitch": {"feature": pitch, "normalization": norm},
+            "energy": {"feature": energy, "normalization": norm},
         },
     }
 
@@ -58,7 +59,7 @@ def model(dec_layers=6, pitch_q="linear", multi=False, vocoder_spk="LJSpeech", r
     }
     return m
 
-def train(name, batch, total=900000, save=10000, init_lr=None, style=False):
+def train(name, batch, total=900000, save=10000, init_lr=None, style=False, anneal=([300000, 400000, 500000], 0.3)):
     t = {
         "ignore_layers": [],
         "path": {
@@ -69,7 +70,7 @@ def train(name, batch, total=900000, save=10000, init_lr=None, style=False):
         "optimizer": {
             "batch_size": batch, "betas": [0.9, 0.98], "eps": 1.0e-9, "weight_decay": 0.0,
             "grad_clip_thresh": 1.0, "grad_acc_step": 1, "warm_up_step": 4000,
-            "anneal_steps": [300000, 400000, 500000], "anneal_rate": 0.3,
+            "anneal_steps": list(anneal[0]), "anneal_rate": anneal[1],
         },
         "step": {"total_step": total, "log_step": 100, "synth_step": 1000, "val_step": 1000, "save_step": save},
         "mi355x": {"dtype": "bf16", "bucket_mb": 32, "seed": 1234, "num_workers": 4},
@@ -83,13 +84,19 @@ def train(name, batch, total=900000, save=10000, init_lr=None, style=False):
 
 SETS = {
     "LJSpeech": (preprocess("LJSpeech"), model(), train("LJSpeech", 200, save=1000)),
-    "LJSpeech_paper": (preprocess("LJSpeech"), model(dec_layers=4, pitch_q="log"), train("LJSpeech_paper", 48, total=160000)),
-    "LibriTTS": (preprocess("LibriTTS"), model(multi=True, vocoder_spk="universal"), train("LibriTTS", 16)),
-    "AISHELL3": (preprocess("AISHELL3", lang="zh", cleaners=()), model(multi=True, vocoder_spk="universal"), train("AISHELL3", 16)),
+    # reference config/LJSpeech_paper/{preprocess,train}.yaml: frame-level, unnormalised pitch / energy
+    # (log pitch bins over Hz), no LR annealing
+    "LJSpeech_paper": (preprocess("LJSpeech_paper", pitch="frame_level", energy="frame_level", norm=False),
+                       model(dec_layers=4, pitch_q="log"),
+                       train("LJSpeech_paper", 48, total=160000, anneal=([], 1.0))),
+    "LibriTTS": (preprocess("LibriTTS"), model(multi=True, vocoder_spk="universal"), train("LibriTTS", 16, save=100000)),
+    "AISHELL3": (preprocess("AISHELL3", lang="zh", cleaners=()), model(multi=True, vocoder_spk="universal"),
+                 train("AISHELL3", 16, save=100000)),
     "BC2013": (preprocess("BC2013"), model(ref_enc=True), train("BC2013", 75, init_lr=(1e-4, 1e-3), style=True)),
     "BC2013_GST": (preprocess("BC2013"), model(gst=True), train("BC2013_GST", 75, init_lr=(1e-4, 1e-3), style=True)),
 }
 SETS["LJSpeech"][0]["path"]["preprocessed_path"] = "./preprocessed_data/LJSpeech"
+SETS["LJSpeech_paper"][0]["path"]["raw_path"] = "./raw_data/LJSpeech"  # shares LJSpeech's aligned corpus
 
 if __name__ == "__main__":
     for name, trip in SETS.items():
