@@ -4,7 +4,7 @@
 Same measurement as the ``synth_rtf`` field of ``bench.py`` (FastSpeech2 + style
 encoder on a reference mel + HiFi-GAN V1, int16 on the device, batch 256 per
 GPU; see ``speakingstyle_amd/benchmark.py``), without the training phase -- for
-profiling the inference path (``tools/gpu_prof_synth.sh``).  ``--gpus N`` starts
+profiling the inference path (``tools/gpu.sh synthprof``).  ``--gpus N`` starts
 N independent-shard ranks like bench.py.  Prints one JSON line; lower is better.
 """
 from __future__ import annotations

@@ -68,6 +68,25 @@ static __device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, 
   return uniform01(seed, idx) >= p ? 1.f / (1.f - p) : 0.f;
 }
 
+// BatchNorm activations (k_bn.hip forward / backward and the GEMM epilogue that starts the PostNet
+// BatchNorm backward, k_gemm.hip): act 0 none, 1 tanh (PostNet), 2 ReLU (GST Conv2d stack)
+static __device__ __forceinline__ float bn_fast_tanh(float z) {
+  // 1 - 2/(exp(2z)+1): one exp + one rcp; saturates correctly for |z| large
+  const float e = __expf(2.f * z);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);  // v_rcp_f32: no IEEE division sequence
+}
+static __device__ __forceinline__ float bn_act_fwd(int act, float z) {
+  if (act == 1) return bn_fast_tanh(z);
+  if (act == 2) return fmaxf(z, 0.f);
+  return z;
+}
+// derivative of act at the pre-activation z
+static __device__ __forceinline__ float bn_act_grad(int act, float z) {
+  if (act == 1) { const float t = bn_fast_tanh(z); return 1.f - t * t; }
+  if (act == 2) return z > 0.f ? 1.f : 0.f;
+  return 1.f;
+}
+
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Allow > 64 KiB of dynamic LDS for a kernel (gfx950: 160 KiB per CU).  Once per kernel.

@@ -18,24 +18,8 @@ namespace {
 constexpr int NT = 256;
 constexpr int BN_U = 4;  // rows per thread and load batch in the streaming kernels
 
-__device__ __forceinline__ float fast_tanh(float z) {
-  // 1 - 2/(exp(2z)+1): one exp + one rcp; saturates correctly for |z| large
-  const float e = __expf(2.f * z);
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);  // v_rcp_f32: no IEEE division sequence
-}
-
-// act: 0 none, 1 tanh (PostNet), 2 ReLU (GST Conv2d stack)
-__device__ __forceinline__ float act_fwd(int act, float z) {
-  if (act == 1) return fast_tanh(z);
-  if (act == 2) return fmaxf(z, 0.f);
-  return z;
-}
-// derivative of act at the pre-activation z
-__device__ __forceinline__ float act_grad(int act, float z) {
-  if (act == 1) { const float t = fast_tanh(z); return 1.f - t * t; }
-  if (act == 2) return z > 0.f ? 1.f : 0.f;
-  return 1.f;
-}
+__device__ __forceinline__ float act_fwd(int act, float z) { return bn_act_fwd(act, z); }
+__device__ __forceinline__ float act_grad(int act, float z) { return bn_act_grad(act, z); }
 
 struct RowMap {
   int chunks;      // C / 8
@@ -334,6 +318,60 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
   }
 }
 
+// dh = k1 * dz + k2 * h + k3 from dz that the producing data-gradient GEMM already formed (dy * keep *
+// act'), k_gemm.hip EpiX.bn_*: a pure two-read / one-write stream (no dropout hash, no tanh here)
+__global__ void __launch_bounds__(NT) bn_bwd_apply_dz_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ h,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ stats,
+                                                             const float* __restrict__ dbeta,
+                                                             const float* __restrict__ dgamma, bf16_t* __restrict__ dh,
+                                                             long R, int C, int training) {
+  const RowMap m = rowmap(C);
+  const int c8 = threadIdx.x % m.chunks, ro = threadIdx.x / m.chunks;
+  if (ro >= m.rows_iter) return;
+  const int c0 = c8 * 8;
+  const float invR = 1.f / (float)R;
+  float k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    const float mean = stats[c], rs = stats[C + c];
+    if (training) {
+      const float gr = gamma[c] * rs;
+      k1[i] = gr;
+      k2[i] = -gr * rs * dgamma[c] * invR;
+      k3[i] = -gr * dbeta[c] * invR - k2[i] * mean;
+    } else {
+      k1[i] = stats[2 * C + c];
+      k2[i] = 0.f;
+      k3[i] = 0.f;
+    }
+  }
+  constexpr int U = 8;  // rows per thread and load batch: 16 loads of 16 B in flight per lane
+  const long stride = (long)gridDim.x * m.rows_iter;
+  for (long r0 = (long)blockIdx.x * m.rows_iter + ro; r0 < R; r0 += U * stride) {
+    short8 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = r0 + u * stride;
+      if (r < R) {
+        a[u] = __builtin_nontemporal_load(reinterpret_cast<const short8*>(dz + r * C + c0));
+        b[u] = *reinterpret_cast<const short8*>(h + r * C + c0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long r = r0 + u * stride;
+      if (r >= R) break;
+      short8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        o[i] = (short)f2bf(k1[i] * bf2f((bf16_t)a[u][i]) + k2[i] * bf2f((bf16_t)b[u][i]) + k3[i]);
+      *reinterpret_cast<short8*>(dh + r * C + c0) = o;
+    }
+  }
+}
+
 }  // namespace
 
 static int blocks_for(long R) {
@@ -398,5 +436,28 @@ SSAMD_API int ssamd_bn_bwd(const void* dy, int dy_f32, const bf16_t* h, const fl
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(g), dim3(NT), 0, s, dy, h, gamma, scale, shift, mean, rstd,
                        dbeta, dgamma, dh, R, C, act_tanh, p, (uint64_t)seed, training);
+  return (int)hipGetLastError();
+}
+
+// Second half of the BatchNorm backward when the data-gradient GEMM produced dz and the column partials
+// (ssamd_conv_gemm_bnbwd): fixed-order combine of the nparts per-tile partials -> dbeta / dgamma, then
+// dh = k1 * dz + k2 * h + k3.  stats = [mean | rstd | scale | shift] x C (the forward's).
+SSAMD_API int ssamd_bn_bwd_dz(const bf16_t* dz, const bf16_t* h, const float* gamma, const float* stats,
+                              const float* part, int nparts, bf16_t* dh, float* dgamma, float* dbeta, long R, int C,
+                              int training, hipStream_t s) {
+  if (C % 8 || C / 8 > NT) return -2;
+  if (R == 0) {
+    hipMemsetAsync(dgamma, 0, C * 4, s);
+    hipMemsetAsync(dbeta, 0, C * 4, s);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, s, part, part + (long)nparts * C, nparts,
+                     C, dbeta, dgamma);
+  const RowMap m = {C / 8, NT / (C / 8)};
+  // one row batch (8 rows per thread) per block and pass: >= 2048 blocks keep every CU streaming
+  const long per = (long)m.rows_iter * 8;
+  const int g = (int)max(1L, min((R + per - 1) / per, 8192L));
+  hipLaunchKernelGGL(bn_bwd_apply_dz_kernel, dim3(g), dim3(NT), 0, s, dz, h, gamma, stats, dbeta, dgamma, dh, R, C,
+                     training);
   return (int)hipGetLastError();
 }

@@ -102,6 +102,18 @@ struct EpiX {
   // bf16 aux operand (16x fewer bytes for the FFN hidden layer's dgrad)
   unsigned char* mask_out;
   const unsigned char* mask_in;
+  // BatchNorm backward head (PostNet; big64 LDS-staged epilogue, bf16 out, ldy == N): the GEMM output is
+  // dy = dL/d(BN-act-dropout output) of the layer whose pre-BN input is bn_h [M][N]; the epilogue stores
+  //   dz = dy * keep(seed, p) * act'(bn_h * scale + shift)
+  // instead of dy and writes the tile's column partials  sum_rows dz  and  sum_rows dz * (bn_h - mean) * rstd
+  // to bn_part[tm][N] and bn_part[nM + tm][N] (tm = M tile; fixed order, no atomics).  bn_stats = the
+  // forward's [mean | rstd | scale | shift] x N.  The partial sums replace k_bn.hip's bn_bwd_reduce pass
+  // (a full re-read of dy and bn_h); the dropout mask and act' are bit-identical to it.
+  const bf16_t* bn_h;
+  const float* bn_stats;
+  float* bn_part;
+  int bn_act;
+  float bn_p;
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -807,7 +819,8 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false>
+// PH4 (BUF only): the 4-phase main loop -- see the comment at its loop below.
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool PH4 = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
@@ -945,6 +958,124 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     nk = min(nk_all, kt0 + per);
     Yv = reinterpret_cast<float*>(Yv) + (long)blockIdx.y * g.M * ldy;
   }
+  if constexpr (PH4) {
+    // 4-phase main loop (MI355X: keeps LDS-DMA in flight across barriers, never drains to 0 in steady
+    // state).  A k-tile (256 x 64 of A and of B, 64 KiB) is staged as four 16-KiB UNITS, each the rows
+    // one output quadrant-phase reads:  U0 = A rows of quadrant qa = 0 (both wave rows), U1 = B rows of
+    // qb = 1, U2 = A rows of qa = 1, U3 = B rows of qb = 0.  Phase p of tile t computes quadrant
+    // (qa, qb) = (0,0) (0,1) (1,1) (1,0) -- 16 MFMAs per wave -- and restages the unit its predecessor
+    // phase finished reading, for tile t + 2 into the same buffer (U3 of tile t + 1 in phase 0):
+    //   phase 0: U3(t+1) -> buf^1 | read A(qa0) B(qb0) | MFMA (0,0)
+    //   phase 1: U0(t+2) -> buf   | read B(qb1)        | MFMA (0,1)
+    //   phase 2: U1(t+2) -> buf   | read A(qa1)        | MFMA (1,1)
+    //   phase 3: U2(t+2) -> buf   | (B(qb0) from regs) | MFMA (1,0) | vmcnt(6): tile t+1 landed
+    // Every phase ends with a barrier (WAR: a unit is restaged one phase after its last read, which
+    // retired before the barrier); RAW: tile t+1's last unit was issued in phase 0 of tile t, so the
+    // counted vmcnt(6) in phase 3 (the 3 units issued after it stay in flight) + the barrier order it
+    // before phase 0 of tile t+1.  Two units per wave-thread: 2 LDS-DMA instructions per phase.
+    int bblk[4], bvo2[4];  // B 8-row blocks of this wave: U3 (qb = 0) -> [0], [1]; U1 (qb = 1) -> [2], [3]
+    bblk[0] = 8 * (wave >> 2) + (wave & 3);
+    bblk[1] = bblk[0] + 16;
+    bblk[2] = bblk[0] + 4;
+    bblk[3] = bblk[1] + 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = bblk[u] * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      bvo2[u] = (n0 + row < g.N) ? ((n0 + row) * g.K + ch * 8) * 2 : kOOB;
+    }
+    // A 8-row blocks: load i covers block i * 8 + wave (rows 64 i + 8 wave ..): U0 = i in {0, 2}, U2 = {1, 3}
+    auto stage_a = [&](int kt, int q, int buf) {
+      char* As = smem + buf * STG64_BYTES;
+      const int k0 = kt * 64;
+      const int tap = k0 / g.Cin;
+      const int cin0 = k0 - tap * g.Cin;
+      const int shift = tap * g.dil - g.pad;
+      const int aoff = (shift * g.Cin + cin0) * 2;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int i = q + 2 * jj;
+        const int ts = a_t[i] + shift;
+        const bool ok = (unsigned)ts < (unsigned)a_lim[i];
+        buf_lds16(rA, ok ? avo[i] + aoff : kOOB, 0, As + (i * 8 + wave) * 1024);
+      }
+    };
+    auto stage_b = [&](int kt, int q, int buf) {  // q = 0: U3 (qb = 0 rows), q = 1: U1 (qb = 1 rows)
+      char* Bs = smem + buf * STG64_BYTES + BG * 64 * 2;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) buf_lds16(rB, bvo2[q * 2 + jj], kt * 128, Bs + bblk[q * 2 + jj] * 1024);
+    };
+    const int nkt = nk - kt0;
+    if (nkt > 0) {
+      stage_a(kt0, 0, 0); stage_b(kt0, 1, 0); stage_a(kt0, 1, 0); stage_b(kt0, 0, 0);
+    }
+    if (nkt > 1) {
+      stage_a(kt0 + 1, 0, 1); stage_b(kt0 + 1, 1, 1); stage_a(kt0 + 1, 1, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    short8 fa[2][4], fb0[2][2], fb1[2][2];
+    auto read_a = [&](const char* As, int qa) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          fa[kk][i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + qa * 64 + i * 16 + (lane & 15), c));
+      }
+    };
+    auto read_b = [&](const char* Bs, int qb, short8 (&fb)[2][2]) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          fb[kk][j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + qb * 32 + j * 16 + (lane & 15), c));
+      }
+    };
+    auto mma = [&](int qa, int qb, const short8 (&fb)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qa * 4 + i][qb * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    for (int t = 0; t < nkt; ++t) {
+      const int buf = t & 1, kt = kt0 + t;
+      const char* As = smem + buf * STG64_BYTES;
+      const char* Bs = As + BG * 64 * 2;
+      const bool n1 = t + 1 < nkt, n2 = t + 2 < nkt;
+      // phase 0
+      if (n1) stage_b(kt + 1, 0, buf ^ 1);
+      read_a(As, 0);
+      read_b(Bs, 0, fb0);
+      mma(0, 0, fb0);
+      pp_barrier();
+      // phase 1
+      if (n2) stage_a(kt + 2, 0, buf);
+      read_b(Bs, 1, fb1);
+      mma(0, 1, fb1);
+      pp_barrier();
+      // phase 2
+      if (n2) stage_b(kt + 2, 1, buf);
+      read_a(As, 1);
+      mma(1, 1, fb1);
+      pp_barrier();
+      // phase 3
+      if (n2) stage_a(kt + 2, 1, buf);
+      mma(1, 0, fb0);
+      if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+    }
+  } else {
   // double buffer: stage kt+1 is DMA'd while stage kt is computed (one stage = 1024 MFMA cycles
   // per wave, far longer than an L2-warm LDS-DMA), one barrier per 64-wide k slab
   if (kt0 < nk) stage(kt0, 0);
@@ -971,6 +1102,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
+  }  // !PH4
   if constexpr (!OUT_F32) {
     if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
       // LDS-staged epilogue: the accumulator layout gives each lane 4 columns of one row, i.e.
@@ -1097,7 +1229,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         }
         return;
       }
-      const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_in;
+      const bool bnb = ex.bn_h != nullptr;
+      const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_in || bnb;
       // Thread (c = tid & 31, r0 = tid >> 5) owns the 16-B column chunk c of rows r0 + 16 it.  The
       // global operands of EPG rows (aux / residual / accumulator segments, mask bytes, sequence
       // lengths) are all loaded before any is used: one loop iteration per row would expose a full
@@ -1108,7 +1241,21 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       const int c = tid & 31, r0 = tid >> 5;
       const int n = n0 + c * 8;
       const bool col_ok = n < g.N;
-      const bool loads = aux || resid || ex.acc || ex.mask_in || lens;
+      const bool loads = aux || resid || ex.acc || ex.mask_in || lens || bnb;
+      // BatchNorm-backward head: per-thread column constants and running column partials (8 columns)
+      float bmu[8], brs[8], bsc[8], bsh[8], bs1[8], bs2[8];
+      if (bnb) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int nq = col_ok ? n + q : 0;
+          bmu[q] = ex.bn_stats[nq];
+          brs[q] = ex.bn_stats[g.N + nq];
+          bsc[q] = ex.bn_stats[2 * g.N + nq];
+          bsh[q] = ex.bn_stats[3 * g.N + nq];
+          bs1[q] = 0.f;
+          bs2[q] = 0.f;
+        }
+      }
       if (!loads && !xon) {  // store-only epilogue (+ the ReLU bitmask): the plain row loop
         for (int e = tid; e < BG * 32; e += NT3) {
           const int r = e >> 5, cc = e & 31;
@@ -1139,6 +1286,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             if (in && aux) va[u] = *reinterpret_cast<const short8*>(aux + off);
             if (in && resid) vr[u] = *reinterpret_cast<const short8*>(resid + off);
             if (in && ex.acc) vc[u] = *reinterpret_cast<const short8*>(ex.acc + off);
+            if (in && bnb) va[u] = *reinterpret_cast<const short8*>(ex.bn_h + off);
             mb[u] = (in && ex.mask_in) ? (unsigned)ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : 0xffu;
             vv[u] = true;
             if (in && lens) {
@@ -1181,6 +1329,19 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 #pragma unroll
               for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)vc[u][q]);
             }
+            if (bnb) {
+              float ks[8];
+              drop_scales<8>(ex.seed, (uint64_t)off, ex.bn_p, ks);
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const float hv = bf2f((bf16_t)va[u][q]);
+                float d = f[q] * ks[q];
+                if (ex.bn_act) d *= bn_act_grad(ex.bn_act, hv * bsc[q] + bsh[q]);
+                f[q] = d;
+                bs1[q] += d;
+                bs2[q] += d * (hv - bmu[q]) * brs[q];
+              }
+            }
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] = valid ? f[q] * ex.scale : 0.f;
             if (ex.y2) {
@@ -1197,6 +1358,24 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             for (int q = 0; q < 8; ++q) v[q] = (short)f2bf(f[q]);
           }
           *reinterpret_cast<short8*>(Y + off) = v;
+        }
+      }
+      if (bnb) {
+        // column partials of the tile: the 16 threads of a column chunk (r0 = 0..15) in fixed order
+        __syncthreads();  // every Ct read is done: reuse the staging LDS
+        float* red = reinterpret_cast<float*>(smem);  // [2][16][256]
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          red[r0 * 256 + c * 8 + q] = bs1[q];
+          red[4096 + r0 * 256 + c * 8 + q] = bs2[q];
+        }
+        __syncthreads();
+        const int which = tid >> 8, col = tid & 255;  // threads 0..255: sum dz, 256..511: sum dz*xhat
+        if (n0 + col < g.N) {
+          float a = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) a += red[which * 4096 + r * 256 + col];
+          ex.bn_part[((long)which * nM + tm) * g.N + n0 + col] = a;
         }
       }
       return;
@@ -2264,6 +2443,8 @@ SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 static int g_gemm_buf = 1;  // big64 (FASTK) LDS-DMA through buffer descriptors (0: flat global_load_lds)
 SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
+static int g_gemm_ph4 = 0;  // big64 buffer-descriptor path: 1 = the 4-phase unit-staged main loop
+SSAMD_API void ssamd_gemm_set_ph4(int v) { g_gemm_ph4 = v; }
 
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
 static bool big64_buf_ok(const ConvGeom& g) {
@@ -2318,7 +2499,8 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   {
     const int tiles = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
     const int nk64 = (g.K + 63) / 64;
-    const bool plain = !(ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.ln_out || ex.mask_out || ex.mask_in);
+    const bool plain = !(ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.ln_out || ex.mask_out || ex.mask_in ||
+                         ex.bn_h);
     int S = 0;
     if (g_splitk > 0) S = g_splitk;
     else if (g_splitk < 0 && g_gemm_variant < 0 && tiles <= 128 && nk64 >= 16)
@@ -2364,6 +2546,12 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     if (N >= 256) variant = 4;
     else if (variant != 2) return -3;
   }
+  if (ex.bn_h) {  // BatchNorm-backward head: big64 LDS-staged epilogue, bf16 dz, whole-N partial rows
+    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act != 0 || aux || resid || lens || ex.ln_out || xon ||
+        ex.mask_out || ex.mask_in || !ex.bn_stats || !ex.bn_part)
+      return -3;
+    variant = 4;
+  }
   if (ex.ln_out) {  // the LayerNorm tail needs whole rows in one tile and the plain bf16 store
     if (xon || N != 256 || ldy != 256 || out_f32 || !reg || act != 0 || aux || resid || lens) return -3;
     variant = 4;
@@ -2383,6 +2571,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, false, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, false, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, true, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -2391,6 +2583,11 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
+      if constexpr (BF) {                                                                                \
+        if (g_gemm_ph4)                                                                                  \
+          kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, true, true>                              \
+                        : conv_gemm_big64_kernel<F32, FK, false, true, true>;                            \
+      }                                                                                                  \
       hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
     const bool bf = fastk && big64_buf_ok(g);
@@ -2484,6 +2681,23 @@ SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* 
   return conv_gemm_impl(X, W, bias, nullptr, resid, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, nullptr, ex, s);
 }
 
+// Data gradient of a conv whose input came out of BatchNorm (+act, dropout): Y = dz (see EpiX.bn_*) and the
+// per-M-tile column partials bn_part [2][ceil(M/256)][N] of dz and dz * xhat.
+SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, int B, int L, int Cin, int ks, int dil,
+                                    int pad, int N, const bf16_t* bn_h, const float* bn_stats, float* bn_part,
+                                    int bn_act, float p, unsigned long long seed, hipStream_t s) {
+  if (!bn_h) return -2;
+  EpiX ex{};
+  ex.scale = 1.f;
+  ex.bn_h = bn_h;
+  ex.bn_stats = bn_stats;
+  ex.bn_part = bn_part;
+  ex.bn_act = bn_act;
+  ex.bn_p = p;
+  ex.seed = seed;
+  return conv_gemm_impl(X, W, nullptr, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, nullptr, ex, s);
+}
+
 // conv_gemm with a ReLU bitmask: mask_out (act must be ReLU) stores bit (y > 0) per output element,
 // mask_in zeroes the outputs whose bit is clear (the dgrad of a ReLU layer).  [M][N/8] bytes.
 SSAMD_API int ssamd_conv_gemm_mask(const bf16_t* X, const bf16_t* W, const float* bias, void* Y, int B, int L,
@@ -2567,8 +2781,12 @@ static int device_cus() {
 static int g_wgrad_blocks = 0;   // > 0: fixed split-M target (blocks per launch) instead of the cost model
 // > 0: plan the split-M rounds for this many CUs instead of the device's (a weight gradient on the side
 // stream then leaves the other CUs to the data-gradient chain instead of holding every CU's LDS)
+// The budget applies to launches on ONE stream (the weight-gradient side stream): a main-stream weight
+// gradient (first step, --no-side-wgrad) keeps the whole-device plan, so the split-M count -- and with it
+// the fp32 reduction order -- of a main-stream launch does not depend on the side-stream setting.
 static int g_wgrad_cus = 0;
-static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits) {
+static hipStream_t g_wgrad_cus_stream = nullptr;
+static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits, int cus) {
   const int steps_all = (M + 63) / 64;
   int smax = max_splits;
   if (smax > steps_all / 4) smax = steps_all / 4 > 0 ? steps_all / 4 : 1;  // >= 4 row steps per split
@@ -2578,7 +2796,6 @@ static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits)
     const int sp = (g_wgrad_blocks + tiles - 1) / tiles;
     return sp < smax ? sp : smax;
   }
-  const int cus = g_wgrad_cus > 0 ? g_wgrad_cus : device_cus();
   int best = 1;
   double best_c = 1e30;
   for (int sp = 1; sp <= smax; ++sp) {
@@ -2592,7 +2809,10 @@ static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits)
 
 static int g_wgrad_variant = -1;  // -1 auto (256x256 BK=64 when it applies), 0: force the 128x128 kernels
 SSAMD_API void ssamd_wgrad_set_blocks(int b) { g_wgrad_blocks = b > 0 ? b : 0; }
-SSAMD_API void ssamd_wgrad_set_cus(int n) { g_wgrad_cus = n > 0 ? n : 0; }
+SSAMD_API void ssamd_wgrad_set_cus(hipStream_t s, int n) {
+  g_wgrad_cus = n > 0 ? n : 0;
+  g_wgrad_cus_stream = s;
+}
 SSAMD_API void ssamd_wgrad_set_variant(int v) { g_wgrad_variant = v; }
 
 SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, long ws_floats, float* dW, float* db,
@@ -2631,7 +2851,8 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
       b64_set = true;
     }
     const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
-    int splits = choose_wgrad_splits(tiles, g.M, max_splits, ws_floats / (slab + N));
+    const int cus = (g_wgrad_cus > 0 && s == g_wgrad_cus_stream) ? g_wgrad_cus : device_cus();
+    int splits = choose_wgrad_splits(tiles, g.M, max_splits, ws_floats / (slab + N), cus);
     if (splits < 1) return -3;
     int rows_per_split = (g.M + splits - 1) / splits;
     rows_per_split = (rows_per_split + 63) / 64 * 64;

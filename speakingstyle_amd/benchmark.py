@@ -115,10 +115,6 @@ def train_phase(args, rank, world, device):
     trainer = Trainer(model, (pp, mc, tc), seed=1234)
     # the step's main chain on a high-priority stream, weight gradients on the normal-priority side stream
     trainer.use_priority_stream(cuda and not getattr(args, "normal_priority", False))
-    if cuda and os.environ.get("SSAMD_WGRAD_CUS"):  # experiment: weight-gradient split plan for fewer CUs
-        from .ops import hip
-
-        hip.lib().ssamd_wgrad_set_cus(int(os.environ["SSAMD_WGRAD_CUS"]))
     trainer.timer.enabled = bool(getattr(args, "phase_times", False)) or trainer.timer.enabled
 
     if getattr(args, "force_buckets", False) and world == 1 and cuda:
@@ -142,7 +138,9 @@ def train_phase(args, rank, world, device):
     # largest padded batch first: the first warm-up step sizes the allocator for all others
     pool.sort(key=lambda e: -(len(e[0][0]) * e[0][8]))
 
-    fail_rank = os.environ.get("SSAMD_FAIL_RANK")  # fault injection (launcher failure-path test)
+    from . import experimental
+
+    fail_rank = experimental.get("fail_rank")  # fault injection (launcher failure-path test)
 
     def step(i):
         if fail_rank is not None and int(fail_rank) == rank and i == 1:
@@ -164,8 +162,8 @@ def train_phase(args, rank, world, device):
     t0 = time.perf_counter()
     frames = 0
     host = 0.0  # time inside train_step (enqueue): ~= elapsed when the step is host-bound
-    # SSAMD_HOST_LEAD=1: per step, how far the host's enqueue ran ahead of the GPU finishing the step
-    lead = cuda and os.environ.get("SSAMD_HOST_LEAD") == "1"
+    # diagnostics: per step, how far the host's enqueue ran ahead of the GPU finishing the step
+    lead = cuda and experimental.get("host_lead")
     if lead:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev0.record()

@@ -113,6 +113,8 @@ _TRAIN_DEFAULTS: Config = {
         # run backward on the calling thread (no autograd device worker thread): less host time per step
         "backward_same_thread": True,
         # (non-finite steps are always skipped on the device by the fused clip+Adam kernel: no knob)
+        # validated experiment / diagnostic switches (speakingstyle_amd/experimental.py); empty = production
+        "experimental": {},
     },
 }
 

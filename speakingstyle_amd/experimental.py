@@ -1,0 +1,137 @@
+"""The one place experiment / diagnostic switches are read.
+
+A plain run -- no ``SSAMD_EXPERIMENTAL`` in the environment, no ``mi355x.experimental`` block in
+train.yaml -- takes the measured production path of every switch below and nothing else.  Setting
+one is an explicit, validated act: unknown names and values that do not parse raise, instead of
+silently selecting a default (or an untested path).
+
+    SSAMD_EXPERIMENTAL="wgrad_first=1,ln_fuse=1" python bench.py ...
+
+``mi355x.experimental: {wgrad_first: "0"}`` in train.yaml does the same for ``train.py`` (the trainer
+calls ``configure`` with it; the environment wins on conflicts).
+
+Kernel-internal variant setters of the HIP library (``ssamd_*_set_*`` in ``ops/hip.py:_SIGS``) are
+not switches of the framework: only the GPU tests (to cover every variant against fp32) and the
+``tools/exp_*.py`` experiments call them; no product code path does.
+
+Infrastructure variables that are not experiments stay plain environment variables and are
+documented where they are read: ``SSAMD_BACKEND`` (hip / reference op backend), ``SSAMD_KERNEL_LIB``
+(A/B of a second kernel-library build), ``SSAMD_ALLOW_TORCH_FALLBACK``, ``SSAMD_DIST_BACKEND``,
+``SSAMD_DIST_TIMEOUT_S``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, Optional
+
+# name -> (default, parser, help)
+_BOOL = {"0": False, "1": True, "false": False, "true": True, "off": False, "on": True}
+
+
+def _bool(v):
+    if isinstance(v, bool):
+        return v
+    s = str(v).strip().lower()
+    if s not in _BOOL:
+        raise ValueError(f"expected 0/1, got {v!r}")
+    return _BOOL[s]
+
+
+def _tristate(v):
+    s = str(v).strip().lower()
+    if s not in ("0", "1", "auto"):
+        raise ValueError(f"expected 0 / 1 / auto, got {v!r}")
+    return s
+
+
+def _pos_int(v):
+    i = int(v)
+    if i <= 0:
+        raise ValueError(f"expected a positive integer, got {v!r}")
+    return i
+
+
+def _frac(v):
+    f = float(v)
+    if not 0.0 < f <= 1.0:
+        raise ValueError(f"expected a fraction in (0, 1], got {v!r}")
+    return f
+
+
+KNOBS: Dict[str, tuple] = {
+    # -- compute-path experiments (A/B of measured production choices)
+    "wgrad_first": ("auto", _tristate,
+                    "issue a layer's weight gradient (side stream) before its data gradient: 0 never, 1 always, "
+                    "auto when the data-gradient GEMMs have fewer row tiles than wgrad_first_waves x CUs"),
+    "wgrad_first_waves": (1.25, float, "auto threshold of wgrad_first, in waves of 256-row tiles per CU"),
+    "wgrad_cu_frac": (0.75, _frac, "fraction of the CUs the side-stream weight-gradient split plan is sized for"),
+    "ln_fuse": (False, _bool, "residual + LayerNorm tail in the producing GEMM's epilogue (measured slower)"),
+    "hifigan_hip_train": (True, _bool, "HiFi-GAN generator training on the HIP implicit-GEMM convs"),
+    # -- diagnostics (instrumentation only; no effect on what is computed)
+    "phase_timing": (False, _bool, "per-phase host/device step times (Perf/phase_* scalars)"),
+    "host_tail": (False, _bool, "host timestamps of the step tail (backward return .. optimizer launch)"),
+    "host_lead": (False, _bool, "bench: how far the host enqueue runs ahead of the GPU per step"),
+    "fail_rank": (None, int, "fault injection: this rank raises in its second timed bench step"),
+}
+
+_values: Dict[str, Any] = {}
+_parsed = [False]
+
+
+def _parse_env() -> Dict[str, Any]:
+    raw = os.environ.get("SSAMD_EXPERIMENTAL", "").strip()
+    out = {}
+    if not raw:
+        return out
+    for item in raw.split(","):
+        item = item.strip()
+        if not item:
+            continue
+        if "=" not in item:
+            raise ValueError(f"SSAMD_EXPERIMENTAL: '{item}' is not name=value")
+        k, v = (x.strip() for x in item.split("=", 1))
+        out[k] = v
+    return out
+
+
+def _set(name: str, value, source: str):
+    if name not in KNOBS:
+        raise KeyError(f"{source}: unknown experimental switch '{name}' (known: {', '.join(sorted(KNOBS))})")
+    try:
+        _values[name] = KNOBS[name][1](value)
+    except (TypeError, ValueError) as e:
+        raise ValueError(f"{source}: {name}={value!r}: {e}") from None
+
+
+def _ensure():
+    if not _parsed[0]:
+        for k, v in _parse_env().items():
+            _set(k, v, "SSAMD_EXPERIMENTAL")
+        _parsed[0] = True
+
+
+def configure(block: Optional[dict]):
+    """Apply a train.yaml ``mi355x.experimental`` block (the environment keeps precedence)."""
+    _ensure()
+    env = _parse_env()
+    for k, v in (block or {}).items():
+        if k not in env:
+            _set(k, v, "mi355x.experimental")
+
+
+def get(name: str):
+    _ensure()
+    if name not in KNOBS:
+        raise KeyError(name)
+    return _values.get(name, KNOBS[name][0])
+
+
+def overridden() -> Dict[str, Any]:
+    """Switches set away from their defaults (recorded in bench output / logs)."""
+    _ensure()
+    return {k: v for k, v in _values.items() if v != KNOBS[k][0]}
+
+
+def reset_for_tests():
+    _values.clear()
+    _parsed[0] = False

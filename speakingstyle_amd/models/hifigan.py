@@ -79,7 +79,10 @@ def _wn(conv):
 
 
 # generator training on the HIP implicit-GEMM convs (channel-last); 0: torch / MIOpen NCL convs
-_HIP_TRAIN = os.environ.get("SSAMD_HIFIGAN_HIP_TRAIN", "1") != "0"
+def _hip_train() -> bool:
+    from .. import experimental
+
+    return experimental.get("hifigan_hip_train")
 
 
 class ResBlock1(nn.Module):
@@ -190,7 +193,7 @@ class Generator(nn.Module):
 
     # ------------------------------------------------------------------ training (NCL)
     def forward(self, x):
-        if _HIP_TRAIN and x.is_cuda and ops.use_hip(x) and self._hip_train_ok():
+        if x.is_cuda and _hip_train() and ops.use_hip(x) and self._hip_train_ok():
             return self._forward_hip_train(x)
         x = self.conv_pre(x)
         for i in range(self.num_upsamples):

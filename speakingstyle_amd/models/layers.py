@@ -156,9 +156,11 @@ class PostNet(nn.Module):
         self.dropout = 0.5  # hard-coded in the reference (Layers.py:140-148)
 
     def forward(self, x):
-        h = x
+        # conv_0, then [BN_i + tanh + dropout -> conv_{i+1}] links (the data gradient of conv_{i+1} starts
+        # BN_i's backward in its GEMM epilogue on the GPU), then the last BN (fp32 out)
         last = len(self.convolutions) - 1
-        for i, seq in enumerate(self.convolutions):
-            conv, bn = seq[0], seq[1]
-            h = ops.bn_act(conv(h), bn, self.training, act_tanh=i < last, p=self.dropout, out_f32=i == last)
-        return h
+        h = self.convolutions[0][0](x)
+        for i in range(last):
+            bn, nxt = self.convolutions[i][1], self.convolutions[i + 1][0]
+            h = ops.bn_act_conv(h, bn, self.training, True, self.dropout, nxt.conv.weight, nxt.conv.bias, nxt.pad)
+        return ops.bn_act(h, self.convolutions[last][1], self.training, act_tanh=False, p=self.dropout, out_f32=True)

@@ -224,6 +224,14 @@ def predictor_head(h, w, b, lengths=None):
     return out if lengths is None else out.masked_fill(ref.lengths_to_mask(lengths, out.shape[1]), 0.0)
 
 
+def bn_act_conv(h, bn, training, act_tanh, p, w, b, pad):
+    """conv(drop(act(BN(h)))): one PostNet link.  On the GPU the conv's data-gradient GEMM starts the
+    BatchNorm backward in its epilogue (``hip._BNActConvFn``); elsewhere bn_act followed by conv1d."""
+    if use_hip(h) and _hip().bn_act_conv_ok(h.shape[-1], w):
+        return _hip().bn_act_conv(h, bn, training, act_tanh, p, w, b, pad)
+    return conv1d(bn_act(h, bn, training, act_tanh, p), w, b, pad)
+
+
 def bn_act(h, bn, training, act_tanh, p, out_f32=False):
     """PostNet stage: BatchNorm1d (batch stats over all B*L rows) -> [tanh] -> dropout.
     ``act_tanh="relu"`` applies ReLU instead (GST BatchNorm2d over NHWC rows)."""

@@ -48,6 +48,7 @@ _SIGS = {
     "ssamd_gemm_set_ngrp": [I],
     "ssamd_wgrad_set_buf": [I],
     "ssamd_gemm_set_buf": [I],
+    "ssamd_gemm_set_ph4": [I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],
@@ -55,7 +56,7 @@ _SIGS = {
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],
     "ssamd_wgrad_set_blocks": [I],
-    "ssamd_wgrad_set_cus": [I],
+    "ssamd_wgrad_set_cus": [P, I],
     "ssamd_head_fwd": [P, P, P, P, L_, I, I, P, P],
     "ssamd_head_bwd": [P, P, P, P, L_, I, I, P, P, P, P, L_, P],
     "ssamd_head_bwd_ws": [L_, I],
@@ -123,6 +124,21 @@ def _load_fast(handle):
     spec = importlib.util.spec_from_file_location("ssamd_fast", _FAST_PATH)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    # built from the current signature table? (an edited _SIGS entry without a rebuild would convert
+    # arguments with the old types)
+    import sys
+
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "csrc")
+    if csrc not in sys.path:
+        sys.path.insert(0, csrc)
+    import gen_fastcall
+
+    if getattr(mod, "sig_hash", None) != gen_fastcall.sig_hash(_SIGS, _RESTYPES):
+        import warnings
+
+        warnings.warn(f"{_FAST_PATH} was generated from a different signature table (rebuild with "
+                      "`python csrc/build.py`); using ctypes bindings")
+        return None
     # one mapping of the kernel library (one set of its globals: workspaces, LDS opt-ins, variant state)
     mine = ctypes.cast(getattr(handle, mod.entry_name), ctypes.c_void_p).value
     if mod._entry_addr() != mine:
@@ -202,8 +218,7 @@ _FALLBACK_OK = os.environ.get("SSAMD_ALLOW_TORCH_FALLBACK") == "1"
 # LayerNorm tails in the producing GEMM's epilogue (ssamd_conv_gemm_ln) are opt-in: measured on MI355X
 # (tools/exp_ln.py, 100k rows, profiles/README.md r2) the fused epilogue of the one-block-per-CU 256x256
 # GEMM costs more (+62 us at K=256) than the separate, fully occupied addln kernel (+31 us): the epilogue
-# does not overlap any MFMA work.  SSAMD_LN_FUSE=1 enables it.
-_NO_LN_FUSE = os.environ.get("SSAMD_LN_FUSE") != "1"
+# does not overlap any MFMA work.  Experiment switch ``ln_fuse`` (speakingstyle_amd/experimental.py).
 _fallback_seen = set()
 
 
@@ -370,18 +385,29 @@ _side_used = {}
 _side_by_handle = {}  # raw handle -> torch Stream (workspace allocation under the side stream)
 _side_keep = {}       # device -> inputs of queued side-stream kernels, released at the join
 # issue a layer's weight gradient (side stream) BEFORE its data gradient (main stream): the side stream
-# then waits only for the operands, not for the data-gradient GEMM too (A/B knob SSAMD_WGRAD_FIRST)
-# (A/B knob SSAMD_WGRAD_FIRST = 0 / 1 / auto).  Measured (profiles/r3_v10_wgrad_first_ab.txt): +0.8 %
-# BC2013 and +1.5 % GST (M ~ 40-50k-row layers whose data-gradient GEMMs leave CUs idle in their
-# last wave), -0.7 % LJSpeech (~110k rows); "auto" (default): first only below _WGRAD_FIRST_ROWS rows --
-# +0.6 % LJSpeech, +0.7 % BC2013, +1.2 % GST vs off, two repetitions each.
-_WGRAD_FIRST = [{"0": 0, "1": 1}.get(os.environ.get("SSAMD_WGRAD_FIRST", "auto"), 2)]
-_WGRAD_FIRST_ROWS = int(os.environ.get("SSAMD_WGRAD_FIRST_ROWS", 80000))
+# then waits only for the operands, not for the data-gradient GEMM too.  It pays when the data-gradient
+# GEMMs leave CUs idle: fewer 256-row tiles than ~1.25 waves of the device's CUs (e.g. 320 tiles = 82k
+# rows on 256 CUs).  Measured (profiles/r3_v10_wgrad_first_ab.txt, as a row threshold of 80k): +0.6 %
+# LJSpeech (~113k rows: not first), +0.7 % BC2013, +1.2 % GST (40-50k rows: first), vs never; always-first
+# -0.7 % on LJSpeech.  Experiment switches ``wgrad_first`` (0 / 1 / auto) and ``wgrad_first_waves``.
+_CUS = {}
+
+
+def _device_cus(dev_index=None) -> int:
+    i = torch.cuda.current_device() if dev_index is None else dev_index
+    n = _CUS.get(i)
+    if n is None:
+        n = _CUS[i] = torch.cuda.get_device_properties(i).multi_processor_count
+    return n
 
 
 def _wgrad_first(rows: int) -> bool:
-    m = _WGRAD_FIRST[0]
-    return m == 1 or (m == 2 and rows < _WGRAD_FIRST_ROWS)
+    from .. import experimental
+
+    m = experimental.get("wgrad_first")
+    if m != "auto":
+        return m == "1"
+    return (rows + 255) // 256 < experimental.get("wgrad_first_waves") * _device_cus()
 
 
 _SIDE_WGRAD = [True]
@@ -390,6 +416,11 @@ _SIDE_LN = [True]  # LayerNorm weight-gradient reductions on the side stream too
 
 def set_wgrad_stream(enabled: bool):
     _SIDE_WGRAD[0] = bool(enabled)
+
+
+def side_stream_handle(device):
+    """Raw handle of the weight-gradient side stream of ``device`` (created on first use)."""
+    return _side_stream(device).cuda_stream
 
 
 def _side_stream(device):
@@ -433,6 +464,20 @@ def wgrad_async(launch, inputs, slots_ok: bool, params=()):
     if len(keep) > 4096:  # a caller that never joins (no optimizer step): bound the held references
         join_side_streams()
     return out
+
+
+def side_stream_for_collective(device):
+    """The side stream, made to wait for the current (compute) stream, when weight-gradient kernels are
+    queued on it since the last join -- else None.  A collective issued with this stream current is
+    ordered after both streams' gradient writes while the compute stream itself does not wait
+    (``parallel/ddp.py::GradBuckets._launch``).  The side stream only gains an order it already had:
+    every later side-stream launch waits for the compute stream anyway (``wgrad_async``)."""
+    idx = device.index
+    if not _side_used.get(idx):
+        return None
+    s = _side[idx]
+    _check(lib().ssamd_stream_wait(s.cuda_stream, _stream()), "ssamd_stream_wait")
+    return s
 
 
 def join_side_streams(defer_release=False):
@@ -537,7 +582,9 @@ _SIGS.update({"ssamd_conv_gemm_ln": [P, P, P, P, I, I, I, I, I, I, I, P, P, P, P
 def ln_spec(residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None, lengths=None,
             eps=1e-5, pack=None):
     """LNSpec for ``add_layernorm(a, residual, ...)`` when its ``a`` comes from a d=256 GEMM, else None."""
-    if _NO_LN_FUSE or residual.dtype != torch.bfloat16 or residual.shape[-1] != 256 or not residual.is_cuda:
+    from .. import experimental
+
+    if not experimental.get("ln_fuse") or residual.dtype != torch.bfloat16 or residual.shape[-1] != 256 or not residual.is_cuda:
         return None
     sp = LNSpec()
     sp.res = residual.contiguous()
@@ -1652,6 +1699,105 @@ class _BNActFn(torch.autograd.Function):
                                 p, seed, _ptr(ws), _stream())
         _check(rc, "ssamd_bn_bwd")
         return dh, dg, db, None, None, None, None, None, None, None, None, None
+
+
+_SIGS.update({
+    "ssamd_conv_gemm_bnbwd": [P, P, P, I, I, I, I, I, I, I, P, P, P, I, F, U64, P],
+    "ssamd_bn_bwd_dz": [P, P, P, P, P, I, P, P, P, L_, I, I, P],
+})
+
+
+class _BNActConvFn(torch.autograd.Function):
+    """h_out = conv(drop(act(BN(h))))  -- one PostNet link (``transformer/Layers.py:140-148``).
+
+    Forward = ``ssamd_bn_fwd`` + the conv GEMM.  Backward: the conv's data-gradient GEMM starts the
+    BatchNorm backward in its epilogue (``ssamd_conv_gemm_bnbwd``: dz = dy * keep * act' and the per-tile
+    column partials of dz and dz * xhat), so the separate BatchNorm reduction pass over dy and h is gone;
+    ``ssamd_bn_bwd_dz`` combines the partials (fixed order) and streams dh = k1 dz + k2 h + k3.  The
+    weight gradient reads the saved BN output y, as a plain conv's would."""
+
+    @staticmethod
+    def forward(ctx, h, gamma, beta, rmean, rvar, w, b, training, momentum, eps, act, p, seed, pad):
+        B, L, C = h.shape
+        R = B * L
+        hc = h.contiguous()
+        _need(hc, torch.bfloat16, "bn_conv.h")
+        dev = h.device
+        stats = torch.empty(4, C, device=dev, dtype=torch.float32)  # mean, rstd, scale, shift
+        y = torch.empty(B, L, C, device=dev, dtype=torch.bfloat16)
+        ws = _bn_ws(dev, R, C)
+        rc = lib().ssamd_bn_fwd(_ptr(hc), _ptr(gamma), _ptr(beta), _ptr(rmean), _ptr(rvar), _ptr(stats[0]),
+                                _ptr(stats[1]), _ptr(stats[2]), _ptr(stats[3]), _ptr(y), 0, R, C, int(training),
+                                float(momentum), float(eps), int(act), float(p), seed, _ptr(ws), _stream())
+        _check(rc, "ssamd_bn_fwd")
+        ks = w.shape[2]
+        N = w.shape[0]
+        bf = None if b is None else b.detach().float().contiguous()
+        out = conv_gemm_raw(y, weight_fwd(w), bf, B, L, C, ks, 1, pad, N)
+        ctx.save_for_backward(hc, y, gamma, stats, w)
+        ctx.beta, ctx.b = beta, b
+        ctx.cfg = (B, L, C, ks, pad, N, int(training), int(act), float(p), seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        hc, y, gamma, stats, w = ctx.saved_tensors
+        B, L, C, ks, pad, N, training, act, p, seed = ctx.cfg
+        R = B * L
+        dev = hc.device
+        dout = dout.to(torch.bfloat16).contiguous()
+        first = _wgrad_first(R)
+
+        def dgrad():
+            nparts = (R + 255) // 256
+            part = torch.empty(2 * nparts * C, device=dev, dtype=torch.float32)
+            dz = torch.empty(B, L, C, device=dev, dtype=torch.bfloat16)
+            rc = lib().ssamd_conv_gemm_bnbwd(_ptr(dout), _ptr(weight_dgrad(w)), _ptr(dz), B, L, N, ks, 1,
+                                             (ks - 1) - pad, C, _ptr(hc), _ptr(stats), _ptr(part), act, p, seed,
+                                             _stream())
+            _check(rc, "ssamd_conv_gemm_bnbwd")
+            dh = torch.empty_like(hc)
+            dg, db = gradslots.claim(gamma), gradslots.claim(ctx.beta)
+            if dg is None:
+                dg = torch.empty(C, device=dev, dtype=torch.float32)
+            if db is None:
+                db = torch.empty(C, device=dev, dtype=torch.float32)
+            rc = lib().ssamd_bn_bwd_dz(_ptr(dz), _ptr(hc), _ptr(gamma), _ptr(stats), _ptr(part), nparts, _ptr(dh),
+                                       _ptr(dg), _ptr(db), R, C, training, _stream())
+            _check(rc, "ssamd_bn_bwd_dz")
+            return dh, dg, db
+
+        if not first:
+            dh, dg, dbeta = dgrad()
+        want_b = ctx.b is not None and ctx.needs_input_grad[6]
+        sb = gradslots.claim(ctx.b) if want_b else None
+        dw = dbias = None
+        if ctx.needs_input_grad[5]:
+            sw = gradslots.claim(w)
+            res = wgrad_async(lambda: conv_wgrad_raw(y, dout, B, L, C, ks, 1, pad, N, with_bias=want_b, dW=sw, db=sb),
+                              (y, dout), sw is not None and (sb is not None or not want_b),
+                              (w, ctx.b) if want_b else (w,))
+            dw, dbias = res if want_b else (res, None)
+        elif want_b:
+            dbias = colsum_raw(dout, N, sb)
+        if first:
+            dh, dg, dbeta = dgrad()
+        return dh, dg, dbeta, None, None, dw, dbias, None, None, None, None, None, None, None
+
+
+def bn_act_conv(h, bn, training, act_tanh, p, w, b, pad):
+    """conv(drop(act(BN(h)))) -- see _BNActConvFn.  The BN channel count C must satisfy C % 8 == 0 and
+    C >= 256 (the data-gradient GEMM's 256x256-tile epilogue); ``bn_act_conv_ok`` tells callers."""
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    if training and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    act = 2 if act_tanh == "relu" else int(bool(act_tanh))
+    return _BNActConvFn.apply(h.to(torch.bfloat16), bn.weight, bn.bias, bn.running_mean, bn.running_var, w, b,
+                              bool(training), momentum, bn.eps, act, float(p if training else 0.0), _next_seed(), pad)
+
+
+def bn_act_conv_ok(C: int, w) -> bool:
+    return C >= 256 and C % 8 == 0 and w.dim() == 3 and w.shape[0] % 8 == 0
 
 
 def bn_act(h, bn, training, act_tanh, p, out_f32=False):

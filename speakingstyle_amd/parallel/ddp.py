@@ -188,7 +188,17 @@ class GradBuckets:
         if self.arena.grad.is_cuda:
             from ..ops import hip
 
-            hip.join_side_streams()  # the bucket's weight gradients may still be on the side stream
+            # The bucket's weight gradients may still be queued on the side stream.  Order the collective
+            # after BOTH streams without making the compute stream wait: the side stream waits for the
+            # compute stream's hook point and the collective is issued with the side stream current
+            # (ProcessGroupNCCL makes its RCCL stream wait on the current stream).  The compute stream
+            # runs on into the rest of backward; finish() orders it after every bucket.
+            side = hip.side_stream_for_collective(self.arena.grad.device)
+            if side is not None:
+                with torch.cuda.stream(side):
+                    self.works[bi] = dist.all_reduce(self.arena.grad[s:e], op=dist.ReduceOp.SUM, group=self.group,
+                                                     async_op=True)
+                return
         self.works[bi] = dist.all_reduce(self.arena.grad[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _launch_ready(self):

@@ -57,21 +57,20 @@ class Trainer:
 
         from ..utils.timing import PhaseTimer
 
-        # SSAMD_HOST_TAIL=1: host timestamps of the step tail (backward return .. optimizer launch)
-        self._host_tail = [] if os.environ.get("SSAMD_HOST_TAIL") == "1" else None
-        self._defer_release = os.environ.get("SSAMD_DEFER_RELEASE", "1") == "1"
-        self._held = None
+        from .. import experimental
+
         mi = train_config.get("mi355x", {}) or {}
+        experimental.configure(mi.get("experimental"))
+        # host timestamps of the step tail (backward return .. optimizer launch): diagnostics only
+        self._host_tail = [] if experimental.get("host_tail") else None
         # backward on the calling thread instead of autograd's per-device worker thread: no thread
         # hand-off per backward and less engine bookkeeping -- host enqueue per step 15.7 -> 12.1 ms
         # (BC2013_GST), 18.6 -> 15.1 (BC2013), 12.2 -> 10.3 (LJSpeech); profiles/r3_v10_host_lead.txt
-        same = mi.get("backward_same_thread", True)
-        if os.environ.get("SSAMD_BWD_SAME_THREAD") in ("0", "1"):
-            same = os.environ["SSAMD_BWD_SAME_THREAD"] == "1"
+        same = bool(mi.get("backward_same_thread", True))
         torch.autograd.set_multithreading_enabled(not same)
-        self.timer = PhaseTimer(bool(mi.get("phase_timing", False)) or os.environ.get("SSAMD_PHASE_TIMING") == "1")
+        self.timer = PhaseTimer(bool(mi.get("phase_timing", False)) or experimental.get("phase_timing"))
 
-    def use_priority_stream(self, enabled: bool = True, wgrad_cu_frac: float = 0.75):
+    def use_priority_stream(self, enabled: bool = True, wgrad_cu_frac: Optional[float] = None):
         """Run the step's main chain on a HIGH-priority HIP stream (made the current stream of this
         thread).  The weight gradients go to a normal-priority side stream (``ops/hip.py::wgrad_async``)
         and only fill the CUs the data-gradient chain leaves idle; with both at one priority the
@@ -80,7 +79,9 @@ class Trainer:
 
         The weight-gradient split plan is also sized for ``wgrad_cu_frac`` of the CUs: its 256x256
         blocks hold a CU's whole LDS, so a plan for every CU locks the data-gradient GEMMs out of the
-        GPU until its blocks drain (LJSpeech +0.5 % at 3/4, ``profiles/r3_v10_wgrad_cus_ab.txt``)."""
+        GPU until its blocks drain (LJSpeech +0.5 % at 3/4, ``profiles/r3_v10_wgrad_cus_ab.txt``).  The
+        reduced plan applies to side-stream launches only (``ssamd_wgrad_set_cus`` takes the stream): a
+        main-stream weight gradient keeps the whole-device split plan and its reduction order."""
         dev = self.opt.arena.data.device
         if not (enabled and dev.type == "cuda"):
             return None
@@ -89,11 +90,13 @@ class Trainer:
         s = torch.cuda.Stream(device=dev, priority=hi)
         torch.cuda.set_stream(s)
         self.compute_stream = s
-        if wgrad_cu_frac and wgrad_cu_frac < 1.0:
-            from ..ops import hip
+        from .. import experimental
+        from ..ops import hip
 
+        frac = experimental.get("wgrad_cu_frac") if wgrad_cu_frac is None else wgrad_cu_frac
+        if frac and frac < 1.0:
             cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            hip.lib().ssamd_wgrad_set_cus(max(1, int(cus * wgrad_cu_frac)))
+            hip.lib().ssamd_wgrad_set_cus(hip.side_stream_handle(dev), max(1, int(cus * frac)))
         return s
 
     def take_frames(self) -> int:
@@ -151,7 +154,6 @@ class Trainer:
         last_micro = (self.micro + 1) % self.grad_acc == 0
         tm.phase("forward")
         output = self.model(*batch[2:])
-        self._held = None  # previous backward's side-stream inputs (see join_side_streams)
         if work is not None:
             work.wait()
         tm.phase("loss")
@@ -176,9 +178,9 @@ class Trainer:
         if cuda:
             from ..ops import hip
 
-            # weight gradients computed on the side stream; their inputs are dropped during the
-            # next forward (host time here is GPU idle time)
-            self._held = hip.join_side_streams(defer_release=self._defer_release)
+            # weight gradients computed on the side stream; their inputs are released here (holding them
+            # into the next forward measured within noise and would raise the peak by a step's activations)
+            hip.join_side_streams()
         if ht is not None:
             ht.append(("joined", time.perf_counter()))
         self.opt.arena.finalize_grads()
@@ -213,7 +215,7 @@ class Trainer:
         return losses, output, lr
 
     def host_tail_summary(self):
-        """Mean host ms between consecutive step-tail marks (SSAMD_HOST_TAIL=1), or None."""
+        """Mean host ms between consecutive step-tail marks (``host_tail`` diagnostics switch), or None."""
         ht = self._host_tail
         if not ht:
             return None

@@ -2,7 +2,7 @@
 device time (HIP events on the current stream) of the phases of a training step.
 
 Used by ``Trainer`` when enabled (``mi355x.phase_timing: true`` in train.yaml, ``bench.py
---phase-times`` or ``SSAMD_PHASE_TIMING=1``): the training loop logs ``Perf/phase_*_ms``
+--phase-times`` or the ``phase_timing`` experiment switch): the training loop logs ``Perf/phase_*_ms``
 scalars at every log step and the bench prints a per-phase table.  Disabled it costs one
 attribute test per phase.
 

@@ -65,7 +65,7 @@ def test_bench_single_process_default():
 
 def test_bench_failing_rank_exits_nonzero():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--synth-steps", "0"] + ARGS, cwd=ROOT,
-                       env=_env(SSAMD_FAIL_RANK="1", SSAMD_DIST_TIMEOUT_S="60"), capture_output=True, text=True,
+                       env=_env(SSAMD_EXPERIMENTAL="fail_rank=1", SSAMD_DIST_TIMEOUT_S="60"), capture_output=True, text=True,
                        timeout=900)
     assert r.returncode != 0
     assert "[rank 1] FAILED" in r.stderr and "injected failure on rank 1" in r.stderr

@@ -44,11 +44,28 @@ def _capture(tr):
     return grads
 
 
-@pytest.mark.parametrize("name", ["LJSpeech", "BC2013"])
-def test_rccl_bucket_path_single_rank(name):
+@pytest.mark.parametrize("name,prio", [("LJSpeech", False), ("BC2013", False), ("LJSpeech", True)])
+def test_rccl_bucket_path_single_rank(name, prio, monkeypatch):
     """BC2013 adds the FiLM sites: scalar gradients folded with the L2 term into their slots and the
-    shared style gamma/beta buffer must keep the per-parameter hook counts stable across steps."""
+    shared style gamma/beta buffer must keep the per-parameter hook counts stable across steps.
+
+    ``prio``: the bench / train.py stream layout (high-priority compute stream, weight gradients on the
+    side stream).  Buckets whose weight gradients are still queued on the side stream are issued with
+    the side stream current (ordered after both streams, the compute stream does not wait): the
+    reduced gradients must still equal the plain step's bitwise."""
     import torch.distributed as dist
+
+    from speakingstyle_amd.ops import hip
+
+    side_issued = []
+    orig_side = hip.side_stream_for_collective
+
+    def counting(dev):
+        s = orig_side(dev)
+        side_issued.append(s is not None)
+        return s
+
+    monkeypatch.setattr(hip, "side_stream_for_collective", counting)
 
     from speakingstyle_amd.config import load_named
     from speakingstyle_amd.data.synthetic import SyntheticBatches
@@ -61,6 +78,8 @@ def test_rccl_bucket_path_single_rank(name):
     batches = [SyntheticBatches(8, device="cuda", seed=3 + i, frame_level=fl).make_batch() for i in range(3)]
 
     ref = _trainer(cfg)
+    if prio:
+        ref.use_priority_stream()
     g_ref = _capture(ref)
     for b in batches:
         ref.train_step(b)
@@ -68,6 +87,8 @@ def test_rccl_bucket_path_single_rank(name):
     dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_port()}")
     try:
         tr = _trainer(cfg)
+        if prio:
+            tr.use_priority_stream()
         tr.buckets = ddp.GradBuckets(tr.opt.arena, bucket_mb=4.0, force=True)  # many buckets
         nb = len(tr.buckets.buckets)
         assert nb >= 4
@@ -90,5 +111,9 @@ def test_rccl_bucket_path_single_rank(name):
         for a, r in zip(g, g_ref):
             assert torch.equal(a, r)
         assert torch.equal(tr.opt.arena.data, ref.opt.arena.data)
+        if prio:
+            assert any(side_issued), "no bucket was issued behind queued side-stream weight gradients"
     finally:
         dist.destroy_process_group()
+        if prio:
+            torch.cuda.set_stream(torch.cuda.default_stream())

@@ -94,3 +94,21 @@ def test_kernel_library_bindings_agree():
         assert not isinstance(getattr(L, fn), ctypes._CFuncPtr)  # the generated wrapper, not ctypes
     # struct-by-value entry points stay on ctypes
     assert isinstance(L.ssamd_var_loss_fwd, ctypes._CFuncPtr)
+
+
+def test_sig_hash_tracks_argument_types():
+    """A signature edited without a rebuild changes the digest that hip._load_fast compares, so stale
+    bindings fall back to ctypes instead of converting arguments with the old types."""
+    import ctypes
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc"))
+    import gen_fastcall
+
+    P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    a = gen_fastcall.sig_hash({"ssamd_x": [P, I, F]}, {})
+    assert a == gen_fastcall.sig_hash({"ssamd_x": [P, I, F]}, {})
+    assert a != gen_fastcall.sig_hash({"ssamd_x": [P, F, F]}, {})  # same count, different type
+    assert a != gen_fastcall.sig_hash({"ssamd_x": [P, I, F]}, {"ssamd_x": ctypes.c_long})
+    assert f'"sig_hash", "{a}"' in gen_fastcall.generate({"ssamd_x": [P, I, F]}, {})

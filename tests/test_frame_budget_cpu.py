@@ -9,6 +9,7 @@ reference's global-batch split (``train.py:27-45``).
 * ``train.py --synthetic`` at world 2 sizes each rank's batch by frames, not batch_size / world."""
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -219,10 +220,10 @@ def test_train_cli_world2_frame_budget(tmp_path):
            "-t", files[2], "--synthetic", "--cpu", "--no_vocoder"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if "first batch:" in l]
-    assert len(lines) == 2, r.stdout
-    for l in lines:
-        n = int(l.split("first batch:")[1].split()[0])
-        frames = int(l.split("utterances,")[1].split()[0])
-        assert n > 2 and frames <= 6000 and "frames_per_gpu=6000" in l
+    # the two ranks print concurrently: their lines may interleave, so match the records, not lines
+    recs = re.findall(r"\[rank (\d)\] first batch: (\d+) utterances, (\d+) padded mel frames \(frames_per_gpu=(\d+)\)",
+                      r.stdout)
+    assert sorted(int(x[0]) for x in recs) == [0, 1], r.stdout
+    for _, n, frames, budget in recs:
+        assert int(n) > 2 and int(frames) <= 6000 and budget == "6000"
     assert "Step 2/2" in r.stdout

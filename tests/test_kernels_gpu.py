@@ -326,6 +326,40 @@ def test_attention(D, H):
     assert _rel(qh.grad, qr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("D,H", [(128, 2), (32, 8)])
+@pytest.mark.parametrize("L", [1000, 4096])
+@pytest.mark.parametrize("packed", [False, True])
+def test_attention_long(D, H, L, packed):
+    """Long sequences (training decoder / reference encoder up to max_seq_len = 1000 frames; eval-mode
+    long-form synthesis past it, reference ``transformer/Models.py:82-87,145-152``): forward and
+    backward vs fp32 torch, padded layout and packed rows, sequences that end mid-tile."""
+    from speakingstyle_amd.ops.packing import PackInfo, pack, unpack
+
+    torch.manual_seed(30 + L + D)
+    lens = torch.tensor([L, L - 37, L // 3 + 5], device=DEV)
+    B = lens.numel()
+    qkv = (torch.randn(B, L, 3 * H * D, device=DEV)).to(torch.bfloat16)
+    qr = qkv.float().requires_grad_(True)
+    orr = ref.attention(qr, lens, H)
+    g = torch.randn_like(orr).to(torch.bfloat16)
+    orr.backward(g.float())
+    if packed:
+        pk = PackInfo.build(lens, L, int(lens.sum()))
+        qp = pack(qkv, pk).detach().requires_grad_(True)
+        op = hip.attention(qp, None, H, pk)
+        o = unpack(op, pk)
+        op.backward(pack(g, pk))
+        dq = unpack(qp.grad, pk)
+    else:
+        qh = qkv.clone().requires_grad_(True)
+        o = hip.attention(qh, lens, H)
+        o.backward(g)
+        dq = qh.grad
+    assert _rel(o, orr) < 1e-2
+    # padded rows of the query / key / value gradient are zero in both
+    assert _rel(dq, qr.grad) < 3e-2
+
+
 @pytest.mark.parametrize("cfg", ["LJSpeech", "LibriTTS", "BC2013", "BC2013_GST"])
 def test_model_step_hip_vs_reference(cfg):
     """Full FastSpeech2 forward+backward, HIP bf16 vs torch fp32: LJSpeech (no style), LibriTTS
@@ -490,6 +524,69 @@ def test_bn_dropout_rate():
     y = hip.bn_act(h, bn, True, True, 0.5)
     frac = (y == 0).float().mean().item()
     assert 0.47 < frac < 0.53
+
+
+@pytest.mark.parametrize("N,training,R", [(512, True, (5, 93)), (80, True, (3, 700)), (512, False, (4, 61)),
+                                          (512, True, (2, 1)), (512, True, (1, 300))])
+def test_bn_act_conv_fused(N, training, R):
+    """One PostNet link conv(tanh(BN(h))) with the BatchNorm backward started in the data-gradient GEMM's
+    epilogue (dz + per-tile column partials) vs fp32 torch: BN running stats, h / gamma / beta / W / bias
+    gradients.  Row counts that are not a multiple of the 256-row tile and a single-row batch included."""
+    torch.manual_seed(21)
+    B, L = R
+    C, ks, pad = 512, 5, 2
+    bn = torch.nn.BatchNorm1d(C).to(DEV)
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-0.3, 0.3)
+    bn.running_mean.uniform_(-0.2, 0.2)
+    bn.running_var.uniform_(0.5, 2.0)
+    bnr = torch.nn.BatchNorm1d(C).to(DEV)
+    bnr.load_state_dict(bn.state_dict())
+    w = (torch.randn(N, C, ks, device=DEV) / math.sqrt(C * ks)).requires_grad_(True)
+    b = torch.randn(N, device=DEV).requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    h = (torch.randn(B, L, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    hh = h.clone().requires_grad_(True)
+    hr = h.float().requires_grad_(True)
+    assert hip.bn_act_conv_ok(C, w)
+    y = hip.bn_act_conv(hh, bn, training, True, 0.0, w, b, pad)
+    z = F.batch_norm(hr.reshape(-1, C), bnr.running_mean, bnr.running_var, bnr.weight, bnr.bias, training, 0.1,
+                     1e-5).reshape(B, L, C)
+    yr = ref.conv1d(torch.tanh(z).to(torch.bfloat16).float(), wr, br, pad, 1, None)
+    assert _rel(y, yr) < 1e-2
+    torch.testing.assert_close(bn.running_mean, bnr.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, bnr.running_var, rtol=1e-4, atol=1e-5)
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    assert _rel(hh.grad, hr.grad) < 2e-2
+    assert _rel(bn.weight.grad, bnr.weight.grad) < 2e-2 and _rel(bn.bias.grad, bnr.bias.grad) < 1e-2
+    assert _rel(w.grad, wr.grad) < 2e-2 and _rel(b.grad, br.grad) < 1e-2
+
+
+def test_bn_act_conv_dropout_matches_unfused():
+    """Same seed: the fused link regenerates bn_act's dropout mask bit for bit in the GEMM epilogue, so it
+    agrees with bn_act -> conv1d (the unfused HIP path) up to dz's bf16 rounding and partial-sum order."""
+    torch.manual_seed(22)
+    B, L, C, N = 3, 211, 512, 512
+    bn1, bn2 = torch.nn.BatchNorm1d(C).to(DEV), torch.nn.BatchNorm1d(C).to(DEV)
+    bn2.load_state_dict(bn1.state_dict())
+    w = (torch.randn(N, C, 5, device=DEV) / math.sqrt(C * 5)).requires_grad_(True)
+    w2 = w.detach().clone().requires_grad_(True)
+    h = (torch.randn(B, L, C, device=DEV)).to(torch.bfloat16)
+    h1, h2 = h.clone().requires_grad_(True), h.clone().requires_grad_(True)
+    g = torch.randn(B, L, N, device=DEV).to(torch.bfloat16)
+    hip.set_seed(777)
+    y1 = hip.bn_act_conv(h1, bn1, True, True, 0.5, w, None, 2)
+    hip.set_seed(777)
+    y2 = hip.conv1d(hip.bn_act(h2, bn2, True, True, 0.5), w2, None, 2, 1, None)
+    assert torch.equal(y1, y2)  # same forward kernels, same mask
+    y1.backward(g)
+    y2.backward(g)
+    assert _rel(h1.grad, h2.grad) < 1e-2
+    assert _rel(bn1.weight.grad, bn2.weight.grad) < 1e-2 and _rel(bn1.bias.grad, bn2.bias.grad) < 1e-2
+    assert torch.equal(w.grad, w2.grad)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 4])
@@ -1262,12 +1359,13 @@ def test_hifigan_generator_hip_training_vs_torch():
     (y - target).abs().mean().backward()
     grads = {n: p.grad.clone() for n, p in g.named_parameters() if p.grad is not None}
     g.zero_grad(set_to_none=True)
-    H._HIP_TRAIN = False
+    saved = H._hip_train
+    H._hip_train = lambda: False
     try:
         yr = g(mel)
         (yr - target).abs().mean().backward()
     finally:
-        H._HIP_TRAIN = True
+        H._hip_train = saved
     assert _rel(y, yr) < 4e-2
     bad = []
     for n, p in g.named_parameters():

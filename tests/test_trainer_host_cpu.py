@@ -1,5 +1,5 @@
 """Trainer host-side knobs (CPU): backward on the calling thread (``mi355x.backward_same_thread``,
-``torch.autograd.set_multithreading_enabled``), the step-tail marks (``SSAMD_HOST_TAIL``) and that
+``torch.autograd.set_multithreading_enabled``), the step-tail marks (``host_tail`` switch) and that
 the calling-thread backward leaves the gradients unchanged."""
 import torch
 
@@ -22,7 +22,6 @@ def _setup(same_thread):
 
 
 def test_calling_thread_backward_is_configurable_and_exact(monkeypatch):
-    monkeypatch.delenv("SSAMD_BWD_SAME_THREAD", raising=False)
     before = torch.autograd.is_multithreading_enabled()
     try:
         out = {}
@@ -38,7 +37,10 @@ def test_calling_thread_backward_is_configurable_and_exact(monkeypatch):
 
 
 def test_host_tail_marks(monkeypatch):
-    monkeypatch.setenv("SSAMD_HOST_TAIL", "1")
+    from speakingstyle_amd import experimental
+
+    monkeypatch.setenv("SSAMD_EXPERIMENTAL", "host_tail=1")
+    experimental.reset_for_tests()
     before = torch.autograd.is_multithreading_enabled()
     try:
         tr, b = _setup(True)
@@ -50,3 +52,5 @@ def test_host_tail_marks(monkeypatch):
         assert all(v >= 0 for v in tail.values())
     finally:
         torch.autograd.set_multithreading_enabled(before)
+        monkeypatch.delenv("SSAMD_EXPERIMENTAL")
+        experimental.reset_for_tests()

@@ -32,19 +32,19 @@ def torch_fp32_only():
     from speakingstyle_amd.models import hifigan as H
     from speakingstyle_amd.ops import hip
 
-    saved = (hip.lib, H._HIP_TRAIN, ops._FORCED)
+    saved = (hip.lib, H._hip_train, ops._FORCED)
 
     def _no_kernels(*a, **k):
         raise AssertionError("an ssamd_ kernel was reached inside the fp32 oracle")
 
     hip.lib = _no_kernels
-    H._HIP_TRAIN = False
+    H._hip_train = lambda: False
     ops.set_backend("reference")
     try:
         yield
     finally:
         hip.lib = saved[0]
-        H._HIP_TRAIN = saved[1]
+        H._hip_train = saved[1]
         ops.set_backend(saved[2])
 
 
@@ -114,17 +114,39 @@ def test_bc2013_fs2_vocoder_int16_e2e_vs_fp32_oracle():
         mel_ref, len_ref = out_r[1], out_r[9]
         wav_ref = voc(mel_ref.transpose(1, 2)).squeeze(1)
         pcm_ref = (wav_ref * mx).clamp(-32768, 32767).to(torch.int16)
+        # the FS2 error propagated through the fp32 generator
+        wav_prop = voc(mel_hip.float().transpose(1, 2)).squeeze(1)
+    with torch.no_grad():
+        wav_voc = voc.infer(mel_ref.to(torch.bfloat16).contiguous()).float()
     assert torch.equal(len_hip.cpu(), len_ref.cpu())
     assert pcm_hip.shape == pcm_ref.shape
-    # compare the valid samples of every utterance
+    # Error budget per utterance (relative L2 over its valid samples).  By the triangle inequality
+    #   e_total = |pcm_hip - pcm_ref| <= e_voc + e_prop + e_q (+ the vocoder's error difference between
+    #   its two inputs, second order), with
+    #   e_fs2  = FS2 bf16 vs fp32 mel: bf16 operands / fp32 accumulation, <= 3e-2 (model-step budget);
+    #   e_voc  = HIP bf16 vocoder vs fp32 oracle on the SAME (oracle) mel, <= 5e-2 (generator-only test);
+    #   e_prop = fp32 generator on the HIP mel vs on the oracle mel: the FS2 error through the generator;
+    #            on these inputs the generator's relative gain e_prop / e_fs2 is ~1-2;
+    #   e_q    = int16 quantisation of both sides, 2 x 0.5 LSB / RMS(wav) -- negligible at these levels.
+    # The 8e-2 acceptance bound is e_voc's 5e-2 plus a 3e-2 allowance for e_prop + e_q; each term is
+    # also checked on its own so a regression names its stage.
     hop = 256
-    errs = []
+    mel_err = _rel(mel_hip, mel_ref)
+    assert mel_err < 3e-2
+    report = []
     for i, n in enumerate(len_ref.tolist()):
         a = pcm_hip[i, : n * hop].float()
         r = pcm_ref[i, : n * hop].float()
-        errs.append(_rel(a, r))
-    assert _rel(mel_hip, mel_ref) < 3e-2
-    assert max(errs) < 8e-2, errs
+        e_total = _rel(a, r)
+        e_voc = _rel(wav_voc[i, : n * hop], wav_ref[i, : n * hop])
+        e_prop = _rel(wav_prop[i, : n * hop], wav_ref[i, : n * hop])
+        rms = wav_ref[i, : n * hop].float().pow(2).mean().sqrt().item()
+        e_q = (2 * 0.5 / mx) / max(rms, 1e-12) / (12 ** 0.5)
+        report.append((round(e_total, 4), round(e_voc, 4), round(e_prop, 4), round(e_q, 6)))
+        assert e_voc < 5e-2, report
+        assert e_prop < 3e-2 and e_q < 1e-2, report
+        assert e_total <= 1.05 * (e_voc + e_prop + e_q) + 1e-3, report
+        assert e_total < 8e-2, report
 
 
 def test_bucketed_vocoding_matches_padded_batch():
@@ -144,3 +166,41 @@ def test_bucketed_vocoding_matches_padded_batch():
     for i, n in enumerate(lengths):
         a, r = buck[i, : n * 256].float(), pad[i, : n * 256].float()
         assert _rel(a, r) < 1e-2, (i, _rel(a, r))
+
+
+def test_fs2_long_form_eval_vs_fp32_oracle():
+    """Long-form synthesis: eval-mode FastSpeech2 on utterances past max_seq_len = 1000 frames (the
+    reference regenerates the positional table in eval, ``transformer/Models.py:82-87,145-152``): the
+    HIP bf16 path (decoder attention over ~1.8k frames, PE rows generated past the table) vs the fp32
+    torch oracle, mel and PostNet output over the valid frames."""
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+
+    pp, mc, tc = load_named("LJSpeech")
+    torch.manual_seed(2)
+    model = FastSpeech2(pp, mc).to(DEV).eval()
+    model.requires_grad_(False)
+    T = torch.tensor([80, 61], device=DEV)
+    Tm = int(T.max())
+    g = torch.Generator(device="cpu").manual_seed(3)
+    texts = torch.randint(1, 360, (2, Tm), generator=g).to(DEV)
+    texts[1, 61:] = 0
+    dur = torch.randint(15, 30, (2, Tm), generator=g).to(DEV)
+    dur[1, 61:] = 0
+    mel_lens = dur.sum(1)
+    M = int(mel_lens.max())
+    assert M > 1000 and int(mel_lens.min()) > 1000
+    pit = torch.randn(2, Tm, generator=g).to(DEV)
+    ene = torch.randn(2, Tm, generator=g).to(DEV)
+    spk = torch.zeros(2, dtype=torch.long, device=DEV)
+    args = (spk, texts, T, Tm, None, mel_lens, M, pit, ene, dur)
+    with torch.no_grad():
+        model.set_compute_dtype(torch.bfloat16)
+        out = model(*args)
+    with torch_fp32_only(), torch.no_grad():
+        model.set_compute_dtype(torch.float32)
+        out_r = model(*args)
+    assert out[1].shape[1] == out_r[1].shape[1] == M
+    for i, n in enumerate(mel_lens.tolist()):
+        assert _rel(out[0][i, :n], out_r[0][i, :n]) < 3e-2
+        assert _rel(out[1][i, :n], out_r[1][i, :n]) < 3e-2

@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Aggregate rocprofv3 --pmc counter CSVs per kernel (tools/gpu_pmc_step.sh output).
+"""Aggregate rocprofv3 --pmc counter CSVs per kernel (tools/gpu.sh pmc / synthpmc output).
 
 For each run directory: per kernel name (top by SQ_WAVE_CYCLES or FETCH_SIZE), dispatches,
 MFMA busy / GRBM_GUI_ACTIVE (per-dispatch average, ~fraction of the time the matrix cores were
