@@ -102,18 +102,15 @@ struct EpiX {
   // bf16 aux operand (16x fewer bytes for the FFN hidden layer's dgrad)
   unsigned char* mask_out;
   const unsigned char* mask_in;
-  // BatchNorm backward head (PostNet; big64 LDS-staged epilogue, bf16 out, ldy == N): the GEMM output is
-  // dy = dL/d(BN-act-dropout output) of the layer whose pre-BN input is bn_h [M][N]; the epilogue stores
-  //   dz = dy * keep(seed, p) * act'(bn_h * scale + shift)
-  // instead of dy and writes the tile's column partials  sum_rows dz  and  sum_rows dz * (bn_h - mean) * rstd
-  // to bn_part[tm][N] and bn_part[nM + tm][N] (tm = M tile; fixed order, no atomics).  bn_stats = the
+  // BatchNorm backward head (PostNet; the BNH instantiation of the big64 LDS-staged epilogue, bf16 out,
+  // ldy == N): the GEMM output is dy = dL/d(BN-act-dropout output) of the layer whose pre-BN input is
+  // bn_h [M][N]; the epilogue stores  dz = dy * keep(seed, p) * act'(bn_h * scale + shift)  instead of dy
+  // and writes the tile's column partials  sum_rows dz  and  sum_rows dz * (bn_h - mean) * rstd  to
+  // bn_part[tm][N] and bn_part[nM + tm][N] (tm = M tile; fixed order, no atomics).  bn_stats = the
   // forward's [mean | rstd | scale | shift] x N.  The partial sums replace k_bn.hip's bn_bwd_reduce pass
-  // (a full re-read of dy and bn_h); the dropout mask and act' are bit-identical to it.
-  const bf16_t* bn_h;
-  const float* bn_stats;
-  float* bn_part;
-  int bn_act;
-  float bn_p;
+  // (a full re-read of dy and bn_h); the dropout mask and act' are bit-identical to it.  The fields
+  // alias members the BNH variant does not otherwise use, so EpiX (the kernel argument block of every
+  // variant) keeps its size: bn_h = acc, bn_stats = ln_w, bn_part = mean, bn_act = post_act, p = pre_p.
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -819,8 +816,10 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// PH4 (BUF only): the 4-phase main loop -- see the comment at its loop below.
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool PH4 = false>
+// BNH: the BatchNorm-backward head epilogue (EpiX.bn_*) -- a separate instantiation, so the other
+// variants' epilogues do not carry its registers / code (measured: folded into every variant as a runtime
+// branch it slowed the ReLU-mask data gradient ~25 % and the step ~1.5 %).
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool BNH = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
@@ -958,124 +957,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     nk = min(nk_all, kt0 + per);
     Yv = reinterpret_cast<float*>(Yv) + (long)blockIdx.y * g.M * ldy;
   }
-  if constexpr (PH4) {
-    // 4-phase main loop (MI355X: keeps LDS-DMA in flight across barriers, never drains to 0 in steady
-    // state).  A k-tile (256 x 64 of A and of B, 64 KiB) is staged as four 16-KiB UNITS, each the rows
-    // one output quadrant-phase reads:  U0 = A rows of quadrant qa = 0 (both wave rows), U1 = B rows of
-    // qb = 1, U2 = A rows of qa = 1, U3 = B rows of qb = 0.  Phase p of tile t computes quadrant
-    // (qa, qb) = (0,0) (0,1) (1,1) (1,0) -- 16 MFMAs per wave -- and restages the unit its predecessor
-    // phase finished reading, for tile t + 2 into the same buffer (U3 of tile t + 1 in phase 0):
-    //   phase 0: U3(t+1) -> buf^1 | read A(qa0) B(qb0) | MFMA (0,0)
-    //   phase 1: U0(t+2) -> buf   | read B(qb1)        | MFMA (0,1)
-    //   phase 2: U1(t+2) -> buf   | read A(qa1)        | MFMA (1,1)
-    //   phase 3: U2(t+2) -> buf   | (B(qb0) from regs) | MFMA (1,0) | vmcnt(6): tile t+1 landed
-    // Every phase ends with a barrier (WAR: a unit is restaged one phase after its last read, which
-    // retired before the barrier); RAW: tile t+1's last unit was issued in phase 0 of tile t, so the
-    // counted vmcnt(6) in phase 3 (the 3 units issued after it stay in flight) + the barrier order it
-    // before phase 0 of tile t+1.  Two units per wave-thread: 2 LDS-DMA instructions per phase.
-    int bblk[4], bvo2[4];  // B 8-row blocks of this wave: U3 (qb = 0) -> [0], [1]; U1 (qb = 1) -> [2], [3]
-    bblk[0] = 8 * (wave >> 2) + (wave & 3);
-    bblk[1] = bblk[0] + 16;
-    bblk[2] = bblk[0] + 4;
-    bblk[3] = bblk[1] + 4;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int row = bblk[u] * 8 + (lane >> 3);
-      const int ch = (lane & 7) ^ ((row >> 1) & 7);
-      bvo2[u] = (n0 + row < g.N) ? ((n0 + row) * g.K + ch * 8) * 2 : kOOB;
-    }
-    // A 8-row blocks: load i covers block i * 8 + wave (rows 64 i + 8 wave ..): U0 = i in {0, 2}, U2 = {1, 3}
-    auto stage_a = [&](int kt, int q, int buf) {
-      char* As = smem + buf * STG64_BYTES;
-      const int k0 = kt * 64;
-      const int tap = k0 / g.Cin;
-      const int cin0 = k0 - tap * g.Cin;
-      const int shift = tap * g.dil - g.pad;
-      const int aoff = (shift * g.Cin + cin0) * 2;
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int i = q + 2 * jj;
-        const int ts = a_t[i] + shift;
-        const bool ok = (unsigned)ts < (unsigned)a_lim[i];
-        buf_lds16(rA, ok ? avo[i] + aoff : kOOB, 0, As + (i * 8 + wave) * 1024);
-      }
-    };
-    auto stage_b = [&](int kt, int q, int buf) {  // q = 0: U3 (qb = 0 rows), q = 1: U1 (qb = 1 rows)
-      char* Bs = smem + buf * STG64_BYTES + BG * 64 * 2;
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) buf_lds16(rB, bvo2[q * 2 + jj], kt * 128, Bs + bblk[q * 2 + jj] * 1024);
-    };
-    const int nkt = nk - kt0;
-    if (nkt > 0) {
-      stage_a(kt0, 0, 0); stage_b(kt0, 1, 0); stage_a(kt0, 1, 0); stage_b(kt0, 0, 0);
-    }
-    if (nkt > 1) {
-      stage_a(kt0 + 1, 0, 1); stage_b(kt0 + 1, 1, 1); stage_a(kt0 + 1, 1, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    pp_barrier();
-    short8 fa[2][4], fb0[2][2], fb1[2][2];
-    auto read_a = [&](const char* As, int qa) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int c = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          fa[kk][i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + qa * 64 + i * 16 + (lane & 15), c));
-      }
-    };
-    auto read_b = [&](const char* Bs, int qb, short8 (&fb)[2][2]) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int c = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          fb[kk][j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + qb * 32 + j * 16 + (lane & 15), c));
-      }
-    };
-    auto mma = [&](int qa, int qb, const short8 (&fb)[2][2]) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[qa * 4 + i][qb * 2 + j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    for (int t = 0; t < nkt; ++t) {
-      const int buf = t & 1, kt = kt0 + t;
-      const char* As = smem + buf * STG64_BYTES;
-      const char* Bs = As + BG * 64 * 2;
-      const bool n1 = t + 1 < nkt, n2 = t + 2 < nkt;
-      // phase 0
-      if (n1) stage_b(kt + 1, 0, buf ^ 1);
-      read_a(As, 0);
-      read_b(Bs, 0, fb0);
-      mma(0, 0, fb0);
-      pp_barrier();
-      // phase 1
-      if (n2) stage_a(kt + 2, 0, buf);
-      read_b(Bs, 1, fb1);
-      mma(0, 1, fb1);
-      pp_barrier();
-      // phase 2
-      if (n2) stage_b(kt + 2, 1, buf);
-      read_a(As, 1);
-      mma(1, 1, fb1);
-      pp_barrier();
-      // phase 3
-      if (n2) stage_a(kt + 2, 1, buf);
-      mma(1, 0, fb0);
-      if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      pp_barrier();
-    }
-  } else {
   // double buffer: stage kt+1 is DMA'd while stage kt is computed (one stage = 1024 MFMA cycles
   // per wave, far longer than an L2-warm LDS-DMA), one barrier per 64-wide k slab
   if (kt0 < nk) stage(kt0, 0);
@@ -1102,7 +983,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  }  // !PH4
   if constexpr (!OUT_F32) {
     if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
       // LDS-staged epilogue: the accumulator layout gives each lane 4 columns of one row, i.e.
@@ -1142,6 +1022,75 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       }
       __syncthreads();
       bf16_t* Y = reinterpret_cast<bf16_t*>(Yv);
+      if constexpr (BNH) {
+        // BatchNorm-backward head (EpiX aliases: acc = bn_h, ln_w = [mean | rstd | scale | shift] x N,
+        // mean = partials, post_act = act code, pre_p = dropout p).  Thread (c = tid & 31, r0 = tid >> 5)
+        // owns column chunk c of rows r0 + 16 it, loads h for EPG rows before use, stores dz and keeps
+        // its 8 columns' running sums; the tile's 16 per-column partials are then combined in fixed order.
+        constexpr int EPI = BG * 32 / NT3;
+        constexpr int EPG = 8;
+        const int c = tid & 31, r0 = tid >> 5;
+        const int n = n0 + c * 8;
+        const bool col_ok = n < g.N;
+        float bmu[8], brs[8], bsc[8], bsh[8], bs1[8], bs2[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int nq = col_ok ? n + q : 0;
+          bmu[q] = ex.ln_w[nq];
+          brs[q] = ex.ln_w[g.N + nq];
+          bsc[q] = ex.ln_w[2 * g.N + nq];
+          bsh[q] = ex.ln_w[3 * g.N + nq];
+          bs1[q] = 0.f;
+          bs2[q] = 0.f;
+        }
+        const int act_c = ex.post_act;
+#pragma unroll
+        for (int g0 = 0; g0 < EPI; g0 += EPG) {
+          short8 hb[EPG];
+#pragma unroll
+          for (int u = 0; u < EPG; ++u) {
+            const int m = m0 + r0 + 16 * (g0 + u);
+            if (col_ok && m < g.M) hb[u] = *reinterpret_cast<const short8*>(ex.acc + (long)m * ldy + n);
+          }
+#pragma unroll
+          for (int u = 0; u < EPG; ++u) {
+            const int r = r0 + 16 * (g0 + u);
+            const int m = m0 + r;
+            if (m >= g.M || !col_ok) continue;
+            const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
+            const long off = (long)m * ldy + n;
+            float ks[8];
+            drop_scales<8>(ex.seed, (uint64_t)off, ex.pre_p, ks);
+            short8 o;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const float hv = bf2f((bf16_t)hb[u][q]);
+              float d = bf2f((bf16_t)v[q]) * ks[q];
+              if (act_c) d *= bn_act_grad(act_c, hv * bsc[q] + bsh[q]);
+              bs1[q] += d;
+              bs2[q] += d * (hv - bmu[q]) * brs[q];
+              o[q] = (short)f2bf(d);
+            }
+            *reinterpret_cast<short8*>(Y + off) = o;
+          }
+        }
+        __syncthreads();  // every Ct read is done: reuse the staging LDS for the partials
+        float* red = reinterpret_cast<float*>(smem);  // [2][16][256]
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          red[r0 * 256 + c * 8 + q] = bs1[q];
+          red[4096 + r0 * 256 + c * 8 + q] = bs2[q];
+        }
+        __syncthreads();
+        const int which = tid >> 8, col = tid & 255;  // threads 0..255: sum dz, 256..511: sum dz*xhat
+        if (n0 + col < g.N) {
+          float a = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) a += red[which * 4096 + r * 256 + col];
+          ex.mean[((long)which * nM + tm) * g.N + n0 + col] = a;
+        }
+        return;
+      }
       if (ex.ln_out) {
         // Residual + LayerNorm tail (N == 256, n0 == 0): half-wave h = tid >> 5 owns rows h, h+16, ...
         // of the tile, lane c = tid & 31 owns columns 8c..8c+7.  Every global operand of the 16 rows
@@ -1229,8 +1178,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         }
         return;
       }
-      const bool bnb = ex.bn_h != nullptr;
-      const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_in || bnb;
+      const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_in;
       // Thread (c = tid & 31, r0 = tid >> 5) owns the 16-B column chunk c of rows r0 + 16 it.  The
       // global operands of EPG rows (aux / residual / accumulator segments, mask bytes, sequence
       // lengths) are all loaded before any is used: one loop iteration per row would expose a full
@@ -1241,21 +1189,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       const int c = tid & 31, r0 = tid >> 5;
       const int n = n0 + c * 8;
       const bool col_ok = n < g.N;
-      const bool loads = aux || resid || ex.acc || ex.mask_in || lens || bnb;
-      // BatchNorm-backward head: per-thread column constants and running column partials (8 columns)
-      float bmu[8], brs[8], bsc[8], bsh[8], bs1[8], bs2[8];
-      if (bnb) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int nq = col_ok ? n + q : 0;
-          bmu[q] = ex.bn_stats[nq];
-          brs[q] = ex.bn_stats[g.N + nq];
-          bsc[q] = ex.bn_stats[2 * g.N + nq];
-          bsh[q] = ex.bn_stats[3 * g.N + nq];
-          bs1[q] = 0.f;
-          bs2[q] = 0.f;
-        }
-      }
+      const bool loads = aux || resid || ex.acc || ex.mask_in || lens;
       if (!loads && !xon) {  // store-only epilogue (+ the ReLU bitmask): the plain row loop
         for (int e = tid; e < BG * 32; e += NT3) {
           const int r = e >> 5, cc = e & 31;
@@ -1286,7 +1220,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             if (in && aux) va[u] = *reinterpret_cast<const short8*>(aux + off);
             if (in && resid) vr[u] = *reinterpret_cast<const short8*>(resid + off);
             if (in && ex.acc) vc[u] = *reinterpret_cast<const short8*>(ex.acc + off);
-            if (in && bnb) va[u] = *reinterpret_cast<const short8*>(ex.bn_h + off);
             mb[u] = (in && ex.mask_in) ? (unsigned)ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : 0xffu;
             vv[u] = true;
             if (in && lens) {
@@ -1329,19 +1262,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 #pragma unroll
               for (int q = 0; q < 8; ++q) f[q] += bf2f((bf16_t)vc[u][q]);
             }
-            if (bnb) {
-              float ks[8];
-              drop_scales<8>(ex.seed, (uint64_t)off, ex.bn_p, ks);
-#pragma unroll
-              for (int q = 0; q < 8; ++q) {
-                const float hv = bf2f((bf16_t)va[u][q]);
-                float d = f[q] * ks[q];
-                if (ex.bn_act) d *= bn_act_grad(ex.bn_act, hv * bsc[q] + bsh[q]);
-                f[q] = d;
-                bs1[q] += d;
-                bs2[q] += d * (hv - bmu[q]) * brs[q];
-              }
-            }
 #pragma unroll
             for (int q = 0; q < 8; ++q) f[q] = valid ? f[q] * ex.scale : 0.f;
             if (ex.y2) {
@@ -1358,24 +1278,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             for (int q = 0; q < 8; ++q) v[q] = (short)f2bf(f[q]);
           }
           *reinterpret_cast<short8*>(Y + off) = v;
-        }
-      }
-      if (bnb) {
-        // column partials of the tile: the 16 threads of a column chunk (r0 = 0..15) in fixed order
-        __syncthreads();  // every Ct read is done: reuse the staging LDS
-        float* red = reinterpret_cast<float*>(smem);  // [2][16][256]
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          red[r0 * 256 + c * 8 + q] = bs1[q];
-          red[4096 + r0 * 256 + c * 8 + q] = bs2[q];
-        }
-        __syncthreads();
-        const int which = tid >> 8, col = tid & 255;  // threads 0..255: sum dz, 256..511: sum dz*xhat
-        if (n0 + col < g.N) {
-          float a = 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) a += red[which * 4096 + r * 256 + col];
-          ex.bn_part[((long)which * nM + tm) * g.N + n0 + col] = a;
         }
       }
       return;
@@ -2443,8 +2345,6 @@ SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 static int g_gemm_buf = 1;  // big64 (FASTK) LDS-DMA through buffer descriptors (0: flat global_load_lds)
 SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
-static int g_gemm_ph4 = 0;  // big64 buffer-descriptor path: 1 = the 4-phase unit-staged main loop
-SSAMD_API void ssamd_gemm_set_ph4(int v) { g_gemm_ph4 = v; }
 
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
 static bool big64_buf_ok(const ConvGeom& g) {
@@ -2466,7 +2366,8 @@ static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N
 
 static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
                           const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
-                          int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, EpiX ex, hipStream_t s) {
+                          int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, EpiX ex, hipStream_t s,
+                          bool bnh = false) {
   if (Cin % 8 != 0) return -2;
   if ((long)B * L == 0 || N == 0) return 0;
   ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
@@ -2500,7 +2401,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     const int tiles = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
     const int nk64 = (g.K + 63) / 64;
     const bool plain = !(ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.ln_out || ex.mask_out || ex.mask_in ||
-                         ex.bn_h);
+                         bnh);
     int S = 0;
     if (g_splitk > 0) S = g_splitk;
     else if (g_splitk < 0 && g_gemm_variant < 0 && tiles <= 128 && nk64 >= 16)
@@ -2535,6 +2436,12 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       return (int)hipGetLastError();
     }
   }
+  if (bnh) {  // BatchNorm-backward head (EpiX aliases: acc = bn_h, ln_w = stats, mean = partials): big64 only
+    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act != 0 || aux || resid || lens || !ex.acc || !ex.ln_w ||
+        !ex.mean || rinfo || ex.y2 || ex.ln_out || ex.mask_out || ex.mask_in)
+      return -3;
+    variant = 4;
+  } else {
   if (ex.mask_out || ex.mask_in) {  // the bitmask lives in the big64 LDS-staged epilogue only
     if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act < 0 || ex.ln_out) return -3;
     if (ex.mask_out && act != ACT_RELU) return -3;
@@ -2546,16 +2453,11 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     if (N >= 256) variant = 4;
     else if (variant != 2) return -3;
   }
-  if (ex.bn_h) {  // BatchNorm-backward head: big64 LDS-staged epilogue, bf16 dz, whole-N partial rows
-    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act != 0 || aux || resid || lens || ex.ln_out || xon ||
-        ex.mask_out || ex.mask_in || !ex.bn_stats || !ex.bn_part)
-      return -3;
-    variant = 4;
-  }
   if (ex.ln_out) {  // the LayerNorm tail needs whole rows in one tile and the plain bf16 store
     if (xon || N != 256 || ldy != 256 || out_f32 || !reg || act != 0 || aux || resid || lens) return -3;
     variant = 4;
   }
+  }  // !bnh
   if (reg && variant == 4 && N >= 256) {
     static bool b64_set = false;
     if (!b64_set) {
@@ -2571,10 +2473,9 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, false, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<true, true, false, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, false, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<true, true, true, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, true, true, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, false, false, false, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -2583,10 +2484,8 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
-      if constexpr (BF) {                                                                                \
-        if (g_gemm_ph4)                                                                                  \
-          kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, true, true>                              \
-                        : conv_gemm_big64_kernel<F32, FK, false, true, true>;                            \
+      if constexpr (!F32) {                                                                              \
+        if (bnh) kfn = conv_gemm_big64_kernel<false, FK, false, BF, true>;                              \
       }                                                                                                  \
       hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
@@ -2686,16 +2585,17 @@ SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* 
 SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, int B, int L, int Cin, int ks, int dil,
                                     int pad, int N, const bf16_t* bn_h, const float* bn_stats, float* bn_part,
                                     int bn_act, float p, unsigned long long seed, hipStream_t s) {
-  if (!bn_h) return -2;
+  if (!bn_h || !bn_stats || !bn_part) return -2;
   EpiX ex{};
   ex.scale = 1.f;
-  ex.bn_h = bn_h;
-  ex.bn_stats = bn_stats;
-  ex.bn_part = bn_part;
-  ex.bn_act = bn_act;
-  ex.bn_p = p;
+  ex.acc = bn_h;          // EpiX aliases of the BNH variant (see EpiX)
+  ex.ln_w = bn_stats;
+  ex.mean = bn_part;
+  ex.post_act = bn_act;
+  ex.pre_p = p;
   ex.seed = seed;
-  return conv_gemm_impl(X, W, nullptr, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, nullptr, ex, s);
+  return conv_gemm_impl(X, W, nullptr, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, nullptr, ex, s,
+                        true);
 }
 
 // conv_gemm with a ReLU bitmask: mask_out (act must be ReLU) stores bit (y > 0) per output element,
@@ -2851,7 +2751,8 @@ SSAMD_API int ssamd_conv_wgrad(const bf16_t* X, const bf16_t* dY, float* ws, lon
       b64_set = true;
     }
     const int tiles = ((N + 255) / 256) * ((g.K + 255) / 256);
-    const int cus = (g_wgrad_cus > 0 && s == g_wgrad_cus_stream) ? g_wgrad_cus : device_cus();
+    const bool on = g_wgrad_cus_stream == reinterpret_cast<hipStream_t>(-1) || s == g_wgrad_cus_stream;
+    const int cus = (g_wgrad_cus > 0 && on) ? g_wgrad_cus : device_cus();
     int splits = choose_wgrad_splits(tiles, g.M, max_splits, ws_floats / (slab + N), cus);
     if (splits < 1) return -3;
     int rows_per_split = (g.M + splits - 1) / splits;

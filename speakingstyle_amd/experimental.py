@@ -65,7 +65,11 @@ KNOBS: Dict[str, tuple] = {
                     "auto when the data-gradient GEMMs have fewer row tiles than wgrad_first_waves x CUs"),
     "wgrad_first_waves": (1.25, float, "auto threshold of wgrad_first, in waves of 256-row tiles per CU"),
     "wgrad_cu_frac": (0.75, _frac, "fraction of the CUs the side-stream weight-gradient split plan is sized for"),
+    "wgrad_cus_all": (False, _bool, "apply the reduced weight-gradient CU plan to every stream (round-3 behaviour)"),
     "ln_fuse": (False, _bool, "residual + LayerNorm tail in the producing GEMM's epilogue (measured slower)"),
+    "bn_fuse": (True, _bool, "PostNet BatchNorm backward started in the data-gradient GEMM's epilogue"),
+    "defer_release": (False, _bool, "hand the side-stream weight-gradient inputs back to the trainer, freed "
+                                    "during the next forward (holds a step's activations into it)"),
     "hifigan_hip_train": (True, _bool, "HiFi-GAN generator training on the HIP implicit-GEMM convs"),
     # -- diagnostics (instrumentation only; no effect on what is computed)
     "phase_timing": (False, _bool, "per-phase host/device step times (Perf/phase_* scalars)"),

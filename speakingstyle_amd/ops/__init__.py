@@ -227,7 +227,9 @@ def predictor_head(h, w, b, lengths=None):
 def bn_act_conv(h, bn, training, act_tanh, p, w, b, pad):
     """conv(drop(act(BN(h)))): one PostNet link.  On the GPU the conv's data-gradient GEMM starts the
     BatchNorm backward in its epilogue (``hip._BNActConvFn``); elsewhere bn_act followed by conv1d."""
-    if use_hip(h) and _hip().bn_act_conv_ok(h.shape[-1], w):
+    from .. import experimental
+
+    if use_hip(h) and experimental.get("bn_fuse") and _hip().bn_act_conv_ok(h.shape[-1], w):
         return _hip().bn_act_conv(h, bn, training, act_tanh, p, w, b, pad)
     return conv1d(bn_act(h, bn, training, act_tanh, p), w, b, pad)
 

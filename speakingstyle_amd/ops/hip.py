@@ -48,7 +48,6 @@ _SIGS = {
     "ssamd_gemm_set_ngrp": [I],
     "ssamd_wgrad_set_buf": [I],
     "ssamd_gemm_set_buf": [I],
-    "ssamd_gemm_set_ph4": [I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],

@@ -63,6 +63,8 @@ class Trainer:
         experimental.configure(mi.get("experimental"))
         # host timestamps of the step tail (backward return .. optimizer launch): diagnostics only
         self._host_tail = [] if experimental.get("host_tail") else None
+        self._defer = experimental.get("defer_release")
+        self._held = None
         # backward on the calling thread instead of autograd's per-device worker thread: no thread
         # hand-off per backward and less engine bookkeeping -- host enqueue per step 15.7 -> 12.1 ms
         # (BC2013_GST), 18.6 -> 15.1 (BC2013), 12.2 -> 10.3 (LJSpeech); profiles/r3_v10_host_lead.txt
@@ -96,7 +98,8 @@ class Trainer:
         frac = experimental.get("wgrad_cu_frac") if wgrad_cu_frac is None else wgrad_cu_frac
         if frac and frac < 1.0:
             cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            hip.lib().ssamd_wgrad_set_cus(hip.side_stream_handle(dev), max(1, int(cus * frac)))
+            stream = -1 if experimental.get("wgrad_cus_all") else hip.side_stream_handle(dev)
+            hip.lib().ssamd_wgrad_set_cus(stream, max(1, int(cus * frac)))
         return s
 
     def take_frames(self) -> int:
@@ -154,6 +157,7 @@ class Trainer:
         last_micro = (self.micro + 1) % self.grad_acc == 0
         tm.phase("forward")
         output = self.model(*batch[2:])
+        self._held = None  # defer_release: the previous backward's side-stream inputs
         if work is not None:
             work.wait()
         tm.phase("loss")
@@ -180,7 +184,7 @@ class Trainer:
 
             # weight gradients computed on the side stream; their inputs are released here (holding them
             # into the next forward measured within noise and would raise the peak by a step's activations)
-            hip.join_side_streams()
+            self._held = hip.join_side_streams(defer_release=self._defer)
         if ht is not None:
             ht.append(("joined", time.perf_counter()))
         self.opt.arena.finalize_grads()

@@ -9,10 +9,14 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            bench.py $BENCHARGS (repeat REP times)                  -> gpurun_out/bench_<i>.log
 #   prof             rocprofv3 kernel trace of $BENCHARGS training steps      -> gpurun_out/$TAG_{summary,last_step,grid,split}.txt
+#                    (TREE=ab/base profiles the A/B base tree's bench.py instead)
 #   synthprof        rocprofv3 kernel trace of bench_synth.py $SYNTHARGS     -> gpurun_out/$TAG_synth_summary.txt
 #   pmc              PMC (SQ + HBM passes) of one training step              -> gpurun_out/$TAG_pmc/summary.txt
 #   synthpmc         PMC of one synthesis step (bench_synth.py --batch 64)
 #   ab               same-box A/B: ab/libssamd_kernels_$BASE.so (A) vs in-tree (B), ROUNDS x CONFIGS
+#   abtree           same-box A/B of whole trees: ab/base (git worktree, pre-built) (A) vs this tree (B)
+#   abexp            same-box A/B of experiment switches: EXPS="arm1|arm2|..." (arm = name=v,name=v, - = defaults,
+#                    base = the ab/base tree)
 #   py:<script>      python <script> (a tools/ experiment), output -> gpurun_out/<script>.log
 set -o pipefail
 R="$(cd "$(dirname "$0")/.." && pwd)"
@@ -53,7 +57,7 @@ for task in "$@"; do
         tail -1 gpurun_out/bench_$i.log >> gpurun_out/bench_lines.jsonl
       done ;;
     prof)
-      prof_py "$TAG" "$R/bench.py" --steps 3 --warmup 2 --synth-steps 0 ${BENCHARGS} || exit 1
+      prof_py "$TAG" "$R/${TREE:+$TREE/}bench.py" --steps 3 --warmup 2 --synth-steps 0 ${BENCHARGS} || exit 1
       t=$(find gpurun_out/$TAG -name "*kernel_trace.csv" | head -1)
       f=$(find gpurun_out/$TAG -name "*kernel_stats.csv" | head -1)
       python tools/prof_summary.py "$f" "$t" > gpurun_out/${TAG}_summary.txt
@@ -90,6 +94,31 @@ for task in "$@"; do
           echo "A $cfg $(tail -1 gpurun_out/ab_A.log | jv)"
           timeout -k 10 300 python bench.py --steps 10 --warmup 3 --config $cfg --synth-steps 0 ${BENCHARGS} > gpurun_out/ab_B.log 2>&1 || { tail -20 gpurun_out/ab_B.log; exit 1; }
           echo "B $cfg $(tail -1 gpurun_out/ab_B.log | jv)"
+        done
+      done ;;
+    abtree)
+      # same-box A/B of the whole tree: ab/base (a git worktree of BASE, built on the CPU) = A, this tree = B
+      [ -f ab/base/bench.py ] || { echo "missing ab/base (git worktree add ab/base <rev> && (cd ab/base && python csrc/build.py))"; exit 1; }
+      for i in $(seq 1 ${ROUNDS:-2}); do
+        for cfg in ${CONFIGS:-LJSpeech}; do
+          (cd ab/base && timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --config $cfg --synth-steps 0 ${BENCHARGS} > ../../gpurun_out/ab_A.log 2>&1) || { tail -20 gpurun_out/ab_A.log; exit 1; }
+          echo "A $cfg $(tail -1 gpurun_out/ab_A.log | jv)"
+          timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --config $cfg --synth-steps 0 ${BENCHARGS} > gpurun_out/ab_B.log 2>&1 || { tail -20 gpurun_out/ab_B.log; exit 1; }
+          echo "B $cfg $(tail -1 gpurun_out/ab_B.log | jv)"
+        done
+      done ;;
+    abexp)
+      # same-box A/B of experiment switches in this tree: EXPS="name=v,name=v|name=v" (| separates arms; "-" = defaults)
+      IFS='|' read -ra ARMS <<< "${EXPS:--}"
+      for i in $(seq 1 ${ROUNDS:-2}); do
+        for cfg in ${CONFIGS:-LJSpeech}; do
+          for arm in "${ARMS[@]}"; do
+            e=$arm; [ "$e" = "-" ] && e=""
+            d=.; [ "$e" = "base" ] && { d=ab/base; e=""; }
+            case "$e" in tree:*) d=${e#tree:}; e="";; esac
+            (cd $d && SSAMD_EXPERIMENTAL="$e" timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --config $cfg --synth-steps 0 ${BENCHARGS} > $R/gpurun_out/abexp.log 2>&1) || { tail -20 gpurun_out/abexp.log; exit 1; }
+            echo "[$arm] $cfg $(tail -1 gpurun_out/abexp.log | jv)"
+          done
         done
       done ;;
     py:*)
