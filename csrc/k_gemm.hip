@@ -819,7 +819,8 @@ __device__ __forceinline__ void pp_barrier() {
 // BNH: the BatchNorm-backward head epilogue (EpiX.bn_*) -- a separate instantiation, so the other
 // variants' epilogues do not carry its registers / code (measured: folded into every variant as a runtime
 // branch it slowed the ReLU-mask data gradient ~25 % and the step ~1.5 %).
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool BNH = false>
+// STG (BUF only): the staggered 8-phase main loop -- see the comment at its loop below.
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool BNH = false, bool STG = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
@@ -957,6 +958,137 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     nk = min(nk_all, kt0 + per);
     Yv = reinterpret_cast<float*>(Yv) + (long)blockIdx.y * g.M * ldy;
   }
+  if constexpr (STG) {
+    // Staggered 8-phase main loop (MI355X: one wave of each group per SIMD, so one wave's MFMA cluster runs
+    // while its partner issues LDS reads and LDS-DMA; loads stay in flight across barriers).
+    // Groups: G0 = waves 0-3 (A rows 0-127), G1 = waves 4-7 (A rows 128-255).  A k-tile is computed in 4
+    // phases, each a quadrant (qa, qb) = (0,0) (0,1) (1,1) (1,0) of the wave's 128 x 64 output (16 MFMAs);
+    // a phase is  R: [LDS-DMA of one staging unit] [ds_reads of the quadrant] [vmcnt]  barrier
+    //             M: setprio(1) [16 MFMAs] setprio(0)  barrier
+    // and G1 runs one barrier behind G0 (an extra barrier before the loop), so G0's M segments pair with
+    // G1's R segments and vice versa.  Units (16 KiB, 2 DMA instructions per lane): U0 = A rows of qa 0
+    // (both groups), U1 = B rows of qb 1, U2 = A rows of qa 1, U3 = B rows of qb 0; the qb 0 B fragments
+    // stay in registers from phase 0 to phase 3, so a unit's last read is in phase 0 (U0, U3), 1 (U1) or
+    // 2 (U2).  With the stagger a unit is rewritten >= 2 phases after its last read (its reads are
+    // retired by both groups' lgkmcnt before the barrier that follows their next segment):
+    //   P2(t): U0(t+2)   P3(t): U1(t+2)   P0(t+1): U2(t+2)   P1(t+1): U3(t+2)    (into tile t's buffer)
+    // RAW: U3(t+2), the last unit of tile t+2, is waited for in P3(t+1)'s R segment -- vmcnt(4) leaves the
+    // 2 units issued after it in flight -- and first read in P0(t+2), a barrier later for both groups.
+    int bblk[4], bvo2[4];  // B 8-row blocks of this wave: U3 (qb = 0) -> [0], [1]; U1 (qb = 1) -> [2], [3]
+    bblk[0] = 8 * (wave >> 2) + (wave & 3);
+    bblk[1] = bblk[0] + 16;
+    bblk[2] = bblk[0] + 4;
+    bblk[3] = bblk[1] + 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = bblk[u] * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      bvo2[u] = (n0 + row < g.N) ? ((n0 + row) * g.K + ch * 8) * 2 : kOOB;
+    }
+    // A 8-row blocks: load i covers block i * 8 + wave (rows 64 i + 8 wave ..): U0 = i in {0, 2}, U2 = {1, 3}
+    auto stage_a = [&](int kt, int q, int buf) {
+      char* As = smem + buf * STG64_BYTES;
+      const int k0 = kt * 64;
+      const int tap = k0 / g.Cin;
+      const int cin0 = k0 - tap * g.Cin;
+      const int shift = tap * g.dil - g.pad;
+      const int aoff = (shift * g.Cin + cin0) * 2;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int i = q + 2 * jj;
+        const int ts = a_t[i] + shift;
+        const bool ok = (unsigned)ts < (unsigned)a_lim[i];
+        buf_lds16(rA, ok ? avo[i] + aoff : kOOB, 0, As + (i * 8 + wave) * 1024);
+      }
+    };
+    auto stage_b = [&](int kt, int q, int buf) {  // q = 0: U3 (qb = 0 rows), q = 1: U1 (qb = 1 rows)
+      char* Bs = smem + buf * STG64_BYTES + BG * 64 * 2;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) buf_lds16(rB, bvo2[q * 2 + jj], kt * 128, Bs + bblk[q * 2 + jj] * 1024);
+    };
+    short8 fa[2][4], fb0[2][2], fb1[2][2];
+    auto read_a = [&](const char* As, int qa) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          fa[kk][i] = *reinterpret_cast<const short8*>(As + swz128(wm * 128 + qa * 64 + i * 16 + (lane & 15), c));
+      }
+    };
+    auto read_b = [&](const char* Bs, int qb, short8 (&fb)[2][2]) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          fb[kk][j] = *reinterpret_cast<const short8*>(Bs + swz128(wn * 64 + qb * 32 + j * 16 + (lane & 15), c));
+      }
+    };
+    auto mma = [&](int qa, int qb, const short8 (&fb)[2][2]) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qa * 4 + i][qb * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[kk][j], fa[kk][i], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    const int nkt = nk - kt0;
+    // prologue: tiles kt0 and kt0 + 1 whole; tile kt0 landed (the 8 younger DMA instructions in flight)
+    if (nkt > 0) { stage_a(kt0, 0, 0); stage_b(kt0, 1, 0); stage_a(kt0, 1, 0); stage_b(kt0, 0, 0); }
+    if (nkt > 1) {
+      stage_a(kt0 + 1, 0, 1); stage_b(kt0 + 1, 1, 1); stage_a(kt0 + 1, 1, 1); stage_b(kt0 + 1, 0, 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    if (wm == 1) pp_barrier();  // G1 runs one barrier behind G0
+    for (int t = 0; t < nkt; ++t) {
+      const int buf = t & 1, kt = kt0 + t;
+      const char* As = smem + buf * STG64_BYTES;
+      const char* Bs = As + BG * 64 * 2;
+      const bool s1 = t >= 1 && t + 1 < nkt;  // U2 / U3 of tile t+1 go out in P0 / P1 of tile t
+      const bool s2 = t + 2 < nkt;            // U0 / U1 of tile t+2 go out in P2 / P3 of tile t
+      // P0
+      if (s1) stage_a(kt + 1, 1, buf ^ 1);
+      read_a(As, 0);
+      read_b(Bs, 0, fb0);
+      pp_barrier();
+      mma(0, 0, fb0);
+      pp_barrier();
+      // P1
+      if (s1) stage_b(kt + 1, 0, buf ^ 1);
+      read_b(Bs, 1, fb1);
+      pp_barrier();
+      mma(0, 1, fb1);
+      pp_barrier();
+      // P2
+      if (s2) stage_a(kt + 2, 0, buf);
+      read_a(As, 1);
+      pp_barrier();
+      mma(1, 1, fb1);
+      pp_barrier();
+      // P3: tile t+1 must be complete before P0(t+1): its last unit (U3, issued in P1) retired here
+      if (s2) stage_b(kt + 2, 1, buf);
+      if (t + 1 < nkt) {
+        if (s2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp_barrier();
+      mma(1, 0, fb0);
+      pp_barrier();
+    }
+    if (wm == 0) pp_barrier();  // equal barrier counts: G0 catches up with G1's extra one
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+  } else {
   // double buffer: stage kt+1 is DMA'd while stage kt is computed (one stage = 1024 MFMA cycles
   // per wave, far longer than an L2-warm LDS-DMA), one barrier per 64-wide k slab
   if (kt0 < nk) stage(kt0, 0);
@@ -983,6 +1115,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
+  }  // !STG
   if constexpr (!OUT_F32) {
     if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
       // LDS-staged epilogue: the accumulator layout gives each lane 4 columns of one row, i.e.
@@ -2345,6 +2478,10 @@ SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 static int g_gemm_buf = 1;  // big64 (FASTK) LDS-DMA through buffer descriptors (0: flat global_load_lds)
 SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
+// big64 buffer-descriptor path: 1 = the staggered 8-phase main loop for K >= 512 (tools/exp_stg.py: +5 % on
+// the k9 convs and K = 1024, +2 % PostNet k5, -1..4 % at K = 256 where the prologue / epilogue dominate)
+static int g_gemm_stg = 1;
+SSAMD_API void ssamd_gemm_set_stg(int v) { g_gemm_stg = v; }
 
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
 static bool big64_buf_ok(const ConvGeom& g) {
@@ -2476,6 +2613,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, false, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, false, false, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, false, false, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, false, true, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, true, true, false, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -2486,6 +2627,11 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
       if constexpr (!F32) {                                                                              \
         if (bnh) kfn = conv_gemm_big64_kernel<false, FK, false, BF, true>;                              \
+      }                                                                                                  \
+      if constexpr (BF) {                                                                                \
+        if (g_gemm_stg && !bnh && g.K >= 512)                                                            \
+          kfn = g.rinfo ? conv_gemm_big64_kernel<F32, true, true, true, false, true>                     \
+                        : conv_gemm_big64_kernel<F32, true, false, true, false, true>;                   \
       }                                                                                                  \
       hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)

@@ -356,6 +356,65 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
   out[c] = acc;
 }
 
+// Style-token bank (reference GST, models/style.py::token_bank): keys = tanh(E) [N][dt];
+//   K[h][n][d] = sum_c keys[n][c] Wk[h*D + d][c],  V likewise with Wv  (T = NH * D outputs per token).
+// Tiny (N <= 64 tokens, dt, T <= 512): one workgroup, fp32, fixed-order sums (bitwise reproducible).
+__global__ void __launch_bounds__(256) token_bank_fwd_kernel(const float* __restrict__ E, const float* __restrict__ Wk,
+                                                             const float* __restrict__ Wv, int N, int dt, int T,
+                                                             int D, float* __restrict__ K, float* __restrict__ V,
+                                                             float* __restrict__ tE) {
+  extern __shared__ float te[];  // [N][dt]
+  for (int i = threadIdx.x; i < N * dt; i += blockDim.x) {
+    const float t = tanhf(E[i]);
+    te[i] = t;
+    tE[i] = t;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N * T; i += blockDim.x) {
+    const int n = i / T, t = i - n * T;
+    float a = 0.f, b = 0.f;
+    for (int c = 0; c < dt; ++c) {
+      const float x = te[n * dt + c];
+      a = fmaf(x, Wk[t * dt + c], a);
+      b = fmaf(x, Wv[t * dt + c], b);
+    }
+    const int h = t / D, d = t - h * D;
+    K[((long)h * N + n) * D + d] = a;
+    V[((long)h * N + n) * D + d] = b;
+  }
+}
+
+// dWk[t][c] = sum_n dK[n][t] tE[n][c];  dE[n][c] = (1 - tE^2) sum_t (dK[n][t] Wk[t][c] + dV[n][t] Wv[t][c])
+__global__ void __launch_bounds__(256) token_bank_bwd_kernel(const float* __restrict__ dK, const float* __restrict__ dV,
+                                                             const float* __restrict__ tE,
+                                                             const float* __restrict__ Wk,
+                                                             const float* __restrict__ Wv, int N, int dt, int T,
+                                                             int D, float* __restrict__ dE, float* __restrict__ dWk,
+                                                             float* __restrict__ dWv) {
+  auto gk = [&](const float* g, int n, int t) {
+    const int h = t / D, d = t - h * D;
+    return g[((long)h * N + n) * D + d];
+  };
+  for (int i = threadIdx.x; i < T * dt; i += blockDim.x) {
+    const int t = i / dt, c = i - t * dt;
+    float a = 0.f, b = 0.f;
+    for (int n = 0; n < N; ++n) {
+      const float x = tE[n * dt + c];
+      a = fmaf(gk(dK, n, t), x, a);
+      b = fmaf(gk(dV, n, t), x, b);
+    }
+    dWk[i] = a;
+    dWv[i] = b;
+  }
+  for (int i = threadIdx.x; i < N * dt; i += blockDim.x) {
+    const int n = i / dt, c = i - n * dt;
+    float a = 0.f;
+    for (int t = 0; t < T; ++t) a = fmaf(gk(dK, n, t), Wk[t * dt + c], fmaf(gk(dV, n, t), Wv[t * dt + c], a));
+    const float x = tE[i];
+    dE[i] = a * (1.f - x * x);
+  }
+}
+
 }  // namespace
 
 static inline int out_dim(int n) { return (n - 1) / 2 + 1; }  // k3, s2, p1
@@ -417,5 +476,22 @@ SSAMD_API int ssamd_token_attn_bwd(const float* dout, const float* q, const floa
   }
   hipLaunchKernelGGL(token_attn_bwd_kernel, dim3(B), dim3(64), 0, s, dout, q, K, V, w, dw, NH, N, D, scale, dq, part);
   hipLaunchKernelGGL(colsum_f32_kernel, dim3(cdiv(ncol, 256)), dim3(256), 0, s, part, (long)B, ncol, dKV);
+  return (int)hipGetLastError();
+}
+
+// K / V [NH][N][D] and tanh(E) [N][dt] of the style-token bank (Wk / Wv: [T = NH*D][dt] Linear weights)
+SSAMD_API int ssamd_token_bank_fwd(const float* E, const float* Wk, const float* Wv, int N, int dt, int T, int NH,
+                                   float* K, float* V, float* tE, hipStream_t s) {
+  if (N <= 0 || NH <= 0 || T % NH || (size_t)N * dt * 4 > 64 * 1024) return -2;
+  hipLaunchKernelGGL(token_bank_fwd_kernel, dim3(1), dim3(256), (size_t)N * dt * 4, s, E, Wk, Wv, N, dt, T, T / NH, K,
+                     V, tE);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_token_bank_bwd(const float* dK, const float* dV, const float* tE, const float* Wk, const float* Wv,
+                                   int N, int dt, int T, int NH, float* dE, float* dWk, float* dWv, hipStream_t s) {
+  if (N <= 0 || NH <= 0 || T % NH) return -2;
+  hipLaunchKernelGGL(token_bank_bwd_kernel, dim3(1), dim3(256), 0, s, dK, dV, tE, Wk, Wv, N, dt, T, T / NH, dE, dWk,
+                     dWv);
   return (int)hipGetLastError();
 }

@@ -65,8 +65,10 @@ KNOBS: Dict[str, tuple] = {
                     "auto when the data-gradient GEMMs have fewer row tiles than wgrad_first_waves x CUs"),
     "wgrad_first_waves": (1.25, float, "auto threshold of wgrad_first, in waves of 256-row tiles per CU"),
     "wgrad_cu_frac": (0.75, _frac, "fraction of the CUs the side-stream weight-gradient split plan is sized for"),
-    "wgrad_cus_all": (False, _bool, "apply the reduced weight-gradient CU plan to every stream (round-3 behaviour)"),
+    "wgrad_cus_all": (True, _bool, "apply the reduced weight-gradient CU plan to every stream (0: side stream "
+                                   "only -- main-stream weight gradients then reduce in a different order)"),
     "ln_fuse": (False, _bool, "residual + LayerNorm tail in the producing GEMM's epilogue (measured slower)"),
+    "gemm_stg": (True, _bool, "staggered 8-phase main loop of the 256x256 GEMM for K >= 512 (+0.7 % LJSpeech)"),
     "bn_fuse": (True, _bool, "PostNet BatchNorm backward started in the data-gradient GEMM's epilogue"),
     "defer_release": (False, _bool, "hand the side-stream weight-gradient inputs back to the trainer, freed "
                                     "during the next forward (holds a step's activations into it)"),
@@ -134,6 +136,24 @@ def overridden() -> Dict[str, Any]:
     """Switches set away from their defaults (recorded in bench output / logs)."""
     _ensure()
     return {k: v for k, v in _values.items() if v != KNOBS[k][0]}
+
+
+class overrides:
+    """Context manager for tests / experiments in one process: ``with overrides(ln_fuse=True): ...``."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        _ensure()
+        self.saved = dict(_values)
+        for k, v in self.kw.items():
+            _set(k, v, "overrides")
+        return self
+
+    def __exit__(self, *a):
+        _values.clear()
+        _values.update(self.saved)
 
 
 def reset_for_tests():

@@ -160,11 +160,7 @@ class GlobalStyleTokens(nn.Module):
 
     def token_bank(self):
         """Keys / values of the style-token bank, [heads, n_tok, token_size/heads] each."""
-        keys = torch.tanh(self.embed)  # [N, ts/h]
-        d = self.token_size // self.n_head
-        k = self.w_key(keys).view(-1, self.n_head, d).transpose(0, 1).contiguous()
-        v = self.w_value(keys).view(-1, self.n_head, d).transpose(0, 1).contiguous()
-        return k, v
+        return ops.token_bank(self.embed, self.w_key.weight, self.w_value.weight, self.n_head)
 
     def token_attention(self, query):
         """query [B, token_size] -> style embedding [B, token_size] and weights [B, heads, n_tok]."""
@@ -183,8 +179,7 @@ class GlobalStyleTokens(nn.Module):
 
     def from_token_weights(self, weights):
         """weights [B, n_tok] (or [B, heads, n_tok]) -> FiLM params; style without audio."""
-        keys = torch.tanh(self.embed)
-        v = self.w_value(keys).view(-1, self.n_head, self.token_size // self.n_head).transpose(0, 1)  # [h,N,d]
+        _, v = self.token_bank()  # [h, N, d]
         if weights.dim() == 2:
             weights = weights.unsqueeze(1).expand(-1, self.n_head, -1)
         o = torch.einsum("bhn,hnd->bhd", weights.float(), v.float()).reshape(weights.shape[0], self.token_size)

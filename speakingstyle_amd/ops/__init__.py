@@ -281,6 +281,18 @@ def gru_last(x, gru, last):
     return out.gather(1, idx).squeeze(1)
 
 
+def token_bank(E, Wk, Wv, n_head):
+    """GST token bank: keys = tanh(E) [N, dt]; K / V = keys @ Wk^T / Wv^T as [n_head, N, D] (fp32)."""
+    if use_hip(E):
+        return _hip().token_bank(E, Wk, Wv, n_head)
+    keys = torch.tanh(E.float())
+    N = keys.shape[0]
+    D = Wk.shape[0] // n_head
+    k = (keys @ Wk.float().t()).view(N, n_head, D).transpose(0, 1).contiguous()
+    v = (keys @ Wv.float().t()).view(N, n_head, D).transpose(0, 1).contiguous()
+    return k, v
+
+
 def token_attention(q, K, V):
     """Multi-head attention of q [B, NH*D] over a token bank K/V [NH, N, D]:
     returns (style [B, NH*D] fp32, weights [B, NH, N])."""

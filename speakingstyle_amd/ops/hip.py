@@ -48,6 +48,7 @@ _SIGS = {
     "ssamd_gemm_set_ngrp": [I],
     "ssamd_wgrad_set_buf": [I],
     "ssamd_gemm_set_buf": [I],
+    "ssamd_gemm_set_stg": [I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],
@@ -1981,6 +1982,51 @@ class _TokenAttnFn(torch.autograd.Function):
 def token_attention(q, K, V):
     """q [B, NH*D], K/V [NH, N, D] -> (style [B, NH*D] fp32, weights [B, NH, N])."""
     return _TokenAttnFn.apply(q, K, V)
+
+
+_SIGS.update({"ssamd_token_bank_fwd": [P, P, P, I, I, I, I, P, P, P, P],
+              "ssamd_token_bank_bwd": [P, P, P, P, P, I, I, I, I, P, P, P, P]})
+
+
+class _TokenBankFn(torch.autograd.Function):
+    """keys = tanh(E); K / V = keys @ Wk^T / Wv^T split into heads [NH, N, D] (reference GST token bank)."""
+
+    @staticmethod
+    def forward(ctx, E, Wk, Wv, n_head):
+        N, dt = E.shape
+        T = Wk.shape[0]
+        Ec, Wkc, Wvc = (t.detach().float().contiguous() for t in (E, Wk, Wv))
+        D = T // n_head
+        K = torch.empty(n_head, N, D, device=E.device, dtype=torch.float32)
+        V = torch.empty_like(K)
+        tE = torch.empty(N, dt, device=E.device, dtype=torch.float32)
+        _check(lib().ssamd_token_bank_fwd(_ptr(Ec), _ptr(Wkc), _ptr(Wvc), N, dt, T, n_head, _ptr(K), _ptr(V), _ptr(tE),
+                                          _stream()), "ssamd_token_bank_fwd")
+        ctx.save_for_backward(tE, Wkc, Wvc)
+        ctx.n_head = n_head
+        ctx.owners = (E, Wk, Wv)
+        return K, V
+
+    @staticmethod
+    def backward(ctx, dK, dV):
+        tE, Wkc, Wvc = ctx.saved_tensors
+        N, dt = tE.shape
+        T = Wkc.shape[0]
+        dK = torch.zeros(ctx.n_head, N, T // ctx.n_head, device=tE.device) if dK is None else dK.float().contiguous()
+        dV = torch.zeros_like(dK) if dV is None else dV.float().contiguous()
+        outs = []
+        for p, shape in zip(ctx.owners, ((N, dt), (T, dt), (T, dt))):
+            slot = gradslots.claim(p)
+            outs.append(slot if slot is not None else torch.empty(shape, device=tE.device, dtype=torch.float32))
+        dE, dWk, dWv = outs
+        _check(lib().ssamd_token_bank_bwd(_ptr(dK), _ptr(dV), _ptr(tE), _ptr(Wkc), _ptr(Wvc), N, dt, T, ctx.n_head,
+                                          _ptr(dE), _ptr(dWk), _ptr(dWv), _stream()), "ssamd_token_bank_bwd")
+        return dE, dWk, dWv, None
+
+
+def token_bank(E, Wk, Wv, n_head):
+    """GST style-token bank keys / values [NH, N, D] (fp32) from the token table E [N, dt]."""
+    return _TokenBankFn.apply(E, Wk, Wv, n_head)
 
 
 # ------------------------------------------------------------------------ vocoder (inference)

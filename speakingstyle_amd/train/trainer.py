@@ -64,6 +64,11 @@ class Trainer:
         # host timestamps of the step tail (backward return .. optimizer launch): diagnostics only
         self._host_tail = [] if experimental.get("host_tail") else None
         self._defer = experimental.get("defer_release")
+        if torch.cuda.is_available():
+            from ..ops import hip
+
+            if hip.available():
+                hip.lib().ssamd_gemm_set_stg(int(experimental.get("gemm_stg")))
         self._held = None
         # backward on the calling thread instead of autograd's per-device worker thread: no thread
         # hand-off per backward and less engine bookkeeping -- host enqueue per step 15.7 -> 12.1 ms
@@ -82,8 +87,12 @@ class Trainer:
         The weight-gradient split plan is also sized for ``wgrad_cu_frac`` of the CUs: its 256x256
         blocks hold a CU's whole LDS, so a plan for every CU locks the data-gradient GEMMs out of the
         GPU until its blocks drain (LJSpeech +0.5 % at 3/4, ``profiles/r3_v10_wgrad_cus_ab.txt``).  The
-        reduced plan applies to side-stream launches only (``ssamd_wgrad_set_cus`` takes the stream): a
-        main-stream weight gradient keeps the whole-device split plan and its reduction order."""
+        plan (and with it the split-M count, i.e. the fp32 reduction order) applies to every stream, so a
+        weight gradient reduces identically whether it runs on the side stream or on the main stream (the
+        first step after a resume, before the single-contribution flags are known): a resumed run
+        continues bit for bit (tests/test_train_gpu.py).  Bitwise reproduction across runs therefore
+        needs the same ``mi355x.stream_priority`` / ``wgrad_cu_frac`` setting; ``ssamd_wgrad_set_cus``
+        can also scope the plan to one stream (switch ``wgrad_cus_all=0``)."""
         dev = self.opt.arena.data.device
         if not (enabled and dev.type == "cuda"):
             return None

@@ -204,22 +204,20 @@ def test_gemm_fused_layernorm(packed, film):
         x0 = hip_pack(x0, lens)
 
     def run(no_fuse):
-        hip._NO_LN_FUSE = no_fuse
-        hip.set_seed(77)
-        blk.zero_grad()
-        x = x0.clone().requires_grad_(True)
-        y = blk(x, lens, style if film else None, pack=pk)
-        g = torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).to(torch.bfloat16)
-        y.backward(g)
-        grads = [p.grad.clone() for p in blk.parameters() if p.grad is not None]
-        return y.detach().float(), x.grad.float(), grads
+        from speakingstyle_amd import experimental
 
-    old = hip._NO_LN_FUSE
-    try:
-        y1, gx1, gp1 = run(False)
-        y2, gx2, gp2 = run(True)
-    finally:
-        hip._NO_LN_FUSE = old
+        with experimental.overrides(ln_fuse=not no_fuse):
+            hip.set_seed(77)
+            blk.zero_grad()
+            x = x0.clone().requires_grad_(True)
+            y = blk(x, lens, style if film else None, pack=pk)
+            g = torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).to(torch.bfloat16)
+            y.backward(g)
+            grads = [p.grad.clone() for p in blk.parameters() if p.grad is not None]
+            return y.detach().float(), x.grad.float(), grads
+
+    y1, gx1, gp1 = run(False)
+    y2, gx2, gp2 = run(True)
     assert _rel(y1, y2) < 2e-3 and _rel(gx1, gx2) < 5e-3
     assert len(gp1) == len(gp2)
     # the two runs may use different GEMM tilings (the fused tail forces the 256x256 kernel), so
@@ -846,6 +844,42 @@ def test_wgrad_ring_vs_reference(Cin, N, ks):
             hip.lib().ssamd_wgrad_set_variant(-1)
         assert _rel(dW, dW_ref) < 1e-2, variant
         assert _rel(db, db_ref) < 1e-2, variant
+
+
+@pytest.mark.parametrize("Cin,N,ks,packed,M", [(256, 1024, 9, True, 61111), (1024, 256, 9, True, 40000),
+                                                (1024, 256, 1, False, 70001), (512, 512, 5, False, 3000),
+                                                (1024, 768, 3, False, 257), (512, 80 * 8, 5, False, 9999)])
+def test_gemm_staggered_loop_bitwise(Cin, N, ks, packed, M):
+    """The staggered 8-phase main loop (ssamd_gemm_set_stg, K >= 512) accumulates every output in the same
+    order as the double-buffer loop: outputs are bitwise equal -- packed / padded rows, ragged M, partial
+    N tiles; a fp32 check anchors both."""
+    torch.manual_seed(31)
+    x = torch.randn(1, M, Cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, ks, Cin, device=DEV) / math.sqrt(ks * Cin)).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    pad = (ks - 1) // 2
+    rinfo = None
+    if packed:
+        from speakingstyle_amd.ops.packing import PackInfo
+
+        n = M // 5
+        lens = torch.tensor([n, n + 7, n - 3, n + 1, M - 4 * n - 5], device=DEV)
+        pk = PackInfo.build(lens, int(lens.max()), int(lens.sum()))
+        assert pk.R == M
+        rinfo = pk.rinfo
+    lib = hip.lib()
+    try:
+        lib.ssamd_gemm_set_stg(0)
+        y0 = hip.conv_gemm_raw(x, w, bias, 1, M, Cin, ks, 1, pad, N, 1, rinfo=rinfo)
+        lib.ssamd_gemm_set_stg(1)
+        y1 = hip.conv_gemm_raw(x, w, bias, 1, M, Cin, ks, 1, pad, N, 1, rinfo=rinfo)
+    finally:
+        lib.ssamd_gemm_set_stg(1)
+    assert torch.equal(y0, y1)
+    if not packed:
+        m = min(M, 600)
+        yr = ref.conv1d(x[:, :m].float(), w.float().permute(0, 2, 1), bias, pad, 1, "relu")
+        assert _rel(y1[:, : m - ks], yr[:, : m - ks]) < 1e-2
 
 
 @pytest.mark.parametrize("Cin,N,ks,packed", [(256, 768, 1, False), (256, 1024, 9, True), (1024, 256, 9, False)])

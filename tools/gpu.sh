@@ -24,7 +24,7 @@ cd "$R"; mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 TAG=${TAG:-run}
 
-jv() { python -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d["value"], d["ms_per_step"], d.get("synth_rtf"))'; }
+jv() { python -c 'import json,sys; d=json.loads([l for l in sys.stdin.read().strip().splitlines() if l.startswith("{")][-1]); print(d["value"], d["ms_per_step"], d.get("synth_rtf"))'; }
 
 prof_py() {  # tag script args...: kernel trace + stats of a python run
   local tag=$1; shift
@@ -91,9 +91,9 @@ for task in "$@"; do
       for i in $(seq 1 ${ROUNDS:-2}); do
         for cfg in ${CONFIGS:-LJSpeech}; do
           SSAMD_KERNEL_LIB=$A timeout -k 10 300 python bench.py --steps 10 --warmup 3 --config $cfg --synth-steps 0 ${BENCHARGS} > gpurun_out/ab_A.log 2>&1 || { tail -20 gpurun_out/ab_A.log; exit 1; }
-          echo "A $cfg $(tail -1 gpurun_out/ab_A.log | jv)"
+          echo "A $cfg $(jv < gpurun_out/ab_A.log)"
           timeout -k 10 300 python bench.py --steps 10 --warmup 3 --config $cfg --synth-steps 0 ${BENCHARGS} > gpurun_out/ab_B.log 2>&1 || { tail -20 gpurun_out/ab_B.log; exit 1; }
-          echo "B $cfg $(tail -1 gpurun_out/ab_B.log | jv)"
+          echo "B $cfg $(jv < gpurun_out/ab_B.log)"
         done
       done ;;
     abtree)
@@ -102,9 +102,9 @@ for task in "$@"; do
       for i in $(seq 1 ${ROUNDS:-2}); do
         for cfg in ${CONFIGS:-LJSpeech}; do
           (cd ab/base && timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --config $cfg --synth-steps 0 ${BENCHARGS} > ../../gpurun_out/ab_A.log 2>&1) || { tail -20 gpurun_out/ab_A.log; exit 1; }
-          echo "A $cfg $(tail -1 gpurun_out/ab_A.log | jv)"
+          echo "A $cfg $(jv < gpurun_out/ab_A.log)"
           timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --config $cfg --synth-steps 0 ${BENCHARGS} > gpurun_out/ab_B.log 2>&1 || { tail -20 gpurun_out/ab_B.log; exit 1; }
-          echo "B $cfg $(tail -1 gpurun_out/ab_B.log | jv)"
+          echo "B $cfg $(jv < gpurun_out/ab_B.log)"
         done
       done ;;
     abexp)
@@ -117,7 +117,7 @@ for task in "$@"; do
             d=.; [ "$e" = "base" ] && { d=ab/base; e=""; }
             case "$e" in tree:*) d=${e#tree:}; e="";; esac
             (cd $d && SSAMD_EXPERIMENTAL="$e" timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --config $cfg --synth-steps 0 ${BENCHARGS} > $R/gpurun_out/abexp.log 2>&1) || { tail -20 gpurun_out/abexp.log; exit 1; }
-            echo "[$arm] $cfg $(tail -1 gpurun_out/abexp.log | jv)"
+            echo "[$arm] $cfg $(jv < gpurun_out/abexp.log)"
           done
         done
       done ;;
