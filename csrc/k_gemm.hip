@@ -816,11 +816,16 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// BNH: the BatchNorm-backward head epilogue (EpiX.bn_*) -- a separate instantiation, so the other
-// variants' epilogues do not carry its registers / code (measured: folded into every variant as a runtime
-// branch it slowed the ReLU-mask data gradient ~25 % and the step ~1.5 %).
+// EPIM: epilogue specialisations, each its own instantiation so the other variants' code / registers are
+// untouched (measured: the BatchNorm head folded into every variant as a runtime branch slowed the
+// ReLU-mask data gradient ~25 % and the step ~1.5 %):
+//   EPI_BNH   the BatchNorm-backward head (EpiX aliases, see EpiX);
+//   EPI_MASK  the ReLU-bitmask data gradient (mask_in only): the thread's 16 mask bytes (one per row it
+//             stores) are loaded before the prologue's drain, instead of as dependent byte loads inside the
+//             epilogue (one exposed memory round trip per 8 rows with nothing else in flight).
 // STG (BUF only): the staggered 8-phase main loop -- see the comment at its loop below.
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, bool BNH = false, bool STG = false>
+constexpr int EPI_GEN = 0, EPI_BNH = 1, EPI_MASK = 2;
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, int EPIM = EPI_GEN, bool STG = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
@@ -948,6 +953,18 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (float4v){0.f, 0.f, 0.f, 0.f};
 
+  // EPI_MASK: this thread's epilogue mask bytes (rows r0 + 16 it of column chunk c), loaded now so that
+  // they land with the prologue's LDS-DMA instead of as dependent loads in the epilogue
+  unsigned char mpre[16];
+  if constexpr (EPIM == EPI_MASK) {
+    const int c = tid & 31, r0 = tid >> 5;
+    const int n = n0 + c * 8;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int m = m0 + r0 + 16 * it;
+      mpre[it] = (n < g.N && m < g.M) ? ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : (unsigned char)0;
+    }
+  }
   // split-K (gridDim.y > 1): block y owns the k slabs [kt0, kt1) and writes its fp32 partial
   // tile to slice y of the workspace (Yv), reduced afterwards in a fixed order (splitk_reduce)
   const int nk_all = (g.K + 63) / 64;
@@ -1155,7 +1172,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       }
       __syncthreads();
       bf16_t* Y = reinterpret_cast<bf16_t*>(Yv);
-      if constexpr (BNH) {
+      if constexpr (EPIM == EPI_BNH) {
         // BatchNorm-backward head (EpiX aliases: acc = bn_h, ln_w = [mean | rstd | scale | shift] x N,
         // mean = partials, post_act = act code, pre_p = dropout p).  Thread (c = tid & 31, r0 = tid >> 5)
         // owns column chunk c of rows r0 + 16 it, loads h for EPG rows before use, stores dz and keeps
@@ -1353,7 +1370,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             if (in && aux) va[u] = *reinterpret_cast<const short8*>(aux + off);
             if (in && resid) vr[u] = *reinterpret_cast<const short8*>(resid + off);
             if (in && ex.acc) vc[u] = *reinterpret_cast<const short8*>(ex.acc + off);
-            mb[u] = (in && ex.mask_in) ? (unsigned)ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : 0xffu;
+            if constexpr (EPIM == EPI_MASK) mb[u] = mpre[g0 + u];
+            else mb[u] = (in && ex.mask_in) ? (unsigned)ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : 0xffu;
             vv[u] = true;
             if (in && lens) {
               const int bb = m / g.L, tt = m - bb * g.L;
@@ -2481,6 +2499,8 @@ SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
 // big64 buffer-descriptor path: 1 = the staggered 8-phase main loop for K >= 512 (tools/exp_stg.py: +5 % on
 // the k9 convs and K = 1024, +2 % PostNet k5, -1..4 % at K = 256 where the prologue / epilogue dominate)
 static int g_gemm_stg = 1;
+static int g_gemm_mask_pre = 1;  // EPI_MASK for the ReLU-mask data gradient (0: the generic epilogue, A/B)
+SSAMD_API void ssamd_gemm_set_mask_pre(int v) { g_gemm_mask_pre = v; }
 SSAMD_API void ssamd_gemm_set_stg(int v) { g_gemm_stg = v; }
 
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
@@ -2610,28 +2630,43 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, false, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, false, true, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, false, false, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, false, false, false, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, false, true, false, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, true, true, false, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<true, true, false, true, false, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<true, true, true, true, false, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_BNH>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, false, EPI_BNH>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, false, false, false, EPI_BNH>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_GEN, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_GEN, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, false, true, EPI_GEN, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<true, true, true, true, EPI_GEN, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_MASK>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_MASK>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_MASK, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_MASK, true>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
     const bool fastk = (Cin % 64) == 0;
     const size_t LB = B64_LDS;
+    // the ReLU-mask data gradient with nothing else in its epilogue: mask bytes prefetched (EPI_MASK)
+    const bool mask_pre = ex.mask_in && !ex.mask_out && !bnh && !aux && !resid && !lens && !ex.acc && !ex.y2 &&
+                          !ex.post_act && ex.scale == 1.f && !ex.ln_out && !out_f32 && act >= 0 && ldy == N;
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
+      const bool stg_ = g_gemm_stg && g.K >= 512;                                                        \
       if constexpr (!F32) {                                                                              \
-        if (bnh) kfn = conv_gemm_big64_kernel<false, FK, false, BF, true>;                              \
+        if (bnh) kfn = conv_gemm_big64_kernel<false, FK, false, BF, EPI_BNH>;                           \
       }                                                                                                  \
       if constexpr (BF) {                                                                                \
-        if (g_gemm_stg && !bnh && g.K >= 512)                                                            \
-          kfn = g.rinfo ? conv_gemm_big64_kernel<F32, true, true, true, false, true>                     \
-                        : conv_gemm_big64_kernel<F32, true, false, true, false, true>;                   \
+        if (stg_ && !bnh)                                                                                \
+          kfn = g.rinfo ? conv_gemm_big64_kernel<F32, true, true, true, EPI_GEN, true>                   \
+                        : conv_gemm_big64_kernel<F32, true, false, true, EPI_GEN, true>;                 \
+        if constexpr (!F32) {                                                                            \
+          if (g_gemm_mask_pre && mask_pre)                                                               \
+            kfn = stg_ ? (g.rinfo ? conv_gemm_big64_kernel<false, true, true, true, EPI_MASK, true>       \
+                                  : conv_gemm_big64_kernel<false, true, false, true, EPI_MASK, true>)    \
+                       : (g.rinfo ? conv_gemm_big64_kernel<false, true, true, true, EPI_MASK>             \
+                                  : conv_gemm_big64_kernel<false, true, false, true, EPI_MASK>);         \
+        }                                                                                                \
       }                                                                                                  \
       hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)

@@ -49,6 +49,7 @@ _SIGS = {
     "ssamd_wgrad_set_buf": [I],
     "ssamd_gemm_set_buf": [I],
     "ssamd_gemm_set_stg": [I],
+    "ssamd_gemm_set_mask_pre": [I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],

@@ -1285,6 +1285,18 @@ def test_relu_bitmask_epilogue_gpu():
     d_mask = hip.conv_gemm_mask_raw(dz, w2, None, B, L, C, 1, 0, H, 0, mask_in=mask)
     d_aux = hip.conv_gemm_raw(dz, w2, None, B, L, C, 1, 1, 0, H, 0, aux=h)
     assert torch.equal(d_mask, d_aux)
+    # the EPI_MASK instantiation (mask bytes prefetched before the prologue drain) == the generic epilogue;
+    # K = 256 (double buffer) and K = 1024 (staggered loop), ragged row count
+    for K_ in (C, 1024):
+        dz2 = torch.randn(1, 1001, K_, device=DEV).to(torch.bfloat16)
+        w3 = (torch.randn(H, 1, K_, device=DEV) / K_ ** 0.5).to(torch.bfloat16)
+        m2 = torch.randint(0, 256, (1001, H // 8), device=DEV, dtype=torch.uint8)
+        try:
+            hip.lib().ssamd_gemm_set_mask_pre(0)
+            ref_ = hip.conv_gemm_mask_raw(dz2, w3, None, 1, 1001, K_, 1, 0, H, 0, mask_in=m2)
+        finally:
+            hip.lib().ssamd_gemm_set_mask_pre(1)
+        assert torch.equal(hip.conv_gemm_mask_raw(dz2, w3, None, 1, 1001, K_, 1, 0, H, 0, mask_in=m2), ref_)
 
 
 @pytest.mark.parametrize("act,use_bias,use_res,packed", [(0, False, True, False), (1, True, False, False),
