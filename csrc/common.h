@@ -82,7 +82,10 @@ static __device__ __forceinline__ float bn_act_fwd(int act, float z) {
 }
 // derivative of act at the pre-activation z
 static __device__ __forceinline__ float bn_act_grad(int act, float z) {
-  if (act == 1) { const float t = bn_fast_tanh(z); return 1.f - t * t; }
+  if (act == 1) {  // 1 - tanh^2 = 4 r (1 - r), r = 1 / (exp(2z) + 1): no cancellation where |tanh| -> 1
+    const float r = __builtin_amdgcn_rcpf(__expf(2.f * z) + 1.f);
+    return 4.f * (r - r * r);
+  }
   if (act == 2) return z > 0.f ? 1.f : 0.f;
   return 1.f;
 }

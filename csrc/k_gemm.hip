@@ -965,6 +965,19 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       mpre[it] = (n < g.N && m < g.M) ? ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : (unsigned char)0;
     }
   }
+  // EPI_BNH: the BatchNorm input h of this thread's 16 epilogue rows (64 VGPRs, free in the double-buffer
+  // loop): the 128-KiB tile read lands under the main loop instead of as a chip-wide burst in the epilogue
+  short8 hpre[16];
+  if constexpr (EPIM == EPI_BNH) {
+    const int c = tid & 31, r0 = tid >> 5;
+    const int n = n0 + c * 8;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int m = m0 + r0 + 16 * it;
+      hpre[it] = (short8){0, 0, 0, 0, 0, 0, 0, 0};  // rows / columns out of range: h = 0 (their dz is 0 too)
+      if (n < g.N && m < g.M) hpre[it] = *reinterpret_cast<const short8*>(ex.acc + (long)m * ldy + n);
+    }
+  }
   // split-K (gridDim.y > 1): block y owns the k slabs [kt0, kt1) and writes its fp32 partial
   // tile to slice y of the workspace (Yv), reduced afterwards in a fixed order (splitk_reduce)
   const int nk_all = (g.K + 63) / 64;
@@ -1171,42 +1184,47 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         }
       }
       __syncthreads();
+      // the prefetched mask bytes were retired by the main loop's inline-asm waits, which the waitcnt pass
+      // does not see: without this counted wait it drains every earlier row's store before each row
+      if constexpr (EPIM == EPI_MASK) __builtin_amdgcn_s_waitcnt(0x0F70);
       bf16_t* Y = reinterpret_cast<bf16_t*>(Yv);
       if constexpr (EPIM == EPI_BNH) {
         // BatchNorm-backward head (EpiX aliases: acc = bn_h, ln_w = [mean | rstd | scale | shift] x N,
         // mean = partials, post_act = act code, pre_p = dropout p).  Thread (c = tid & 31, r0 = tid >> 5)
         // owns column chunk c of rows r0 + 16 it, loads h for EPG rows before use, stores dz and keeps
         // its 8 columns' running sums; the tile's 16 per-column partials are then combined in fixed order.
+        // The epilogue runs while the CU's MFMAs idle (one workgroup per CU), so its VALU count is the
+        // cost: the activation is a compile-time branch of the row loop (a per-element runtime branch
+        // split every row into 8 basic blocks), tanh' = 4 r (1 - r) with r = 1 / (exp(2z) + 1) and the
+        // exp2 scale folded into the BatchNorm affine, the rstd of sum dz * xhat applied once per column.
         constexpr int EPI = BG * 32 / NT3;
-        constexpr int EPG = 8;
         const int c = tid & 31, r0 = tid >> 5;
         const int n = n0 + c * 8;
         const bool col_ok = n < g.N;
-        float bmu[8], brs[8], bsc[8], bsh[8], bs1[8], bs2[8];
+        float bmu[8], bsc[8], bsh[8], bs1[8], bs2[8];
+        const int act_c = ex.post_act;
+        const float zs = act_c == 1 ? 2.8853900817779268f : 1.f;  // 2 log2(e): exp(2z) = exp2(zs z)
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int nq = col_ok ? n + q : 0;
           bmu[q] = ex.ln_w[nq];
-          brs[q] = ex.ln_w[g.N + nq];
-          bsc[q] = ex.ln_w[2 * g.N + nq];
-          bsh[q] = ex.ln_w[3 * g.N + nq];
+          bsc[q] = ex.ln_w[2 * g.N + nq] * zs;
+          bsh[q] = ex.ln_w[3 * g.N + nq] * zs;
           bs1[q] = 0.f;
           bs2[q] = 0.f;
         }
-        const int act_c = ex.post_act;
+        // vmcnt counts stores as well as loads: a load the waitcnt pass still thinks outstanding (the h
+        // prefetch, retired by the main loop's inline-asm waits it cannot see; the column constants) makes
+        // it wait with vmcnt(0) -- i.e. for every dz store issued so far -- before the first use in each
+        // row.  One counted wait here retires them all for the pass; the rows are straight-line code (no
+        // per-row skip: out-of-range rows have dz = 0 and h = 0 and only their store is predicated).
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unconstrained
+        auto rows = [&](auto actc) {
+          constexpr int A = decltype(actc)::value;
 #pragma unroll
-        for (int g0 = 0; g0 < EPI; g0 += EPG) {
-          short8 hb[EPG];
-#pragma unroll
-          for (int u = 0; u < EPG; ++u) {
-            const int m = m0 + r0 + 16 * (g0 + u);
-            if (col_ok && m < g.M) hb[u] = *reinterpret_cast<const short8*>(ex.acc + (long)m * ldy + n);
-          }
-#pragma unroll
-          for (int u = 0; u < EPG; ++u) {
-            const int r = r0 + 16 * (g0 + u);
+          for (int it = 0; it < EPI; ++it) {
+            const int r = r0 + 16 * it;
             const int m = m0 + r;
-            if (m >= g.M || !col_ok) continue;
             const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
             const long off = (long)m * ldy + n;
             float ks[8];
@@ -1214,16 +1232,26 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             short8 o;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-              const float hv = bf2f((bf16_t)hb[u][q]);
+              const float hv = bf2f((bf16_t)hpre[it][q]);
               float d = bf2f((bf16_t)v[q]) * ks[q];
-              if (act_c) d *= bn_act_grad(act_c, hv * bsc[q] + bsh[q]);
+              if constexpr (A == 1) {
+                const float rr = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(hv * bsc[q] + bsh[q]) + 1.f);
+                d *= 4.f * (rr - rr * rr);
+              } else if constexpr (A == 2) {
+                d = hv * bsc[q] + bsh[q] > 0.f ? d : 0.f;
+              }
               bs1[q] += d;
-              bs2[q] += d * (hv - bmu[q]) * brs[q];
+              bs2[q] += d * (hv - bmu[q]);
               o[q] = (short)f2bf(d);
             }
-            *reinterpret_cast<short8*>(Y + off) = o;
+            if (m < g.M && col_ok) *reinterpret_cast<short8*>(Y + off) = o;
           }
-        }
+        };
+        if (act_c == 1) rows(std::integral_constant<int, 1>{});
+        else if (act_c == 2) rows(std::integral_constant<int, 2>{});
+        else rows(std::integral_constant<int, 0>{});
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bs2[q] *= ex.ln_w[g.N + (col_ok ? n + q : 0)];  // x rstd
         __syncthreads();  // every Ct read is done: reuse the staging LDS for the partials
         float* red = reinterpret_cast<float*>(smem);  // [2][16][256]
 #pragma unroll

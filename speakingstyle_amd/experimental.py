@@ -69,6 +69,7 @@ KNOBS: Dict[str, tuple] = {
                                    "only -- main-stream weight gradients then reduce in a different order)"),
     "ln_fuse": (False, _bool, "residual + LayerNorm tail in the producing GEMM's epilogue (measured slower)"),
     "gemm_stg": (True, _bool, "staggered 8-phase main loop of the 256x256 GEMM for K >= 512 (+0.7 % LJSpeech)"),
+    "gemm_mask_pre": (True, _bool, "ReLU-mask data gradient with its mask bytes prefetched before the main loop"),
     "bn_fuse": (True, _bool, "PostNet BatchNorm backward started in the data-gradient GEMM's epilogue"),
     "defer_release": (False, _bool, "hand the side-stream weight-gradient inputs back to the trainer, freed "
                                     "during the next forward (holds a step's activations into it)"),

@@ -1,7 +1,7 @@
 """PostNet BatchNorm backward costs at the LJSpeech shape (R = 200 x 680 padded rows, C = 512, k5): the
 plain data-gradient GEMM vs the GEMM with the BatchNorm-backward head (EPI_BNH: dz + column partials in
 the epilogue), the dz apply pass, and the unfused reduce + apply pair (ssamd_bn_bwd) for reference.
-Usage (GPU box): python tools/exp_bnh.py"""
+Usage (GPU box): python tools/exp_bnh.py [pmc]   (pmc: 3 launches per arm, no timing -- for rocprofv3 --pmc)"""
 import json
 import statistics
 import sys
@@ -42,9 +42,14 @@ def main():
     def plain():
         return hip.conv_gemm_raw(dout, wimg, None, 1, R, C, ks, 1, 2, C)
 
-    def bnh(p):
+    def plain_nostg():
+        lib.ssamd_gemm_set_stg(0)
+        plain()
+        lib.ssamd_gemm_set_stg(1)
+
+    def bnh(p, act=1):
         return lambda: lib.ssamd_conv_gemm_bnbwd(_ptr(dout), _ptr(wimg), _ptr(dz), 1, R, C, ks, 1, 2, C, _ptr(h),
-                                                 _ptr(stats), _ptr(part), 1, p, 1234, _stream())
+                                                 _ptr(stats), _ptr(part), act, p, 1234, _stream())
 
     def apply_dz():
         return lib.ssamd_bn_bwd_dz(_ptr(dz), _ptr(h), _ptr(gamma), _ptr(stats), _ptr(part), nparts, _ptr(dh),
@@ -55,8 +60,14 @@ def main():
                                 _ptr(stats[1]), _ptr(dh), _ptr(dg), _ptr(db), R, C, 1, 1, 0.5, 1234, _ptr(ws),
                                 _stream())
 
-    arms = {"gemm_plain": plain, "gemm_bnh_p0.5": bnh(0.5), "gemm_bnh_p0": bnh(0.0), "apply_dz": apply_dz,
+    arms = {"gemm_plain": plain, "gemm_plain_nostg": plain_nostg, "gemm_bnh_p0.5": bnh(0.5), "gemm_bnh_p0": bnh(0.0), "gemm_bnh_p0_noact": bnh(0.0, 0), "apply_dz": apply_dz,
             "bn_bwd_unfused(reduce+apply)": unfused}
+    if len(sys.argv) > 1 and sys.argv[1] == "pmc":
+        for f in arms.values():
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+        return
     t = {k: [] for k in arms}
     for f in arms.values():
         f()

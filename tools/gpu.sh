@@ -18,6 +18,7 @@
 #   abexp            same-box A/B of experiment switches: EXPS="arm1|arm2|..." (arm = name=v,name=v, - = defaults,
 #                    base = the ab/base tree)
 #   py:<script>      python <script> (a tools/ experiment), output -> gpurun_out/<script>.log
+#   pmcpy:<script>   PMC passes (PASSES="ctr ctr ...|ctr ...") of python <script> $PYARGS -> gpurun_out/<script>_pmc.txt
 set -o pipefail
 R="$(cd "$(dirname "$0")/.." && pwd)"
 cd "$R"; mkdir -p gpurun_out
@@ -125,6 +126,17 @@ for task in "$@"; do
       s=${task#py:}; b=$(basename "$s" .py)
       timeout -k 10 400 python -u "$s" ${PYARGS} > gpurun_out/$b.log 2>&1 || { tail -40 gpurun_out/$b.log; exit 1; }
       tail -${PYTAIL:-25} gpurun_out/$b.log ;;
+    pmcpy:*)
+      s=${task#pmcpy:}; b=$(basename "$s" .py)
+      IFS='|' read -ra PS <<< "${PASSES:-$SQ}"
+      rm -rf gpurun_out/${b}_pmc; i=0
+      for ctr in "${PS[@]}"; do
+        i=$((i + 1))
+        pmc_py ${b}_pmc/p$i "$ctr" "$R/$s" ${PYARGS} || exit 1
+      done
+      python tools/pmc_kernels.py gpurun_out/${b}_pmc "${PMCFILT:-}" > gpurun_out/${b}_pmc.txt || exit 1
+      rm -rf gpurun_out/${b}_pmc
+      cat gpurun_out/${b}_pmc.txt ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done
