@@ -244,7 +244,8 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const void* __restric
 
 __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ pdb, const float* __restrict__ pdg,
                                                              int nblk, int C, float* __restrict__ dbeta,
-                                                             float* __restrict__ dgamma) {
+                                                             float* __restrict__ dgamma,
+                                                             const float* __restrict__ gscale = nullptr) {
   const int c = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
@@ -254,7 +255,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __rest
   for (int o = 32; o > 0; o >>= 1) { x += __shfl_xor(x, o, 64); y += __shfl_xor(y, o, 64); }
   if (lane == 0) {
     dbeta[c] = (float)x;
-    dgamma[c] = (float)y;
+    dgamma[c] = gscale ? (float)(y * (double)gscale[c]) : (float)y;  // gscale: per-column rstd (GEMM partials)
   }
 }
 
@@ -320,6 +321,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const void* __restrict
 
 // dh = k1 * dz + k2 * h + k3 from dz that the producing data-gradient GEMM already formed (dy * keep *
 // act'), k_gemm.hip EpiX.bn_*: a pure two-read / one-write stream (no dropout hash, no tanh here)
+template <int U>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_dz_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ h,
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ stats,
@@ -347,7 +349,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_dz_kernel(const bf16_t* __res
       k3[i] = 0.f;
     }
   }
-  constexpr int U = 8;  // rows per thread and load batch: 16 loads of 16 B in flight per lane
+  // U rows per thread and load batch: 2U loads of 16 B in flight per lane
   const long stride = (long)gridDim.x * m.rows_iter;
   for (long r0 = (long)blockIdx.x * m.rows_iter + ro; r0 < R; r0 += U * stride) {
     short8 a[U], b[U];
@@ -439,6 +441,14 @@ SSAMD_API int ssamd_bn_bwd(const void* dy, int dy_f32, const bf16_t* h, const fl
   return (int)hipGetLastError();
 }
 
+// apply-dz geometry: 8 rows per thread, <= 1024 blocks (4 per CU) looping -- 4.8 TB/s at the PostNet shape vs
+// 3.3 with one pass per block over 4250 blocks (tools/exp_bnh.py sweep, profiles/r4_exp_bn_apply_dz.jsonl)
+static int g_bn_dz_u = 8, g_bn_dz_grid = 1024;
+SSAMD_API void ssamd_bn_set_dz_cfg(int u, int grid) {
+  g_bn_dz_u = u;
+  g_bn_dz_grid = grid;
+}
+
 // Second half of the BatchNorm backward when the data-gradient GEMM produced dz and the column partials
 // (ssamd_conv_gemm_bnbwd): fixed-order combine of the nparts per-tile partials -> dbeta / dgamma, then
 // dh = k1 * dz + k2 * h + k3.  stats = [mean | rstd | scale | shift] x C (the forward's).
@@ -451,13 +461,22 @@ SSAMD_API int ssamd_bn_bwd_dz(const bf16_t* dz, const bf16_t* h, const float* ga
     hipMemsetAsync(dbeta, 0, C * 4, s);
     return (int)hipGetLastError();
   }
+  // the GEMM head's second partial is sum dz * (h - mean): rstd is applied here, once per column
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(NT), 0, s, part, part + (long)nparts * C, nparts,
-                     C, dbeta, dgamma);
+                     C, dbeta, dgamma, stats + C);
   const RowMap m = {C / 8, NT / (C / 8)};
-  // one row batch (8 rows per thread) per block and pass: >= 2048 blocks keep every CU streaming
-  const long per = (long)m.rows_iter * 8;
-  const int g = (int)max(1L, min((R + per - 1) / per, 8192L));
-  hipLaunchKernelGGL(bn_bwd_apply_dz_kernel, dim3(g), dim3(NT), 0, s, dz, h, gamma, stats, dbeta, dgamma, dh, R, C,
-                     training);
+  // one row batch (U rows per thread) per block and pass: >= 2048 blocks keep every CU streaming
+  const int U = g_bn_dz_u;
+  const long per = (long)m.rows_iter * U;
+  const int g = (int)max(1L, min((R + per - 1) / per, (long)g_bn_dz_grid));
+  if (U == 4)
+    hipLaunchKernelGGL(bn_bwd_apply_dz_kernel<4>, dim3(g), dim3(NT), 0, s, dz, h, gamma, stats, dbeta, dgamma, dh, R,
+                       C, training);
+  else if (U == 16)
+    hipLaunchKernelGGL(bn_bwd_apply_dz_kernel<16>, dim3(g), dim3(NT), 0, s, dz, h, gamma, stats, dbeta, dgamma, dh, R,
+                       C, training);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_dz_kernel<8>, dim3(g), dim3(NT), 0, s, dz, h, gamma, stats, dbeta, dgamma, dh, R,
+                       C, training);
   return (int)hipGetLastError();
 }

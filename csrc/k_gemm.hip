@@ -105,7 +105,7 @@ struct EpiX {
   // BatchNorm backward head (PostNet; the BNH instantiation of the big64 LDS-staged epilogue, bf16 out,
   // ldy == N): the GEMM output is dy = dL/d(BN-act-dropout output) of the layer whose pre-BN input is
   // bn_h [M][N]; the epilogue stores  dz = dy * keep(seed, p) * act'(bn_h * scale + shift)  instead of dy
-  // and writes the tile's column partials  sum_rows dz  and  sum_rows dz * (bn_h - mean) * rstd  to
+  // and writes the tile's column partials  sum_rows dz  and  sum_rows dz * (bn_h - mean)  to
   // bn_part[tm][N] and bn_part[nM + tm][N] (tm = M tile; fixed order, no atomics).  bn_stats = the
   // forward's [mean | rstd | scale | shift] x N.  The partial sums replace k_bn.hip's bn_bwd_reduce pass
   // (a full re-read of dy and bn_h); the dropout mask and act' are bit-identical to it.  The fields
@@ -689,20 +689,47 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
     __builtin_amdgcn_s_barrier();
     buf = (buf + 1) % NSTAGE;
   }
+  // Every global operand of the 16 (i, j) fragments (bias columns, row validity, aux / residual /
+  // accumulator segments) is loaded before the first store: one load per fragment between stores made
+  // each wait (vmcnt counts stores too) drain the stores before it -- 16 serialised round trips per wave.
+  float4 bvj[4];
+  short4v xa[4][4], xr[4][4], xc[4][4];
+  bool vrow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+    bvj[j] = (bias && n < g.N) ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    const int mm = m < g.M ? m : 0;
+    const int bb = mm / g.L, tt = mm - bb * g.L;
+    vrow[i] = lens == nullptr || tt < (int)lens[bb];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      const bool in = m < g.M && n < g.N;
+      const long off = (long)m * ldy + n;
+      if (in && aux) xa[i][j] = *reinterpret_cast<const short4v*>(aux + off);
+      if (in && resid) xr[i][j] = *reinterpret_cast<const short4v*>(resid + off);
+      if constexpr (!OUT_F32) {
+        if (in && ex.acc) xc[i][j] = *reinterpret_cast<const short4v*>(ex.acc + off);
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
     if (m >= g.M) continue;
-    const int bb = m / g.L, tt = m - bb * g.L;
-    const bool valid = lens == nullptr || tt < (int)lens[bb];
+    const bool valid = vrow[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
       if (n >= g.N) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (bias) {
-        const float4 bv = *reinterpret_cast<const float4*>(bias + n);
-        v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+        v[0] += bvj[j].x; v[1] += bvj[j].y; v[2] += bvj[j].z; v[3] += bvj[j].w;
       }
       if (act == ACT_RELU) {
 #pragma unroll
@@ -716,23 +743,20 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_ring_kernel(const bf16_t* __
       }
       const long off = (long)m * ldy + n;
       if (aux) {
-        const short4v x = *reinterpret_cast<const short4v*>(aux + off);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
+        for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)xa[i][j][q]) > 0.f ? v[q] : 0.f;
       }
       if (resid) {
-        const short4v x = *reinterpret_cast<const short4v*>(resid + off);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
+        for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)xr[i][j][q]);
       }
       if (!valid) v[0] = v[1] = v[2] = v[3] = 0.f;
       if constexpr (OUT_F32) {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         if (ex.acc) {
-          const short4v x = *reinterpret_cast<const short4v*>(ex.acc + off);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
+          for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)xc[i][j][q]);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = valid ? v[q] * ex.scale : 0.f;
@@ -965,18 +989,25 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       mpre[it] = (n < g.N && m < g.M) ? ex.mask_in[(long)m * (g.N >> 3) + (n >> 3)] : (unsigned char)0;
     }
   }
-  // EPI_BNH: the BatchNorm input h of this thread's 16 epilogue rows (64 VGPRs, free in the double-buffer
-  // loop): the 128-KiB tile read lands under the main loop instead of as a chip-wide burst in the epilogue
+  // EPI_BNH: the BatchNorm input h of this thread's 16 epilogue rows.  The first BNH_PRE rows (4 VGPRs each)
+  // are loaded now and land under the main loop; the rest (register budget: the whole 16 would push the
+  // epilogue past 256 VGPRs) are issued right after the accumulator staging, before its barrier
+  constexpr int BNH_PRE = 16;
   short8 hpre[16];
-  if constexpr (EPIM == EPI_BNH) {
+  unsigned long long dbg_t[5];  // EXPERIMENT stamps (BNH only), written once at the end
+  auto load_h = [&](int it0, int it1) {
     const int c = tid & 31, r0 = tid >> 5;
     const int n = n0 + c * 8;
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
+    for (int it = it0; it < it1; ++it) {
       const int m = m0 + r0 + 16 * it;
       hpre[it] = (short8){0, 0, 0, 0, 0, 0, 0, 0};  // rows / columns out of range: h = 0 (their dz is 0 too)
       if (n < g.N && m < g.M) hpre[it] = *reinterpret_cast<const short8*>(ex.acc + (long)m * ldy + n);
     }
+  };
+  if constexpr (EPIM == EPI_BNH) {
+    load_h(0, BNH_PRE);
+    dbg_t[0] = __builtin_amdgcn_s_memrealtime();
   }
   // split-K (gridDim.y > 1): block y owns the k slabs [kt0, kt1) and writes its fp32 partial
   // tile to slice y of the workspace (Yv), reduced afterwards in a fixed order (splitk_reduce)
@@ -1146,6 +1177,9 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     __builtin_amdgcn_s_barrier();
   }
   }  // !STG
+  if constexpr (EPIM == EPI_BNH) {
+    dbg_t[1] = __builtin_amdgcn_s_memrealtime();
+  }
   if constexpr (!OUT_F32) {
     if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
       // LDS-staged epilogue: the accumulator layout gives each lane 4 columns of one row, i.e.
@@ -1155,33 +1189,59 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       // (Measured: the direct register stores cost up to 55 % of a K = 256 GEMM.)
       constexpr int RSB = 528;
       char* Ct = smem;
+      // bias and activation are compile-time branches of the staging loop: as runtime checks inside the
+      // unrolled 8 x 4 loop they cost ~350 scalar branches per tile, and the bias float4 was re-loaded
+      // (behind a full vmcnt wait) for every (i, j) -- 32 serialised L2 round trips per tile
+      auto stage_tile = [&](auto actc, auto biasc) {
+        constexpr int A = decltype(actc)::value;
+        constexpr bool HB = decltype(biasc)::value;
+        float4 bv[4];
+        if constexpr (HB) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int ml = wm * 128 + i * 16 + (lane & 15);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int nl = wn * 64 + j * 16 + 4 * (lane >> 4);
-          const int n = n0 + nl;
-          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          if (bias && n < g.N) {
-            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
-            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+          for (int j = 0; j < 4; ++j) {
+            const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+            bv[j] = n < g.N ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
           }
-          if (act == ACT_RELU) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-          } else if (act == ACT_LRELU) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
-          } else if (act == ACT_TANH) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
-          }
-          short4v o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
-          *reinterpret_cast<short4v*>(Ct + ml * RSB + nl * 2) = o;
         }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int ml = wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int nl = wn * 64 + j * 16 + 4 * (lane >> 4);
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if constexpr (HB) {
+              v[0] += bv[j].x; v[1] += bv[j].y; v[2] += bv[j].z; v[3] += bv[j].w;
+            }
+            if constexpr (A == ACT_RELU) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+            } else if constexpr (A == ACT_LRELU) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+            } else if constexpr (A == ACT_TANH) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+            }
+            short4v o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
+            *reinterpret_cast<short4v*>(Ct + ml * RSB + nl * 2) = o;
+          }
+        }
+      };
+      auto stage_act = [&](auto biasc) {
+        if (act == ACT_RELU) stage_tile(std::integral_constant<int, ACT_RELU>{}, biasc);
+        else if (act == ACT_LRELU) stage_tile(std::integral_constant<int, ACT_LRELU>{}, biasc);
+        else if (act == ACT_TANH) stage_tile(std::integral_constant<int, ACT_TANH>{}, biasc);
+        else stage_tile(std::integral_constant<int, ACT_NONE>{}, biasc);
+      };
+      if constexpr (EPIM == EPI_BNH) stage_tile(std::integral_constant<int, ACT_NONE>{}, std::false_type{});  // no bias / act
+      else if (bias) stage_act(std::true_type{});
+      else stage_act(std::false_type{});
+      if constexpr (EPIM == EPI_BNH) {
+        load_h(BNH_PRE, 16);
+        dbg_t[4] = __builtin_amdgcn_s_memrealtime();
       }
       __syncthreads();
       // the prefetched mask bytes were retired by the main loop's inline-asm waits, which the waitcnt pass
@@ -1196,7 +1256,8 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         // The epilogue runs while the CU's MFMAs idle (one workgroup per CU), so its VALU count is the
         // cost: the activation is a compile-time branch of the row loop (a per-element runtime branch
         // split every row into 8 basic blocks), tanh' = 4 r (1 - r) with r = 1 / (exp(2z) + 1) and the
-        // exp2 scale folded into the BatchNorm affine, the rstd of sum dz * xhat applied once per column.
+        // exp2 scale folded into the BatchNorm affine; the second partial is sum dz * (h - mean) (the
+        // finalize applies rstd once per column).
         constexpr int EPI = BG * 32 / NT3;
         const int c = tid & 31, r0 = tid >> 5;
         const int n = n0 + c * 8;
@@ -1219,6 +1280,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         // row.  One counted wait here retires them all for the pass; the rows are straight-line code (no
         // per-row skip: out-of-range rows have dz = 0 and h = 0 and only their store is predicated).
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unconstrained
+        dbg_t[2] = __builtin_amdgcn_s_memrealtime();
         auto rows = [&](auto actc) {
           constexpr int A = decltype(actc)::value;
 #pragma unroll
@@ -1247,19 +1309,23 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
             if (m < g.M && col_ok) *reinterpret_cast<short8*>(Y + off) = o;
           }
         };
-        if (act_c == 1) rows(std::integral_constant<int, 1>{});
-        else if (act_c == 2) rows(std::integral_constant<int, 2>{});
+        if (act_c == 1) rows(std::integral_constant<int, 1>{});  // tanh (PostNet); ReLU is rejected on the host
         else rows(std::integral_constant<int, 0>{});
-#pragma unroll
-        for (int q = 0; q < 8; ++q) bs2[q] *= ex.ln_w[g.N + (col_ok ? n + q : 0)];  // x rstd
-        __syncthreads();  // every Ct read is done: reuse the staging LDS for the partials
+        dbg_t[3] = __builtin_amdgcn_s_memrealtime();
+        // every Ct read is done: reuse the staging LDS for the partials.  LDS-only barriers: __syncthreads
+        // would also drain this thread's 16 dz stores (vmcnt counts stores), ~7 us per tile-round chip-wide
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         float* red = reinterpret_cast<float*>(smem);  // [2][16][256]
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           red[r0 * 256 + c * 8 + q] = bs1[q];
           red[4096 + r0 * 256 + c * 8 + q] = bs2[q];
         }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const int which = tid >> 8, col = tid & 255;  // threads 0..255: sum dz, 256..511: sum dz*xhat
         if (n0 + col < g.N) {
           float a = 0.f;
@@ -1267,8 +1333,16 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
           for (int r = 0; r < 16; ++r) a += red[which * 4096 + r * 256 + col];
           ex.mean[((long)which * nM + tm) * g.N + n0 + col] = a;
         }
+        if (ex.rstd && tid == 0) {
+          unsigned long long* d = reinterpret_cast<unsigned long long*>(ex.rstd) + blockIdx.x * 8;
+          d[4] = __builtin_amdgcn_s_memrealtime();
+          for (int q = 0; q < 4; ++q) d[q] = dbg_t[q];
+          d[5] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+          d[6] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+          d[7] = dbg_t[4];
+        }
         return;
-      }
+      } else {  // !EPI_BNH: the BNH instantiation compiles none of the code below
       if (ex.ln_out) {
         // Residual + LayerNorm tail (N == 256, n0 == 0): half-wave h = tid >> 5 owns rows h, h+16, ...
         // of the tile, lane c = tid & 31 owns columns 8c..8c+7.  Every global operand of the 16 rows
@@ -1460,8 +1534,10 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         }
       }
       return;
+      }  // !EPI_BNH
     }
   }
+  if constexpr (EPIM == EPI_BNH) return;  // unreachable: conv_gemm_impl validates the staged-path shape
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wm * 128 + i * 16 + (lane & 15);
@@ -2622,7 +2698,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     }
   }
   if (bnh) {  // BatchNorm-backward head (EpiX aliases: acc = bn_h, ln_w = stats, mean = partials): big64 only
-    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act != 0 || aux || resid || lens || !ex.acc || !ex.ln_w ||
+    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act != 0 || ex.post_act == 2 || aux || resid || lens || !ex.acc || !ex.ln_w ||
         !ex.mean || rinfo || ex.y2 || ex.ln_out || ex.mask_out || ex.mask_in)
       return -3;
     variant = 4;
@@ -2790,7 +2866,9 @@ SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* 
 }
 
 // Data gradient of a conv whose input came out of BatchNorm (+act, dropout): Y = dz (see EpiX.bn_*) and the
-// per-M-tile column partials bn_part [2][ceil(M/256)][N] of dz and dz * xhat.
+// per-M-tile column partials bn_part [2][ceil(M/256)][N] of dz and dz * (h - mean) (ssamd_bn_bwd_dz applies rstd).
+static void* g_bnh_dbg = nullptr;  // EXPERIMENT: per-block s_memrealtime stamps of the BNH epilogue
+SSAMD_API void ssamd_gemm_set_bnh_dbg(void* p) { g_bnh_dbg = p; }
 SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, int B, int L, int Cin, int ks, int dil,
                                     int pad, int N, const bf16_t* bn_h, const float* bn_stats, float* bn_part,
                                     int bn_act, float p, unsigned long long seed, hipStream_t s) {
@@ -2803,6 +2881,7 @@ SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, i
   ex.post_act = bn_act;
   ex.pre_p = p;
   ex.seed = seed;
+  ex.rstd = reinterpret_cast<float*>(g_bnh_dbg);
   return conv_gemm_impl(X, W, nullptr, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, nullptr, ex, s,
                         true);
 }

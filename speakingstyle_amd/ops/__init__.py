@@ -229,7 +229,7 @@ def bn_act_conv(h, bn, training, act_tanh, p, w, b, pad):
     BatchNorm backward in its epilogue (``hip._BNActConvFn``); elsewhere bn_act followed by conv1d."""
     from .. import experimental
 
-    if use_hip(h) and experimental.get("bn_fuse") and _hip().bn_act_conv_ok(h.shape[-1], w):
+    if use_hip(h) and experimental.get("bn_fuse") and act_tanh != "relu" and _hip().bn_act_conv_ok(h.shape[-1], w):
         return _hip().bn_act_conv(h, bn, training, act_tanh, p, w, b, pad)
     return conv1d(bn_act(h, bn, training, act_tanh, p), w, b, pad)
 

@@ -50,6 +50,8 @@ _SIGS = {
     "ssamd_gemm_set_buf": [I],
     "ssamd_gemm_set_stg": [I],
     "ssamd_gemm_set_mask_pre": [I],
+    "ssamd_bn_set_dz_cfg": [I, I],
+    "ssamd_gemm_set_bnh_dbg": [P],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],
@@ -1713,7 +1715,7 @@ class _BNActConvFn(torch.autograd.Function):
 
     Forward = ``ssamd_bn_fwd`` + the conv GEMM.  Backward: the conv's data-gradient GEMM starts the
     BatchNorm backward in its epilogue (``ssamd_conv_gemm_bnbwd``: dz = dy * keep * act' and the per-tile
-    column partials of dz and dz * xhat), so the separate BatchNorm reduction pass over dy and h is gone;
+    column partials of dz and dz * (h - mean)), so the separate BatchNorm reduction pass over dy and h is gone;
     ``ssamd_bn_bwd_dz`` combines the partials (fixed order) and streams dh = k1 dz + k2 h + k3.  The
     weight gradient reads the saved BN output y, as a plain conv's would."""
 
