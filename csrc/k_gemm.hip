@@ -2180,9 +2180,17 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
     // 64-B pieces.  The stage buffers and the cu table are dead after the main loop.
     constexpr int RSF = 1088;
     char* Ct = smem;
+    // barriers between the halves order LDS only: __syncthreads would also drain the first half's
+    // 128 KiB of slab stores (vmcnt counts stores) before the second half could be staged
+    auto lds_barrier = [] {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      __syncthreads();
+      if (half == 0) __syncthreads();
+      else lds_barrier();
       if (wn == half) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -2195,7 +2203,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
               *reinterpret_cast<float*>(Ct + nl * RSF + kl * 4) = acc[i][j][r];
             }
       }
-      __syncthreads();
+      lds_barrier();
       for (int e = tid; e < 128 * 64; e += NT3) {
         const int nl = e >> 6, c4 = e & 63;
         const int n = n0 + half * 128 + nl, k = k0 + c4 * 4;
