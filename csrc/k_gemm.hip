@@ -2982,6 +2982,10 @@ static int g_wgrad_blocks = 0;   // > 0: fixed split-M target (blocks per launch
 // the fp32 reduction order -- of a main-stream launch does not depend on the side-stream setting.
 static int g_wgrad_cus = 0;
 static hipStream_t g_wgrad_cus_stream = nullptr;
+// >= 1: the fewest block rounds a split plan may have -- shorter blocks, so a concurrent main-stream kernel
+// (higher queue priority) gets each CU back sooner (experimental.wgrad_min_rounds)
+static int g_wgrad_min_rounds = 1;
+SSAMD_API void ssamd_wgrad_set_min_rounds(int r) { g_wgrad_min_rounds = r > 1 ? r : 1; }
 static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits, int cus) {
   const int steps_all = (M + 63) / 64;
   int smax = max_splits;
@@ -2996,6 +3000,7 @@ static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits,
   double best_c = 1e30;
   for (int sp = 1; sp <= smax; ++sp) {
     const long rounds = ((long)tiles * sp + cus - 1) / cus;
+    if (rounds < g_wgrad_min_rounds && sp < smax) continue;
     const long steps = (steps_all + sp - 1) / sp;
     const double c = (double)rounds * (double)steps + 0.08 * (double)sp * tiles;
     if (c < best_c - 1e-9) { best_c = c; best = sp; }

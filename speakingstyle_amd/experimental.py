@@ -67,6 +67,8 @@ KNOBS: Dict[str, tuple] = {
     "wgrad_cu_frac": (0.75, _frac, "fraction of the CUs the side-stream weight-gradient split plan is sized for"),
     "wgrad_cus_all": (True, _bool, "apply the reduced weight-gradient CU plan to every stream (0: side stream "
                                    "only -- main-stream weight gradients then reduce in a different order)"),
+    "wgrad_min_rounds": (1, int, "fewest block rounds of a 256x256 weight-gradient split plan (shorter side-stream "
+                                 "blocks hand CUs back to the main stream sooner; measured slower, profiles/r4_exp_wgrad_min_rounds.txt)"),
     "ln_fuse": (False, _bool, "residual + LayerNorm tail in the producing GEMM's epilogue (measured slower)"),
     "gemm_stg": (True, _bool, "staggered 8-phase main loop of the 256x256 GEMM for K >= 512 (+0.7 % LJSpeech)"),
     "gemm_mask_pre": (True, _bool, "ReLU-mask data gradient with its mask bytes prefetched before the main loop"),

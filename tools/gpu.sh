@@ -64,7 +64,7 @@ for task in "$@"; do
       python tools/prof_summary.py "$f" "$t" > gpurun_out/${TAG}_summary.txt
       python tools/last_step.py "$t" 70 > gpurun_out/${TAG}_last_step.txt
       python tools/grid_census.py "$t" --top 60 > gpurun_out/${TAG}_grid.txt
-      python tools/stream_split.py "$t" --last 2 --detail > gpurun_out/${TAG}_split.txt 2>&1 || true
+      python tools/stream_split.py "$t" --last 2 --detail --gaps 25 --tail ${TAILN:-0} > gpurun_out/${TAG}_split.txt 2>&1 || true
       rm -f "$t"; rm -rf gpurun_out/$TAG
       head -25 gpurun_out/${TAG}_last_step.txt ;;
     synthprof)

@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--last", type=int, default=5)
     ap.add_argument("--tail", type=int, default=0, help="print the last N kernels (both streams) before Adam")
     ap.add_argument("--detail", action="store_true", help="per-stream top kernels and the kernels after main-stream gaps")
+    ap.add_argument("--gaps", type=int, default=0,
+                    help="print the N largest main-stream gaps: kernels around them and the side-stream kernel "
+                         "that ended last before the gap closed (an event wait ends with it)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     skey = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
@@ -69,6 +72,17 @@ def main():
         gaps = [((mk[i + 1][0] - mk[i][1]) / 1e3, mk[i + 1][2]) for i in range(len(mk) - 1)]
         print(f"   main-stream gaps: total {sum(g for g, _ in gaps if g > 0) / 1e3:.3f} ms, "
               f">20us: {sum(1 for g, _ in gaps if g > 20)}")
+        if a.gaps:
+            gi = sorted(range(len(mk) - 1), key=lambda i: -(mk[i + 1][0] - mk[i][1]))[:a.gaps]
+            sk = sorted((s, e, n) for s, e, n, q in seg if q != main_q)
+            for i in sorted(gi):
+                g0, g1 = mk[i][1], mk[i + 1][0]
+                ended = [x for x in sk if g0 <= x[1] <= g1]
+                last_side = max(ended, key=lambda x: x[1]) if ended else None
+                running = sum(1 for x in sk if x[0] < g1 and x[1] > g0)
+                print(f"   gap {(g1 - g0) / 1e3:7.1f} us at {(g0 - t0) / 1e3:8.1f}: {short(mk[i][2])} -> {short(mk[i + 1][2])}"
+                      + (f"  | side ended {(g1 - last_side[1]) / 1e3:6.1f} us before close: {short(last_side[2])}"
+                         if last_side else "") + f"  side kernels overlapping {running}")
         if a.detail:
             by = defaultdict(float)
             for g, n in gaps:
