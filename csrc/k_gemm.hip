@@ -994,7 +994,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
   // epilogue past 256 VGPRs) are issued right after the accumulator staging, before its barrier
   constexpr int BNH_PRE = 16;
   short8 hpre[16];
-  unsigned long long dbg_t[5];  // EXPERIMENT stamps (BNH only), written once at the end
   auto load_h = [&](int it0, int it1) {
     const int c = tid & 31, r0 = tid >> 5;
     const int n = n0 + c * 8;
@@ -1007,7 +1006,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
   };
   if constexpr (EPIM == EPI_BNH) {
     load_h(0, BNH_PRE);
-    dbg_t[0] = __builtin_amdgcn_s_memrealtime();
   }
   // split-K (gridDim.y > 1): block y owns the k slabs [kt0, kt1) and writes its fp32 partial
   // tile to slice y of the workspace (Yv), reduced afterwards in a fixed order (splitk_reduce)
@@ -1177,9 +1175,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
     __builtin_amdgcn_s_barrier();
   }
   }  // !STG
-  if constexpr (EPIM == EPI_BNH) {
-    dbg_t[1] = __builtin_amdgcn_s_memrealtime();
-  }
   if constexpr (!OUT_F32) {
     if (act >= 0 && (g.N & 7) == 0 && (ldy & 7) == 0) {
       // LDS-staged epilogue: the accumulator layout gives each lane 4 columns of one row, i.e.
@@ -1240,8 +1235,7 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       else if (bias) stage_act(std::true_type{});
       else stage_act(std::false_type{});
       if constexpr (EPIM == EPI_BNH) {
-        load_h(BNH_PRE, 16);
-        dbg_t[4] = __builtin_amdgcn_s_memrealtime();
+        if constexpr (BNH_PRE < 16) load_h(BNH_PRE, 16);
       }
       __syncthreads();
       // the prefetched mask bytes were retired by the main loop's inline-asm waits, which the waitcnt pass
@@ -1280,7 +1274,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         // row.  One counted wait here retires them all for the pass; the rows are straight-line code (no
         // per-row skip: out-of-range rows have dz = 0 and h = 0 and only their store is predicated).
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unconstrained
-        dbg_t[2] = __builtin_amdgcn_s_memrealtime();
         auto rows = [&](auto actc) {
           constexpr int A = decltype(actc)::value;
 #pragma unroll
@@ -1311,7 +1304,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
         };
         if (act_c == 1) rows(std::integral_constant<int, 1>{});  // tanh (PostNet); ReLU is rejected on the host
         else rows(std::integral_constant<int, 0>{});
-        dbg_t[3] = __builtin_amdgcn_s_memrealtime();
         // every Ct read is done: reuse the staging LDS for the partials.  LDS-only barriers: __syncthreads
         // would also drain this thread's 16 dz stores (vmcnt counts stores), ~7 us per tile-round chip-wide
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1332,14 +1324,6 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
 #pragma unroll
           for (int r = 0; r < 16; ++r) a += red[which * 4096 + r * 256 + col];
           ex.mean[((long)which * nM + tm) * g.N + n0 + col] = a;
-        }
-        if (ex.rstd && tid == 0) {
-          unsigned long long* d = reinterpret_cast<unsigned long long*>(ex.rstd) + blockIdx.x * 8;
-          d[4] = __builtin_amdgcn_s_memrealtime();
-          for (int q = 0; q < 4; ++q) d[q] = dbg_t[q];
-          d[5] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
-          d[6] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
-          d[7] = dbg_t[4];
         }
         return;
       } else {  // !EPI_BNH: the BNH instantiation compiles none of the code below
@@ -2875,8 +2859,6 @@ SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* 
 
 // Data gradient of a conv whose input came out of BatchNorm (+act, dropout): Y = dz (see EpiX.bn_*) and the
 // per-M-tile column partials bn_part [2][ceil(M/256)][N] of dz and dz * (h - mean) (ssamd_bn_bwd_dz applies rstd).
-static void* g_bnh_dbg = nullptr;  // EXPERIMENT: per-block s_memrealtime stamps of the BNH epilogue
-SSAMD_API void ssamd_gemm_set_bnh_dbg(void* p) { g_bnh_dbg = p; }
 SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, int B, int L, int Cin, int ks, int dil,
                                     int pad, int N, const bf16_t* bn_h, const float* bn_stats, float* bn_part,
                                     int bn_act, float p, unsigned long long seed, hipStream_t s) {
@@ -2889,7 +2871,6 @@ SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, i
   ex.post_act = bn_act;
   ex.pre_p = p;
   ex.seed = seed;
-  ex.rstd = reinterpret_cast<float*>(g_bnh_dbg);
   return conv_gemm_impl(X, W, nullptr, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, nullptr, ex, s,
                         true);
 }

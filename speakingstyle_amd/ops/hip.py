@@ -51,7 +51,6 @@ _SIGS = {
     "ssamd_gemm_set_stg": [I],
     "ssamd_gemm_set_mask_pre": [I],
     "ssamd_bn_set_dz_cfg": [I, I],
-    "ssamd_gemm_set_bnh_dbg": [P],
     "ssamd_wgrad_set_min_rounds": [I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],

@@ -1,7 +1,8 @@
 """PostNet BatchNorm backward costs at the LJSpeech shape (R = 200 x 680 padded rows, C = 512, k5): the
 plain data-gradient GEMM vs the GEMM with the BatchNorm-backward head (EPI_BNH: dz + column partials in
 the epilogue), the dz apply pass, and the unfused reduce + apply pair (ssamd_bn_bwd) for reference.
-Usage (GPU box): python tools/exp_bnh.py [pmc]   (pmc: 3 launches per arm, no timing -- for rocprofv3 --pmc)"""
+Usage (GPU box): python tools/exp_bnh.py [pmc]   (pmc: 3 launches per arm, no timing -- for rocprofv3 --pmc)
+(The per-block s_memrealtime stamp build behind profiles/r4_exp_bnh_stamps.jsonl was a diagnostic build, removed.)"""
 import json
 import statistics
 import sys
@@ -62,42 +63,6 @@ def main():
 
     arms = {"gemm_plain": plain, "gemm_plain_nostg": plain_nostg, "gemm_bnh_p0.5": bnh(0.5), "gemm_bnh_p0": bnh(0.0), "gemm_bnh_p0_noact": bnh(0.0, 0), "apply_dz": apply_dz,
             "bn_bwd_unfused(reduce+apply)": unfused}
-    if len(sys.argv) > 1 and sys.argv[1] == "stamps":
-        # per-block s_memrealtime (100 MHz) stamps of the BNH kernel: start, main loop done, staged, rows done, end
-        nb = ((R + 255) // 256) * ((C + 255) // 256)
-        buf = torch.zeros(nb * 8, dtype=torch.int64, device=dev)
-        for p_, act_ in ((0.5, 1), (0.0, 0)):
-            lib.ssamd_gemm_set_bnh_dbg(_ptr(buf))
-            bnh(p_, act_)()
-            torch.cuda.synchronize()
-            lib.ssamd_gemm_set_bnh_dbg(None)
-            b = buf.view(nb, 8).cpu()
-            t = b[:, :5].double() * 10.0 / 1000.0  # us
-            t0 = t[:, 0].min()
-            t = t - t0
-            ts = b[:, 7].double() * 10.0 / 1000.0 - t0
-            seg = {"loop": (t[:, 1] - t[:, 0]), "stage_write": (ts - t[:, 1]), "stage_sync": (t[:, 2] - ts), "rows": (t[:, 3] - t[:, 2]),
-                   "partials": (t[:, 4] - t[:, 3])}
-            rec = {"p": p_, "act": act_, "span_us": round(float(t[:, 4].max()), 1)}
-            for k, v in seg.items():
-                rec[k + "_med_us"] = round(float(v.median()), 2)
-                rec[k + "_max_us"] = round(float(v.max()), 2)
-            # per CU: gap between a block's end stamp and the next block's start on the same CU
-            cu = (b[:, 6] << 16) | ((b[:, 5] >> 8) & 0xFFFF)
-            gaps = []
-            for u in cu.unique():
-                idx = (cu == u).nonzero().flatten()
-                o = idx[t[idx, 0].argsort()]
-                for a_, c_ in zip(o[:-1].tolist(), o[1:].tolist()):
-                    gaps.append(float(t[c_, 0] - t[a_, 4]))
-            g = torch.tensor(gaps)
-            rec["cus"] = int(cu.unique().numel())
-            rec["blk_gap_med_us"] = round(float(g.median()), 2) if len(gaps) else None
-            rec["blk_gap_max_us"] = round(float(g.max()), 2) if len(gaps) else None
-            starts = t[:, 0].sort().values
-            rec["start_quartiles_us"] = [round(float(starts[int(q * (nb - 1))]), 1) for q in (0.25, 0.5, 0.75, 1.0)]
-            print(json.dumps(rec), flush=True)
-        return
     if len(sys.argv) > 1 and sys.argv[1] == "pmc":
         for f in arms.values():
             for _ in range(3):
