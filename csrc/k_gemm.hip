@@ -1419,9 +1419,11 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       // global operands of EPG rows (aux / residual / accumulator segments, mask bytes, sequence
       // lengths) are all loaded before any is used: one loop iteration per row would expose a full
       // memory round trip per row (16 in a row per tile -- the K = 256 ReLU-mask data gradient
-      // spent most of its time there).  Same arithmetic, same order as the one-row form.
+      // spent most of its time there).  All 16 rows are loaded before the first store (the accumulators
+      // are dead here, 3 x 16 x 16 B fit): a second load batch after stores would wait for those stores
+      // too (vmcnt counts both).  Same arithmetic, same order as the one-row form.
       constexpr int EPI = BG * 32 / NT3;  // 16 rows per thread
-      constexpr int EPG = 8;              // rows per load batch (register budget: 3 x 8 x 16 B)
+      constexpr int EPG = 16;             // rows per load batch: all 16 before the first store (see below)
       const int c = tid & 31, r0 = tid >> 5;
       const int n = n0 + c * 8;
       const bool col_ok = n < g.N;
