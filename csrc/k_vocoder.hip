@@ -209,6 +209,18 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   const int col = lane & 15, quad = lane >> 4;
   const int h1 = d * (K - 1) / 2;
   const bf16_t* xb = x + (long)b * T * C;
+  // both convs' bias columns of this lane (they depend on the sub-tile s only): loaded up front, not as
+  // one exposed L2 round trip per (row block, sub-tile) between the two convolutions
+  float bias1[R::NSW], bias2[R::NSW];
+  {
+    const int wc0 = wave / R::WR;
+#pragma unroll
+    for (int s = 0; s < R::NSW; ++s) {
+      const int ch = (wc0 * R::NSW + s) * 16 + col;
+      bias1[s] = b1[ch];
+      bias2[s] = b2[ch];
+    }
+  }
 
   // 1. lrelu(x) rows [t0 - h1 - H2, ...) -- all global loads of the thread first, then convert + store
   {
@@ -255,7 +267,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
 #pragma unroll
       for (int s = 0; s < R::NSW; ++s) {
         const int ch = (wc * R::NSW + s) * 16 + col;
-        const float bias = b1[ch];
+        const float bias = bias1[s];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = rb * 16 + 4 * quad + i;
@@ -277,7 +289,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
 #pragma unroll
       for (int s = 0; s < R::NSW; ++s) {
         const int ch = (wc * R::NSW + s) * 16 + col;
-        const float bias = b2[ch];
+        const float bias = bias2[s];
 #pragma unroll
         for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + ch] = acc[r][s][i] + bias;
       }
@@ -617,6 +629,15 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
 #pragma unroll
   for (int pp = 0; pp < 3; ++pp) {
     const int d = p.d[pp];
+    // this pair's bias columns, issued before the weight prefetch: their waits (after each conv) then
+    // neither stall on an exposed L2 round trip nor drain the younger weight loads still in flight
+    float bb1[R::NSW], bb2[R::NSW];
+#pragma unroll
+    for (int s = 0; s < R::NSW; ++s) {
+      const int ch = (wc * R::NSW + s) * 16 + col;
+      bb1[s] = p.b[2 * pp][ch];
+      bb2[s] = p.b[2 * pp + 1][ch];
+    }
     // conv 2pp = conv1 (dilation d) of lrelu(x_p) -> T = lrelu(. + b1), zero outside [0, T)
     if constexpr (R::RING) {
       conv_rf_ring<C, K>(As, d, p.w[2 * pp], Ws, tid, wave, wr, wc, col, quad, acc);
@@ -625,11 +646,10 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
       conv_rf<C, K>(As, d, Ws, wr, wc, col, quad, acc);
     }
     {
-      const float* b1 = p.b[2 * pp];
 #pragma unroll
       for (int s = 0; s < R::NSW; ++s) {
         const int ch = (wc * R::NSW + s) * 16 + col;
-        const float bias = b1[ch];
+        const float bias = bb1[s];
 #pragma unroll
         for (int j = 0; j < R::MAXRB; ++j)
 #pragma unroll
@@ -660,11 +680,10 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
     if constexpr (R::RING) conv_rf_ring<C, K>(Ts, 1, p.w[2 * pp + 1], Ws, tid, wave, wr, wc, col, quad, acc);
     else conv_rf<C, K>(Ts, 1, Ws, wr, wc, col, quad, acc);
     {
-      const float* b2 = p.b[2 * pp + 1];
 #pragma unroll
       for (int s = 0; s < R::NSW; ++s) {
         const int ch = (wc * R::NSW + s) * 16 + col;
-        const float bias = b2[ch];
+        const float bias = bb2[s];
 #pragma unroll
         for (int j = 0; j < R::MAXRB; ++j)
 #pragma unroll
