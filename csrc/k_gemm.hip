@@ -135,6 +135,81 @@ __device__ __forceinline__ short8 load_a_chunk(const bf16_t* __restrict__ X, con
   return v;
 }
 
+// Register epilogue of a 4 x 4 grid of 16x16 accumulator fragments (the 128x128 kernels): every global
+// operand (bias columns, row validity, aux / residual segments) is loaded before the first store -- one
+// load per fragment between stores made each wait drain the stores before it (vmcnt counts both).
+template <bool OUT_F32>
+__device__ __forceinline__ void epi4x4_prefetch(const float4v (&acc)[4][4], int mb, int nb, int lane, const ConvGeom& g,
+                                                const float* __restrict__ bias, const bf16_t* __restrict__ aux,
+                                                const bf16_t* __restrict__ resid, const int64_t* __restrict__ lens,
+                                                int act, int ldy, void* __restrict__ Yv) {
+  float4 bvj[4];
+  short4v xa[4][4], xr[4][4];
+  bool vrow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = nb + j * 16 + 4 * (lane >> 4);
+    bvj[j] = (bias && n < g.N) ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mb + i * 16 + (lane & 15);
+    const int mm = m < g.M ? m : 0;
+    const int bb = mm / g.L, tt = mm - bb * g.L;
+    vrow[i] = lens == nullptr || tt < (int)lens[bb];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nb + j * 16 + 4 * (lane >> 4);
+      const bool in = m < g.M && n < g.N;
+      const long off = (long)m * ldy + n;
+      if (in && aux) xa[i][j] = *reinterpret_cast<const short4v*>(aux + off);
+      if (in && resid) xr[i][j] = *reinterpret_cast<const short4v*>(resid + off);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mb + i * 16 + (lane & 15);
+    if (m >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nb + j * 16 + 4 * (lane >> 4);
+      if (n >= g.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (bias) {
+        v[0] += bvj[j].x; v[1] += bvj[j].y; v[2] += bvj[j].z; v[3] += bvj[j].w;
+      }
+      if (act == ACT_RELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      } else if (act == ACT_LRELU) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+      } else if (act == ACT_TANH) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+      }
+      const long off = (long)m * ldy + n;
+      if (aux) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)xa[i][j][q]) > 0.f ? v[q] : 0.f;
+      }
+      if (resid) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)xr[i][j][q]);
+      }
+      if (!vrow[i]) v[0] = v[1] = v[2] = v[3] = 0.f;
+      if constexpr (OUT_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        short4v o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
+        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
+      }
+    }
+  }
+}
+
 template <bool OUT_F32, bool REG_EPI>
 __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                           const float* __restrict__ bias, const bf16_t* __restrict__ aux,
@@ -228,53 +303,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(const bf16_t* __restri
 
   if constexpr (REG_EPI) {
     // ---- register epilogue (no LDS round trip): fragment (i, j) -> row m, columns n..n+3
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-      if (m >= g.M) continue;
-      const int bb = m / g.L, tt = m - bb * g.L;
-      const bool valid = lens == nullptr || tt < (int)lens[bb];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-        if (n >= g.N) continue;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (bias) {
-          const float4 bv = *reinterpret_cast<const float4*>(bias + n);
-          v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
-        }
-        if (act == ACT_RELU) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-        } else if (act == ACT_LRELU) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
-        } else if (act == ACT_TANH) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
-        }
-        const long off = (long)m * ldy + n;
-        if (aux) {
-          const short4v x = *reinterpret_cast<const short4v*>(aux + off);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
-        }
-        if (resid) {
-          const short4v x = *reinterpret_cast<const short4v*>(resid + off);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
-        }
-        if (!valid) v[0] = v[1] = v[2] = v[3] = 0.f;
-        if constexpr (OUT_F32) {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-          short4v o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
-          *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
-        }
-      }
-    }
+    epi4x4_prefetch<OUT_F32>(acc, m0 + wm * 64, n0 + wn * 64, lane, g, bias, aux, resid, lens, act, ldy, Yv);
     return;
   }
 
@@ -468,53 +497,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_glds_kernel(const bf16_t* __r
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-    if (m >= g.M) continue;
-    const int bb = m / g.L, tt = m - bb * g.L;
-    const bool valid = lens == nullptr || tt < (int)lens[bb];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-      if (n >= g.N) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (bias) {
-        const float4 bv = *reinterpret_cast<const float4*>(bias + n);
-        v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
-      }
-      if (act == ACT_RELU) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-      } else if (act == ACT_LRELU) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
-      } else if (act == ACT_TANH) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
-      }
-      const long off = (long)m * ldy + n;
-      if (aux) {
-        const short4v x = *reinterpret_cast<const short4v*>(aux + off);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = bf2f((bf16_t)x[q]) > 0.f ? v[q] : 0.f;
-      }
-      if (resid) {
-        const short4v x = *reinterpret_cast<const short4v*>(resid + off);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] += bf2f((bf16_t)x[q]);
-      }
-      if (!valid) v[0] = v[1] = v[2] = v[3] = 0.f;
-      if constexpr (OUT_F32) {
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(Yv) + off) = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        short4v o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
-        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(Yv) + off) = o;
-      }
-    }
-  }
+  epi4x4_prefetch<OUT_F32>(acc, m0 + wm * 64, n0 + wn * 64, lane, g, bias, aux, resid, lens, act, ldy, Yv);
 }
 
 // ----------------------------------------------------------------------------
