@@ -40,17 +40,14 @@ static __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
-static __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
-  uint32_t h = hash_u32((uint32_t)idx ^ hash_u32((uint32_t)seed ^ (uint32_t)(idx >> 32) * 0x9E3779B9U)
-                        ^ (uint32_t)(seed >> 32));
-  return (h >> 8) * (1.0f / 16777216.0f);
-}
-// Keep-scales of the N consecutive elements idx0 .. idx0+N-1, bit-identical to N drop_scale calls:
-// the seed half of the hash depends only on idx >> 32, which a chunk starting at a multiple of N
-// (N | 2^32) shares, so it is computed once per chunk; the uniform test is an integer compare
-// (u = (h >> 8) / 2^24 >= p  <=>  (h >> 8) >= ceil(p * 2^24), exact in fp32).
+// Keep-scales of the N (even) consecutive elements idx0 .. idx0+N-1 (idx0 even): one 32-bit hash per element
+// PAIR, its high / low 16 bits the two elements' uniforms (u = bits / 2^16, kept iff bits >= ceil(p * 2^16)).
+// Half the hashing of one hash per element (the BatchNorm-backward GEMM head and the LayerNorm kernels run
+// it on every element they touch), p resolved to 2^-16.  The seed half of the hash depends only on
+// idx >> 32, which a chunk starting at a multiple of N (N | 2^32) shares, so it is computed once per chunk.
 template <int N>
 static __device__ __forceinline__ void drop_scales(uint64_t seed, uint64_t idx0, float p, float* ks) {
+  static_assert(N % 2 == 0, "drop_scales: even chunks");
   if (p <= 0.f) {
 #pragma unroll
     for (int i = 0; i < N; ++i) ks[i] = 1.f;
@@ -58,14 +55,14 @@ static __device__ __forceinline__ void drop_scales(uint64_t seed, uint64_t idx0,
   }
   const float keep = 1.f / (1.f - p);
   const uint32_t S = hash_u32((uint32_t)seed ^ (uint32_t)(idx0 >> 32) * 0x9E3779B9U) ^ (uint32_t)(seed >> 32);
-  const uint32_t thr = (uint32_t)ceilf(p * 16777216.0f);
+  const uint32_t thr = (uint32_t)ceilf(p * 65536.0f);
+  const uint32_t pair0 = (uint32_t)idx0 >> 1;
 #pragma unroll
-  for (int i = 0; i < N; ++i) ks[i] = (hash_u32(((uint32_t)idx0 + (uint32_t)i) ^ S) >> 8) >= thr ? keep : 0.f;
-}
-// keep-scale for element idx: 0 (dropped) or 1/(1-p)
-static __device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, float p) {
-  if (p <= 0.f) return 1.f;
-  return uniform01(seed, idx) >= p ? 1.f / (1.f - p) : 0.f;
+  for (int i = 0; i < N / 2; ++i) {
+    const uint32_t h = hash_u32((pair0 + (uint32_t)i) ^ S);
+    ks[2 * i] = (h >> 16) >= thr ? keep : 0.f;
+    ks[2 * i + 1] = (h & 0xFFFFu) >= thr ? keep : 0.f;
+  }
 }
 
 // BatchNorm activations (k_bn.hip forward / backward and the GEMM epilogue that starts the PostNet

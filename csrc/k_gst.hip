@@ -358,19 +358,22 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
 
 // Style-token bank (reference GST, models/style.py::token_bank): keys = tanh(E) [N][dt];
 //   K[h][n][d] = sum_c keys[n][c] Wk[h*D + d][c],  V likewise with Wv  (T = NH * D outputs per token).
-// Tiny (N <= 64 tokens, dt, T <= 512): one workgroup, fp32, fixed-order sums (bitwise reproducible).
+// Tiny (N <= 64 tokens, dt, T <= 512), fp32, fixed-order sums (bitwise reproducible).  One output element
+// per thread over as many workgroups as there are outputs (one serial workgroup took ~100 us per backward).
 __global__ void __launch_bounds__(256) token_bank_fwd_kernel(const float* __restrict__ E, const float* __restrict__ Wk,
                                                              const float* __restrict__ Wv, int N, int dt, int T,
                                                              int D, float* __restrict__ K, float* __restrict__ V,
                                                              float* __restrict__ tE) {
-  extern __shared__ float te[];  // [N][dt]
+  extern __shared__ float te[];  // [N][dt], recomputed by every workgroup
   for (int i = threadIdx.x; i < N * dt; i += blockDim.x) {
     const float t = tanhf(E[i]);
     te[i] = t;
-    tE[i] = t;
+    if (blockIdx.x == 0) tE[i] = t;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < N * T; i += blockDim.x) {
+  {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * T) return;
     const int n = i / T, t = i - n * T;
     float a = 0.f, b = 0.f;
     for (int c = 0; c < dt; ++c) {
@@ -395,7 +398,10 @@ __global__ void __launch_bounds__(256) token_bank_bwd_kernel(const float* __rest
     const int h = t / D, d = t - h * D;
     return g[((long)h * N + n) * D + d];
   };
-  for (int i = threadIdx.x; i < T * dt; i += blockDim.x) {
+  const int nb1 = (T * dt + blockDim.x - 1) / blockDim.x;  // workgroups [0, nb1): dWk / dWv, the rest: dE
+  if ((int)blockIdx.x < nb1) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T * dt) return;
     const int t = i / dt, c = i - t * dt;
     float a = 0.f, b = 0.f;
     for (int n = 0; n < N; ++n) {
@@ -405,8 +411,11 @@ __global__ void __launch_bounds__(256) token_bank_bwd_kernel(const float* __rest
     }
     dWk[i] = a;
     dWv[i] = b;
+    return;
   }
-  for (int i = threadIdx.x; i < N * dt; i += blockDim.x) {
+  {
+    const int i = (blockIdx.x - nb1) * blockDim.x + threadIdx.x;
+    if (i >= N * dt) return;
     const int n = i / dt, c = i - n * dt;
     float a = 0.f;
     for (int t = 0; t < T; ++t) a = fmaf(gk(dK, n, t), Wk[t * dt + c], fmaf(gk(dV, n, t), Wv[t * dt + c], a));
@@ -483,15 +492,15 @@ SSAMD_API int ssamd_token_attn_bwd(const float* dout, const float* q, const floa
 SSAMD_API int ssamd_token_bank_fwd(const float* E, const float* Wk, const float* Wv, int N, int dt, int T, int NH,
                                    float* K, float* V, float* tE, hipStream_t s) {
   if (N <= 0 || NH <= 0 || T % NH || (size_t)N * dt * 4 > 64 * 1024) return -2;
-  hipLaunchKernelGGL(token_bank_fwd_kernel, dim3(1), dim3(256), (size_t)N * dt * 4, s, E, Wk, Wv, N, dt, T, T / NH, K,
-                     V, tE);
+  hipLaunchKernelGGL(token_bank_fwd_kernel, dim3(cdiv((long)N * T, 256)), dim3(256), (size_t)N * dt * 4, s, E, Wk, Wv,
+                     N, dt, T, T / NH, K, V, tE);
   return (int)hipGetLastError();
 }
 
 SSAMD_API int ssamd_token_bank_bwd(const float* dK, const float* dV, const float* tE, const float* Wk, const float* Wv,
                                    int N, int dt, int T, int NH, float* dE, float* dWk, float* dWv, hipStream_t s) {
   if (N <= 0 || NH <= 0 || T % NH) return -2;
-  hipLaunchKernelGGL(token_bank_bwd_kernel, dim3(1), dim3(256), 0, s, dK, dV, tE, Wk, Wv, N, dt, T, T / NH, dE, dWk,
-                     dWv);
+  hipLaunchKernelGGL(token_bank_bwd_kernel, dim3(cdiv((long)T * dt, 256) + cdiv((long)N * dt, 256)), dim3(256), 0, s,
+                     dK, dV, tE, Wk, Wv, N, dt, T, T / NH, dE, dWk, dWv);
   return (int)hipGetLastError();
 }

@@ -1181,79 +1181,96 @@ SSAMD_API int ssamd_pad_colsum(const void* dout, int f32, const int64_t* lens, i
 // FiLM parameter gradients of one LayerNorm site (reference model/blocks.py:43-62):
 //   d gamma = S1 * s_g,  d beta = S2 * s_b            (bf16 or fp32 [n])
 //   d s_g = sum(S1 * gamma),  d s_b = sum(S2 * beta)   (scalars, fixed-order block reduction)
-// S1 / S2 = per-(b, c) sums from the LayerNorm backward.  One block.  accum != 0: d gamma / d beta
+// S1 / S2 = per-(b, c) sums from the LayerNorm backward.  accum != 0: d gamma / d beta
 // are added to (running sums over the sites that share gamma / beta, in backward order on one
 // stream: deterministic) instead of one gradient per site summed by autograd.  l2_sg / l2_sb (optional):
 // this site's entries of the FiLM L2 term's gradient (ops/hip.py film_scalars_cat), folded into the
 // scalar gradients so each scalar gets ONE gradient, written straight into its arena slot.
 // ----------------------------------------------------------------------------
 namespace {
-// One block of 1024 threads: every thread owns float4 groups i = 4*(tid + 1024*u), all U loads of an
-// outer iteration issued before any use (the per-element strided loop of one 256-thread block was a
-// chain of dependent memory round trips: ~80 us for n = 19200), fixed-order tree for the two scalars.
-constexpr int FG_T = 1024, FG_U = 4;
+// Many 256-thread blocks, one float4 group per thread (one 1024-thread block looping over n was
+// ~24 us per site, latency-bound on one CU); each block writes its two partial sums, a one-block
+// finish adds them in a fixed order (deterministic) and folds in the L2 term.
+constexpr int FG_T = 256;
 __global__ void __launch_bounds__(FG_T) film_grads_kernel(const float* __restrict__ S1, const float* __restrict__ S2,
                                                           const float* __restrict__ g, const float* __restrict__ bt,
                                                           const float* __restrict__ sg, const float* __restrict__ sb,
                                                           int n, int out_f32, void* __restrict__ dg,
-                                                          void* __restrict__ dbt, float* __restrict__ dsg,
-                                                          float* __restrict__ dsb, const float* __restrict__ l2_sg,
-                                                          const float* __restrict__ l2_sb, int accum) {
-  __shared__ float red[2][FG_T];
+                                                          void* __restrict__ dbt, float* __restrict__ part, int accum) {
+  __shared__ float red[2][FG_T / 64];
   const float a = *sg, c = *sb;
-  float s1 = 0.f, s2 = 0.f;
   const int tid = threadIdx.x;
-  for (int base = 0; base < n; base += 4 * FG_T * FG_U) {
-    float4 x1[FG_U], x2[FG_U], gg[FG_U], bb[FG_U], o1[FG_U], o2[FG_U];
-#pragma unroll
-    for (int u = 0; u < FG_U; ++u) {
-      const int i = base + 4 * (tid + FG_T * u);
-      const bool ok = i < n;  // n % 4 == 0 (host check)
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      x1[u] = ok ? *reinterpret_cast<const float4*>(S1 + i) : z;
-      x2[u] = ok ? *reinterpret_cast<const float4*>(S2 + i) : z;
-      gg[u] = ok ? *reinterpret_cast<const float4*>(g + i) : z;
-      bb[u] = ok ? *reinterpret_cast<const float4*>(bt + i) : z;
-      o1[u] = z;
-      o2[u] = z;
-      if (ok && accum) {
-        if (out_f32) {
-          o1[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dg) + i);
-          o2[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dbt) + i);
-        } else {
-          const short4v p1 = *reinterpret_cast<const short4v*>(reinterpret_cast<const bf16_t*>(dg) + i);
-          const short4v p2 = *reinterpret_cast<const short4v*>(reinterpret_cast<const bf16_t*>(dbt) + i);
-          o1[u] = make_float4(bf2f((bf16_t)p1[0]), bf2f((bf16_t)p1[1]), bf2f((bf16_t)p1[2]), bf2f((bf16_t)p1[3]));
-          o2[u] = make_float4(bf2f((bf16_t)p2[0]), bf2f((bf16_t)p2[1]), bf2f((bf16_t)p2[2]), bf2f((bf16_t)p2[3]));
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < FG_U; ++u) {
-      const int i = base + 4 * (tid + FG_T * u);
-      if (i >= n) continue;
-      // accumulate rounds like autograd's add of per-site gradients (fp32 add, one rounding)
-      const float4 r1 = make_float4(o1[u].x + x1[u].x * a, o1[u].y + x1[u].y * a, o1[u].z + x1[u].z * a,
-                                    o1[u].w + x1[u].w * a);
-      const float4 r2 = make_float4(o2[u].x + x2[u].x * c, o2[u].y + x2[u].y * c, o2[u].z + x2[u].z * c,
-                                    o2[u].w + x2[u].w * c);
+  const int i = 4 * (blockIdx.x * FG_T + tid);
+  float s1 = 0.f, s2 = 0.f;
+  if (i < n) {  // n % 4 == 0 (host check)
+    const float4 x1 = *reinterpret_cast<const float4*>(S1 + i);
+    const float4 x2 = *reinterpret_cast<const float4*>(S2 + i);
+    const float4 gg = *reinterpret_cast<const float4*>(g + i);
+    const float4 bb = *reinterpret_cast<const float4*>(bt + i);
+    float4 o1 = make_float4(0.f, 0.f, 0.f, 0.f), o2 = o1;
+    if (accum) {
       if (out_f32) {
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(dg) + i) = r1;
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(dbt) + i) = r2;
+        o1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dg) + i);
+        o2 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(dbt) + i);
       } else {
-        const short4v q1 = {(short)f2bf(r1.x), (short)f2bf(r1.y), (short)f2bf(r1.z), (short)f2bf(r1.w)};
-        const short4v q2 = {(short)f2bf(r2.x), (short)f2bf(r2.y), (short)f2bf(r2.z), (short)f2bf(r2.w)};
-        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(dg) + i) = q1;
-        *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(dbt) + i) = q2;
+        const short4v p1 = *reinterpret_cast<const short4v*>(reinterpret_cast<const bf16_t*>(dg) + i);
+        const short4v p2 = *reinterpret_cast<const short4v*>(reinterpret_cast<const bf16_t*>(dbt) + i);
+        o1 = make_float4(bf2f((bf16_t)p1[0]), bf2f((bf16_t)p1[1]), bf2f((bf16_t)p1[2]), bf2f((bf16_t)p1[3]));
+        o2 = make_float4(bf2f((bf16_t)p2[0]), bf2f((bf16_t)p2[1]), bf2f((bf16_t)p2[2]), bf2f((bf16_t)p2[3]));
       }
-      s1 += x1[u].x * gg[u].x + x1[u].y * gg[u].y + x1[u].z * gg[u].z + x1[u].w * gg[u].w;
-      s2 += x2[u].x * bb[u].x + x2[u].y * bb[u].y + x2[u].z * bb[u].z + x2[u].w * bb[u].w;
     }
+    // accumulate rounds like autograd's add of per-site gradients (fp32 add, one rounding)
+    const float4 r1 = make_float4(o1.x + x1.x * a, o1.y + x1.y * a, o1.z + x1.z * a, o1.w + x1.w * a);
+    const float4 r2 = make_float4(o2.x + x2.x * c, o2.y + x2.y * c, o2.z + x2.z * c, o2.w + x2.w * c);
+    if (out_f32) {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(dg) + i) = r1;
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(dbt) + i) = r2;
+    } else {
+      const short4v q1 = {(short)f2bf(r1.x), (short)f2bf(r1.y), (short)f2bf(r1.z), (short)f2bf(r1.w)};
+      const short4v q2 = {(short)f2bf(r2.x), (short)f2bf(r2.y), (short)f2bf(r2.z), (short)f2bf(r2.w)};
+      *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(dg) + i) = q1;
+      *reinterpret_cast<short4v*>(reinterpret_cast<bf16_t*>(dbt) + i) = q2;
+    }
+    s1 = x1.x * gg.x + x1.y * gg.y + x1.z * gg.z + x1.w * gg.w;
+    s2 = x2.x * bb.x + x2.y * bb.y + x2.z * bb.z + x2.w * bb.w;
   }
-  red[0][tid] = s1;
-  red[1][tid] = s2;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = s1;
+    red[1][tid >> 6] = s2;
+  }
   __syncthreads();
-  for (int w = FG_T / 2; w > 0; w >>= 1) {
+  if (tid == 0) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < FG_T / 64; ++w) {
+      t1 += red[0][w];
+      t2 += red[1][w];
+    }
+    part[2 * blockIdx.x] = t1;
+    part[2 * blockIdx.x + 1] = t2;
+  }
+}
+
+__global__ void __launch_bounds__(256) film_grads_finish_kernel(const float* __restrict__ part, int nblk,
+                                                                float* __restrict__ dsg, float* __restrict__ dsb,
+                                                                const float* __restrict__ l2_sg,
+                                                                const float* __restrict__ l2_sb) {
+  __shared__ float red[2][256];
+  const int tid = threadIdx.x;
+  float t1 = 0.f, t2 = 0.f;
+  for (int b = tid; b < nblk; b += 256) {
+    t1 += part[2 * b];
+    t2 += part[2 * b + 1];
+  }
+  red[0][tid] = t1;
+  red[1][tid] = t2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
     if (tid < w) {
       red[0][tid] += red[0][tid + w];
       red[1][tid] += red[1][tid + w];
@@ -1267,12 +1284,27 @@ __global__ void __launch_bounds__(FG_T) film_grads_kernel(const float* __restric
 }
 }  // namespace
 
+// per-device partial-sum buffer of the film_grads blocks (2 floats per block; stream-ordered reuse)
+static float* g_fg_part[16];
+static int g_fg_cap[16];
 SSAMD_API int ssamd_film_grads(const float* S1, const float* S2, const float* g, const float* bt, const float* sg,
                                const float* sb, int n, int out_f32, void* dg, void* dbt, float* dsg, float* dsb,
                                const float* l2_sg, const float* l2_sb, int accum, hipStream_t s) {
   if (n % 4) return -2;
-  hipLaunchKernelGGL(film_grads_kernel, dim3(1), dim3(FG_T), 0, s, S1, S2, g, bt, sg, sb, n, out_f32, dg, dbt, dsg,
-                     dsb, l2_sg, l2_sb, accum);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -3;
+  const int nblk = n > 0 ? cdiv(n / 4, FG_T) : 0;
+  if (nblk > g_fg_cap[dev]) {
+    // a larger buffer; the old one may still be read by queued kernels: keep it (rare, bounded growth)
+    float* p = nullptr;
+    if (hipMalloc(&p, (size_t)2 * nblk * sizeof(float)) != hipSuccess) return -4;
+    g_fg_part[dev] = p;
+    g_fg_cap[dev] = nblk;
+  }
+  if (nblk > 0)
+    hipLaunchKernelGGL(film_grads_kernel, dim3(nblk), dim3(FG_T), 0, s, S1, S2, g, bt, sg, sb, n, out_f32, dg, dbt,
+                       g_fg_part[dev], accum);
+  hipLaunchKernelGGL(film_grads_finish_kernel, dim3(1), dim3(256), 0, s, g_fg_part[dev], nblk, dsg, dsb, l2_sg, l2_sb);
   return (int)hipGetLastError();
 }
 

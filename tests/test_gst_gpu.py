@@ -186,14 +186,15 @@ def test_style_tuner_gpu():
     assert res["accuracy"] == 1.0
 
 
-def test_token_bank_kernel_vs_torch():
+@pytest.mark.parametrize("N,dt,NH,T", [(10, 32, 4, 128), (10, 256, 8, 256), (7, 40, 2, 72)])
+def test_token_bank_kernel_vs_torch(N, dt, NH, T):
     """GST token bank (tanh(E) -> key / value projections split into heads) on the HIP kernels vs the
-    torch fp32 formulation, forward and the three parameter gradients."""
+    torch fp32 formulation, forward and the three parameter gradients (multi-workgroup grids, ragged
+    last workgroup)."""
     from speakingstyle_amd import ops
     from speakingstyle_amd.ops import hip
 
     torch.manual_seed(5)
-    N, dt, NH, T = 10, 32, 4, 128
     E = (torch.randn(N, dt, device="cuda") * 0.5).requires_grad_(True)
     Wk = (torch.randn(T, dt, device="cuda") * 0.2).requires_grad_(True)
     Wv = (torch.randn(T, dt, device="cuda") * 0.2).requires_grad_(True)

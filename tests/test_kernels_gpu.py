@@ -213,7 +213,11 @@ def test_gemm_fused_layernorm(packed, film):
             y = blk(x, lens, style if film else None, pack=pk)
             g = torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).to(torch.bfloat16)
             y.backward(g)
-            grads = [p.grad.clone() for p in blk.parameters() if p.grad is not None]
+            # the key-projection bias has an exactly zero true gradient (softmax is invariant to a shift
+            # shared by all keys of a query), so its computed gradient is rounding noise on both paths:
+            # comparing two noise vectors says nothing -- it is left out of the per-parameter check
+            grads = [p.grad.clone() for n, p in blk.named_parameters()
+                     if p.grad is not None and n != "slf_attn.w_ks.bias"]
             return y.detach().float(), x.grad.float(), grads
 
     y1, gx1, gp1 = run(False)
