@@ -1027,6 +1027,27 @@ __device__ __forceinline__ void st_from_f<float>(float* p, float v) { *p = v; }
 template <>
 __device__ __forceinline__ void st_from_f<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
 
+// 8 consecutive channels as fp32: one 16-B access for bf16 rows, two for fp32 rows (16/32-B aligned: C % 8 == 0)
+__device__ __forceinline__ void ld8f(const bf16_t* p, float* v) {
+  const short8 x = *reinterpret_cast<const short8*>(p);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = bf2f((bf16_t)x[q]);
+}
+__device__ __forceinline__ void ld8f(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8f(bf16_t* p, const float* v) {
+  short8 o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = (short)f2bf(v[q]);
+  *reinterpret_cast<short8*>(p) = o;
+}
+__device__ __forceinline__ void st8f(float* p, const float* v) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) pack_rows_kernel(const T* __restrict__ x, const int64_t* __restrict__ dst,
                                                         const bf16_t* __restrict__ pe, int M, long R, int C,
@@ -1038,14 +1059,15 @@ __global__ void __launch_bounds__(256) pack_rows_kernel(const T* __restrict__ x,
     const long s = dst[r];
     const T* xs = x + s * C + c0;
     T* o = out + r * C + c0;
+    float v[8];
+    ld8f(xs, v);
     if (pe) {
-      const bf16_t* p = pe + (s % M) * C + c0;
+      float pv[8];
+      ld8f(pe + (s % M) * C + c0, pv);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) st_from_f<T>(o + i, ld_as_f<T>(xs + i) + bf2f(p[i]));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = xs[i];
+      for (int i = 0; i < 8; ++i) v[i] += pv[i];
     }
+    st8f(o, v);
   }
 }
 
@@ -1078,14 +1100,16 @@ __global__ void __launch_bounds__(256) repack_rows_kernel(const T* __restrict__ 
     const long d = dst_out[i];
     const int b = (int)(d / M_out), t = (int)(d - (long)b * M_out);
     const bool ok = t < lens_src[b];
-    const T* xs = src + (cu_src[b] + t) * C + c0;
     T* o = out + i * C + c0;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ok) ld8f(src + (cu_src[b] + t) * C + c0, v);
+    if (pe) {
+      float pv[8];
+      ld8f(pe + (long)t * C + c0, pv);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      float v = ok ? ld_as_f<T>(xs + q) : 0.f;
-      if (pe) v += bf2f(pe[(long)t * C + c0 + q]);
-      st_from_f<T>(o + q, v);
+      for (int q = 0; q < 8; ++q) v[q] += pv[q];
     }
+    st8f(o, v);
   }
 }
 
