@@ -19,6 +19,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("command", choices=["variance", "inspect"])
     ap.add_argument("--restore_step", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=1234, help="parameter init seed (restore_step 0: reproducible runs)")
     ap.add_argument("-p", "--preprocess_config", required=True)
     ap.add_argument("-m", "--model_config", required=True)
     ap.add_argument("-t", "--train_config", required=True)
@@ -40,6 +41,7 @@ def main(argv=None):
 
     configs = load_configs(a.preprocess_config, a.model_config, a.train_config)
     dev = torch.device("cuda" if torch.cuda.is_available() and not a.cpu else "cpu")
+    torch.manual_seed(a.seed)
     model = get_model(a.restore_step, configs, dev, train=False, ignore_layers=configs[2].get("ignore_layers", []))
     if a.command == "variance":
         from speakingstyle_amd.analysis.variance import analyze

@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
 //   part[blk][2C..3C) S1[b]     part[blk][3C..4C) S2[b]       (FiLM: S1 = sum_t dout*yd, S2 = sum_t dout)
 // (blk = b * gridDim.x + blockIdx.x) and the host finishes them with fixed-order column sums
 // (k_reduce.hip) -- no float atomics.
-template <int EPL, int LPR>
+template <int EPL, int LPR, bool RELU = false>
 __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ a, const bf16_t* __restrict__ res,
     const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ fg,
@@ -196,6 +196,14 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     }
     float h[EPL], m1[EPL];
     load_row<EPL>(a + row * C + c0, h);
+    // RELU: a is a ReLU output and its producer's backward leaves the ReLU mask to this kernel (it
+    // reads a anyway): d a = dh * (a > 0) -- no residual, no pre-dropout (host check).  Its own
+    // instantiation, the mask as bits: the common kernel keeps its register count (occupancy).
+    uint32_t pos = 0;
+    if constexpr (RELU) {
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) pos |= (h[i] > 0.f ? 1u : 0u) << i;
+    }
     drop_scales<EPL>(seed, (uint64_t)row * C + c0, pre_p, m1);
 #pragma unroll
     for (int i = 0; i < EPL; ++i) h[i] *= m1[i];
@@ -229,6 +237,10 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     sum2 = row_sum<EPL, LPR>(sum2) * invC;
 #pragma unroll
     for (int i = 0; i < EPL; ++i) dh[i] = rs * (dx[i] - sum1 - xh[i] * sum2);
+    if constexpr (RELU) {
+#pragma unroll
+      for (int i = 0; i < EPL; ++i) dh[i] = (pos >> i) & 1u ? dh[i] : 0.f;
+    }
     store_row<EPL>(dh_out + row * C + c0, dh);
     if (da_out) {
 #pragma unroll
@@ -288,8 +300,9 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
                               const float* bias, const float* fg, const float* s_g, const int64_t* lens,
                               const int64_t* cu, const float* mean, const float* rstd, bf16_t* dh, bf16_t* da, float* dw, float* db,
                               float* S1, float* S2, int B, int L, int C, float pre_p, float post_p,
-                              unsigned long long seed, float* ws, long ws_floats, hipStream_t stream) {
+                              unsigned long long seed, int relu_in, float* ws, long ws_floats, hipStream_t stream) {
   if (B == 0 || L == 0) return 0;
+  if (relu_in && (res || da || pre_p > 0.f)) return -2;
   const int film = S1 != nullptr && S2 != nullptr;
   const int gx = cdiv(L, ROWS_PER_BLOCK);
   const long nblk = (long)gx * B;
@@ -297,9 +310,15 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
   if (ws_floats < ssamd_addln_bwd_ws(B, L, C, film)) return -3;
   dim3 grid(gx, B);
   size_t lds = (size_t)WAVES * 2 * C * sizeof(float);  // [WAVES * rows per wave][C]
-  DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR>), grid, dim3(256), lds, stream, dout, a, res, w, bias, fg,
-                                     s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
-                                     (uint64_t)seed));
+  if (relu_in) {
+    DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR, true>), grid, dim3(256), lds, stream, dout, a, res,
+                                       w, bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
+                                       (uint64_t)seed));
+  } else {
+    DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR>), grid, dim3(256), lds, stream, dout, a, res, w,
+                                       bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
+                                       (uint64_t)seed));
+  }
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   float* scratch = ws + nblk * nk * C;

@@ -143,13 +143,13 @@ class VariancePredictor(nn.Module):
 
     def forward(self, x, lengths, style=None):
         cl = self.conv_layer
-        h = cl.conv1d_1(x, act="relu")
-        h = ops.add_layernorm(h, None, cl.layer_norm_1.weight, cl.layer_norm_1.bias,
-                              post_drop=self.dropout, training=self.training)
-        h = cl.conv1d_2(h, act="relu")
+        c1, c2 = cl.conv1d_1, cl.conv1d_2
+        h = ops.conv_relu_layernorm(x, c1.conv.weight, c1.conv.bias, c1.pad, c1.dil, cl.layer_norm_1.weight,
+                                    cl.layer_norm_1.bias, post_drop=self.dropout, training=self.training)
         fp = self.film.pack(style) if (style is not None and hasattr(self, "film")) else None
-        h = ops.add_layernorm(h, None, cl.layer_norm_2.weight, cl.layer_norm_2.bias,
-                              post_drop=self.dropout, training=self.training, film_params=fp)
+        h = ops.conv_relu_layernorm(h, c2.conv.weight, c2.conv.bias, c2.pad, c2.dil, cl.layer_norm_2.weight,
+                                    cl.layer_norm_2.bias, post_drop=self.dropout, training=self.training,
+                                    film_params=fp)
         return ops.predictor_head(h, self.linear_layer.weight, self.linear_layer.bias, lengths)
 
 

@@ -94,6 +94,16 @@ def conv1d(x, w, b=None, pad=0, dil=1, act=None, pack: Optional[PackInfo] = None
     return ref.conv1d(x, w, b, pad, dil, act)
 
 
+def conv_relu_layernorm(x, w, b, pad, dil, ln_w, ln_b, **kw):
+    """LayerNorm(ReLU(conv1d(x))) (+ post-dropout / FiLM via ``kw``): the variance-predictor block
+    (``model/modules.py:221-240``).  On the GPU the conv's backward leaves the ReLU mask to the LayerNorm
+    backward, which reads the ReLU output anyway -- one elementwise pass over the gradient fewer."""
+    if use_hip(x) and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and w.shape[0] in (256, 512, 1024):
+        h = _hip().conv1d(x, w, b, pad, dil, "relu_ln")
+        return _hip().add_layernorm(h, None, ln_w, ln_b, relu_input=True, **kw)
+    return add_layernorm(conv1d(x, w, b, pad, dil, "relu"), None, ln_w, ln_b, **kw)
+
+
 def repack_rows(x, src_pack: PackInfo, out_pack: PackInfo, pe=None):
     """Rows of one packed layout -> another over the same sequences (+ ``pe[t]``); rows past the
     source length are 0 (e.g. the halo-packed FiLM conv stack -> the FFT blocks' packed rows)."""

@@ -67,7 +67,7 @@ _SIGS = {
     "ssamd_colsum": [P, P, L_, I, P, L_, P],
     "ssamd_colsum_ws": [L_, I],
     "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
-    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, P, L_, P],
+    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, I, P, L_, P],
     "ssamd_addln_bwd_ws": [I, I, I, I],
     "ssamd_addln_wb_reduce": [P, I, I, I, I, P, P, P, P],
     "ssamd_lr_fwd": [P, P, P, P, P, P, I, I, I, I, P],
@@ -354,7 +354,7 @@ def weight_dgrad(w: torch.Tensor, owner: Optional[torch.Tensor] = None) -> torch
     return _cached(o, "dgrad", 1, lambda x: x.flip(2).permute(1, 2, 0).to(torch.bfloat16).contiguous(), w)
 
 
-_ACT = {None: 0, "relu": 1, "lrelu": 2, "tanh": 3}
+_ACT = {None: 0, "relu": 1, "lrelu": 2, "tanh": 3, "relu_ln": 1}  # relu_ln: ReLU, mask left to the consumer LN
 
 _ws = {}
 
@@ -728,6 +728,8 @@ class _ConvFn(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         if ctx.act == "relu":
             dy = relu_mask_(dy, y, out=torch.empty_like(dy))  # out of place: dy may be shared
+        elif ctx.act == "relu_ln":
+            pass  # the consuming add_layernorm(relu_input=True) applied the ReLU mask in its backward
         elif ctx.act is not None:
             raise NotImplementedError("backward for activation " + str(ctx.act))
         dx = dw = db = None
@@ -1042,8 +1044,11 @@ def film_scalars_cat(ps):
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox, fused=None):
+    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox, fused=None,
+                relu_in=False):
         B, L, C = a.shape if geom is None else geom  # packed: (sequences, longest, C) over [1, R, C] rows
+        # relu_in: a = ReLU(conv) whose backward left the ReLU mask to this one (conv1d act "relu_ln")
+        ctx.relu_in = bool(relu_in)
         ac = a.contiguous()
         rc_ = None if res is None else res.contiguous()
         gf = None if g is None else _f32_view(g)
@@ -1102,7 +1107,7 @@ class _AddLNFn(torch.autograd.Function):
         rc = lib().ssamd_addln_bwd(_ptr(dout), _ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(sg), _ptr(lens),
                                    _ptr(ctx.cu), _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da),
                                    None if side else _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
-                                   B, L, C, pre_p, post_p, seed, _ptr(ws), ws.numel(), _stream())
+                                   B, L, C, pre_p, post_p, seed, int(ctx.relu_in), _ptr(ws), ws.numel(), _stream())
         _check(rc, "ssamd_addln_bwd")
         if side:
             scratch = ws[nws - 16 * 2 * C:]  # the tail of the buffer is the column-sum scratch
@@ -1150,13 +1155,16 @@ class _AddLNFn(torch.autograd.Function):
                 dg, dbt = (dg.view(ctx.gshape), dbt.view(ctx.gshape)) if first else (None, None)
             else:
                 dg, dbt = dg.to(ctx.gdtype[0]), dbt.to(ctx.gdtype[1])
-        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None, None
+        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None, None, None
 
 
 def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None,
-                  lengths=None, eps=1e-5, pack=None, mailbox=None, fused=None):
+                  lengths=None, eps=1e-5, pack=None, mailbox=None, fused=None, relu_input=False):
+    """``relu_input``: ``a`` came from ``conv1d(..., act="relu_ln")``, whose backward skips the ReLU mask: this
+    LayerNorm's backward applies it (it reads ``a`` anyway).  Needs no residual and no pre-dropout."""
     C = a.shape[-1]
     if fused is not None and fused.used:
+        assert not relu_input, "relu_input: the separate LayerNorm kernel only"
         g = bt = sg = sb = None
         if film_params is not None:
             g, bt, sg, sb = film_params
@@ -1170,6 +1178,8 @@ def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, train
     if C not in (256, 512, 1024) or a.dtype != torch.bfloat16:
         if pack is not None:
             raise ValueError("packed add_layernorm needs C in (256, 512, 1024) and bf16")
+        if relu_input:
+            raise ValueError("add_layernorm(relu_input=True) needs the HIP kernel (C in 256/512/1024, bf16)")
         _torch_fallback(f"add_layernorm C={C} dtype={a.dtype} (kernel: C in 256/512/1024, bf16)")
         return ref.add_layernorm(a, residual, ln_w, ln_b, pre_drop=pre_drop, post_drop=post_drop, training=training,
                                  film_params=film_params, lengths=lengths, eps=eps)
@@ -1186,8 +1196,10 @@ def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, train
         lens = None if lengths is None else lengths.to(torch.int64).contiguous()
     if residual is not None:
         residual = residual.to(a.dtype)
+    if relu_input and (residual is not None or pre_drop > 0):
+        raise ValueError("add_layernorm(relu_input=True) needs no residual and no pre-dropout")
     out = _AddLNFn.apply(a, residual, ln_w, ln_b, g, bt, sg, sb, lens, float(pre_drop), float(post_drop),
-                         _next_seed(), float(eps), cu, geom, mailbox)
+                         _next_seed(), float(eps), cu, geom, mailbox, None, bool(relu_input))
     return out
 
 
