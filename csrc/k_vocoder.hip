@@ -194,7 +194,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
                                                             const float* __restrict__ b1, const bf16_t* __restrict__ w2,
                                                             const float* __restrict__ b2, const bf16_t* acc_in,
                                                             bf16_t* out, int T, int tiles, int d, float slope,
-                                                            float out_scale, int post_lrelu, int dbg) {
+                                                            float out_scale, int post_lrelu) {
   using R = RB<C, K>;
   constexpr int NT = R::NT;
   constexpr int CH = C / 8;                                  // 16-B chunks per row
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     for (int it = 0; it < IT; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
       const int t = t0 - h1 - R::H2 + r;
-      if (r < rows_x && t >= 0 && t < T && !(dbg & 4)) {
+      if (r < rows_x && t >= 0 && t < T) {
         v[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
       } else {
 #pragma unroll
@@ -254,12 +254,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   // 2. conv1 (dilation d): t1 row i <- x rows i + tap*d
   float4v acc[R::MAXRB][R::NSW];
   const int wr = wave % R::WR, wc = wave / R::WR;
-  if (!(dbg & 1)) conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
-  else
-#pragma unroll
-    for (int r = 0; r < R::MAXRB; ++r)
-#pragma unroll
-      for (int s = 0; s < R::NSW; ++s) acc[r][s] = float4v{0.f, 0.f, 0.f, 0.f};
+  conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
     const int rb = wr + R::WR * r;
@@ -281,7 +276,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   __syncthreads();  // t1 complete; the x tile is dead from here on (os aliases it)
 
   // 3. conv2 (dilation 1): out row j <- t1 rows j + tap
-  if (!(dbg & 2)) conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
+  conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
     const int rb = wr + R::WR * r;
@@ -335,7 +330,6 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   }
 }
 
-static int g_rb_debug = 0;  // A/B timing switch: bit 0 skip conv1 MFMAs, bit 1 conv2, bit 2 x loads
 
 template <int C, int K>
 int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
@@ -349,7 +343,7 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
   }
   const int tiles = (T + R::BM - 1) / R::BM;
   hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
-                     acc_in, out, T, tiles, d, slope, out_scale, post_lrelu, g_rb_debug);
+                     acc_in, out, T, tiles, d, slope, out_scale, post_lrelu);
   return (int)hipGetLastError();
 }
 
@@ -770,7 +764,6 @@ int launch_rf(const bf16_t* x, const RFW& p, const bf16_t* acc_in, bf16_t* out, 
 
 }  // namespace
 
-SSAMD_API void ssamd_resblock_debug(int v) { g_rb_debug = v; }
 
 // Whole ResBlock1 (see resblock_fused_kernel).  x / out / acc_in [B, T, C] bf16 (out must not alias x;
 // acc_in may alias out, or be null); w: 6 bf16 [C][K][C] images (c1_0, c2_0, c1_1, c2_1, c1_2, c2_2);
