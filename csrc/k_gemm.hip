@@ -832,18 +832,18 @@ __device__ __forceinline__ void pp_barrier() {
 //             epilogue (one exposed memory round trip per 8 rows with nothing else in flight).
 // STG (BUF only): the staggered 8-phase main loop -- see the comment at its loop below.
 constexpr int EPI_GEN = 0, EPI_BNH = 1, EPI_MASK = 2;
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, int EPIM = EPI_GEN, bool STG = false>
-__global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
-                                                               const float* __restrict__ bias,
-                                                               const bf16_t* __restrict__ aux,
-                                                               const bf16_t* __restrict__ resid,
-                                                               const int64_t* __restrict__ lens, void* __restrict__ Yv,
-                                                               ConvGeom g, int act, int ldy, EpiX ex) {
+// One 256x256 output tile (virtual block vb) of the big64 GEMM; the __global__ wrapper below runs one tile
+// per workgroup (TPB = 1) or TPB tiles per workgroup in sequence.
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF, int EPIM, bool STG>
+__device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                           const float* __restrict__ bias, const bf16_t* __restrict__ aux,
+                                           const bf16_t* __restrict__ resid, const int64_t* __restrict__ lens,
+                                           void* __restrict__ Yv, ConvGeom g, int act, int ldy, EpiX ex, int vb) {
   const void* const g_zero_chunk = zero_chunk_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nN = (g.N + BG - 1) / BG;
   const int nM = (g.M + BG - 1) / BG;
-  const int2 tmn = tile_of(xcd_remap(blockIdx.x, nN * nM), nM, nN, g.ngrp);
+  const int2 tmn = tile_of(xcd_remap(vb, nN * nM), nM, nN, g.ngrp);
   const int tm = tmn.x, tn = tmn.y;
   const int m0 = tm * BG, n0 = tn * BG;
   // wave index as a scalar: LDS-DMA destinations (M0) and per-wave offsets stay in SGPRs
@@ -1522,6 +1522,29 @@ __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* _
       if (n >= g.N) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       epi_store4<OUT_F32>(v, m, n, bias, aux, resid, valid, act, ldy, Yv);
+    }
+  }
+}
+
+// TPB > 1: each workgroup runs tiles blockIdx.x, blockIdx.x + gridDim.x, ... in sequence (gridDim.x a multiple
+// of 8, so every tile of a workgroup stays on its XCD under xcd_remap): a CU goes from one tile's epilogue to the
+// next tile's prologue without a workgroup retire / dispatch (~3 us per tile-round, measured with per-block
+// stamps).  Every exit of big64_tile is workgroup-uniform, so all waves reach the barrier that orders the
+// epilogue's LDS reads before the next tile's staging.
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, int EPIM = EPI_GEN, bool STG = false, int TPB = 1>
+__global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                               const float* __restrict__ bias,
+                                                               const bf16_t* __restrict__ aux,
+                                                               const bf16_t* __restrict__ resid,
+                                                               const int64_t* __restrict__ lens, void* __restrict__ Yv,
+                                                               ConvGeom g, int act, int ldy, EpiX ex) {
+  if constexpr (TPB == 1) {
+    big64_tile<OUT_F32, FASTK, PACKED, BUF, EPIM, STG>(X, W, bias, aux, resid, lens, Yv, g, act, ldy, ex, blockIdx.x);
+  } else {
+    const int total = ((g.N + BG - 1) / BG) * ((g.M + BG - 1) / BG);
+    for (int vb = blockIdx.x; vb < total; vb += gridDim.x) {
+      if (vb != (int)blockIdx.x) __syncthreads();
+      big64_tile<OUT_F32, FASTK, PACKED, BUF, EPIM, STG>(X, W, bias, aux, resid, lens, Yv, g, act, ldy, ex, vb);
     }
   }
 }
@@ -2583,6 +2606,11 @@ static int g_gemm_stg = 1;
 static int g_gemm_mask_pre = 1;  // EPI_MASK for the ReLU-mask data gradient (0: the generic epilogue, A/B)
 SSAMD_API void ssamd_gemm_set_mask_pre(int v) { g_gemm_mask_pre = v; }
 SSAMD_API void ssamd_gemm_set_stg(int v) { g_gemm_stg = v; }
+// tiles per workgroup of the short-K (K < 512, double-buffer loop) generic big64 GEMM when its tiles outnumber
+// the CUs (experimental.gemm_tpb; 1 = one tile per workgroup)
+static int g_gemm_tpb = 1;
+static int device_cus();
+SSAMD_API void ssamd_gemm_set_tpb(int v) { g_gemm_tpb = v == 2 ? 2 : 1; }
 
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
 static bool big64_buf_ok(const ConvGeom& g) {
@@ -2722,6 +2750,8 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_MASK>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_MASK, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_MASK, true>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_GEN, false, 2>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_GEN, false, 2>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -2734,6 +2764,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
       const bool stg_ = g_gemm_stg && g.K >= 512;                                                        \
+      int grid_x = nwgb;                                                                                 \
       if constexpr (!F32) {                                                                              \
         if (bnh) kfn = conv_gemm_big64_kernel<false, FK, false, BF, EPI_BNH>;                           \
       }                                                                                                  \
@@ -2747,9 +2778,14 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
                                   : conv_gemm_big64_kernel<false, true, false, true, EPI_MASK, true>)    \
                        : (g.rinfo ? conv_gemm_big64_kernel<false, true, true, true, EPI_MASK>             \
                                   : conv_gemm_big64_kernel<false, true, false, true, EPI_MASK>);         \
+          if (g_gemm_tpb == 2 && !stg_ && !bnh && !(g_gemm_mask_pre && mask_pre) && nwgb > device_cus()) { \
+            kfn = g.rinfo ? conv_gemm_big64_kernel<false, true, true, true, EPI_GEN, false, 2>           \
+                          : conv_gemm_big64_kernel<false, true, false, true, EPI_GEN, false, 2>;         \
+            grid_x = ((nwgb + 1) / 2 + 7) / 8 * 8;                                                       \
+          }                                                                                              \
         }                                                                                                \
       }                                                                                                  \
-      hipLaunchKernelGGL(kfn, dim3(nwgb), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
+      hipLaunchKernelGGL(kfn, dim3(grid_x), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
     } while (0)
     const bool bf = fastk && big64_buf_ok(g);
     if (out_f32) {

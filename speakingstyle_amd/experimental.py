@@ -71,6 +71,8 @@ KNOBS: Dict[str, tuple] = {
                                  "blocks hand CUs back to the main stream sooner; measured slower, profiles/r4_exp_wgrad_min_rounds.txt)"),
     "ln_fuse": (False, _bool, "residual + LayerNorm tail in the producing GEMM's epilogue (measured slower)"),
     "gemm_stg": (True, _bool, "staggered 8-phase main loop of the 256x256 GEMM for K >= 512 (+0.7 % LJSpeech)"),
+    "gemm_tpb": (1, int, "tiles per workgroup (1 or 2) of the short-K generic 256x256 GEMM when its tiles outnumber "
+                         "the CUs (2 measured -0.8 %, profiles/r4_exp_gemm_tpb.txt)"),
     "gemm_mask_pre": (True, _bool, "ReLU-mask data gradient with its mask bytes prefetched before the main loop"),
     "bn_fuse": (True, _bool, "PostNet BatchNorm backward started in the data-gradient GEMM's epilogue"),
     "defer_release": (False, _bool, "hand the side-stream weight-gradient inputs back to the trainer, freed "

@@ -52,6 +52,7 @@ _SIGS = {
     "ssamd_gemm_set_mask_pre": [I],
     "ssamd_bn_set_dz_cfg": [I, I],
     "ssamd_wgrad_set_min_rounds": [I],
+    "ssamd_gemm_set_tpb": [I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
     "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],

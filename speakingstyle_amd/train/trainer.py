@@ -71,6 +71,7 @@ class Trainer:
                 hip.lib().ssamd_gemm_set_stg(int(experimental.get("gemm_stg")))
                 hip.lib().ssamd_gemm_set_mask_pre(int(experimental.get("gemm_mask_pre")))
                 hip.lib().ssamd_wgrad_set_min_rounds(int(experimental.get("wgrad_min_rounds")))
+                hip.lib().ssamd_gemm_set_tpb(int(experimental.get("gemm_tpb")))
         self._held = None
         # backward on the calling thread instead of autograd's per-device worker thread: no thread
         # hand-off per backward and less engine bookkeeping -- host enqueue per step 15.7 -> 12.1 ms

@@ -1425,3 +1425,36 @@ def test_hifigan_generator_hip_training_vs_torch():
             bad.append((n, _rel(grads[n], p.grad)))
     assert len(grads) > 50 and not bad, bad
 
+
+
+@pytest.mark.parametrize("Cin,N,ks,packed,M,resid", [(256, 256, 1, False, 70001, False), (256, 768, 1, True, 90000, False),
+                                                     (256, 256, 1, False, 66000, True), (128, 256, 3, False, 75003, False)])
+def test_gemm_two_tiles_per_block_bitwise(Cin, N, ks, packed, M, resid):
+    """Two 256x256 tiles per workgroup (ssamd_gemm_set_tpb(2), short-K generic GEMM with more tiles than CUs)
+    computes every tile exactly as one tile per workgroup: bitwise-equal outputs, ragged M, packed rows,
+    residual epilogue operand."""
+    torch.manual_seed(37)
+    x = torch.randn(1, M, Cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, ks, Cin, device=DEV) / math.sqrt(ks * Cin)).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    r = torch.randn(1, M, N, device=DEV).to(torch.bfloat16) if resid else None
+    pad = (ks - 1) // 2
+    rinfo = None
+    if packed:
+        from speakingstyle_amd.ops.packing import PackInfo
+
+        n = M // 5
+        lens = torch.tensor([n, n + 7, n - 3, n + 1, M - 4 * n - 5], device=DEV)
+        pk = PackInfo.build(lens, int(lens.max()), int(lens.sum()))
+        assert pk.R == M
+        rinfo = pk.rinfo
+    lib = hip.lib()
+    try:
+        lib.ssamd_gemm_set_tpb(1)
+        y0 = hip.conv_gemm_raw(x, w, bias, 1, M, Cin, ks, 1, pad, N, 1, resid=r, rinfo=rinfo)
+        lib.ssamd_gemm_set_tpb(2)
+        y1 = hip.conv_gemm_raw(x, w, bias, 1, M, Cin, ks, 1, pad, N, 1, resid=r, rinfo=rinfo)
+    finally:
+        lib.ssamd_gemm_set_tpb(1)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
