@@ -61,7 +61,27 @@ __device__ __forceinline__ float row_sum(float v) {
   return v;
 }
 
-template <int EPL, int LPR>
+// A row piece kept as raw bf16 (EPL / 8 x 16 B) so its load can be issued an iteration ahead: converting at
+// the load site would make the wait (and, vmcnt counting stores too, the drain of the previous row's stores)
+// happen right there.
+template <int EPL>
+struct RawRow {
+  short8 x[EPL / 8];
+};
+template <int EPL>
+__device__ __forceinline__ void load_raw(const bf16_t* p, RawRow<EPL>& r) {
+#pragma unroll
+  for (int j = 0; j < EPL / 8; ++j) r.x[j] = *reinterpret_cast<const short8*>(p + 8 * j);
+}
+template <int EPL>
+__device__ __forceinline__ void raw_to_f(const RawRow<EPL>& r, float* v) {
+#pragma unroll
+  for (int j = 0; j < EPL / 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[8 * j + i] = bf2f((bf16_t)r.x[j][i]);
+}
+
+template <int EPL, int LPR, bool RES>
 __global__ void __launch_bounds__(256) addln_fwd_kernel(
     const bf16_t* __restrict__ a, const bf16_t* __restrict__ res, const float* __restrict__ w,
     const float* __restrict__ bias, const float* __restrict__ fg, const float* __restrict__ fb,
@@ -95,21 +115,37 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
     }
   }
   const float invC = 1.f / C;
-  for (int r = 0; r < ROWS_PER_WAVE / RPW; ++r) {
-    const int t = blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub;
-    if (t >= Lb) continue;  // per-half guard (the row reductions stay inside a half)
+  // Rows are software-pipelined one ahead (row r+1's a / res loads are issued before row r's store) in
+  // straight-line code: a half-wave past the sequence end recomputes and rewrites the last row (identical
+  // bytes) instead of branching, and the per-row statistics are stored after the loop, so the waitcnt pass
+  // never merges paths with different outstanding stores (which turns every wait into a full drain).
+  constexpr int NR = ROWS_PER_WAVE / RPW;
+  RawRow<EPL> ra[2], rr[2];
+  float mus[NR], rss[NR];
+  auto t_of = [&](int r) { return min(blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub, Lb - 1); };
+  auto fetch = [&](int r, int q) {
+    const long row = rowb + t_of(r);
+    load_raw<EPL>(a + row * C + c0, ra[q]);
+    if constexpr (RES) load_raw<EPL>(res + row * C + c0, rr[q]);
+  };
+  fetch(0, 0);
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int cur = r & 1;
+    if (r + 1 < NR) fetch(r + 1, cur ^ 1);
+    const int t = t_of(r);
     const long row = rowb + t;
     float h[EPL];
-    load_row<EPL>(a + row * C + c0, h);
+    raw_to_f<EPL>(ra[cur], h);
     if (pre_p > 0.f) {
       float ks[EPL];
       drop_scales<EPL>(seed, (uint64_t)row * C + c0, pre_p, ks);
 #pragma unroll
       for (int i = 0; i < EPL; ++i) h[i] *= ks[i];
     }
-    if (res) {
+    if constexpr (RES) {
       float rv[EPL];
-      load_row<EPL>(res + row * C + c0, rv);
+      raw_to_f<EPL>(rr[cur], rv);
 #pragma unroll
       for (int i = 0; i < EPL; ++i) h[i] += rv[i];
     }
@@ -135,9 +171,15 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
       y[i] = valid ? v : 0.f;
     }
     store_row<EPL>(out + row * C + c0, y);
-    if (rl == 0 && mean_out) {
-      mean_out[row] = mu;
-      rstd_out[row] = rs;
+    mus[r] = mu;
+    rss[r] = rs;
+  }
+  if (rl == 0 && mean_out) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const long row = rowb + t_of(r);
+      mean_out[row] = mus[r];
+      rstd_out[row] = rss[r];
     }
   }
 }
@@ -285,8 +327,13 @@ SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w
   if (C % 256 != 0 && C != 256 && C != 512 && C != 1024) return -1;
   if (B == 0 || L == 0) return 0;
   dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
-  DISPATCH_EPL(C, hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR>), grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
+  if (res) {
+    DISPATCH_EPL(C, hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR, true>), grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
                                      s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
+  } else {
+    DISPATCH_EPL(C, hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR, false>), grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
+                                     s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
+  }
   return (int)hipGetLastError();
 }
 
