@@ -27,9 +27,14 @@ same per-GPU batch semantics ``train.py`` uses when that key is set; without it
 Synthesis (``synth_rtf`` field, BASELINE's second metric): text ids -> int16 wav
 through FastSpeech2 + style encoder (``--synth-config``, default BC2013_GST = the
 GST reference encoder + style-token attention on a reference mel, BASELINE #5) +
-HiFi-GAN V1, batch 256 per GPU, independent shards per rank; RTF = max-over-ranks
-wall / total audio seconds.  ``synth.rtf_also`` repeats it with ``--synth-also``
-(default BC2013: the reference's FiLM reference encoder).
+HiFi-GAN V1, batch 256 per GPU over ``--synth-steps`` distinct batches, independent
+shards per rank; RTF = max-over-ranks wall / total audio seconds.  ``synth.rtf_also``
+repeats it with ``--synth-also`` (default BC2013: the reference's FiLM reference
+encoder).  ``synth_rtf_b1``: the like-for-like point of the reference's only
+synthesis number (batch 1, one 113-frame utterance, RTF 1.33 in
+``notebooks/control.ipynb:778``): median wall time of ``--synth-b1-runs`` runs of one
+~113-frame utterance (text ids -> int16 waveform on the host) / its audio seconds;
+``synth_vs_baseline`` compares THAT with 1.33.
 See ``speakingstyle_amd/benchmark.py`` for the duration-injection detail.
 """
 from __future__ import annotations
@@ -63,7 +68,11 @@ def parse(argv=None):
     ap.add_argument("--synth-also", default="BC2013",
                     help="second synthesis config reported as synth.rtf_also ('' disables): the FiLM encoder")
     ap.add_argument("--synth-batch", type=int, default=256)
-    ap.add_argument("--synth-steps", type=int, default=3, help="0 disables the synthesis phase")
+    ap.add_argument("--synth-steps", type=int, default=10,
+                    help="timed batch-256 synthesis steps, each on a distinct batch (0 disables the synthesis phase)")
+    ap.add_argument("--synth-b1-runs", type=int, default=30,
+                    help="batch-1 latency runs (one ~113-frame utterance, text -> int16 wav on the host; 0 disables)")
+    ap.add_argument("--synth-b1-phones", type=int, default=14, help="phonemes of the batch-1 utterance")
     ap.add_argument("--synth-warmup", type=int, default=1)
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--vocoder-buckets", type=int, default=8,
@@ -140,6 +149,7 @@ def run(args):
 
         a2 = copy.copy(args)
         a2.synth_config = args.synth_also
+        a2.synth_b1_runs = 0
         sy2 = B.synth_phase(a2, rank, world, device)
 
     value = tr["frames"] / tr["elapsed"]
@@ -181,20 +191,29 @@ def run(args):
         rec["phase_ms"] = {k: {"host": round(v["host_ms"], 3), "device": round(v["device_ms"], 3)}
                            for k, v in tr["phases"].items()}
     if sy is not None:
+        b1 = sy.get("b1")
         rec.update({
             "synth_rtf": sy["rtf"],
-            "synth_vs_baseline": round(BASELINE_RTF / sy["rtf"], 1),
+            "synth_rtf_b1": None if b1 is None else b1["rtf"],
+            "synth_vs_baseline": None if b1 is None else round(BASELINE_RTF / b1["rtf"], 1),
             "synth": {
                 "metric": "synth RTF (text ids -> int16 wav; lower is better)",
                 "model": f"FastSpeech2 ({args.synth_config}, style encoder on a reference mel) + HiFi-GAN V1"
                          + (" tiny" if args.tiny else ""),
                 "batch_per_gpu": args.synth_batch, "steps": args.synth_steps, "warmup": args.synth_warmup,
+                "distinct_batches": sy["distinct_batches"],
                 "audio_seconds": round(sy["audio_s"], 2), "wall_s": round(sy["wall"], 4),
                 "mel_frames_per_utt": round(sy["frames_per_utt"], 1),
                 "vocoder_length_buckets": args.vocoder_buckets,
                 "parallelism": f"dp{world} (independent shards)",
             },
         })
+        if b1 is not None:
+            rec["synth"]["b1"] = {"metric": "batch-1 latency: one utterance, text ids -> int16 wav on the host",
+                                  "median_ms": round(1e3 * b1["median_s"], 3), "min_ms": round(1e3 * b1["min_s"], 3),
+                                  "max_ms": round(1e3 * b1["max_s"], 3), "runs": b1["runs"],
+                                  "mel_frames": b1["mel_frames"], "audio_seconds": round(b1["audio_s"], 4),
+                                  "baseline": "RTF 1.33: 113 frames, batch 1 (notebooks/control.ipynb:778)"}
         if sy2 is not None:
             rec["synth"]["rtf_also"] = {"model": f"FastSpeech2 ({args.synth_also}) + HiFi-GAN V1", "rtf": sy2["rtf"],
                                         "audio_seconds": round(sy2["audio_s"], 2)}

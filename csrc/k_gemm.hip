@@ -76,27 +76,13 @@ struct EpiX {
   bf16_t* y2;
   float scale;
   int post_act;
-  // Fused residual + LayerNorm tail (big64 only, N == 256: one 256x256 tile owns whole rows).
-  // With ln_out set, the GEMM output a (bias added, bf16) is stored as usual AND
-  //   ln_out = rowmask( FiLM( post_drop( LN( pre_drop(a) + ln_res ) ) ) ), mean / rstd per row,
-  // bit-identical to the separate addln_fwd kernel (k_norm.hip) on the same a, whose backward
-  // consumes (a, ln_res, mean, rstd) unchanged.  Rows: unpacked (m = b*Lseq + t, valid t < lens[b])
-  // or packed (dst[m] = b*Mseq + t, all rows valid).
-  const bf16_t* ln_res;
-  const float* ln_w;
-  const float* ln_b;
-  const float* film_g;
-  const float* film_b;
-  const float* s_g;
-  const float* s_b;
-  const int64_t* ln_lens;
-  const int64_t* dst;
-  bf16_t* ln_out;
-  float* mean;
-  float* rstd;
-  int Lseq, Mseq;
-  float pre_p, post_p, eps;
-  unsigned long long seed;
+  // BatchNorm-backward head operands (EPI_BNH only, see below): bn_stats = the forward's
+  // [mean | rstd | scale | shift] x N, bn_part = the per-M-tile column partials, bn_p / bn_seed = the
+  // dropout that followed the BatchNorm (bn_h = acc, bn_act = post_act)
+  const float* bn_stats;
+  float* bn_part;
+  float bn_p;
+  unsigned long long bn_seed;
   // ReLU bitmask (big64 LDS-staged epilogue, N % 8 == 0): mask_out[m][n/8] bit q = (y[m][n+q] > 0)
   // written by a ReLU GEMM; mask_in multiplies the output by the stored bits instead of reading a
   // bf16 aux operand (16x fewer bytes for the FFN hidden layer's dgrad)
@@ -108,9 +94,7 @@ struct EpiX {
   // and writes the tile's column partials  sum_rows dz  and  sum_rows dz * (bn_h - mean)  to
   // bn_part[tm][N] and bn_part[nM + tm][N] (tm = M tile; fixed order, no atomics).  bn_stats = the
   // forward's [mean | rstd | scale | shift] x N.  The partial sums replace k_bn.hip's bn_bwd_reduce pass
-  // (a full re-read of dy and bn_h); the dropout mask and act' are bit-identical to it.  The fields
-  // alias members the BNH variant does not otherwise use, so EpiX (the kernel argument block of every
-  // variant) keeps its size: bn_h = acc, bn_stats = ln_w, bn_part = mean, bn_act = post_act, p = pre_p.
+  // (a full re-read of dy and bn_h); the dropout mask and act' are bit-identical to it.
 };
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -832,8 +816,7 @@ __device__ __forceinline__ void pp_barrier() {
 //             epilogue (one exposed memory round trip per 8 rows with nothing else in flight).
 // STG (BUF only): the staggered 8-phase main loop -- see the comment at its loop below.
 constexpr int EPI_GEN = 0, EPI_BNH = 1, EPI_MASK = 2;
-// One 256x256 output tile (virtual block vb) of the big64 GEMM; the __global__ wrapper below runs one tile
-// per workgroup (TPB = 1) or TPB tiles per workgroup in sequence.
+// One 256x256 output tile (block vb) of the big64 GEMM.
 template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF, int EPIM, bool STG>
 __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                            const float* __restrict__ bias, const bf16_t* __restrict__ aux,
@@ -1226,8 +1209,8 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
       if constexpr (EPIM == EPI_MASK) __builtin_amdgcn_s_waitcnt(0x0F70);
       bf16_t* Y = reinterpret_cast<bf16_t*>(Yv);
       if constexpr (EPIM == EPI_BNH) {
-        // BatchNorm-backward head (EpiX aliases: acc = bn_h, ln_w = [mean | rstd | scale | shift] x N,
-        // mean = partials, post_act = act code, pre_p = dropout p).  Thread (c = tid & 31, r0 = tid >> 5)
+        // BatchNorm-backward head (EpiX: acc = bn_h, bn_stats = [mean | rstd | scale | shift] x N,
+        // bn_part = partials, post_act = act code, bn_p = dropout p).  Thread (c = tid & 31, r0 = tid >> 5)
         // owns column chunk c of rows r0 + 16 it, loads h for EPG rows before use, stores dz and keeps
         // its 8 columns' running sums; the tile's 16 per-column partials are then combined in fixed order.
         // The epilogue runs while the CU's MFMAs idle (one workgroup per CU), so its VALU count is the
@@ -1245,9 +1228,9 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int nq = col_ok ? n + q : 0;
-          bmu[q] = ex.ln_w[nq];
-          bsc[q] = ex.ln_w[2 * g.N + nq] * zs;
-          bsh[q] = ex.ln_w[3 * g.N + nq] * zs;
+          bmu[q] = ex.bn_stats[nq];
+          bsc[q] = ex.bn_stats[2 * g.N + nq] * zs;
+          bsh[q] = ex.bn_stats[3 * g.N + nq] * zs;
           bs1[q] = 0.f;
           bs2[q] = 0.f;
         }
@@ -1266,7 +1249,7 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
             const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
             const long off = (long)m * ldy + n;
             float ks[8];
-            drop_scales<8>(ex.seed, (uint64_t)off, ex.pre_p, ks);
+            drop_scales<8>(ex.bn_seed, (uint64_t)off, ex.bn_p, ks);
             short8 o;
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -1306,97 +1289,10 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
           float a = 0.f;
 #pragma unroll
           for (int r = 0; r < 16; ++r) a += red[which * 4096 + r * 256 + col];
-          ex.mean[((long)which * nM + tm) * g.N + n0 + col] = a;
+          ex.bn_part[((long)which * nM + tm) * g.N + n0 + col] = a;
         }
         return;
       } else {  // !EPI_BNH: the BNH instantiation compiles none of the code below
-      if (ex.ln_out) {
-        // Residual + LayerNorm tail (N == 256, n0 == 0): half-wave h = tid >> 5 owns rows h, h+16, ...
-        // of the tile, lane c = tid & 31 owns columns 8c..8c+7.  Every global operand of the 16 rows
-        // (residual segments, row -> sequence / validity) is loaded up front and the FiLM rows one
-        // row ahead, so the epilogue is not a chain of exposed load latencies.
-        const int c = tid & 31, h = tid >> 5, n = c * 8;
-        float lw[8], lb[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          lw[q] = ex.ln_w[n + q];
-          lb[q] = ex.ln_b[n + q];
-        }
-        short8 rr[16];
-        int bq[16];
-        bool rv[16];
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-          const int m = m0 + h + it * 16;
-          const int mm = m < g.M ? m : g.M - 1;
-          rr[it] = *reinterpret_cast<const short8*>(ex.ln_res + (long)mm * 256 + n);
-          if (ex.dst) {
-            bq[it] = (int)(ex.dst[mm] / ex.Mseq);
-            rv[it] = true;
-          } else {
-            bq[it] = mm / ex.Lseq;
-            rv[it] = ex.ln_lens ? (mm - bq[it] * ex.Lseq) < (int)ex.ln_lens[bq[it]] : true;
-          }
-        }
-        const bool film = ex.film_g != nullptr;
-        const float sg = film ? *ex.s_g : 0.f, sb = film ? *ex.s_b : 0.f;
-        float fg[8], fb[8];
-        auto load_film = [&](int b) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            fg[q] = film ? ex.film_g[(long)b * 256 + n + q] : 0.f;
-            fb[q] = film ? ex.film_b[(long)b * 256 + n + q] : 0.f;
-          }
-        };
-        load_film(bq[0]);
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-          const int r = h + it * 16, m = m0 + r;
-          float G[8], Bt[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            G[q] = sg * fg[q] + 1.f;
-            Bt[q] = sb * fb[q];
-          }
-          if (it + 1 < 16 && film && bq[it + 1] != bq[it]) load_film(bq[it + 1]);  // one row ahead
-          if (m >= g.M) continue;  // uniform over the half-wave
-          const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
-          const long ro = (long)m * 256 + n;
-          *reinterpret_cast<short8*>(Y + ro) = v;  // a (the pre-LN GEMM output: the backward reads it)
-          float hv[8], sum = 0.f, k1[8], k2[8];
-          drop_scales<8>(ex.seed, (uint64_t)ro, ex.pre_p, k1);
-          drop_scales<8>(ex.seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)ro, ex.post_p, k2);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            hv[q] = bf2f((bf16_t)v[q]) * k1[q];
-            hv[q] += bf2f((bf16_t)rr[it][q]);
-            sum += hv[q];
-          }
-#pragma unroll
-          for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-          const float mu = sum * (1.f / 256.f);
-          float sq = 0.f;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) sq += (hv[q] - mu) * (hv[q] - mu);
-#pragma unroll
-          for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
-          const float rs = rsqrtf(sq * (1.f / 256.f) + ex.eps);
-          short8 o8;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            float y = (hv[q] - mu) * rs * lw[q] + lb[q];
-            y *= k2[q];
-            y = G[q] * y + Bt[q];
-            o8[q] = (short)f2bf(rv[it] ? y : 0.f);
-          }
-          *reinterpret_cast<short8*>(ex.ln_out + ro) = o8;
-          if (c == 0) {
-            ex.mean[m] = mu;
-            ex.rstd[m] = rs;
-          }
-        }
-        return;
-      }
       const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_in;
       // Thread (c = tid & 31, r0 = tid >> 5) owns the 16-B column chunk c of rows r0 + 16 it.  The
       // global operands of EPG rows (aux / residual / accumulator segments, mask bytes, sequence
@@ -1526,27 +1422,14 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
   }
 }
 
-// TPB > 1: each workgroup runs tiles blockIdx.x, blockIdx.x + gridDim.x, ... in sequence (gridDim.x a multiple
-// of 8, so every tile of a workgroup stays on its XCD under xcd_remap): a CU goes from one tile's epilogue to the
-// next tile's prologue without a workgroup retire / dispatch (~3 us per tile-round, measured with per-block
-// stamps).  Every exit of big64_tile is workgroup-uniform, so all waves reach the barrier that orders the
-// epilogue's LDS reads before the next tile's staging.
-template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, int EPIM = EPI_GEN, bool STG = false, int TPB = 1>
+template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF = false, int EPIM = EPI_GEN, bool STG = false>
 __global__ void __launch_bounds__(NT3, 1) conv_gemm_big64_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
                                                                const bf16_t* __restrict__ aux,
                                                                const bf16_t* __restrict__ resid,
                                                                const int64_t* __restrict__ lens, void* __restrict__ Yv,
                                                                ConvGeom g, int act, int ldy, EpiX ex) {
-  if constexpr (TPB == 1) {
-    big64_tile<OUT_F32, FASTK, PACKED, BUF, EPIM, STG>(X, W, bias, aux, resid, lens, Yv, g, act, ldy, ex, blockIdx.x);
-  } else {
-    const int total = ((g.N + BG - 1) / BG) * ((g.M + BG - 1) / BG);
-    for (int vb = blockIdx.x; vb < total; vb += gridDim.x) {
-      if (vb != (int)blockIdx.x) __syncthreads();
-      big64_tile<OUT_F32, FASTK, PACKED, BUF, EPIM, STG>(X, W, bias, aux, resid, lens, Yv, g, act, ldy, ex, vb);
-    }
-  }
+  big64_tile<OUT_F32, FASTK, PACKED, BUF, EPIM, STG>(X, W, bias, aux, resid, lens, Yv, g, act, ldy, ex, blockIdx.x);
 }
 
 
@@ -2606,11 +2489,6 @@ static int g_gemm_stg = 1;
 static int g_gemm_mask_pre = 1;  // EPI_MASK for the ReLU-mask data gradient (0: the generic epilogue, A/B)
 SSAMD_API void ssamd_gemm_set_mask_pre(int v) { g_gemm_mask_pre = v; }
 SSAMD_API void ssamd_gemm_set_stg(int v) { g_gemm_stg = v; }
-// tiles per workgroup of the short-K (K < 512, double-buffer loop) generic big64 GEMM when its tiles outnumber
-// the CUs (experimental.gemm_tpb; 1 = one tile per workgroup)
-static int g_gemm_tpb = 1;
-static int device_cus();
-SSAMD_API void ssamd_gemm_set_tpb(int v) { g_gemm_tpb = v == 2 ? 2 : 1; }
 
 // every byte offset of the descriptors must stay below the out-of-range marker 0x80000000
 static bool big64_buf_ok(const ConvGeom& g) {
@@ -2666,8 +2544,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   {
     const int tiles = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
     const int nk64 = (g.K + 63) / 64;
-    const bool plain = !(ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.ln_out || ex.mask_out || ex.mask_in ||
-                         bnh);
+    const bool plain = !(ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_out || ex.mask_in || bnh);
     int S = 0;
     if (g_splitk > 0) S = g_splitk;
     else if (g_splitk < 0 && g_gemm_variant < 0 && tiles <= 128 && nk64 >= 16)
@@ -2703,13 +2580,13 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     }
   }
   if (bnh) {  // BatchNorm-backward head (EpiX aliases: acc = bn_h, ln_w = stats, mean = partials): big64 only
-    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act != 0 || ex.post_act == 2 || aux || resid || lens || !ex.acc || !ex.ln_w ||
-        !ex.mean || rinfo || ex.y2 || ex.ln_out || ex.mask_out || ex.mask_in)
+    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act != 0 || ex.post_act == 2 || aux || resid || lens || !ex.acc ||
+        !ex.bn_stats || !ex.bn_part || rinfo || ex.y2 || ex.mask_out || ex.mask_in)
       return -3;
     variant = 4;
   } else {
   if (ex.mask_out || ex.mask_in) {  // the bitmask lives in the big64 LDS-staged epilogue only
-    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act < 0 || ex.ln_out) return -3;
+    if (N < 256 || (N % 8) || ldy != N || out_f32 || !reg || act < 0) return -3;
     if (ex.mask_out && act != ACT_RELU) return -3;
     variant = 4;
   }
@@ -2718,10 +2595,6 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     if (out_f32 || !reg || (N % 8) || (ldy % 8) || act < 0) return -3;
     if (N >= 256) variant = 4;
     else if (variant != 2) return -3;
-  }
-  if (ex.ln_out) {  // the LayerNorm tail needs whole rows in one tile and the plain bf16 store
-    if (xon || N != 256 || ldy != 256 || out_f32 || !reg || act != 0 || aux || resid || lens) return -3;
-    variant = 4;
   }
   }  // !bnh
   if (reg && variant == 4 && N >= 256) {
@@ -2750,8 +2623,6 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_MASK>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_MASK, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_MASK, true>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_GEN, false, 2>, B64_LDS);
-      allow_lds(conv_gemm_big64_kernel<false, true, true, true, EPI_GEN, false, 2>, B64_LDS);
       b64_set = true;
     }
     const int nwgb = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
@@ -2759,7 +2630,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
     const size_t LB = B64_LDS;
     // the ReLU-mask data gradient with nothing else in its epilogue: mask bytes prefetched (EPI_MASK)
     const bool mask_pre = ex.mask_in && !ex.mask_out && !bnh && !aux && !resid && !lens && !ex.acc && !ex.y2 &&
-                          !ex.post_act && ex.scale == 1.f && !ex.ln_out && !out_f32 && act >= 0 && ldy == N;
+                          !ex.post_act && ex.scale == 1.f && !out_f32 && act >= 0 && ldy == N;
 #define B64_LAUNCH(F32, FK)                                                                              \
     do {                                                                                                 \
       auto kfn = g.rinfo ? conv_gemm_big64_kernel<F32, FK, true, BF> : conv_gemm_big64_kernel<F32, FK, false, BF>; \
@@ -2778,11 +2649,6 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
                                   : conv_gemm_big64_kernel<false, true, false, true, EPI_MASK, true>)    \
                        : (g.rinfo ? conv_gemm_big64_kernel<false, true, true, true, EPI_MASK>             \
                                   : conv_gemm_big64_kernel<false, true, false, true, EPI_MASK>);         \
-          if (g_gemm_tpb == 2 && !stg_ && !bnh && !(g_gemm_mask_pre && mask_pre) && nwgb > device_cus()) { \
-            kfn = g.rinfo ? conv_gemm_big64_kernel<false, true, true, true, EPI_GEN, false, 2>           \
-                          : conv_gemm_big64_kernel<false, true, false, true, EPI_GEN, false, 2>;         \
-            grid_x = ((nwgb + 1) / 2 + 7) / 8 * 8;                                                       \
-          }                                                                                              \
         }                                                                                                \
       }                                                                                                  \
       hipLaunchKernelGGL(kfn, dim3(grid_x), dim3(NT3), LB, s, X, W, bias, aux, resid, lens, Y, g, act, ldy, ex); \
@@ -2886,12 +2752,12 @@ SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, i
   if (!bn_h || !bn_stats || !bn_part) return -2;
   EpiX ex{};
   ex.scale = 1.f;
-  ex.acc = bn_h;          // EpiX aliases of the BNH variant (see EpiX)
-  ex.ln_w = bn_stats;
-  ex.mean = bn_part;
+  ex.acc = bn_h;
+  ex.bn_stats = bn_stats;
+  ex.bn_part = bn_part;
   ex.post_act = bn_act;
-  ex.pre_p = p;
-  ex.seed = seed;
+  ex.bn_p = p;
+  ex.bn_seed = seed;
   return conv_gemm_impl(X, W, nullptr, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, nullptr, ex, s,
                         true);
 }
@@ -2906,30 +2772,6 @@ SSAMD_API int ssamd_conv_gemm_mask(const bf16_t* X, const bf16_t* W, const float
   ex.mask_out = mask_out;
   ex.mask_in = mask_in;
   return conv_gemm_impl(X, W, bias, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, rinfo, ex, s);
-}
-
-// conv_gemm (N = 256, bf16 out a) + the fused residual/LayerNorm/dropout/FiLM/mask tail (EpiX.ln_*).
-// rinfo: packed A-operand sequence table (k > 1 convs); dst: packed rows' b*Mseq + t (needed for FiLM
-// on packed rows); ln_lens: unpacked rows' valid lengths (rows t >= lens[b] -> 0).
-SSAMD_API int ssamd_conv_gemm_ln(const bf16_t* X, const bf16_t* W, const float* bias, void* Y, int B, int L, int Cin,
-                                 int ks, int dil, int pad, int N, const int* rinfo, const bf16_t* res,
-                                 const float* ln_w, const float* ln_b, const float* film_g, const float* film_b,
-                                 const float* s_g, const float* s_b, const int64_t* ln_lens, const int64_t* dst,
-                                 int Mseq, bf16_t* ln_out, float* mean, float* rstd, float pre_p, float post_p,
-                                 float eps, unsigned long long seed, hipStream_t s) {
-  if (!res || !ln_w || !ln_b || !ln_out || !mean || !rstd) return -2;
-  if ((film_g != nullptr) != (film_b != nullptr) || (film_g && (!s_g || !s_b))) return -2;
-  if (dst && ln_lens) return -2;  // packed rows (dst) are all valid; unpacked rows use lens
-  EpiX ex{};
-  ex.scale = 1.f;
-  ex.ln_res = res; ex.ln_w = ln_w; ex.ln_b = ln_b;
-  ex.film_g = film_g; ex.film_b = film_b; ex.s_g = s_g; ex.s_b = s_b;
-  ex.ln_lens = ln_lens;
-  ex.dst = dst;
-  ex.ln_out = ln_out; ex.mean = mean; ex.rstd = rstd;
-  ex.Lseq = L; ex.Mseq = Mseq > 0 ? Mseq : 1;
-  ex.pre_p = pre_p; ex.post_p = post_p; ex.eps = eps; ex.seed = seed;
-  return conv_gemm_impl(X, W, bias, nullptr, nullptr, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, 0, N, rinfo, ex, s);
 }
 
 static int g_wgrad_imm = -1;  // -1 auto, 0 / 1: force the big64 wgrad read schedule
@@ -2984,10 +2826,6 @@ static int g_wgrad_blocks = 0;   // > 0: fixed split-M target (blocks per launch
 // the fp32 reduction order -- of a main-stream launch does not depend on the side-stream setting.
 static int g_wgrad_cus = 0;
 static hipStream_t g_wgrad_cus_stream = nullptr;
-// >= 1: the fewest block rounds a split plan may have -- shorter blocks, so a concurrent main-stream kernel
-// (higher queue priority) gets each CU back sooner (experimental.wgrad_min_rounds)
-static int g_wgrad_min_rounds = 1;
-SSAMD_API void ssamd_wgrad_set_min_rounds(int r) { g_wgrad_min_rounds = r > 1 ? r : 1; }
 static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits, int cus) {
   const int steps_all = (M + 63) / 64;
   int smax = max_splits;
@@ -3002,7 +2840,6 @@ static int choose_wgrad_splits(int tiles, int M, int max_splits, long ws_splits,
   double best_c = 1e30;
   for (int sp = 1; sp <= smax; ++sp) {
     const long rounds = ((long)tiles * sp + cus - 1) / cus;
-    if (rounds < g_wgrad_min_rounds && sp < smax) continue;
     const long steps = (steps_all + sp - 1) / sp;
     const double c = (double)rounds * (double)steps + 0.08 * (double)sp * tiles;
     if (c < best_c - 1e-9) { best_c = c; best = sp; }

@@ -1309,26 +1309,19 @@ __global__ void __launch_bounds__(256) film_grads_finish_kernel(const float* __r
 }  // namespace
 
 // per-device partial-sum buffer of the film_grads blocks (2 floats per block; stream-ordered reuse)
-static float* g_fg_part[16];
-static int g_fg_cap[16];
+// partials buffer (caller-allocated, stream-ordered like every other workspace): 2 floats per block
+SSAMD_API long ssamd_film_grads_ws(int n) { return n > 0 ? 2L * cdiv(n / 4, FG_T) : 0; }
 SSAMD_API int ssamd_film_grads(const float* S1, const float* S2, const float* g, const float* bt, const float* sg,
                                const float* sb, int n, int out_f32, void* dg, void* dbt, float* dsg, float* dsb,
-                               const float* l2_sg, const float* l2_sb, int accum, hipStream_t s) {
+                               const float* l2_sg, const float* l2_sb, int accum, float* part, long part_floats,
+                               hipStream_t s) {
   if (n % 4) return -2;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -3;
   const int nblk = n > 0 ? cdiv(n / 4, FG_T) : 0;
-  if (nblk > g_fg_cap[dev]) {
-    // a larger buffer; the old one may still be read by queued kernels: keep it (rare, bounded growth)
-    float* p = nullptr;
-    if (hipMalloc(&p, (size_t)2 * nblk * sizeof(float)) != hipSuccess) return -4;
-    g_fg_part[dev] = p;
-    g_fg_cap[dev] = nblk;
-  }
+  if (part_floats < 2L * nblk || (nblk > 0 && !part)) return -3;
   if (nblk > 0)
     hipLaunchKernelGGL(film_grads_kernel, dim3(nblk), dim3(FG_T), 0, s, S1, S2, g, bt, sg, sb, n, out_f32, dg, dbt,
-                       g_fg_part[dev], accum);
-  hipLaunchKernelGGL(film_grads_finish_kernel, dim3(1), dim3(256), 0, s, g_fg_part[dev], nblk, dsg, dsb, l2_sg, l2_sb);
+                       part, accum);
+  hipLaunchKernelGGL(film_grads_finish_kernel, dim3(1), dim3(256), 0, s, part, nblk, dsg, dsb, l2_sg, l2_sb);
   return (int)hipGetLastError();
 }
 

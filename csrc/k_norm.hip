@@ -11,6 +11,10 @@
 // from a counter hash so the backward regenerates them (no mask tensor).
 // Grid: (ceil(L / 64), B) -> every block works on ONE batch item, which makes
 // the per-(b, c) FiLM gradient sums a block-local reduction.
+// Row stride ``lda`` (elements) of the LayerNorm input a and of its gradient dh: a may be a column slice
+// of a wider GEMM output (the duration and pitch predictors' first convs run as ONE N = 512 GEMM whose
+// halves feed two LayerNorms); every other operand is dense [rows][C].  The dropout hash indexes the
+// logical element (row * C + c) either way.
 #include "common.h"
 
 namespace {
@@ -87,7 +91,7 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
     const float* __restrict__ bias, const float* __restrict__ fg, const float* __restrict__ fb,
     const float* __restrict__ s_g, const float* __restrict__ s_b, const int64_t* __restrict__ lens,
     const int64_t* __restrict__ cu, bf16_t* __restrict__ out, float* __restrict__ mean_out, float* __restrict__ rstd_out, int L, int C,
-    float pre_p, float post_p, uint64_t seed, float eps) {
+    float pre_p, float post_p, uint64_t seed, float eps, int lda) {
   constexpr int RPW = 64 / LPR;  // rows a wave covers per iteration
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -125,7 +129,7 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
   auto t_of = [&](int r) { return min(blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub, Lb - 1); };
   auto fetch = [&](int r, int q) {
     const long row = rowb + t_of(r);
-    load_raw<EPL>(a + row * C + c0, ra[q]);
+    load_raw<EPL>(a + row * lda + c0, ra[q]);
     if constexpr (RES) load_raw<EPL>(res + row * C + c0, rr[q]);
   };
   fetch(0, 0);
@@ -197,8 +201,13 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const float* __restrict__ s_g, const int64_t* __restrict__ lens, const int64_t* __restrict__ cu,
     const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ da_out,
-    float* __restrict__ part, int film, int L, int C, float pre_p, float post_p, uint64_t seed) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [WAVES * RPW][C]
+    float* __restrict__ part, int film, int L, int C, float pre_p, float post_p, uint64_t seed, int lda) {
+  // [WAVES * RPW][CP] partials, CP = C + C / 8: a lane's EPL contiguous floats land at c + (c / 32) * 4, so the
+  // 16-B stores of the 8 lanes of a ds_write_b128 group hit 8 distinct 4-bank groups (unpadded, lanes rl and
+  // rl + 4 -- rl + 2 at EPL = 16 -- collided: a 2- / 4-way conflict on every partial store), and the
+  // column reads stay consecutive dwords
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int CP = C + C / 8;
   constexpr int RPW = 64 / LPR;
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -232,12 +241,12 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     if (t >= len) {  // masked row: zero gradient flows back
 #pragma unroll
       for (int i = 0; i < EPL; ++i) dh[i] = 0.f;
-      store_row<EPL>(dh_out + row * C + c0, dh);
+      store_row<EPL>(dh_out + row * lda + c0, dh);
       if (da_out) store_row<EPL>(da_out + row * C + c0, dh);
       continue;
     }
     float h[EPL], m1[EPL];
-    load_row<EPL>(a + row * C + c0, h);
+    load_row<EPL>(a + row * lda + c0, h);
     // RELU: a is a ReLU output and its producer's backward leaves the ReLU mask to this kernel (it
     // reads a anyway): d a = dh * (a > 0) -- no residual, no pre-dropout (host check).  Its own
     // instantiation, the mask as bits: the common kernel keeps its register count (occupancy).
@@ -283,7 +292,7 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < EPL; ++i) dh[i] = (pos >> i) & 1u ? dh[i] : 0.f;
     }
-    store_row<EPL>(dh_out + row * C + c0, dh);
+    store_row<EPL>(dh_out + row * lda + c0, dh);
     if (da_out) {
 #pragma unroll
       for (int i = 0; i < EPL; ++i) dh[i] *= m1[i];
@@ -297,12 +306,13 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     if (k >= nk) break;
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < EPL; ++i) red[(wave * RPW + sub) * C + c0 + i] = accs[k][i];
+    for (int i = 0; i < EPL; ++i) red[(wave * RPW + sub) * CP + c0 + (c0 >> 5) * 4 + i] = accs[k][i];
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256) {
       float t = 0.f;
+      const int cp = c + (c >> 5) * 4;
 #pragma unroll
-      for (int w = 0; w < WAVES * RPW; ++w) t += red[w * C + c];  // fixed order
+      for (int w = 0; w < WAVES * RPW; ++w) t += red[w * CP + cp];  // fixed order
       pb[k * C + c] = t;
     }
   }
@@ -323,16 +333,18 @@ SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w
                               const float* fb, const float* s_g, const float* s_b, const int64_t* lens,
                               const int64_t* cu, bf16_t* out,
                               float* mean, float* rstd, int B, int L, int C, float pre_p, float post_p,
-                              unsigned long long seed, float eps, hipStream_t stream) {
+                              unsigned long long seed, float eps, int lda, hipStream_t stream) {
   if (C % 256 != 0 && C != 256 && C != 512 && C != 1024) return -1;
+  if (lda == 0) lda = C;
+  if (lda < C || lda % 8) return -2;
   if (B == 0 || L == 0) return 0;
   dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
   if (res) {
     DISPATCH_EPL(C, hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR, true>), grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
-                                     s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
+                                     s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps, lda));
   } else {
     DISPATCH_EPL(C, hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR, false>), grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
-                                     s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps));
+                                     s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps, lda));
   }
   return (int)hipGetLastError();
 }
@@ -347,7 +359,10 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
                               const float* bias, const float* fg, const float* s_g, const int64_t* lens,
                               const int64_t* cu, const float* mean, const float* rstd, bf16_t* dh, bf16_t* da, float* dw, float* db,
                               float* S1, float* S2, int B, int L, int C, float pre_p, float post_p,
-                              unsigned long long seed, int relu_in, float* ws, long ws_floats, hipStream_t stream) {
+                              unsigned long long seed, int relu_in, int lda, float* ws, long ws_floats,
+                              hipStream_t stream) {
+  if (lda == 0) lda = C;
+  if (lda < C || lda % 8) return -2;
   if (B == 0 || L == 0) return 0;
   if (relu_in && (res || da || pre_p > 0.f)) return -2;
   const int film = S1 != nullptr && S2 != nullptr;
@@ -356,15 +371,15 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
   const int nk = film ? 4 : 2;
   if (ws_floats < ssamd_addln_bwd_ws(B, L, C, film)) return -3;
   dim3 grid(gx, B);
-  size_t lds = (size_t)WAVES * 2 * C * sizeof(float);  // [WAVES * rows per wave][C]
+  size_t lds = (size_t)WAVES * 2 * (C + C / 8) * sizeof(float);  // [WAVES * rows per wave][C padded]
   if (relu_in) {
     DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR, true>), grid, dim3(256), lds, stream, dout, a, res,
                                        w, bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
-                                       (uint64_t)seed));
+                                       (uint64_t)seed, lda));
   } else {
     DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR>), grid, dim3(256), lds, stream, dout, a, res, w,
                                        bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
-                                       (uint64_t)seed));
+                                       (uint64_t)seed, lda));
   }
   int rc = (int)hipGetLastError();
   if (rc) return rc;

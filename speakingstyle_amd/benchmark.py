@@ -27,6 +27,8 @@ from __future__ import annotations
 import json
 import math
 import os
+
+import numpy as np
 import socket
 import subprocess
 import sys
@@ -231,11 +233,11 @@ def synth_phase(args, rank, world, device):
     hop = pp["preprocessing"]["stft"]["hop_length"]
     sr = pp["preprocessing"]["audio"]["sampling_rate"]
     mx = float(pp["preprocessing"]["audio"]["max_wav_value"])
-    # texts + a reference mel per utterance (the style input of synthesize.py single/batch mode)
+    # texts + a reference mel per utterance (the style input of synthesize.py single/batch mode): one distinct
+    # synthetic batch per timed step (and per warm-up step), all generated on the device before timing
     gen = SyntheticBatches(args.synth_batch, device=device, seed=7 + rank, max_seq_len=mc["max_seq_len"])
-    b = gen.make_batch()
-    speakers, texts, src_lens, max_src = b[2], b[3], b[4], b[5]
-    ref_mels, ref_lens, ref_max = b[6], b[7], b[8]
+    nb = args.synth_warmup + args.synth_steps
+    batches = [gen.make_batch() for _ in range(max(1, nb))]
 
     # Two-stage pipeline: the vocoder of batch i runs on its own stream while FastSpeech2 of batch i+1
     # runs on the main stream -- FastSpeech2's host syncs (predicted lengths) wait for the main stream
@@ -244,33 +246,37 @@ def synth_phase(args, rank, world, device):
     voc_stream = torch.cuda.Stream(device=device) if (cuda and not getattr(args, "synth_serial", False)) else None
 
     @torch.no_grad()
-    def synth():
+    def synth(b, stream=voc_stream, host_wav=False):
+        speakers, texts, src_lens, max_src = b[2], b[3], b[4], b[5]
+        ref_mels, ref_lens, ref_max = b[6], b[7], b[8]
         out = model(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
         mel, mel_len = out[1], out[9]
         lens = mel_len.cpu()  # host lengths: the vocoder runs length-bucketed (exact on valid samples)
         if cuda:  # int16 conversion fused into the vocoder's conv_post kernel
             mel_b = mel.to(torch.bfloat16).contiguous()
-            if voc_stream is not None:
-                voc_stream.wait_stream(torch.cuda.current_stream())
-                mel_b.record_stream(voc_stream)  # the main stream's allocator must not recycle it early
-                with torch.cuda.stream(voc_stream):
+            if stream is not None:
+                stream.wait_stream(torch.cuda.current_stream())
+                mel_b.record_stream(stream)  # the main stream's allocator must not recycle it early
+                with torch.cuda.stream(stream):
                     pcm = voc.infer(mel_b, int16_scale=mx, lengths=lens.tolist(), max_buckets=args.vocoder_buckets)
             else:
                 pcm = voc.infer(mel_b, int16_scale=mx, lengths=lens.tolist(), max_buckets=args.vocoder_buckets)
         else:
             wav = voc(mel.transpose(1, 2)).squeeze(1)
             pcm = (wav.float() * mx).clamp(-32768, 32767).to(torch.int16)
+        if host_wav:  # the int16 waveform on the host: the end of the text -> wav path (synthesize.py)
+            pcm = pcm.cpu()
         return pcm, lens
 
-    for _ in range(args.synth_warmup):
-        synth()
+    for i in range(args.synth_warmup):
+        synth(batches[i % len(batches)])
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)
     t0 = time.perf_counter()
     samples = 0
-    for _ in range(args.synth_steps):
-        pcm, mel_len = synth()
+    for i in range(args.synth_steps):
+        pcm, mel_len = synth(batches[(args.synth_warmup + i) % len(batches)])
         samples += int(mel_len.sum()) * hop  # valid audio (the D2H of lengths is inside synth())
     _sync(cuda)
     ddp.barrier()
@@ -278,7 +284,32 @@ def synth_phase(args, rank, world, device):
     wall = time.perf_counter() - t0
     wall, audio_s = _max_sum(world, device, wall, samples / sr)
     info = {"wall": wall, "audio_s": audio_s, "rtf": wall / max(audio_s, 1e-12),
-            "frames_per_utt": samples / hop / max(1, args.synth_steps * args.synth_batch)}
+            "frames_per_utt": samples / hop / max(1, args.synth_steps * args.synth_batch),
+            "distinct_batches": min(args.synth_steps, len(batches))}
+    del batches
+
+    # Batch-1 latency, like-for-like with the reference's only synthesis number (one utterance of 113 mel
+    # frames, text -> wav, notebooks/control.ipynb:778): ~14 phonemes at ~8 predicted frames each, one
+    # stream, each run from an idle GPU to the int16 waveform on the host; median over the runs.
+    runs = int(getattr(args, "synth_b1_runs", 0) or 0)
+    if runs > 0:
+        g1 = SyntheticBatches(1, device=device, seed=17 + rank, max_seq_len=mc["max_seq_len"],
+                              phone_counts=np.array([int(getattr(args, "synth_b1_phones", 14))]))
+        b1 = g1.make_batch()
+        for _ in range(max(3, args.synth_warmup)):
+            synth(b1, stream=None, host_wav=True)
+        times, frames = [], 0
+        for _ in range(runs):
+            _sync(cuda)
+            t1 = time.perf_counter()
+            pcm, mel_len = synth(b1, stream=None, host_wav=True)
+            times.append(time.perf_counter() - t1)
+            frames = int(mel_len.sum())
+        med = float(np.median(times))
+        audio1 = frames * hop / sr
+        info["b1"] = {"median_s": med, "min_s": float(min(times)), "max_s": float(max(times)), "runs": runs,
+                      "mel_frames": frames, "audio_s": audio1, "rtf": med / max(audio1, 1e-12),
+                      "samples": int(pcm.numel())}
     del model, voc
     if cuda:
         torch.cuda.empty_cache()

@@ -5,14 +5,17 @@ train.yaml -- takes the measured production path of every switch below and nothi
 one is an explicit, validated act: unknown names and values that do not parse raise, instead of
 silently selecting a default (or an untested path).
 
-    SSAMD_EXPERIMENTAL="wgrad_first=1,ln_fuse=1" python bench.py ...
+    SSAMD_EXPERIMENTAL="wgrad_first=1,gemm_stg=0" python bench.py ...
 
 ``mi355x.experimental: {wgrad_first: "0"}`` in train.yaml does the same for ``train.py`` (the trainer
 calls ``configure`` with it; the environment wins on conflicts).
 
-Kernel-internal variant setters of the HIP library (``ssamd_*_set_*`` in ``ops/hip.py:_SIGS``) are
-not switches of the framework: only the GPU tests (to cover every variant against fp32) and the
-``tools/exp_*.py`` experiments call them; no product code path does.
+Two switches select kernel-library variants (``KERNEL_SWITCHES``: ``gemm_stg``, ``gemm_mask_pre``).
+``apply_kernel_switches()`` pushes their current values into the library; it runs when the library
+is first loaded (``ops/hip.py:lib``), after ``configure()`` and on entry to / exit from ``overrides``,
+so every path -- training, synthesis, kernel tests -- sees the same values.  The library's other
+``ssamd_*_set_*`` setters (``ops/hip.py:_SIGS``) are not framework switches: only the GPU tests (to
+cover every variant against fp32) and the ``tools/exp_*.py`` experiments call them.
 
 Infrastructure variables that are not experiments stay plain environment variables and are
 documented where they are read: ``SSAMD_BACKEND`` (hip / reference op backend), ``SSAMD_KERNEL_LIB``
@@ -67,12 +70,7 @@ KNOBS: Dict[str, tuple] = {
     "wgrad_cu_frac": (0.75, _frac, "fraction of the CUs the side-stream weight-gradient split plan is sized for"),
     "wgrad_cus_all": (True, _bool, "apply the reduced weight-gradient CU plan to every stream (0: side stream "
                                    "only -- main-stream weight gradients then reduce in a different order)"),
-    "wgrad_min_rounds": (1, int, "fewest block rounds of a 256x256 weight-gradient split plan (shorter side-stream "
-                                 "blocks hand CUs back to the main stream sooner; measured slower, profiles/r4_exp_wgrad_min_rounds.txt)"),
-    "ln_fuse": (False, _bool, "residual + LayerNorm tail in the producing GEMM's epilogue (measured slower)"),
     "gemm_stg": (True, _bool, "staggered 8-phase main loop of the 256x256 GEMM for K >= 512 (+0.7 % LJSpeech)"),
-    "gemm_tpb": (1, int, "tiles per workgroup (1 or 2) of the short-K generic 256x256 GEMM when its tiles outnumber "
-                         "the CUs (2 measured -0.8 %, profiles/r4_exp_gemm_tpb.txt)"),
     "gemm_mask_pre": (True, _bool, "ReLU-mask data gradient with its mask bytes prefetched before the main loop"),
     "bn_fuse": (True, _bool, "PostNet BatchNorm backward started in the data-gradient GEMM's epilogue"),
     "defer_release": (False, _bool, "hand the side-stream weight-gradient inputs back to the trainer, freed "
@@ -85,8 +83,13 @@ KNOBS: Dict[str, tuple] = {
     "fail_rank": (None, int, "fault injection: this rank raises in its second timed bench step"),
 }
 
+# switch -> kernel-library setter it drives (applied by apply_kernel_switches)
+KERNEL_SWITCHES = {"gemm_stg": "ssamd_gemm_set_stg", "gemm_mask_pre": "ssamd_gemm_set_mask_pre"}
+
 _values: Dict[str, Any] = {}
 _parsed = [False]
+_lib_ref = [None]  # the loaded kernel library (set by ops/hip.py when it loads it)
+_from_config = set()  # names the last configure() set (replaced by the next one)
 
 
 def _parse_env() -> Dict[str, Any]:
@@ -122,12 +125,32 @@ def _ensure():
 
 
 def configure(block: Optional[dict]):
-    """Apply a train.yaml ``mi355x.experimental`` block (the environment keeps precedence)."""
+    """Apply a train.yaml ``mi355x.experimental`` block (the environment keeps precedence).  Replaces
+    the values of an earlier ``configure`` call (a second Trainer in one process starts from the
+    environment + its own block, not from the first one's)."""
     _ensure()
+    for k in _from_config:
+        _values.pop(k, None)
+    _from_config.clear()
     env = _parse_env()
     for k, v in (block or {}).items():
         if k not in env:
             _set(k, v, "mi355x.experimental")
+            _from_config.add(k)
+    apply_kernel_switches()
+
+
+def apply_kernel_switches(lib=None):
+    """Push the current values of ``KERNEL_SWITCHES`` into the kernel library (no-op until it is loaded)."""
+    if lib is not None:
+        _lib_ref[0] = lib
+    lib = _lib_ref[0]
+    if lib is None:
+        return
+    for name, setter in KERNEL_SWITCHES.items():
+        fn = getattr(lib, setter, None)
+        if fn is not None:
+            fn(int(get(name)))
 
 
 def get(name: str):
@@ -144,7 +167,7 @@ def overridden() -> Dict[str, Any]:
 
 
 class overrides:
-    """Context manager for tests / experiments in one process: ``with overrides(ln_fuse=True): ...``."""
+    """Context manager for tests / experiments in one process: ``with overrides(gemm_stg=False): ...``."""
 
     def __init__(self, **kw):
         self.kw = kw
@@ -154,13 +177,17 @@ class overrides:
         self.saved = dict(_values)
         for k, v in self.kw.items():
             _set(k, v, "overrides")
+        apply_kernel_switches()
         return self
 
     def __exit__(self, *a):
         _values.clear()
         _values.update(self.saved)
+        apply_kernel_switches()
 
 
 def reset_for_tests():
     _values.clear()
+    _from_config.clear()
     _parsed[0] = False
+    apply_kernel_switches()

@@ -143,9 +143,21 @@ class VariancePredictor(nn.Module):
 
     def forward(self, x, lengths, style=None):
         cl = self.conv_layer
-        c1, c2 = cl.conv1d_1, cl.conv1d_2
+        c1 = cl.conv1d_1
         h = ops.conv_relu_layernorm(x, c1.conv.weight, c1.conv.bias, c1.pad, c1.dil, cl.layer_norm_1.weight,
                                     cl.layer_norm_1.bias, post_drop=self.dropout, training=self.training)
+        return self.rest(h, lengths, style)
+
+    def first_block(self):
+        """(conv weight, conv bias, (LN weight, LN bias)) of the first conv block (fused with another
+        predictor's on a shared input: ``ops.dual_conv_relu_layernorm``)."""
+        cl = self.conv_layer
+        return cl.conv1d_1.conv.weight, cl.conv1d_1.conv.bias, (cl.layer_norm_1.weight, cl.layer_norm_1.bias)
+
+    def rest(self, h, lengths, style=None):
+        """Everything after the first block: conv 2 -> ReLU -> LN -> dropout -> [FiLM] -> Linear -> mask."""
+        cl = self.conv_layer
+        c2 = cl.conv1d_2
         fp = self.film.pack(style) if (style is not None and hasattr(self, "film")) else None
         h = ops.conv_relu_layernorm(h, c2.conv.weight, c2.conv.bias, c2.pad, c2.dil, cl.layer_norm_2.weight,
                                     cl.layer_norm_2.bias, post_drop=self.dropout, training=self.training,
@@ -188,8 +200,17 @@ class VarianceAdaptor(nn.Module):
         self.pitch_embedding = nn.Embedding(n_bins, d)
         self.energy_embedding = nn.Embedding(n_bins, d)
 
-    def _variance(self, predictor, bins, table, x, target, lengths, control):
-        pred = predictor(x, lengths)
+    def arena_groups(self):
+        """Duration + pitch first convs adjacent in the flat arena (both read the encoder output x when
+        pitch is phoneme-level): the fused [512, 256, k] weight of ONE GEMM is a view."""
+        if self.pitch_feature_level != "phoneme_level":
+            return []
+        d = self.duration_predictor.conv_layer.conv1d_1.conv
+        p = self.pitch_predictor.conv_layer.conv1d_1.conv
+        return [[d.weight, p.weight], [d.bias, p.bias]]
+
+    def _variance(self, predictor, bins, table, x, target, lengths, control, h1=None):
+        pred = predictor(x, lengths) if h1 is None else predictor.rest(h1, lengths)
         if target is not None:
             values = target
         else:
@@ -204,10 +225,20 @@ class VarianceAdaptor(nn.Module):
 
     def forward(self, x, src_lens, mel_lens=None, max_len=None, pitch_target=None, energy_target=None,
                 duration_target=None, p_control=1.0, e_control=1.0, d_control=1.0, style=None, regulate=True):
-        log_d = self.duration_predictor(x, src_lens, style)
         p_pred = e_pred = None
         if self.pitch_feature_level == "phoneme_level":
-            p_pred, x = self._variance(self.pitch_predictor, self.pitch_bins, self.pitch_embedding, x, pitch_target, src_lens, p_control)
+            # duration and pitch predictors read the same x: their first conv blocks run as one GEMM
+            dp, pp_ = self.duration_predictor, self.pitch_predictor
+            wd, bd, lnd = dp.first_block()
+            wp, bp, lnp = pp_.first_block()
+            c1 = dp.conv_layer.conv1d_1
+            h_d, h_p = ops.dual_conv_relu_layernorm(x, (wd, wp), (bd, bp), c1.pad, c1.dil, (lnd, lnp),
+                                                    post_drop=dp.dropout, training=self.training)
+            log_d = dp.rest(h_d, src_lens, style)
+            p_pred, x = self._variance(pp_, self.pitch_bins, self.pitch_embedding, x, pitch_target, src_lens, p_control,
+                                       h1=h_p)
+        else:
+            log_d = self.duration_predictor(x, src_lens, style)
         if self.energy_feature_level == "phoneme_level":
             e_pred, x = self._variance(self.energy_predictor, self.energy_bins, self.energy_embedding, x, energy_target, src_lens, e_control)
 
@@ -381,10 +412,11 @@ class FastSpeech2(nn.Module):
         style = self.compute_style(mels, mel_lens, max_mel_len, texts.shape[0], dev, style_weights)
         x = self.encoder(texts, src_lens, style, cd)
         if self.speaker_emb is not None:
-            spk = self.speaker_emb(speakers)
-            if self.spker_embed_proj is not None:
-                spk = spk + self.spker_embed_proj(self.spker_table[speakers])
-            x = ops.add_rowvec(x, spk)
+            if self.spker_embed_proj is None:  # table lookup fused into the add (one HIP kernel each way)
+                x = ops.add_table_rows(x, self.speaker_emb.weight, speakers)
+            else:
+                spk = self.speaker_emb(speakers) + self.spker_embed_proj(self.spker_table[speakers])
+                x = ops.add_rowvec(x, spk)
         training_lr = d_targets is not None
         packed = (self.training and training_lr and mel_lens is not None and mel_lens_host is not None
                   and max_mel_len is not None and self.variance_adaptor.packable())

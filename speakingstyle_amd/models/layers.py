@@ -63,11 +63,15 @@ class ConvHolder(nn.Module):
 
 
 def fused_param_groups(module: nn.Module):
-    """All contiguous-parameter groups of the attention layers in ``module`` (``train/optim.py::FlatArena``)."""
+    """All contiguous-parameter groups in ``module`` (``train/optim.py::FlatArena``): the Q/K/V projections of
+    every attention layer and the sub-modules' own ``arena_groups()`` (the variance adaptor's duration +
+    pitch first convs, one N = 512 GEMM)."""
     groups = []
     for m in module.modules():
         if isinstance(m, MultiHeadAttention):
             groups.extend(m.fused_param_groups())
+        elif hasattr(m, "arena_groups"):
+            groups.extend(m.arena_groups())
     return groups
 
 
@@ -98,12 +102,10 @@ class MultiHeadAttention(nn.Module):
         mb = ops.residual_mailbox(x, ws)  # d(residual x) joins the QKV data gradient in its epilogue
         qkv = ops.linear_group(x, ws, (self.w_qs.bias, self.w_ks.bias, self.w_vs.bias), mailbox=mb)
         o = ops.attention(qkv, lengths, self.n_head, pack)
-        # LN(dropout(fc(o)) + x), then the FFT block's pad mask-fill (Layers.py:27-28) -- on the GPU
-        # in the fc GEMM's epilogue (d_model = 256)
+        # LN(dropout(fc(o)) + x), then the FFT block's pad mask-fill (Layers.py:27-28): one addln kernel
         kw = dict(pre_drop=self.dropout, training=self.training, lengths=lengths, pack=pack)
-        spec = ops.ln_spec(x, self.layer_norm.weight, self.layer_norm.bias, **kw)
-        a = ops.linear(o, self.fc.weight, self.fc.bias, ln=spec)
-        return ops.add_layernorm(a, x, self.layer_norm.weight, self.layer_norm.bias, mailbox=mb, fused=spec, **kw)
+        a = ops.linear(o, self.fc.weight, self.fc.bias)
+        return ops.add_layernorm(a, x, self.layer_norm.weight, self.layer_norm.bias, mailbox=mb, **kw)
 
 
 class PositionwiseFeedForward(nn.Module):
@@ -120,9 +122,8 @@ class PositionwiseFeedForward(nn.Module):
     def forward(self, x, lengths, film_params=None, pack=None):
         mb = ops.residual_mailbox(x)  # d(residual x) joins the first conv's data gradient
         kw = dict(pre_drop=self.dropout, training=self.training, film_params=film_params, lengths=lengths, pack=pack)
-        spec = ops.ln_spec(x, self.layer_norm.weight, self.layer_norm.bias, **kw)  # LN in w_2's epilogue (GPU)
-        z = ops.ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias, pack, mailbox=mb, ln=spec)
-        return ops.add_layernorm(z, x, self.layer_norm.weight, self.layer_norm.bias, mailbox=mb, fused=spec, **kw)
+        z = ops.ffn(x, self.w_1.weight, self.w_1.bias, self.w_2.weight, self.w_2.bias, pack, mailbox=mb)
+        return ops.add_layernorm(z, x, self.layer_norm.weight, self.layer_norm.bias, mailbox=mb, **kw)
 
 
 class FFTBlock(nn.Module):

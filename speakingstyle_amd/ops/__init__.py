@@ -48,19 +48,10 @@ lengths_to_mask = ref.lengths_to_mask
 sinusoid_table = ref.sinusoid_table
 
 
-def linear(x, w, b=None, act=None, ln=None):
-    """``ln``: an ``ln_spec`` whose LayerNorm tail the GEMM runs in its epilogue (HIP only)."""
+def linear(x, w, b=None, act=None):
     if use_hip(x):
-        return _hip().linear(x, w, b, act, ln=ln)
+        return _hip().linear(x, w, b, act)
     return ref.linear(x, w, b, act)
-
-
-def ln_spec(residual, ln_w, ln_b, **kw):
-    """The LayerNorm tail ``add_layernorm(a, residual, ln_w, ln_b, **kw)`` packaged for the GEMM that
-    produces ``a`` (HIP path, d_model = 256: fused into its epilogue); None where it does not apply."""
-    if use_hip(residual) and residual.dtype == torch.bfloat16:
-        return _hip().ln_spec(residual, ln_w, ln_b, **kw)
-    return None
 
 
 def residual_mailbox(x, weights=None):
@@ -104,6 +95,20 @@ def conv_relu_layernorm(x, w, b, pad, dil, ln_w, ln_b, **kw):
     return add_layernorm(conv1d(x, w, b, pad, dil, "relu"), None, ln_w, ln_b, **kw)
 
 
+def dual_conv_relu_layernorm(x, ws, bs, pad, dil, lns, post_drop=0.0, training=False):
+    """The first blocks of two variance predictors on the same input x (duration and pitch, reference
+    ``model/modules.py:121-125``): (LN_d(ReLU(conv_d(x))), LN_p(ReLU(conv_p(x)))) with post-dropout.  On the
+    GPU ONE N = 2C GEMM each way (``hip._DualConvReluLNFn``) when the two weights are adjacent in the flat
+    arena; otherwise (and on the CPU) the two blocks separately -- same values."""
+    p = float(post_drop) if training else 0.0
+    if use_hip(x):
+        out = _hip().dual_conv_relu_layernorm(x, ws, bs, pad, dil, lns, p)
+        if out is not None:
+            return out
+    return tuple(conv_relu_layernorm(x, w, b, pad, dil, lw, lb, post_drop=post_drop, training=training)
+                 for w, b, (lw, lb) in zip(ws, bs, lns))
+
+
 def repack_rows(x, src_pack: PackInfo, out_pack: PackInfo, pe=None):
     """Rows of one packed layout -> another over the same sequences (+ ``pe[t]``); rows past the
     source length are 0 (e.g. the halo-packed FiLM conv stack -> the FFT blocks' packed rows)."""
@@ -115,13 +120,12 @@ def repack_rows(x, src_pack: PackInfo, out_pack: PackInfo, pe=None):
     return pack_rows(y[:, : out_pack.M], out_pack, pe)
 
 
-def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None, mailbox=None, ln=None):
+def ffn(x, w1, b1, w2, b2, pack: Optional[PackInfo] = None, mailbox=None):
     """Position-wise FFN core: conv(k0) -> ReLU -> conv(k1) (``SubLayers.py:84-87``).
 
-    ``pack``: x is packed ``[1, R, C]``; the convs zero-pad at every sequence end.
-    ``ln``: an ``ln_spec`` run in the second conv's epilogue (HIP only)."""
+    ``pack``: x is packed ``[1, R, C]``; the convs zero-pad at every sequence end."""
     if use_hip(x):
-        return _hip().ffn(x, w1, b1, w2, b2, pack, mailbox, ln=ln)
+        return _hip().ffn(x, w1, b1, w2, b2, pack, mailbox)
     if pack is not None:
         return pack_rows(ffn(unpack_rows(x, pack), w1, b1, w2, b2), pack)
     h = ref.conv1d(x, w1, b1, (w1.shape[2] - 1) // 2, 1, "relu")
@@ -136,10 +140,9 @@ def attention(qkv, lengths, n_head, pack: Optional[PackInfo] = None):
     return ref.attention(qkv, lengths, n_head)
 
 
-def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, mailbox=None, fused=None, **kw):
-    """``fused``: the ``ln_spec`` the producing GEMM already evaluated (HIP): no kernel, same autograd."""
+def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, mailbox=None, **kw):
     if use_hip(a):
-        return _hip().add_layernorm(a, residual, ln_w, ln_b, pack=pack, mailbox=mailbox, fused=fused, **kw)
+        return _hip().add_layernorm(a, residual, ln_w, ln_b, pack=pack, mailbox=mailbox, **kw)
     if pack is not None:
         kw["lengths"] = pack.lens
         res = None if residual is None else unpack_rows(residual, pack)
@@ -185,6 +188,13 @@ def add_rowvec(x, v):
     if use_hip(x):
         return _hip().add_rowvec(x, v)
     return x + v.to(x.dtype).unsqueeze(1)
+
+
+def add_table_rows(x, table, ids):
+    """x [B, L, C] + table[ids[b]] broadcast over L (the speaker embedding: lookup fused into the add)."""
+    if use_hip(x):
+        return _hip().add_table_rows(x, table, ids)
+    return x + F.embedding(ids, table).to(x.dtype).unsqueeze(1)
 
 
 def pack_rows(x, pack: PackInfo, pe=None):

@@ -162,33 +162,30 @@ def single_contribution(p) -> bool:
     return p is not None and _single.get(id(p), False)
 
 
-race_suspects = [0]  # backward passes in which a side-stream-eligible parameter lost its single slot view
+race_suspects = [0]  # steps skipped because a side-stream-eligible parameter lost its single slot view
+
+
+def report_race(index: int):
+    """Called by ``FlatArena.ensure_slot`` when it poisoned a possibly raced slot (step skipped on device)."""
+    import warnings
+
+    race_suspects[0] += 1
+    warnings.warn(f"gradslots: parameter {index} received a second gradient contribution after being scheduled for "
+                  "the weight-gradient side stream (graph changed between steps); its gradient may have raced the "
+                  "side stream, so this optimizer step is skipped (non-finite guard)", RuntimeWarning)
 
 
 def note_contributions(arena):
     """After a backward (all streams joined): record which parameters ended with their slot view.
 
-    A parameter marked single after the previous backward may have had its weight gradient written by
-    the side stream this time.  If it now ends with a gradient that is NOT its slot view, autograd summed
-    a second contribution on the main stream -- reading a slot the side stream may still have been
-    writing: this step's gradient can be corrupt.  That is reported (RuntimeWarning, counted in
-    ``race_suspects``) instead of passing silently; the flag flip keeps later steps on the main stream."""
+    A parameter marked single here may have its next weight gradient written by the side stream.  The
+    race case -- it then ends a backward with a gradient that is NOT its slot view -- is caught before the
+    optimizer by ``FlatArena.ensure_slot`` (the step is skipped); this only updates the flags."""
     sp = arena._slot_ptr
     copied = getattr(arena, "copied_ids", ())
-    lost = []
-    for i, p in enumerate(arena.params):
+    for p in arena.params:
         g = p.grad
-        now = g is not None and g.data_ptr() == sp[id(p)] and id(p) not in copied
-        if not now and g is not None and _single.get(id(p), False):
-            lost.append(i)
-        _single[id(p)] = now
-    if lost:
-        import warnings
-
-        race_suspects[0] += 1
-        warnings.warn(f"gradslots: parameters {lost[:8]} received a second gradient contribution after being "
-                      "scheduled for the weight-gradient side stream; this step's gradient for them may have "
-                      "raced the side stream (graph changed between steps)", RuntimeWarning)
+        _single[id(p)] = g is not None and g.data_ptr() == sp[id(p)] and id(p) not in copied
 
 
 def split_rows(g: torch.Tensor, params: Sequence[torch.Tensor]) -> List[torch.Tensor]:

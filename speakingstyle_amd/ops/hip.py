@@ -51,11 +51,10 @@ _SIGS = {
     "ssamd_gemm_set_stg": [I],
     "ssamd_gemm_set_mask_pre": [I],
     "ssamd_bn_set_dz_cfg": [I, I],
-    "ssamd_wgrad_set_min_rounds": [I],
-    "ssamd_gemm_set_tpb": [I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],
-    "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P],
+    "ssamd_film_grads": [P, P, P, P, P, P, I, I, P, P, P, P, P, P, I, P, L_, P],
+    "ssamd_film_grads_ws": [I],
     "ssamd_attn_set_fwd": [I, I],
     "ssamd_attn_set_kv_dma": [I],
     "ssamd_attn_set_q_dma": [I, I],
@@ -67,8 +66,8 @@ _SIGS = {
     "ssamd_conv_post": [P, P, P, I, I, I, F, F, P, P, P],
     "ssamd_colsum": [P, P, L_, I, P, L_, P],
     "ssamd_colsum_ws": [L_, I],
-    "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, P],
-    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, I, P, L_, P],
+    "ssamd_addln_fwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, F, I, P],
+    "ssamd_addln_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, F, F, U64, I, I, P, L_, P],
     "ssamd_addln_bwd_ws": [I, I, I, I],
     "ssamd_addln_wb_reduce": [P, I, I, I, I, P, P, P, P],
     "ssamd_lr_fwd": [P, P, P, P, P, P, I, I, I, I, P],
@@ -95,7 +94,7 @@ _SIGS = {
 
 
 _RESTYPES = {"ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws": L_, "ssamd_embed_bwd_ws": L_,
-             "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_}
+             "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_, "ssamd_film_grads_ws": L_}
 
 
 _FAST_PATH = os.path.join(os.path.dirname(_LIB_PATH),
@@ -168,7 +167,11 @@ def lib():
                     if fn is not None:
                         fn.argtypes = args
                         fn.restype = _RESTYPES.get(name, I)
-                _lib = _KernelLib(handle, _load_fast(handle))
+                kl = _KernelLib(handle, _load_fast(handle))
+                from .. import experimental
+
+                experimental.apply_kernel_switches(kl)  # the validated switches reach every entry path
+                _lib = kl
     return _lib
 
 
@@ -219,10 +222,6 @@ def _check(rc, name):
 
 
 _FALLBACK_OK = os.environ.get("SSAMD_ALLOW_TORCH_FALLBACK") == "1"
-# LayerNorm tails in the producing GEMM's epilogue (ssamd_conv_gemm_ln) are opt-in: measured on MI355X
-# (tools/exp_ln.py, 100k rows, profiles/README.md r2) the fused epilogue of the one-block-per-CU 256x256
-# GEMM costs more (+62 us at K=256) than the separate, fully occupied addln kernel (+31 us): the epilogue
-# does not overlap any MFMA work.  Experiment switch ``ln_fuse`` (speakingstyle_amd/experimental.py).
 _fallback_seen = set()
 
 
@@ -563,84 +562,6 @@ def conv_gemm_mask_raw(x, wimg, bias, B, L, Cin, ks, pad, N, act, rinfo=None, ma
     return y
 
 
-class LNSpec:
-    """A residual + LayerNorm (+ dropout, FiLM, row mask) tail that the producing GEMM runs in its
-    epilogue (``ssamd_conv_gemm_ln``; d_model = 256: one 256x256 tile owns whole rows).  Built by
-    ``ln_spec`` before the GEMM, filled by it (``out``, ``mean``, ``rstd``) and consumed by
-    ``add_layernorm(..., fused=spec)``, whose backward is the unchanged ``addln_bwd``."""
-
-    __slots__ = ("res", "w", "b", "g", "bt", "sg", "sb", "lens", "cu", "geom", "dst", "M", "pre_p", "post_p",
-                 "seed", "eps", "out", "mean", "rstd", "used")
-
-    def launch_args(self):
-        return (_ptr(self.res), _ptr(self.w), _ptr(self.b), _ptr(self.g), _ptr(self.bt), _ptr(self.sg),
-                _ptr(self.sb), _ptr(None if self.dst is not None else self.lens), _ptr(self.dst), int(self.M),
-                _ptr(self.out), _ptr(self.mean), _ptr(self.rstd), float(self.pre_p), float(self.post_p),
-                float(self.eps), ctypes.c_ulonglong(self.seed))
-
-
-_SIGS.update({"ssamd_conv_gemm_ln": [P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P, P,
-                                     F, F, F, U64, P]})
-
-
-def ln_spec(residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None, lengths=None,
-            eps=1e-5, pack=None):
-    """LNSpec for ``add_layernorm(a, residual, ...)`` when its ``a`` comes from a d=256 GEMM, else None."""
-    from .. import experimental
-
-    if not experimental.get("ln_fuse") or residual.dtype != torch.bfloat16 or residual.shape[-1] != 256 or not residual.is_cuda:
-        return None
-    sp = LNSpec()
-    sp.res = residual.contiguous()
-    sp.w, sp.b = ln_w, ln_b
-    sp.g = sp.bt = sp.sg = sp.sb = None
-    if film_params is not None:
-        g, bt, sg, sb = film_params
-        sp.g, sp.bt = g.detach().float().contiguous(), bt.detach().float().contiguous()
-        sp.sg, sp.sb = sg, sb
-    sp.pre_p = float(pre_drop) if training else 0.0
-    sp.post_p = float(post_drop) if training else 0.0
-    sp.seed = _next_seed()
-    sp.eps = float(eps)
-    if pack is not None:
-        sp.lens, sp.cu, sp.geom, sp.dst, sp.M = pack.lens, pack.cu, (pack.B, pack.M, 256), pack.dst, pack.M
-    else:
-        sp.lens = None if lengths is None else lengths.to(torch.int64).contiguous()
-        sp.cu = sp.geom = sp.dst = None
-        sp.M = 1
-    sp.out = sp.mean = sp.rstd = None
-    sp.used = False
-    return sp
-
-
-def conv_gemm_ln_raw(x, wimg, bias, B, L, Cin, ks, dil, pad, spec: LNSpec, rinfo=None):
-    """a = conv(x) + bias (bf16 [B, L, 256]) with the LayerNorm tail of ``spec`` in the epilogue."""
-    _need(x, torch.bfloat16, "conv_ln.x")
-    _need(wimg, torch.bfloat16, "conv_ln.w")
-    N = 256
-    assert x.numel() == B * L * Cin and wimg.numel() == N * ks * Cin, "conv_ln: shape"
-    assert spec.res.numel() == B * L * N, "conv_ln: residual shape"
-    _need(spec.w, torch.float32, "conv_ln.ln_w")
-    _need(spec.b, torch.float32, "conv_ln.ln_b")
-    if bias is not None:
-        _need(bias, torch.float32, "conv_ln.bias")
-    if spec.g is not None:
-        nb = spec.geom[0] if spec.geom is not None else B
-        assert spec.g.shape == (nb, N) and spec.bt.shape == (nb, N)
-        assert spec.dst is not None or spec.geom is None, "packed FiLM needs the row map"
-    if spec.lens is not None and spec.dst is None:
-        assert spec.lens.numel() == B
-    y = torch.empty(B, L, N, device=x.device, dtype=torch.bfloat16)
-    spec.out = torch.empty_like(y)
-    spec.mean = torch.empty(B * L, device=x.device, dtype=torch.float32)
-    spec.rstd = torch.empty_like(spec.mean)
-    rc = lib().ssamd_conv_gemm_ln(_ptr(x), _ptr(wimg), _ptr(bias), _ptr(y), B, L, Cin, ks, dil, pad, N,
-                                  _rinfo_ptr(rinfo, B * L), *spec.launch_args(), _stream())
-    _check(rc, "ssamd_conv_gemm_ln")
-    spec.used = True
-    return y
-
-
 def conv_wgrad_raw(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, db=None, rinfo=None, cu=None):
     """-> dW [N, Cin, ks] fp32 (and db [N] when ``with_bias``: fused column sums of dY).
 
@@ -698,7 +619,7 @@ def relu_mask_(dy, y, out=None):
 # ------------------------------------------------------------------------ conv / linear
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, pad, dil, act, out_f32, ln=None, pack=None):
+    def forward(ctx, x, w, b, pad, dil, act, out_f32, pack=None):
         """``pack``: x is packed [1, R, Cin]; the conv zero-pads at every sequence end (rinfo)."""
         B, L, Cin = x.shape
         ks = 1 if w.dim() == 2 else w.shape[2]
@@ -708,12 +629,8 @@ class _ConvFn(torch.autograd.Function):
         rinfo = pack.rinfo if (pack is not None and ks > 1) else None
         if rinfo is not None:
             assert B == 1 and L == pack.R, "packed conv: x must be [1, R, C]"
-        if ln is not None:
-            assert act is None and not out_f32 and N == 256 and rinfo is None
-            y = conv_gemm_ln_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, ln)
-        else:
-            y = conv_gemm_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, N, _ACT[act], out_f32=out_f32,
-                              rinfo=rinfo)
+        y = conv_gemm_raw(xc, weight_fwd(w), bf, B, L, Cin, ks, dil, pad, N, _ACT[act], out_f32=out_f32,
+                          rinfo=rinfo)
         ctx.pack = pack if rinfo is not None else None
         ctx.geom = (B, L, Cin, ks, dil, pad, N)
         ctx.act = act
@@ -755,20 +672,15 @@ class _ConvFn(torch.autograd.Function):
             db = colsum_raw(dy, N, sb)
         if ctx.needs_input_grad[0] and first:
             dx = conv_gemm_raw(dy, weight_dgrad(w), None, B, L, N, ks, dil, (ks - 1) * dil - pad, Cin, rinfo=rinfo)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv1d(x, w, b=None, pad=0, dil=1, act=None, out_f32=False, pack=None):
-    return _ConvFn.apply(x, w, b, pad, dil, act, out_f32, None, pack)
+    return _ConvFn.apply(x, w, b, pad, dil, act, out_f32, pack)
 
 
-def linear(x, w, b=None, act=None, out_f32=False, ln=None):
-    """``ln``: an LNSpec whose LayerNorm tail runs in this GEMM's epilogue (N must be 256)."""
+def linear(x, w, b=None, act=None, out_f32=False):
     shp = x.shape
-    if ln is not None and (w.shape[0] != 256 or act is not None or out_f32 or x.dim() != 3):
-        ln = None
-    if ln is not None:
-        return _ConvFn.apply(x, w, b, 0, 1, None, False, ln)
     x3 = x.reshape(1, -1, shp[-1]) if x.dim() != 3 else x
     if x3.shape[-1] % 8 or w.shape[0] % 8:
         # not MFMA-shaped (the N = 1 variance-predictor head has its own kernel: predictor_head)
@@ -867,7 +779,7 @@ class _FFNFn(torch.autograd.Function):
     data-gradient epilogue of the second conv (aux = h), so no extra pass."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, rinfo, mailbox, ln=None):
+    def forward(ctx, x, w1, b1, w2, b2, rinfo, mailbox):
         B, L, C = x.shape
         ctx.mailbox = mailbox
         k1, k2 = w1.shape[2], w2.shape[2]
@@ -886,10 +798,7 @@ class _FFNFn(torch.autograd.Function):
         else:
             h = conv_gemm_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, 1, (k1 - 1) // 2, H, 1,
                               rinfo=r1)
-        if ln is not None and C == 256:
-            z = conv_gemm_ln_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, ln, rinfo=r2)
-        else:
-            z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0, rinfo=r2)
+        z = conv_gemm_raw(h, weight_fwd(w2), b2.detach().float(), B, L, H, k2, 1, (k2 - 1) // 2, C, 0, rinfo=r2)
         ctx.rinfo = (r1, r2)
         ctx.save_for_backward(xc, h, w1, w2, mask)
         ctx.biases = (b1, b2)
@@ -934,13 +843,13 @@ class _FFNFn(torch.autograd.Function):
                            resid=_resid_for(ctx.mailbox, xc))
         if not first:
             dw1, db1 = _wgrad1()
-        return dx, dw1, db1, dw2, db2, None, None, None
+        return dx, dw1, db1, dw2, db2, None, None
 
 
-def ffn(x, w1, b1, w2, b2, pack=None, mailbox=None, ln=None):
+def ffn(x, w1, b1, w2, b2, pack=None, mailbox=None):
     if pack is not None:
         assert x.shape[0] == 1 and x.shape[1] == pack.R, "packed FFN expects [1, R, C]"
-    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu), mailbox, ln)
+    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu), mailbox)
 
 
 # ------------------------------------------------------------------------ add + LayerNorm
@@ -1045,8 +954,7 @@ def film_scalars_cat(ps):
 
 class _AddLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox, fused=None,
-                relu_in=False):
+    def forward(ctx, a, res, w, b, g, bt, sg, sb, lens, pre_p, post_p, seed, eps, cu, geom, mailbox, relu_in=False):
         B, L, C = a.shape if geom is None else geom  # packed: (sequences, longest, C) over [1, R, C] rows
         # relu_in: a = ReLU(conv) whose backward left the ReLU mask to this one (conv1d act "relu_ln")
         ctx.relu_in = bool(relu_in)
@@ -1054,17 +962,13 @@ class _AddLNFn(torch.autograd.Function):
         rc_ = None if res is None else res.contiguous()
         gf = None if g is None else _f32_view(g)
         bf = None if bt is None else _f32_view(bt)
-        if fused is not None:  # the producing GEMM already ran this LayerNorm in its epilogue
-            out, mean, rstd = fused.out, fused.mean, fused.rstd
-            gf, bf = fused.g, fused.bt
-        else:
-            out = torch.empty_like(ac)
-            mean = torch.empty(a.numel() // C, device=a.device, dtype=torch.float32)
-            rstd = torch.empty_like(mean)
-            rc = lib().ssamd_addln_fwd(_ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb),
-                                       _ptr(lens), _ptr(cu), _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, pre_p,
-                                       post_p, seed, eps, _stream())
-            _check(rc, "ssamd_addln_fwd")
+        out = torch.empty_like(ac)
+        mean = torch.empty(a.numel() // C, device=a.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        rc = lib().ssamd_addln_fwd(_ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb),
+                                   _ptr(lens), _ptr(cu), _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, pre_p,
+                                   post_p, seed, eps, 0, _stream())
+        _check(rc, "ssamd_addln_fwd")
         ctx.cu = cu
         ctx.mailbox = mailbox
         ctx.film_scales = (sg, sb)  # the Parameters themselves: gradient-slot owners
@@ -1108,7 +1012,7 @@ class _AddLNFn(torch.autograd.Function):
         rc = lib().ssamd_addln_bwd(_ptr(dout), _ptr(ac), _ptr(rc_), _ptr(w), _ptr(b), _ptr(gf), _ptr(sg), _ptr(lens),
                                    _ptr(ctx.cu), _ptr(mean), _ptr(rstd), _ptr(dh), _ptr(da),
                                    None if side else _ptr(dw), _ptr(db), _ptr(S1), _ptr(S2),
-                                   B, L, C, pre_p, post_p, seed, int(ctx.relu_in), _ptr(ws), ws.numel(), _stream())
+                                   B, L, C, pre_p, post_p, seed, int(ctx.relu_in), 0, _ptr(ws), ws.numel(), _stream())
         _check(rc, "ssamd_addln_bwd")
         if side:
             scratch = ws[nws - 16 * 2 * C:]  # the tail of the buffer is the column-sum scratch
@@ -1148,34 +1052,27 @@ class _AddLNFn(torch.autograd.Function):
                 dsg = torch.empty(1, device=S1.device, dtype=torch.float32)
             if dsb is None:
                 dsb = torch.empty(1, device=S1.device, dtype=torch.float32)
+            # per-block partials: a stream-ordered allocation of this launch (no library-global buffer two
+            # streams or threads could share)
+            part = torch.empty(max(1, int(lib().ssamd_film_grads_ws(S1.numel()))), device=S1.device,
+                               dtype=torch.float32)
             rc = lib().ssamd_film_grads(_ptr(S1), _ptr(S2), _ptr(gf), _ptr(bf), _ptr(sg), _ptr(sb), S1.numel(),
                                         int(f32), _ptr(dg), _ptr(dbt), _ptr(dsg), _ptr(dsb),
-                                        _ptr(l2g), _ptr(l2b), int(acc is not None and not first), _stream())
+                                        _ptr(l2g), _ptr(l2b), int(acc is not None and not first), _ptr(part),
+                                        part.numel(), _stream())
             _check(rc, "ssamd_film_grads")
             if acc is not None:
                 dg, dbt = (dg.view(ctx.gshape), dbt.view(ctx.gshape)) if first else (None, None)
             else:
                 dg, dbt = dg.to(ctx.gdtype[0]), dbt.to(ctx.gdtype[1])
-        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None, None, None
+        return d_a, d_res, dw, db, dg, dbt, dsg, dsb, None, None, None, None, None, None, None, None, None
 
 
 def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, training=False, film_params=None,
-                  lengths=None, eps=1e-5, pack=None, mailbox=None, fused=None, relu_input=False):
+                  lengths=None, eps=1e-5, pack=None, mailbox=None, relu_input=False):
     """``relu_input``: ``a`` came from ``conv1d(..., act="relu_ln")``, whose backward skips the ReLU mask: this
     LayerNorm's backward applies it (it reads ``a`` anyway).  Needs no residual and no pre-dropout."""
     C = a.shape[-1]
-    if fused is not None and fused.used:
-        assert not relu_input, "relu_input: the separate LayerNorm kernel only"
-        g = bt = sg = sb = None
-        if film_params is not None:
-            g, bt, sg, sb = film_params
-        cu = geom = None
-        if pack is not None:
-            lens, cu, geom = pack.lens, pack.cu, (pack.B, pack.M, C)
-        else:
-            lens = fused.lens
-        return _AddLNFn.apply(a, residual.to(a.dtype), ln_w, ln_b, g, bt, sg, sb, lens, fused.pre_p, fused.post_p,
-                              fused.seed, fused.eps, cu, geom, mailbox, fused)
     if C not in (256, 512, 1024) or a.dtype != torch.bfloat16:
         if pack is not None:
             raise ValueError("packed add_layernorm needs C in (256, 512, 1024) and bf16")
@@ -1200,8 +1097,115 @@ def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, train
     if relu_input and (residual is not None or pre_drop > 0):
         raise ValueError("add_layernorm(relu_input=True) needs no residual and no pre-dropout")
     out = _AddLNFn.apply(a, residual, ln_w, ln_b, g, bt, sg, sb, lens, float(pre_drop), float(post_drop),
-                         _next_seed(), float(eps), cu, geom, mailbox, None, bool(relu_input))
+                         _next_seed(), float(eps), cu, geom, mailbox, bool(relu_input))
     return out
+
+
+def _ln_bwd_strided(dout, a, a_off, lda, w, b, mean, rstd, dh, dh_off, B, L, C, post_p, seed, relu_in):
+    """One LayerNorm backward over a column slice (row stride ``lda``) of ``a`` / ``dh``: the dense dout,
+    no residual / pre-dropout / FiLM / mask.  -> (dw, db), written into the parameters' arena slots when
+    claimable (reduced on the side stream when both are single-contribution, as in _AddLNFn)."""
+    dw, db = gradslots.claim(w), gradslots.claim(b)
+    in_slots = dw is not None and db is not None
+    if dw is None:
+        dw = torch.empty(C, device=dout.device, dtype=torch.float32)
+    if db is None:
+        db = torch.empty(C, device=dout.device, dtype=torch.float32)
+    nws = int(lib().ssamd_addln_bwd_ws(B, L, C, 0))
+    side = (_SIDE_WGRAD[0] and _SIDE_LN[0] and in_slots and gradslots.single_contribution(w)
+            and gradslots.single_contribution(b))
+    ws = torch.empty(nws, device=dout.device, dtype=torch.float32) if side else _workspace(dout.device, nws)
+    rc = lib().ssamd_addln_bwd(_ptr(dout), _ptr(a) + 2 * a_off, None, _ptr(w), _ptr(b), None, None, None, None,
+                               _ptr(mean), _ptr(rstd), _ptr(dh) + 2 * dh_off, None, None if side else _ptr(dw),
+                               _ptr(db), None, None, B, L, C, 0.0, post_p, seed, int(relu_in), lda, _ptr(ws),
+                               ws.numel(), _stream())
+    _check(rc, "ssamd_addln_bwd")
+    if side:
+        scratch = ws[nws - 16 * 2 * C:]
+        p_dw, p_db = dw.data_ptr(), db.data_ptr()
+
+        def _reduce():
+            _check(lib().ssamd_addln_wb_reduce(_ptr(ws), B, L, C, 0, p_dw, p_db, _ptr(scratch), _stream()),
+                   "ssamd_addln_wb_reduce")
+        wgrad_async(_reduce, (ws,), True, (w, b))
+    return dw, db
+
+
+class _DualConvReluLNFn(torch.autograd.Function):
+    """Two variance predictors' first blocks on the SAME input (duration and pitch, reference
+    ``model/modules.py:121-125``): [conv k -> ReLU -> LayerNorm -> dropout] x 2 as ONE
+    N = 2C implicit-GEMM conv (the two weights are adjacent in the flat arena, so the fused [2C, Cin, k]
+    weight and its gradient are views), two LayerNorms over the column halves of its output (row stride
+    2C), and in the backward the two LayerNorm backwards write the halves of one [M, 2C] gradient, which
+    feeds ONE data-gradient GEMM (K = k * 2C: the two predictors' contributions to dx summed inside it)
+    and ONE weight-gradient GEMM (N = 2C, fused bias gradient) into the fused slots.  The ReLU mask of the
+    conv is applied by the LayerNorm backwards (they read its output anyway)."""
+
+    @staticmethod
+    def forward(ctx, x, wf, bf, pad, dil, post_p, w_d, w_p, b_d, b_p, lw_d, lb_d, lw_p, lb_p):
+        B, L, Cin = x.shape
+        N2, _, ks = wf.shape
+        C = N2 // 2
+        xc = x.contiguous()
+        h = conv_gemm_raw(xc, weight_fwd(wf, owner=w_d), bf, B, L, Cin, ks, dil, pad, N2, _ACT["relu_ln"])
+        outs, stats, seeds = [], [], []
+        for half, (lw, lb) in enumerate(((lw_d, lb_d), (lw_p, lb_p))):
+            out = torch.empty(B, L, C, device=x.device, dtype=torch.bfloat16)
+            mean = torch.empty(B * L, device=x.device, dtype=torch.float32)
+            rstd = torch.empty_like(mean)
+            seed = _next_seed()
+            rc = lib().ssamd_addln_fwd(_ptr(h) + 2 * half * C, None, _ptr(lw), _ptr(lb), None, None, None, None,
+                                       None, None, _ptr(out), _ptr(mean), _ptr(rstd), B, L, C, 0.0, post_p, seed,
+                                       1e-5, N2, _stream())
+            _check(rc, "ssamd_addln_fwd")
+            outs.append(out)
+            stats += [mean, rstd]
+            seeds.append(seed)
+        ctx.save_for_backward(xc, h, wf, *stats)
+        ctx.members = (w_d, w_p, b_d, b_p, lw_d, lb_d, lw_p, lb_p)
+        ctx.cfg = (B, L, Cin, C, ks, pad, dil, post_p, tuple(seeds))
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, g_d, g_p):
+        xc, h, wf, m_d, r_d, m_p, r_p = ctx.saved_tensors
+        w_d, w_p, b_d, b_p, lw_d, lb_d, lw_p, lb_p = ctx.members
+        B, L, Cin, C, ks, pad, dil, post_p, seeds = ctx.cfg
+        N2 = 2 * C
+        dh = torch.empty(B, L, N2, device=xc.device, dtype=torch.bfloat16)
+        lngrads = []
+        for half, (g, lw, lb, mean, rstd) in enumerate(((g_d, lw_d, lb_d, m_d, r_d), (g_p, lw_p, lb_p, m_p, r_p))):
+            if g is None:
+                g = torch.zeros(B, L, C, device=xc.device, dtype=torch.bfloat16)
+            gc = g.to(torch.bfloat16).contiguous()
+            lngrads += _ln_bwd_strided(gc, h, half * C, N2, lw, lb, mean, rstd, dh, half * C, B, L, C, post_p,
+                                       seeds[half], True)
+        first = _wgrad_first(B * L)
+        if not first:
+            dx = conv_gemm_raw(dh, weight_dgrad(wf, owner=w_d), None, B, L, N2, ks, dil, (ks - 1) * dil - pad, Cin)
+        ws_, bs_ = (w_d, w_p), (b_d, b_p)
+        sw, sb = gradslots.claim_fused(ws_), gradslots.claim_fused(bs_)
+        dw, db = wgrad_async(lambda: conv_wgrad_raw(xc, dh, B, L, Cin, ks, dil, pad, N2, with_bias=True,
+                                                    dW=sw, db=sb),
+                             (xc, dh), sw is not None and sb is not None, ws_ + bs_)
+        if first:
+            dx = conv_gemm_raw(dh, weight_dgrad(wf, owner=w_d), None, B, L, N2, ks, dil, (ks - 1) * dil - pad, Cin)
+        return (dx, None, None, None, None, None, *gradslots.split_rows(dw, ws_), *gradslots.split_rows(db, bs_),
+                *lngrads)
+
+
+def dual_conv_relu_layernorm(x, ws, bs, pad, dil, lns, post_p):
+    """(LN_d(ReLU(conv_d(x))), LN_p(ReLU(conv_p(x)))) with post-dropout ``post_p`` (0 in eval): one N = 2C
+    GEMM each way when the two conv weights / biases are adjacent in the arena (``_DualConvReluLNFn``);
+    otherwise None (the caller runs the two blocks separately)."""
+    wf, bf = gradslots.fused_data(list(ws)), gradslots.fused_data(list(bs))
+    C = ws[0].shape[0]
+    if (wf is None or bf is None or x.dtype != torch.bfloat16 or C not in (256, 512, 1024) or ws[1].shape[0] != C
+            or x.shape[-1] % 8):
+        return None
+    (lw_d, lb_d), (lw_p, lb_p) = lns
+    return _DualConvReluLNFn.apply(x, wf, bf, pad, dil, float(post_p), ws[0], ws[1], bs[0], bs[1], lw_d, lb_d,
+                                   lw_p, lb_p)
 
 
 # ------------------------------------------------------------------------ length regulator
@@ -2338,6 +2342,60 @@ def add_rowvec(x, v):
         _torch_fallback(f"add_rowvec C={x.shape[-1]}")
         return x + v.to(x.dtype).unsqueeze(1)
     return _AddRowVecFn.apply(x, v)
+
+
+_SIGS.update({"ssamd_rowvec_grad": [P, P, I, I, I, I, P, P, L_, P]})
+
+
+class _AddTableRowsFn(torch.autograd.Function):
+    """x [B, L, C] + table[ids[b]] broadcast over L: the speaker-embedding lookup fused into the add (one
+    kernel, no [B, C] gathered intermediate).  Backward: per-utterance fixed-order row sums of dout, then
+    dtable[v] = sum of the sums of utterances with ids == v, in utterance order (deterministic, no
+    atomics), written straight into the table's arena gradient slot -- every row (0 where unused)."""
+
+    @staticmethod
+    def forward(ctx, x, table, ids):
+        xc = x.to(torch.bfloat16).contiguous()
+        B, L, C = xc.shape
+        idc = ids.to(torch.int64).contiguous()
+        assert idc.numel() == B and table.dim() == 2 and table.shape[1] == C, "add_table_rows: shapes"
+        tf = table.detach()
+        if tf.dtype != torch.float32 or not tf.is_contiguous():
+            tf = tf.float().contiguous()
+        out = torch.empty_like(xc)
+        rc = lib().ssamd_add_rowvec(_ptr(xc), _ptr(tf), _ptr(idc), B, L, C, _ptr(out), _stream())
+        _check(rc, "ssamd_add_rowvec")
+        ctx.save_for_backward(idc)
+        ctx.table = table if isinstance(table, torch.nn.Parameter) else None  # gradient-slot owner
+        ctx.geom = (B, L, C, table.shape[0], table.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (idc,) = ctx.saved_tensors
+        B, L, C, V, tdtype = ctx.geom
+        dt = None
+        if ctx.needs_input_grad[1]:
+            gc = g.to(torch.bfloat16).contiguous()
+            dt = gradslots.claim(ctx.table)
+            if dt is None:
+                dt = torch.empty(V, C, device=g.device, dtype=torch.float32)
+            ws = _workspace(g.device, B * C)
+            rc = lib().ssamd_rowvec_grad(_ptr(gc), _ptr(idc), B, L, C, V, _ptr(dt), _ptr(ws), ws.numel(), _stream())
+            _check(rc, "ssamd_rowvec_grad")
+            if tdtype != torch.float32:
+                dt = dt.to(tdtype)
+        return g, dt, None
+
+
+def add_table_rows(x, table, ids):
+    """x [B, L, C] + table[ids[b]] broadcast over L (bf16 out): the speaker embedding (reference
+    ``model/fastspeech2.py:39-42,74-77``) gathered inside the add kernel; its backward writes the table
+    gradient in place."""
+    if x.shape[-1] % 8:
+        _torch_fallback(f"add_table_rows C={x.shape[-1]}")
+        return x + table[ids].to(x.dtype).unsqueeze(1)
+    return _AddTableRowsFn.apply(x, table, ids)
 
 
 # ------------------------------------------------------------------------ packed <-> padded rows

@@ -196,10 +196,14 @@ class GradBuckets:
             side = hip.side_stream_for_collective(self.arena.grad.device)
             if side is not None:
                 with torch.cuda.stream(side):
-                    self.works[bi] = dist.all_reduce(self.arena.grad[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                                     async_op=True)
+                    self.works[bi] = self.collective(self.arena.grad[s:e])
                 return
-        self.works[bi] = dist.all_reduce(self.arena.grad[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.works[bi] = self.collective(self.arena.grad[s:e])
+
+    def collective(self, t):
+        """The in-place bucket reduction (async work handle), issued on the current stream.  Tests swap
+        in a non-idempotent reduction (e.g. RCCL PREMUL_SUM x 2) to prove the stream ordering."""
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _launch_ready(self):
         """Issue every ready bucket from the next unlaunched index on, in index order."""

@@ -101,14 +101,28 @@ class FlatArena:
         gradslots.reset()
 
     def ensure_slot(self, p, i=None):
-        """Make ``p.grad`` the arena slot (copying a gradient produced outside it)."""
+        """Make ``p.grad`` the arena slot (copying a gradient produced outside it).
+
+        A parameter whose weight gradient may have been written by the side stream this step
+        (``gradslots.single_contribution``) but that arrives here with a gradient that is NOT its slot
+        view received a second contribution summed on the main stream -- possibly while the side stream
+        was still writing the slot.  Its slot is poisoned with NaN instead: the global-norm guard of the
+        fused clip + Adam kernel then skips this step on the device (on every rank under DP: the slot is
+        poisoned before its bucket is all-reduced), and the flag flip in ``note_contributions`` keeps the
+        parameter on the main stream from the next step on."""
+        from ..ops import gradslots
+
         g = p.grad
         if g is None or g.data_ptr() == self._slot_ptr[id(p)]:
             return
         if i is None:
             i = next(j for j, q in enumerate(self.params) if q is p)
         slot = self.grad_view(i)
-        slot.copy_(g)
+        if gradslots.single_contribution(p):
+            slot.fill_(float("nan"))
+            gradslots.report_race(i)
+        else:
+            slot.copy_(g)
         p.grad = slot
         self.copied += 1
         self.copied_ids.add(id(p))

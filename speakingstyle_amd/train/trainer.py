@@ -60,18 +60,10 @@ class Trainer:
         from .. import experimental
 
         mi = train_config.get("mi355x", {}) or {}
-        experimental.configure(mi.get("experimental"))
+        experimental.configure(mi.get("experimental"))  # also pushes the kernel-library switches
         # host timestamps of the step tail (backward return .. optimizer launch): diagnostics only
         self._host_tail = [] if experimental.get("host_tail") else None
         self._defer = experimental.get("defer_release")
-        if torch.cuda.is_available():
-            from ..ops import hip
-
-            if hip.available():
-                hip.lib().ssamd_gemm_set_stg(int(experimental.get("gemm_stg")))
-                hip.lib().ssamd_gemm_set_mask_pre(int(experimental.get("gemm_mask_pre")))
-                hip.lib().ssamd_wgrad_set_min_rounds(int(experimental.get("wgrad_min_rounds")))
-                hip.lib().ssamd_gemm_set_tpb(int(experimental.get("gemm_tpb")))
         self._held = None
         # backward on the calling thread instead of autograd's per-device worker thread: no thread
         # hand-off per backward and less engine bookkeeping -- host enqueue per step 15.7 -> 12.1 ms

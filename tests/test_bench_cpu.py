@@ -39,7 +39,8 @@ def _expected_frames(world, steps=2, warm=1, batch=3, pool=3):
 
 
 def test_bench_launches_two_ranks():
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--synth-batch", "2", "--synth-steps", "1"] + ARGS,
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--synth-batch", "2", "--synth-steps", "2",
+                        "--synth-b1-runs", "3"] + ARGS,
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -50,7 +51,10 @@ def test_bench_launches_two_ranks():
     assert rec["bucket_overlap"] is True
     frames = rec["value"] * rec["ms_per_step"] * rec["steps"] / 1000.0
     np.testing.assert_allclose(frames, _expected_frames(2), rtol=2e-3)
-    assert rec["synth_rtf"] > 0 and rec["synth"]["batch_per_gpu"] == 2
+    assert rec["synth_rtf"] > 0 and rec["synth"]["batch_per_gpu"] == 2 and rec["synth"]["distinct_batches"] == 2
+    b1 = rec["synth"]["b1"]  # batch-1 latency (like-for-like with the reference's 113-frame point)
+    assert rec["synth_rtf_b1"] > 0 and b1["runs"] == 3 and b1["mel_frames"] > 0
+    assert rec["synth_vs_baseline"] == round(1.33 / rec["synth_rtf_b1"], 1)
 
 
 def test_bench_single_process_default():

@@ -32,13 +32,14 @@ def _trainer(cfg, seed=11):
     return Trainer(m, cfg, seed=1234)
 
 
-def _capture(tr):
+def _capture(tr, step=True):
+    """Record the reduced gradient of every step; ``step=False`` also skips Adam (weights stay put)."""
     grads = []
     orig = tr.opt.step_and_update_lr
 
     def hook():
         grads.append(tr.opt.arena.grad.clone())
-        return orig()
+        return orig() if step else 0.0
 
     tr.opt.step_and_update_lr = hook
     return grads
@@ -117,3 +118,92 @@ def test_rccl_bucket_path_single_rank(name, prio, monkeypatch):
         dist.destroy_process_group()
         if prio:
             torch.cuda.set_stream(torch.cuda.default_stream())
+
+
+class _StreamWork:
+    """Work handle of a stream-ordered test reduction: wait() orders the caller's stream after it."""
+
+    def __init__(self):
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+def test_rccl_bucket_order_non_idempotent_with_late_side_stream():
+    """The 1-rank RCCL bucket path with a reduction that is NOT an identity (x2: RCCL PREMUL_SUM, or -- if
+    this RCCL lacks it -- an in-place x2 on the same stream the collective would use) and a ~20 ms spin
+    injected on the weight-gradient side stream ahead of a step's side-stream launches.  A bucket reduced
+    before its last side-stream weight gradient landed would be doubled from a partial slot and then
+    overwritten by the late kernel: the reduced gradients would not equal exactly 2x the plain step's."""
+    import torch.distributed as dist
+
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.ops import hip
+    from speakingstyle_amd.parallel import ddp
+
+    pp, mc, tc = load_named("LJSpeech")
+    mc["transformer"]["encoder_layer"] = mc["transformer"]["decoder_layer"] = 2
+    cfg = (pp, mc, tc)
+    batches = [SyntheticBatches(8, device="cuda", seed=30 + i).make_batch() for i in range(3)]
+    ref = _trainer(cfg)
+    ref.use_priority_stream()
+    g_ref = _capture(ref, step=False)  # no Adam: both runs see the same weights every step
+    for b in batches:
+        ref.train_step(b)
+    torch.cuda.set_stream(torch.cuda.default_stream())
+
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_port()}")
+    try:
+        tr = _trainer(cfg)
+        tr.use_priority_stream()
+        tr.buckets = ddp.GradBuckets(tr.opt.arena, bucket_mb=4.0, force=True)
+        probe = torch.ones(4, device="cuda")
+        try:
+            dist.all_reduce(probe, op=dist._make_nccl_premul_sum(2.0))
+            torch.cuda.synchronize()
+            premul = bool((probe == 2).all())
+        except Exception:  # noqa: BLE001 -- RCCL without ncclRedOpCreatePreMulSum
+            premul = False
+
+        def doubled(t):
+            if premul:
+                return dist.all_reduce(t, op=dist._make_nccl_premul_sum(2.0), async_op=True)
+            t.mul_(2.0)  # same stream the collective would be issued on
+            return _StreamWork()
+
+        tr.buckets.collective = doubled
+        g = _capture(tr, step=False)
+        delayed = [0]
+        orig_async = hip.wgrad_async
+
+        def late(launch, inputs, slots_ok, params=()):
+            side_ok = (hip._SIDE_WGRAD[0] and slots_ok
+                       and all(hip.gradslots.single_contribution(p) for p in params))
+            if side_ok and armed[0] and delayed[0] == 0:
+                with torch.cuda.stream(hip._side_stream(inputs[0].device)):
+                    torch.cuda._sleep(40_000_000)  # ~20 ms spin ahead of this step's side-stream kernels
+                delayed[0] += 1
+            return orig_async(launch, inputs, slots_ok, params)
+
+        armed = [False]
+        hip.wgrad_async = late
+        try:
+            for i, b in enumerate(batches):
+                armed[0] = i >= 1  # after the calibration step: buckets go out from the hooks
+                delayed[0] = 0
+                tr.train_step(b)
+                if i >= 1:
+                    assert delayed[0] == 1, "no side-stream weight gradient to delay"
+        finally:
+            hip.wgrad_async = orig_async
+        torch.cuda.synchronize()
+        assert tr.buckets.calibrated()
+        # step 0 (calibration) launches every bucket at finish() -- also doubled
+        for a, r in zip(g, g_ref):
+            assert torch.equal(a, 2.0 * r), (a - 2.0 * r).abs().max().item()
+    finally:
+        dist.destroy_process_group()
+        torch.cuda.set_stream(torch.cuda.default_stream())

@@ -209,3 +209,47 @@ def test_graph_change_after_calibration_dp2():
         torch.testing.assert_close(torch.from_numpy(res[0][step]), arena.grad, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(torch.from_numpy(res[1][step]), arena.grad, rtol=1e-5, atol=1e-6)
         arena.zero_grad()
+
+
+def test_race_suspect_poisons_slot_and_adam_skips():
+    """A parameter whose previous backward ended with its single slot view (so its next weight gradient may
+    be written by the side stream) but that now receives a second, main-stream-summed contribution: the
+    arena slot is poisoned before the optimizer -> the non-finite guard skips the step, the replica is
+    unchanged, the warning fires, and the flag flip puts it back on the main stream for the next step."""
+    import warnings
+
+    import pytest
+
+    from speakingstyle_amd.ops import gradslots
+    from speakingstyle_amd.train.optim import FlatArena
+
+    torch.manual_seed(1)
+    w = torch.nn.Parameter(torch.randn(8, 8))
+    arena = FlatArena([w])
+    x = torch.randn(4, 8)
+
+    def backward(twice):
+        y = SlotMatmul.apply(x, w)
+        if twice:
+            y = y + SlotMatmul.apply(x, w)  # graph changed: a second contribution (autograd sums them)
+        y.sum().backward()
+
+    backward(False)
+    arena.finalize_grads()
+    gradslots.note_contributions(arena)
+    assert gradslots.single_contribution(w)
+    arena.zero_grad()
+    before = gradslots.race_suspects[0]
+    backward(True)
+    with pytest.warns(RuntimeWarning, match="skipped"):
+        arena.finalize_grads()
+    assert gradslots.race_suspects[0] == before + 1
+    assert torch.isnan(arena.grad[: w.numel()]).all()
+    gradslots.note_contributions(arena)
+    assert not gradslots.single_contribution(w)  # next step: main stream, no race
+    arena.zero_grad()
+    backward(True)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        arena.finalize_grads()
+    assert torch.isfinite(arena.grad[: w.numel()]).all()

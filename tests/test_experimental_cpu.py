@@ -17,15 +17,15 @@ def _clean(monkeypatch):
 def test_defaults_are_production():
     assert experimental.overridden() == {}
     assert experimental.get("wgrad_first") == "auto"
-    assert experimental.get("ln_fuse") is False
+    assert experimental.get("bn_fuse") is True
     assert experimental.get("hifigan_hip_train") is True
 
 
 def test_env_parsing_and_validation(monkeypatch):
-    monkeypatch.setenv("SSAMD_EXPERIMENTAL", "wgrad_first=1, ln_fuse=true")
-    assert experimental.get("wgrad_first") == "1" and experimental.get("ln_fuse") is True
-    assert experimental.overridden() == {"wgrad_first": "1", "ln_fuse": True}
-    for bad in ("wgrad_frist=1", "wgrad_first=off", "ln_fuse=maybe", "wgrad_cu_frac=1.5", "novalue"):
+    monkeypatch.setenv("SSAMD_EXPERIMENTAL", "wgrad_first=1, bn_fuse=false")
+    assert experimental.get("wgrad_first") == "1" and experimental.get("bn_fuse") is False
+    assert experimental.overridden() == {"wgrad_first": "1", "bn_fuse": False}
+    for bad in ("wgrad_frist=1", "wgrad_first=off", "bn_fuse=maybe", "wgrad_cu_frac=1.5", "novalue"):
         experimental.reset_for_tests()
         monkeypatch.setenv("SSAMD_EXPERIMENTAL", bad)
         with pytest.raises((KeyError, ValueError)):
@@ -38,3 +38,28 @@ def test_config_block_env_precedence(monkeypatch):
     assert experimental.get("wgrad_first") == "0" and experimental.get("wgrad_cu_frac") == 0.5
     with pytest.raises(KeyError):
         experimental.configure({"not_a_switch": 1})
+
+
+def test_configure_replaces_previous_block_and_applies_kernel_switches(monkeypatch):
+    calls = []
+
+    class FakeLib:
+        def ssamd_gemm_set_stg(self, v):
+            calls.append(("stg", v))
+
+        def ssamd_gemm_set_mask_pre(self, v):
+            calls.append(("mask_pre", v))
+
+    monkeypatch.setattr(experimental, "_lib_ref", [None])
+    experimental.apply_kernel_switches(FakeLib())
+    assert ("stg", 1) in calls and ("mask_pre", 1) in calls
+    calls.clear()
+    experimental.configure({"gemm_stg": "0"})
+    assert experimental.get("gemm_stg") is False and ("stg", 0) in calls
+    calls.clear()
+    experimental.configure({})  # a second Trainer without the block: back to the default
+    assert experimental.get("gemm_stg") is True and ("stg", 1) in calls
+    calls.clear()
+    with experimental.overrides(gemm_mask_pre=False):
+        assert ("mask_pre", 0) in calls
+    assert calls[-1] == ("mask_pre", 1) or ("mask_pre", 1) in calls[-2:]

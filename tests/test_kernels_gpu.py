@@ -113,6 +113,130 @@ def test_add_layernorm(C, film, res, lens):
             assert _rel(t.grad, tr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("C,film,drop", [(256, True, 0.0), (256, False, 0.5), (512, True, 0.5), (1024, False, 0.0),
+                                         (1024, True, 0.5)])
+def test_conv_relu_layernorm_vs_unfused_and_fp32(C, film, drop):
+    """The variance-predictor block conv -> ReLU -> LayerNorm (+post-dropout, +FiLM) with the ReLU mask moved
+    from the conv backward into the LayerNorm backward (ops.conv_relu_layernorm: conv act 'relu_ln' +
+    addln relu_input) against (a) the unfused HIP path conv1d(act='relu') + add_layernorm with the same dropout
+    seed and (b) the fp32 torch reference (no dropout): dx, dW, db, dLN_w / dLN_b, FiLM gamma / beta / scalars."""
+    from speakingstyle_amd import ops
+
+    torch.manual_seed(40 + C)
+    B, L, Cin, ks = 3, 57, 256, 3
+    x = torch.randn(B, L, Cin, device=DEV).to(torch.bfloat16)
+    w0 = torch.randn(C, Cin, ks, device=DEV) / math.sqrt(Cin * ks)
+    b0 = 0.2 * torch.randn(C, device=DEV)  # a bias shift: a sizable fraction of the ReLU inputs are negative
+    lw0, lb0 = 1 + 0.1 * torch.randn(C, device=DEV), 0.1 * torch.randn(C, device=DEV)
+    f0 = (0.3 * torch.randn(B, C, device=DEV), 0.3 * torch.randn(B, C, device=DEV),
+          torch.tensor([0.7], device=DEV), torch.tensor([-0.4], device=DEV)) if film else None
+    gy = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
+
+    def leaves(dtype=torch.float32):
+        ts = [x.to(dtype), w0, b0, lw0, lb0] + (list(f0) if film else [])
+        return [t.detach().clone().requires_grad_(True) for t in ts]
+
+    def run(fused):
+        xs, w, b, lw, lb, *fp = leaves(torch.bfloat16)
+        hip.set_seed(1234)
+        kw = dict(post_drop=drop, training=True, film_params=tuple(fp) if film else None)
+        if fused:
+            y = ops.conv_relu_layernorm(xs, w, b, 1, 1, lw, lb, **kw)
+        else:
+            y = hip.add_layernorm(hip.conv1d(xs, w, b, 1, 1, "relu"), None, lw, lb, **kw)
+        y.backward(gy)
+        return y.detach().float(), [t.grad.float() for t in [xs, w, b, lw, lb] + fp]
+
+    y1, g1 = run(True)
+    y2, g2 = run(False)
+    assert torch.equal(y1, y2)
+    for a, bb in zip(g1, g2):
+        assert _rel(a, bb) < 1e-3
+    if drop == 0.0:
+        xs, w, b, lw, lb, *fp = leaves()
+        wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+        h = ref.conv1d(xs, wr, b, 1, 1, "relu")
+        yr = ref.add_layernorm(h, None, lw, lb, film_params=tuple(fp) if film else None, training=True)
+        yr.backward(gy.float())
+        assert _rel(y1, yr) < 1e-2
+        for a, t in zip(g1, [xs, wr, b, lw, lb] + fp):
+            assert _rel(a, t.grad) < 3e-2
+
+
+@pytest.mark.parametrize("T", [37, 300])
+def test_dual_predictor_first_convs_one_gemm(T):
+    """Duration + pitch predictors' first blocks as ONE N = 512 GEMM (weights adjacent in the
+    arena) == the two separate conv -> ReLU -> LayerNorm blocks (HIP) and the fp32 torch reference: both
+    outputs, dx (the two contributions summed inside one data-gradient GEMM), the fused weight / bias
+    gradients written into their slots, and the four LayerNorm parameter gradients."""
+    from speakingstyle_amd import ops
+    from speakingstyle_amd.ops import gradslots
+    from speakingstyle_amd.train.optim import FlatArena
+
+    torch.manual_seed(50 + T)
+    B, C, k = 5, 256, 3
+    convs = [torch.nn.Conv1d(C, C, k, padding=1).to(DEV) for _ in range(2)]
+    lns = [torch.nn.LayerNorm(C).to(DEV) for _ in range(2)]
+    with torch.no_grad():
+        for c in convs:
+            c.bias.add_(0.1)
+        for ln in lns:
+            ln.weight.add_(0.1 * torch.randn(C, device=DEV))
+            ln.bias.add_(0.1 * torch.randn(C, device=DEV))
+    ws, bs = [c.weight for c in convs], [c.bias for c in convs]
+    params = ws + bs + [p for ln in lns for p in (ln.weight, ln.bias)]
+    arena = FlatArena(list(reversed(params)), groups=[ws, bs])
+    assert gradslots.fused_data(ws) is not None
+    x0 = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    g = [torch.randn(B, T, C, device=DEV).to(torch.bfloat16) for _ in range(2)]
+
+    def grads():
+        out = [p.grad.detach().float().clone() for p in params]
+        arena.zero_grad()
+        return out
+
+    x = x0.clone().requires_grad_(True)
+    lnp = [(ln.weight, ln.bias) for ln in lns]
+    calls = []
+    orig = hip._DualConvReluLNFn.apply
+
+    def spy(*a):
+        calls.append(1)
+        return orig(*a)
+
+    hip._DualConvReluLNFn.apply = spy
+    try:
+        hd, hp = ops.dual_conv_relu_layernorm(x, ws, bs, 1, 1, lnp, post_drop=0.5, training=False)
+    finally:
+        hip._DualConvReluLNFn.apply = orig
+    assert calls, "the fused path did not run"
+    torch.autograd.backward([hd, hp], g)
+    arena.finalize_grads()
+    assert ws[0].grad.data_ptr() == arena.grad_view(arena.params.index(ws[0])).data_ptr()
+    gx1, gp1 = x.grad.float(), grads()
+    x = x0.clone().requires_grad_(True)
+    sd = ops.conv_relu_layernorm(x, ws[0], bs[0], 1, 1, *lnp[0])
+    sp = ops.conv_relu_layernorm(x, ws[1], bs[1], 1, 1, *lnp[1])
+    torch.autograd.backward([sd, sp], g)
+    arena.finalize_grads()
+    gx2, gp2 = x.grad.float(), grads()
+    assert torch.equal(hd, sd) and torch.equal(hp, sp)
+    assert _rel(gx1, gx2) < 5e-3
+    for a, b in zip(gp1, gp2):
+        assert _rel(a, b) < 1e-3
+    xr = x0.float().requires_grad_(True)
+    leaves = [p.detach().clone().requires_grad_(True) for p in params]
+    wr = [leaves[i].detach().to(torch.bfloat16).float().requires_grad_(True) for i in range(2)]
+    outs = [ref.add_layernorm(ref.conv1d(xr, wr[i], leaves[2 + i], 1, 1, "relu"), None, leaves[4 + 2 * i],
+                              leaves[5 + 2 * i]) for i in range(2)]
+    torch.autograd.backward(outs, [t.float() for t in g])
+    assert _rel(hd, outs[0]) < 1e-2 and _rel(hp, outs[1]) < 1e-2
+    assert _rel(gx1, xr.grad) < 3e-2
+    for a, t in zip(gp1, wr + leaves[2:]):
+        assert _rel(a, t.grad) < 3e-2
+    gradslots.reset()
+
+
 def test_add_layernorm_dropout_consistency():
     torch.manual_seed(3)
     B, L, C = 2, 300, 256
@@ -178,58 +302,6 @@ def test_embeddings():
         o.backward(gg)
         orf.backward(gg.float())
         assert _rel(tb.grad, tr.grad) < 1e-2
-
-
-@pytest.mark.parametrize("packed", [False, True])
-@pytest.mark.parametrize("film", [False, True])
-def test_gemm_fused_layernorm(packed, film):
-    """FFT block with the residual+LayerNorm(+dropout, FiLM, mask) tails in the fc / w_2 GEMM epilogues
-    == the same block with separate addln kernels (same dropout seeds), forward and backward."""
-    from speakingstyle_amd import ops
-    from speakingstyle_amd.models.layers import FFTBlock
-
-    torch.manual_seed(3)
-    blk = FFTBlock(256, 2, 128, 128, 1024, (9, 1), dropout=0.1, film=True).to(DEV).train()
-    B, L = 4, 50
-    lens = torch.tensor([50, 31, 7, 44], device=DEV)
-    x0 = torch.randn(B, L, 256, device=DEV).to(torch.bfloat16)
-    style = (torch.randn(B, 256, device=DEV).to(torch.bfloat16), torch.randn(B, 256, device=DEV).to(torch.bfloat16))
-    with torch.no_grad():
-        blk.film.s_gamma.fill_(0.3)
-        blk.film.s_beta.fill_(-0.2)
-    pk = None
-    if packed:
-        R = int(lens.sum())
-        pk = ops.PackInfo.build(lens, L, R)
-        x0 = hip_pack(x0, lens)
-
-    def run(no_fuse):
-        from speakingstyle_amd import experimental
-
-        with experimental.overrides(ln_fuse=not no_fuse):
-            hip.set_seed(77)
-            blk.zero_grad()
-            x = x0.clone().requires_grad_(True)
-            y = blk(x, lens, style if film else None, pack=pk)
-            g = torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1)).to(torch.bfloat16)
-            y.backward(g)
-            # the key-projection bias has an exactly zero true gradient (softmax is invariant to a shift
-            # shared by all keys of a query), so its computed gradient is rounding noise on both paths:
-            # comparing two noise vectors says nothing -- it is left out of the per-parameter check
-            grads = [p.grad.clone() for n, p in blk.named_parameters()
-                     if p.grad is not None and n != "slf_attn.w_ks.bias"]
-            return y.detach().float(), x.grad.float(), grads
-
-    y1, gx1, gp1 = run(False)
-    y2, gx2, gp2 = run(True)
-    assert _rel(y1, y2) < 2e-3 and _rel(gx1, gx2) < 5e-3
-    assert len(gp1) == len(gp2)
-    # the two runs may use different GEMM tilings (the fused tail forces the 256x256 kernel), so
-    # small cancellation-dominated gradients (biases) differ at bf16 noise: compare all of them at once
-    # and each one loosely
-    assert _rel(torch.cat([a.flatten() for a in gp1]), torch.cat([b.flatten() for b in gp2])) < 1e-2
-    for a, b in zip(gp1, gp2):
-        assert _rel(a, b) < 0.2
 
 
 def hip_pack(x, lens):
@@ -362,10 +434,13 @@ def test_attention_long(D, H, L, packed):
     assert _rel(dq, qr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("mode", ["eval", "train"])
 @pytest.mark.parametrize("cfg", ["LJSpeech", "LibriTTS", "BC2013", "BC2013_GST"])
-def test_model_step_hip_vs_reference(cfg):
-    """Full FastSpeech2 forward+backward, HIP bf16 vs torch fp32: LJSpeech (no style), LibriTTS
-    (multi-speaker: speaker-embedding add + its gradient), BC2013 (FiLM reference encoder), GST."""
+def test_model_step_hip_vs_reference(cfg, mode, monkeypatch):
+    """Full FastSpeech2 forward+backward, HIP bf16 vs torch fp32, every parameter gradient: LJSpeech (no
+    style), LibriTTS (multi-speaker: speaker-embedding add + its gradient), BC2013 (FiLM reference encoder),
+    GST.  ``train``: the production training path -- packed decoder, PostNet BatchNorm on batch statistics,
+    packed reference encoder (HIP) -- against the padded fp32 reference in training mode, dropout 0."""
     import copy
 
     from speakingstyle_amd import ops
@@ -375,10 +450,26 @@ def test_model_step_hip_vs_reference(cfg):
     from speakingstyle_amd.models.loss import FastSpeech2Loss
 
     pp, mc, tc = load_named(cfg)
+    train = mode == "train"
+    if train:  # dropout off everywhere: the two paths draw different masks
+        mc["transformer"]["encoder_dropout"] = mc["transformer"]["decoder_dropout"] = 0.0
+        mc["variance_predictor"]["dropout"] = 0.0
+        if mc.get("reference_encoder"):
+            mc["reference_encoder"]["dropout"] = 0.0
     torch.manual_seed(9)
-    m = FastSpeech2(pp, mc).to(DEV).eval()
+    m = FastSpeech2(pp, mc).to(DEV).train(train)
+    if train:
+        m.postnet.dropout = 0.0  # hard-coded 0.5 in the reference PostNet
     mr = copy.deepcopy(m)
     m.set_compute_dtype(torch.bfloat16)
+    packs = []
+    orig_build = ops.PackInfo.build
+
+    def counting_build(*a, **k):
+        packs.append(a[2] if len(a) > 2 else None)
+        return orig_build(*a, **k)
+
+    monkeypatch.setattr(ops.PackInfo, "build", staticmethod(counting_build))
     # flat arena with fused QKV groups: the kernels write weight gradients into their slots
     from speakingstyle_amd.train.optim import FlatArena
 
@@ -391,6 +482,8 @@ def test_model_step_hip_vs_reference(cfg):
         assert len(set(b[2].tolist())) > 1
     lossf = FastSpeech2Loss(pp, tc)
     out = m(*b[2:])
+    if train:  # the packed decoder ran (and the packed reference encoder for BC2013)
+        assert len(packs) >= (2 if mc.get("reference_encoder") else 1), packs
     lo = lossf(b, out, m.film_scalars())
     lo[0].backward()
     arena.finalize_grads()
@@ -403,6 +496,10 @@ def test_model_step_hip_vs_reference(cfg):
         lr_[0].backward()
     finally:
         ops.set_backend(None)
+    if train:  # BatchNorm batch statistics were used and tracked on both paths
+        for (n, t), (_, tr_) in zip(m.named_buffers(), mr.named_buffers()):
+            if "running_mean" in n:
+                assert _rel(t, tr_) < 2e-2, n
     assert _rel(out[1], outr[1]) < 3e-2
     for a, c in zip(lo[:6], lr_[:6]):
         assert abs(a.item() - c.item()) <= 3e-2 * abs(c.item()) + 1e-3
@@ -1120,6 +1217,33 @@ def test_resblock_whole_block_fused(C, K, T):
         assert torch.equal(via_module, out)
 
 
+def test_add_table_rows_speaker_embedding():
+    """Speaker-embedding lookup fused into the add (LibriTTS: 904 speakers) vs torch fp32: forward, dx, and
+    the table gradient written into its arena slot (repeated ids summed in utterance order, unused rows 0)."""
+    from speakingstyle_amd.ops import gradslots
+    from speakingstyle_amd.train.optim import FlatArena
+
+    torch.manual_seed(21)
+    B, L, C, V = 7, 45, 256, 904
+    emb = torch.nn.Embedding(V, C).to(DEV)
+    arena = FlatArena([emb.weight])
+    ids = torch.tensor([3, 900, 3, 17, 0, 3, 17], device=DEV)
+    x = torch.randn(B, L, C, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    y = hip.add_table_rows(x, emb.weight, ids)
+    xr = x.detach().float().requires_grad_(True)
+    tr = emb.weight.detach().clone().requires_grad_(True)
+    yr = xr + F.embedding(ids, tr).unsqueeze(1)
+    assert _rel(y, yr) < 5e-3
+    g = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    assert torch.equal(x.grad.float(), xr.grad)
+    assert emb.weight.grad.data_ptr() == arena.grad_view(0).data_ptr()  # written in place
+    assert _rel(emb.weight.grad, tr.grad) < 1e-5
+    assert not emb.weight.grad[1].any()  # unused speaker row
+    gradslots.reset()
+
+
 def test_duration_round_seq_mean_add_rowvec():
     """K12 duration rounding (+ scalar / per-phoneme control), K16 mean pool, K1 per-utterance add."""
     from speakingstyle_amd import ops as O
@@ -1424,37 +1548,3 @@ def test_hifigan_generator_hip_training_vs_torch():
         if _rel(grads[n], p.grad) > 0.2:
             bad.append((n, _rel(grads[n], p.grad)))
     assert len(grads) > 50 and not bad, bad
-
-
-
-@pytest.mark.parametrize("Cin,N,ks,packed,M,resid", [(256, 256, 1, False, 70001, False), (256, 768, 1, True, 90000, False),
-                                                     (256, 256, 1, False, 66000, True), (128, 256, 3, False, 75003, False)])
-def test_gemm_two_tiles_per_block_bitwise(Cin, N, ks, packed, M, resid):
-    """Two 256x256 tiles per workgroup (ssamd_gemm_set_tpb(2), short-K generic GEMM with more tiles than CUs)
-    computes every tile exactly as one tile per workgroup: bitwise-equal outputs, ragged M, packed rows,
-    residual epilogue operand."""
-    torch.manual_seed(37)
-    x = torch.randn(1, M, Cin, device=DEV).to(torch.bfloat16)
-    w = (torch.randn(N, ks, Cin, device=DEV) / math.sqrt(ks * Cin)).to(torch.bfloat16)
-    bias = torch.randn(N, device=DEV)
-    r = torch.randn(1, M, N, device=DEV).to(torch.bfloat16) if resid else None
-    pad = (ks - 1) // 2
-    rinfo = None
-    if packed:
-        from speakingstyle_amd.ops.packing import PackInfo
-
-        n = M // 5
-        lens = torch.tensor([n, n + 7, n - 3, n + 1, M - 4 * n - 5], device=DEV)
-        pk = PackInfo.build(lens, int(lens.max()), int(lens.sum()))
-        assert pk.R == M
-        rinfo = pk.rinfo
-    lib = hip.lib()
-    try:
-        lib.ssamd_gemm_set_tpb(1)
-        y0 = hip.conv_gemm_raw(x, w, bias, 1, M, Cin, ks, 1, pad, N, 1, resid=r, rinfo=rinfo)
-        lib.ssamd_gemm_set_tpb(2)
-        y1 = hip.conv_gemm_raw(x, w, bias, 1, M, Cin, ks, 1, pad, N, 1, resid=r, rinfo=rinfo)
-    finally:
-        lib.ssamd_gemm_set_tpb(1)
-    torch.cuda.synchronize()
-    assert torch.equal(y0, y1)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """GEMM census of one training step (GPU box): records every implicit-GEMM launch of a real
-``Trainer.train_step`` (forward / dgrad through ``conv_gemm_raw`` / ``conv_gemm_ln_raw``, weight
+``Trainer.train_step`` (forward / dgrad through ``conv_gemm_raw``, weight
 gradients through ``conv_wgrad_raw``), then replays each distinct shape on random data and times
 it under every GEMM variant, so the auto-selection in ``csrc/k_gemm.hip`` can be checked per
 shape against the step's real mix.
@@ -76,7 +76,7 @@ def record_step(args):
     b = gen.make_batch()
     tr.train_step(b)  # warm (weight images, allocator)
     calls = OrderedDict()
-    orig = (hip.conv_gemm_raw, hip.conv_gemm_ln_raw, hip.conv_wgrad_raw)
+    orig = (hip.conv_gemm_raw, hip.conv_wgrad_raw)
 
     def key_add(k):
         calls[k] = calls.get(k, 0) + 1
@@ -87,21 +87,17 @@ def record_step(args):
                  bool(out_f32), rinfo is not None))
         return orig[0](x, wimg, bias, B, L, Cin, ks, dil, pad, N, act, aux, resid, lens, out_f32, rinfo)
 
-    def gl(x, wimg, bias, B, L, Cin, ks, dil, pad, spec, rinfo=None):
-        key_add(("fwd_ln", B, L, Cin, ks, dil, pad, 256, 0, False, False, False, False, rinfo is not None))
-        return orig[1](x, wimg, bias, B, L, Cin, ks, dil, pad, spec, rinfo)
-
     def w(x, dy, B, L, Cin, ks, dil, pad, N, with_bias=False, dW=None, db=None, rinfo=None, cu=None):
         key_add(("wgrad", B, L, Cin, ks, dil, pad, N, int(bool(with_bias)), False, False, False, False,
                  rinfo is not None))
-        return orig[2](x, dy, B, L, Cin, ks, dil, pad, N, with_bias, dW, db, rinfo, cu)
+        return orig[1](x, dy, B, L, Cin, ks, dil, pad, N, with_bias, dW, db, rinfo, cu)
 
-    hip.conv_gemm_raw, hip.conv_gemm_ln_raw, hip.conv_wgrad_raw = g, gl, w
+    hip.conv_gemm_raw, hip.conv_wgrad_raw = g, w
     try:
         tr.train_step(b)
         torch.cuda.synchronize()
     finally:
-        hip.conv_gemm_raw, hip.conv_gemm_ln_raw, hip.conv_wgrad_raw = orig
+        hip.conv_gemm_raw, hip.conv_wgrad_raw = orig
     del tr, model
     torch.cuda.empty_cache()
     return calls
