@@ -202,12 +202,12 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, bf16_t* __restrict__ dh_out, bf16_t* __restrict__ da_out,
     float* __restrict__ part, int film, int L, int C, float pre_p, float post_p, uint64_t seed, int lda) {
-  // [WAVES * RPW][CP] partials, CP = C + C / 8: a lane's EPL contiguous floats land at c + (c / 32) * 4, so the
-  // 16-B stores of the 8 lanes of a ds_write_b128 group hit 8 distinct 4-bank groups (unpadded, lanes rl and
-  // rl + 4 -- rl + 2 at EPL = 16 -- collided: a 2- / 4-way conflict on every partial store), and the
-  // column reads stay consecutive dwords
+  // [WAVES * RPW][CP] partials, CP = C + C / 32: channel c at c + c / 32, so the dword stores of a 32-lane
+  // half (lane rl: channels EPL*rl + i) hit 32 distinct banks (unpadded, EPL*rl mod 32 took only 32/EPL
+  // values: a 4- / 2-way conflict on every partial store, SQ_LDS_BANK_CONFLICT / IDX_ACTIVE = 0.38), and
+  // the column reads stay consecutive dwords
   extern __shared__ __attribute__((aligned(16))) float red[];
-  const int CP = C + C / 8;
+  const int CP = C + C / 32;
   constexpr int RPW = 64 / LPR;
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -306,11 +306,11 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     if (k >= nk) break;
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < EPL; ++i) red[(wave * RPW + sub) * CP + c0 + (c0 >> 5) * 4 + i] = accs[k][i];
+    for (int i = 0; i < EPL; ++i) red[(wave * RPW + sub) * CP + c0 + (c0 >> 5) + i] = accs[k][i];
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256) {
       float t = 0.f;
-      const int cp = c + (c >> 5) * 4;
+      const int cp = c + (c >> 5);
 #pragma unroll
       for (int w = 0; w < WAVES * RPW; ++w) t += red[w * CP + cp];  // fixed order
       pb[k * C + c] = t;
@@ -371,7 +371,7 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
   const int nk = film ? 4 : 2;
   if (ws_floats < ssamd_addln_bwd_ws(B, L, C, film)) return -3;
   dim3 grid(gx, B);
-  size_t lds = (size_t)WAVES * 2 * (C + C / 8) * sizeof(float);  // [WAVES * rows per wave][C padded]
+  size_t lds = (size_t)WAVES * 2 * (C + C / 32) * sizeof(float);  // [WAVES * rows per wave][C padded]
   if (relu_in) {
     DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR, true>), grid, dim3(256), lds, stream, dout, a, res,
                                        w, bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,

