@@ -40,6 +40,12 @@ static __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
+// Dropout salt of this translation unit (one device global per kernel file, loaded per training step by
+// the file's salt kernel -- SSAMD_DROP_SALT_LOADER -- from a device value the trainer writes): mixed into
+// every dropout mask, so a step captured in a HIP graph draws the masks of the step it replays (the
+// step-dependent part of the dropout seed lives here, not in the per-op seeds baked into the launches).
+static __device__ unsigned long long g_drop_salt;
+
 // Keep-scales of the N (even) consecutive elements idx0 .. idx0+N-1 (idx0 even): one 32-bit hash per element
 // PAIR, its high / low 16 bits the two elements' uniforms (u = bits / 2^16, kept iff bits >= ceil(p * 2^16)).
 // Half the hashing of one hash per element (the BatchNorm-backward GEMM head and the LayerNorm kernels run
@@ -54,6 +60,7 @@ static __device__ __forceinline__ void drop_scales(uint64_t seed, uint64_t idx0,
     return;
   }
   const float keep = 1.f / (1.f - p);
+  seed ^= g_drop_salt * 0x9E3779B97F4A7C15ULL;
   const uint32_t S = hash_u32((uint32_t)seed ^ (uint32_t)(idx0 >> 32) * 0x9E3779B9U) ^ (uint32_t)(seed >> 32);
   const uint32_t thr = (uint32_t)ceilf(p * 65536.0f);
   const uint32_t pair0 = (uint32_t)idx0 >> 1;
@@ -101,3 +108,16 @@ SSAMD_API int ssamd_seg_colsum(const float* P, long ld, int nseg, int rows, int 
 SSAMD_API int ssamd_small_sum(const float* P, int rows, int k, float* out, hipStream_t s);
 // scratch floats seg_colsum needs for its two-level form
 static inline long seg_colsum_ws(int nseg, int ncols) { return (long)nseg * 16 * ncols; }
+
+// The per-step dropout-salt loader of a kernel file: ssamd_<name>_salt_load(src, stream) copies the device
+// value *src into this file's g_drop_salt (one lane stores it).
+#define SSAMD_DROP_SALT_LOADER(NAME)                                                              \
+  namespace {                                                                                     \
+  __global__ void NAME##_salt_kernel(const unsigned long long* __restrict__ src) {              \
+    if (threadIdx.x == 0) g_drop_salt = src[0];                                                   \
+  }                                                                                               \
+  }                                                                                               \
+  SSAMD_API int ssamd_##NAME##_salt_load(const unsigned long long* src, hipStream_t s) {          \
+    hipLaunchKernelGGL(NAME##_salt_kernel, dim3(1), dim3(64), 0, s, src);                         \
+    return (int)hipGetLastError();                                                                \
+  }

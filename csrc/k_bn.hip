@@ -480,3 +480,5 @@ SSAMD_API int ssamd_bn_bwd_dz(const bf16_t* dz, const bf16_t* h, const float* ga
                        C, training);
   return (int)hipGetLastError();
 }
+
+SSAMD_DROP_SALT_LOADER(bn)

@@ -2956,3 +2956,5 @@ SSAMD_API int ssamd_colsum(const bf16_t* dY, float* db, long M, int N, float* ws
   if (rc) return rc;
   return ssamd_seg_colsum(ws, N, 1, chunks, N, db, 0, 0, N, nullptr, ws + (long)chunks * N, seg_colsum_ws(1, N), s);
 }
+
+SSAMD_DROP_SALT_LOADER(gemm)

@@ -405,3 +405,5 @@ SSAMD_API int ssamd_addln_wb_reduce(const float* ws, int B, int L, int C, int fi
   return ssamd_seg_colsum(ws, (long)nk * C, 1, (int)nblk, 2 * C, dw, 0, 0, C, db, scratch, seg_colsum_ws(1, 2 * C),
                           stream);
 }
+
+SSAMD_DROP_SALT_LOADER(norm)

@@ -312,6 +312,18 @@ def _refresh_all(device):
         e[0], e[1] = owner._version, _wgen
 
 
+def refresh_stale_images(device):
+    """Bring every cached weight image up to date now (one batched launch if any is stale).  A captured
+    HIP-graph step reads the images by address and never performs the lookup that refreshes them lazily;
+    the fused Adam launch rewrites the arena's images itself, this covers any other writer."""
+    for e in _wcache.values():
+        owner = e[2]()
+        if owner is not None and (e[0] != owner._version or e[1] != _wgen):
+            _refresh_all(device)
+            return True
+    return False
+
+
 def _cached(param: torch.Tensor, kind: str, mode: int, make, src: Optional[torch.Tensor] = None):
     """Image of ``src`` (default: ``param`` itself), cached under the parameter ``param``."""
     src = param if src is None else src
@@ -867,6 +879,34 @@ def set_seed(s: int):
 
 def get_seed() -> int:
     return _seed_counter[0]
+
+
+# Per-step dropout salt (csrc/common.h g_drop_salt, one copy per kernel file): the step-dependent part of
+# every dropout mask.  ``set_dropout_salt`` writes the value into a device word (an ordinary stream-ordered
+# copy, outside any captured graph); ``load_dropout_salt`` launches the three loaders that copy it into the
+# kernel files' globals -- captured at the start of a HIP-graph step, so each replay draws its own masks.
+_SIGS.update({"ssamd_norm_salt_load": [P, P], "ssamd_bn_salt_load": [P, P], "ssamd_gemm_salt_load": [P, P]})
+_salt = {}
+
+
+def _salt_word(device):
+    w = _salt.get(device)
+    if w is None:
+        w = _salt[device] = torch.zeros(1, device=device, dtype=torch.int64)
+    return w
+
+
+def set_dropout_salt(value: int, device=None):
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    v = int(value) & ((1 << 63) - 1)
+    _salt_word(device).fill_(v)
+
+
+def load_dropout_salt(device=None):
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    w = _salt_word(device)
+    for fn in ("ssamd_norm_salt_load", "ssamd_bn_salt_load", "ssamd_gemm_salt_load"):
+        _check(getattr(lib(), fn)(_ptr(w), _stream()), fn)
 
 
 _F32_MEMO = {}

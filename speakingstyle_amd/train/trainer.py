@@ -144,12 +144,18 @@ class Trainer:
         return c, work
 
     def _step_seed(self):
+        """Dropout randomness of this micro-step: the per-op seeds (host LCG) start from a per-(seed, rank)
+        value that does not change between steps, and the step-dependent part -- (optimizer step, micro-step)
+        -- is the device dropout salt (``hip.set_dropout_salt``), so a step captured in a HIP graph
+        (``train/graphs.py``) replays with the masks of the step it stands for, bit-identical to the eager
+        step, and a resumed run reproduces the masks of an uninterrupted one."""
         if self.seed is None or not self.opt.arena.data.is_cuda:
             return
         from ..ops import hip
 
-        k = (self.seed * 1000003 + self.rank) * 1000003 + self.opt.current_step
-        hip.set_seed((k * 64 + self.micro % self.grad_acc) * 0x9E3779B97F4A7C15)
+        hip.set_seed((self.seed * 1000003 + self.rank) * 0x9E3779B97F4A7C15)
+        hip.set_dropout_salt((self.opt.current_step * 64 + self.micro % self.grad_acc) + 1,
+                             self.opt.arena.data.device)
 
     def train_step(self, batch):
         tm = self.timer
@@ -160,6 +166,20 @@ class Trainer:
         counts, work = self._global_counts(batch) if self.world > 1 else (None, None)
         last_micro = (self.micro + 1) % self.grad_acc == 0
         tm.phase("forward")
+        losses, output = self.forward_backward(batch, counts, work, last_micro)
+        lr = self.step_tail(batch, last_micro)
+        tm.stop()
+        return losses, output, lr
+
+    def forward_backward(self, batch, counts=None, work=None, last_micro=True):
+        """Forward + loss + backward of one micro-step, every gradient in its arena slot at return (side
+        streams joined).  Device work only after ``_step_seed``: the part a HIP graph captures
+        (``train/graphs.py``)."""
+        tm = self.timer
+        if self.opt.arena.data.is_cuda and self.seed is not None:
+            from ..ops import hip
+
+            hip.load_dropout_salt(self.opt.arena.data.device)
         output = self.model(*batch[2:])
         self._held = None  # defer_release: the previous backward's side-stream inputs
         if work is not None:
@@ -194,6 +214,15 @@ class Trainer:
         self.opt.arena.finalize_grads()
         if ht is not None:
             ht.append(("finalized", time.perf_counter()))
+        return losses, output
+
+    def step_tail(self, batch, last_micro=True, graphed=False):
+        """Host bookkeeping + (on the last micro-step) bucket wait, clip + Adam + LR schedule, zero_grad.
+        ``graphed``: the backward was a graph replay -- its parameters' p.grad views and slot decisions are
+        those of the capture, so the single-contribution bookkeeping is skipped."""
+        tm = self.timer
+        ht = self._host_tail
+        cuda = self.opt.arena.data.is_cuda
         self.micro += 1
         hl = getattr(batch[7], "host_lengths", None)
         if hl is not None:  # host copy from the loader: no device work
@@ -208,7 +237,7 @@ class Trainer:
             lr = self.opt.step_and_update_lr()
             if ht is not None:
                 ht.append(("opt_launched", time.perf_counter()))
-        if cuda:
+        if cuda and not graphed:
             # host bookkeeping for the next step AFTER the optimizer launch: the GPU runs clip + Adam
             # meanwhile instead of idling at the end of the step
             from ..ops import gradslots
@@ -219,8 +248,7 @@ class Trainer:
             self.last_lr = lr
         if ht is not None:
             ht.append(("step_end", time.perf_counter()))
-        tm.stop()
-        return losses, output, lr
+        return lr
 
     def host_tail_summary(self):
         """Mean host ms between consecutive step-tail marks (``host_tail`` diagnostics switch), or None."""
