@@ -85,6 +85,32 @@ def _hip_train() -> bool:
     return experimental.get("hifigan_hip_train")
 
 
+class _TorchGlue:
+    """Elementwise glue of the channel-last training path on torch ops (CPU / reference backend)."""
+
+    @staticmethod
+    def lrelu(x, slope):
+        return F.leaky_relu(x, slope)
+
+    @staticmethod
+    def add(a, b):
+        return a + b
+
+    @staticmethod
+    def mean3(a, b, c):
+        return (a + b + c) / 3
+
+
+def _glue(x):
+    """HIP kernels (``vocoder/hip_train.py``: lrelu / residual add / MRF mean / conv_post + tanh as autograd
+    Functions) for bf16 GPU activations, torch ops otherwise."""
+    if x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16:
+        from ..vocoder import hip_train
+
+        return hip_train
+    return _TorchGlue
+
+
 class ResBlock1(nn.Module):
     def __init__(self, channels, kernel_size=3, dilation=(1, 3, 5)):
         super().__init__()
@@ -109,10 +135,11 @@ class ResBlock1(nn.Module):
         """Channel-last training path [B, T, C] bf16 on the HIP convs (autograd): lrelu -> dilated
         conv -> lrelu -> conv -> + x per layer; the conv weights are the weight-normed tensors."""
         k = self.kernel_size
+        glue = _glue(x)
         for c1, c2, d in zip(self.convs1, self.convs2, self.dilation):
-            t = ops.conv1d(F.leaky_relu(x, LRELU_SLOPE), _wn(c1), c1.bias, get_padding(k, d), d, None)
-            t = ops.conv1d(F.leaky_relu(t, LRELU_SLOPE), _wn(c2), c2.bias, get_padding(k, 1), 1, None)
-            x = t + x
+            t = ops.conv1d(glue.lrelu(x, LRELU_SLOPE), _wn(c1), c1.bias, get_padding(k, d), d, None)
+            t = ops.conv1d(glue.lrelu(t, LRELU_SLOPE), _wn(c2), c2.bias, get_padding(k, 1), 1, None)
+            x = glue.add(t, x)
         return x
 
     def fusable(self, channels: int) -> bool:
@@ -223,6 +250,7 @@ class Generator(nn.Module):
         ``hifigan/models.py:124-165``), returns [B, 1, T*hop] fp32."""
         B = x.shape[0]
         h = x.transpose(1, 2).to(torch.bfloat16).contiguous()
+        glue = _glue(h)
         h = ops.conv1d(h, _wn(self.conv_pre), self.conv_pre.bias, 3, 1, None)
         nk = self.num_kernels
         for i in range(self.num_upsamples):
@@ -231,14 +259,20 @@ class Generator(nn.Module):
             wu = convT_as_conv3(_wn(up).float(), s, up.padding[0])
             bt = None if up.bias is None else up.bias.float().repeat(s)
             T = h.shape[1]
-            h = ops.conv1d(F.leaky_relu(h, LRELU_SLOPE), wu, bt, 1, 1, None).reshape(B, T * s, -1)
-            xs = None
-            for j in range(nk):
-                r = self.resblocks[i * nk + j].forward_cl_train(h)
-                xs = r if xs is None else xs + r
-            h = xs / nk
-        z = F.conv1d(F.leaky_relu(h.float(), 0.01).transpose(1, 2), _wn(self.conv_post), self.conv_post.bias,
-                     padding=3)
+            h = ops.conv1d(glue.lrelu(h, LRELU_SLOPE), wu, bt, 1, 1, None).reshape(B, T * s, -1)
+            rs = [self.resblocks[i * nk + j].forward_cl_train(h) for j in range(nk)]
+            if nk == 3:
+                h = glue.mean3(*rs)
+            else:
+                xs = rs[0]
+                for r in rs[1:]:
+                    xs = xs + r
+                h = xs / nk
+        cp = self.conv_post
+        if glue is not _TorchGlue and cp.out_channels == 1:
+            # lrelu(0.01) -> conv (Cout = 1) -> tanh on the HIP sconv kernel, fp32 [B, T, 1] -> [B, 1, T]
+            return glue.conv_post_tanh(h, _wn(cp), cp.bias, cp.padding[0]).reshape(B, 1, -1)
+        z = F.conv1d(F.leaky_relu(h.float(), 0.01).transpose(1, 2), _wn(cp), cp.bias, padding=3)
         return torch.tanh(z)
 
     # ------------------------------------------------------------------ inference (channel-last, HIP)

@@ -93,8 +93,32 @@ _SIGS = {
 }
 
 
+# HiFi-GAN training kernels (csrc/k_disc.hip; speakingstyle_amd/vocoder/hip_train.py)
+_SIGS.update({
+    "ssamd_sconv_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, F, I, P],
+    "ssamd_sconv_tout": [I, I, I, I, I],
+    "ssamd_sconv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
+    "ssamd_sconv_wgrad_ws": [I, I, I, I, I, I, I, I, I],
+    "ssamd_sconv_wgrad": [P, P, P, L_, P, I, I, I, I, I, I, I, I, I, P],
+    "ssamd_act_bwd": [P, P, P, F, P, L_, I, F, P],
+    "ssamd_tanh_bwd_f32": [P, P, P, L_, P],
+    "ssamd_ew": [I, P, P, P, P, L_, F, P],
+    "ssamd_l1_sum": [P, P, L_, I, F, P, P, I, P],
+    "ssamd_sum_parts": [P, I, F, P, I, P],
+    "ssamd_lsgan": [P, I, F, F, P, P, P],
+    "ssamd_avgpool4": [P, P, I, I, P],
+    "ssamd_avgpool4_bwd": [P, P, I, I, I, P],
+    "ssamd_mpd_fold": [P, P, I, I, I, P],
+    "ssamd_mpd_unfold": [P, P, I, I, I, P],
+    "ssamd_stft_prep": [P, P, I, I, I, P],
+    "ssamd_stft_unpad": [P, P, I, I, I, I, P],
+    "ssamd_mel_l1": [P, I, P, I, I, P, I, I, I, I, F, P, P, I, P],
+})
+
+
 _RESTYPES = {"ssamd_addln_bwd_ws": L_, "ssamd_head_bwd_ws": L_, "ssamd_colsum_ws": L_, "ssamd_embed_bwd_ws": L_,
-             "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_, "ssamd_film_grads_ws": L_}
+             "ssamd_clip_adam_ws": L_, "ssamd_l1pair_ws": L_, "ssamd_film_grads_ws": L_,
+             "ssamd_sconv_wgrad_ws": L_}
 
 
 _FAST_PATH = os.path.join(os.path.dirname(_LIB_PATH),

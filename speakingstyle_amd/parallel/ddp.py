@@ -316,3 +316,33 @@ def all_reduce_async(t: torch.Tensor):
     if world_size() <= 1:
         return None
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+
+
+def allreduce_grads_flat(params, bucket_mb: float = 64.0):
+    """Average the ``.grad`` of ``params`` over the ranks: the gradients are packed into flat buckets of at most
+    ``bucket_mb`` MiB (few, large RCCL all-reduces over xGMI instead of one per tensor), reduced, and
+    unpacked.  Parameters without a gradient are skipped (the same on every rank: one model, one graph).
+    Used by the HIP HiFi-GAN path, whose discriminator gradients come from explicit kernels instead of
+    DistributedDataParallel's autograd hooks (``vocoder/train.py:hip_step``)."""
+    W = world_size()
+    if W <= 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    cap = int(bucket_mb * 2 ** 20 // 4)
+    bucket, size = [], 0
+    for g in grads + [None]:
+        if g is not None and (not bucket or size + g.numel() <= cap) and g.dtype == (bucket[0].dtype if bucket else g.dtype):
+            bucket.append(g)
+            size += g.numel()
+            continue
+        if bucket:
+            flat = torch.cat([t.reshape(-1) for t in bucket])
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+            flat.div_(W)
+            off = 0
+            for t in bucket:
+                t.copy_(flat[off:off + t.numel()].view_as(t))
+                off += t.numel()
+        bucket, size = ([g], g.numel()) if g is not None else ([], 0)

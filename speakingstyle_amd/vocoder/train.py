@@ -88,11 +88,15 @@ def train(a):
         mpd.load_state_dict(state_do["mpd"])
         msd.load_state_dict(state_do["msd"])
         steps, last_epoch = state_do["steps"] + 1, state_do["epoch"]
+    # GPU: the discriminators, losses and STFT run on the HIP kernels (vocoder/hip_train.py, explicit
+    # forward + backward); torch modules otherwise
+    use_hip = cuda and H._hip_train() and not getattr(a, "torch_losses", False)
     if world > 1:
         ids = [local_rank] if cuda else None
         gen = torch.nn.parallel.DistributedDataParallel(gen, device_ids=ids)
-        mpd = torch.nn.parallel.DistributedDataParallel(mpd, device_ids=ids)
-        msd = torch.nn.parallel.DistributedDataParallel(msd, device_ids=ids)
+        if not use_hip:  # HIP path: the discriminator gradients are all-reduced as one flat buffer
+            mpd = torch.nn.parallel.DistributedDataParallel(mpd, device_ids=ids)
+            msd = torch.nn.parallel.DistributedDataParallel(msd, device_ids=ids)
     opt_g = torch.optim.AdamW(gen.parameters(), h.learning_rate, betas=(h.adam_b1, h.adam_b2))
     opt_d = torch.optim.AdamW(itertools.chain(msd.parameters(), mpd.parameters()), h.learning_rate,
                               betas=(h.adam_b1, h.adam_b2))
@@ -134,24 +138,10 @@ def train(a):
                 x, y, y_mel = x.to(dev, non_blocking=True), y.to(dev, non_blocking=True), y_mel.to(dev, non_blocking=True)
                 y = y.unsqueeze(1)
                 y_g = gen(x)
-                y_g_mel = mel_for(h, y_g.squeeze(1), loss=True)
-                T = min(y_mel.shape[-1], y_g_mel.shape[-1])
-                # discriminators
-                opt_d.zero_grad()
-                r, g_, _, _ = mpd(y, y_g.detach())
-                r2, g2, _, _ = msd(y, y_g.detach())
-                loss_d = H.discriminator_loss(r, g_)[0] + H.discriminator_loss(r2, g2)[0]
-                loss_d.backward()
-                opt_d.step()
-                # generator
-                opt_g.zero_grad()
-                loss_mel = F.l1_loss(y_mel[..., :T], y_g_mel[..., :T]) * 45
-                _, g_, fr, fg = mpd(y, y_g)
-                _, g2, fr2, fg2 = msd(y, y_g)
-                loss_g = (H.generator_loss(g_)[0] + H.generator_loss(g2)[0] + H.feature_loss(fr, fg)
-                          + H.feature_loss(fr2, fg2) + loss_mel)
-                loss_g.backward()
-                opt_g.step()
+                if use_hip:
+                    loss_g, loss_mel = hip_step(h, mpd, msd, opt_d, opt_g, y.squeeze(1), y_g.squeeze(1), y_mel, world)
+                else:
+                    loss_g, loss_mel = torch_step(h, mpd, msd, opt_d, opt_g, y, y_g, y_mel)
                 if rank == 0:
                     mel_err = float(loss_mel) / 45
                     if steps % a.stdout_interval == 0:
@@ -179,6 +169,48 @@ def train(a):
         if sw is not None:
             sw.close()
     return steps
+
+
+def torch_step(h, mpd, msd, opt_d, opt_g, y, y_g, y_mel):
+    """One D + G update on the torch modules (reference ``hifigan/train.py:113-160``)."""
+    y_g_mel = mel_for(h, y_g.squeeze(1), loss=True)
+    T = min(y_mel.shape[-1], y_g_mel.shape[-1])
+    opt_d.zero_grad()
+    r, g_, _, _ = mpd(y, y_g.detach())
+    r2, g2, _, _ = msd(y, y_g.detach())
+    loss_d = H.discriminator_loss(r, g_)[0] + H.discriminator_loss(r2, g2)[0]
+    loss_d.backward()
+    opt_d.step()
+    opt_g.zero_grad()
+    loss_mel = F.l1_loss(y_mel[..., :T], y_g_mel[..., :T]) * 45
+    _, g_, fr, fg = mpd(y, y_g)
+    _, g2, fr2, fg2 = msd(y, y_g)
+    loss_g = (H.generator_loss(g_)[0] + H.generator_loss(g2)[0] + H.feature_loss(fr, fg) + H.feature_loss(fr2, fg2)
+              + loss_mel)
+    loss_g.backward()
+    opt_g.step()
+    return loss_g, loss_mel
+
+
+def hip_step(h, mpd, msd, opt_d, opt_g, y, y_g, y_mel, world=1):
+    """The same update on the HIP kernels: D loss + gradient into the discriminators (``hip_train.d_step``), then
+    the mel-L1 x45 and adversarial + feature-matching gradients accumulated into ONE d loss / d y_g buffer and a
+    single backward through the generator.  y, y_g: [B, T]."""
+    from . import hip_train as HT
+
+    mpd_m, msd_m = _unwrap(mpd), _unwrap(msd)
+    opt_d.zero_grad()
+    HT.d_step(mpd_m, msd_m, y, y_g.detach())
+    if world > 1:
+        ddp.allreduce_grads_flat(list(mpd_m.parameters()) + list(msd_m.parameters()))
+    opt_d.step()
+    opt_g.zero_grad()
+    dy = torch.zeros(y_g.shape, device=y_g.device, dtype=torch.float32)
+    loss_mel = HT.mel_l1(h, y_g, y_mel, 45.0, dy)
+    loss_adv = HT.g_adv(mpd_m, msd_m, y, y_g, dy)
+    torch.autograd.backward(y_g, dy.to(y_g.dtype))
+    opt_g.step()
+    return loss_mel + loss_adv, loss_mel
 
 
 @torch.no_grad()
