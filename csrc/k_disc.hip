@@ -255,10 +255,11 @@ __global__ void __launch_bounds__(SC_NT) sconv_kernel(const bf16_t* __restrict__
 }
 
 // weight gradient.  grid (n tiles * k tiles, G, splits); slabs [split][Cout][K] fp32
+// bslabs (nullable): [split][Cout] column sums of dz (the bias gradient), from the blocks of k tile 0
 template <bool VZ, bool VX>
 __global__ void __launch_bounds__(SC_NT) sconv_wgrad_kernel(const bf16_t* __restrict__ dz, const bf16_t* __restrict__ x,
-                                                           float* __restrict__ slabs, SConvGeom q, int rows_per_split,
-                                                           int ktiles) {
+                                                           float* __restrict__ slabs, float* __restrict__ bslabs,
+                                                           SConvGeom q, int rows_per_split, int ktiles) {
   __shared__ __attribute__((aligned(16))) char lds[4 * 8192];  // Z[2], X[2]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -268,6 +269,8 @@ __global__ void __launch_bounds__(SC_NT) sconv_wgrad_kernel(const bf16_t* __rest
   const int r_begin = split * rows_per_split;
   const int r_end = min(M, r_begin + rows_per_split);
   const int nsteps = r_end > r_begin ? (r_end - r_begin + 63) / 64 : 0;
+  const bool dobias = bslabs != nullptr && k0 == 0;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // n = n0 + (tid & 7) * 8 + e, over this thread's rows
   short8 rz[2], rx[2];
   auto gload = [&](int st) {
 #pragma unroll
@@ -287,6 +290,10 @@ __global__ void __launch_bounds__(SC_NT) sconv_wgrad_kernel(const bf16_t* __rest
         }
       }
       rz[i] = zv;
+      if (dobias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[e] += bf2f((bf16_t)zv[e]);
+      }
       const int mm = ok ? m : 0;
       const int b = mm / q.Tout, t = mm - b * q.Tout;
       rx[i] = load_xcol<VX>(x, q, g, ok, b * q.Tin, t * q.s - q.p, k0 + ch * 8);
@@ -342,6 +349,17 @@ __global__ void __launch_bounds__(SC_NT) sconv_wgrad_kernel(const bf16_t* __rest
     if (st + 1 < nsteps) lstore(buf ^ 1);
     __syncthreads();
   }
+  if (dobias) {  // 32 threads share each 8-column chunk: LDS reduce (the loop's last barrier freed the tiles)
+    float* red = reinterpret_cast<float*>(lds);  // [32][64]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(tid >> 3) * 64 + (tid & 7) * 8 + e] = bsum[e];
+    __syncthreads();
+    if (tid < 64 && n0 + tid < q.Ng) {
+      float t = 0.f;
+      for (int j = 0; j < 32; ++j) t += red[j * 64 + tid];
+      bslabs[(long)split * q.Cout + g * q.Ng + n0 + tid] = t;
+    }
+  }
   float* S = slabs + (long)split * q.Cout * q.K;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -357,9 +375,17 @@ __global__ void __launch_bounds__(SC_NT) sconv_wgrad_kernel(const bf16_t* __rest
 
 // dW[o][c][j] (torch layout [Cout][Cg][ks]) = sum over splits (fixed order) of slab[s][o][j * Cg + c]
 __global__ void __launch_bounds__(256) sconv_wreduce_kernel(const float* __restrict__ slabs, float* __restrict__ dW,
+                                                            const float* __restrict__ bslabs, float* __restrict__ db,
                                                             int splits, int Cout, int Cg, int ks) {
   const long K = (long)ks * Cg, tot = (long)Cout * K;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < tot; i += (long)gridDim.x * 256) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < tot + (db ? Cout : 0); i += (long)gridDim.x * 256) {
+    if (i >= tot) {  // bias: db[o] = sum over splits (fixed order)
+      const int o = (int)(i - tot);
+      float t = 0.f;
+      for (int sp = 0; sp < splits; ++sp) t += bslabs[(long)sp * Cout + o];
+      db[o] = t;
+      continue;
+    }
     const int o = (int)(i / K);
     const int rem = (int)(i - (long)o * K);
     const int c = rem / ks, j = rem - c * ks;  // torch order
@@ -629,6 +655,41 @@ __global__ void __launch_bounds__(256) mel_l1_kernel(const float* __restrict__ s
   for (int k = 2 * NB + threadIdx.x; k < ldd; k += 256) drow[k] = 0;
 }
 
+// forward image [Cout][Kp] (column j*Cg + c = W[o][c][j], zero past K) and data-gradient image [G*Cg][s][UNp]
+// (column u*Ng + n of residue r = W[g*Ng + n][c][r + s*u], zero past ks / U*Ng) from the fp32 weight [Cout][Cg][ks]
+__global__ void __launch_bounds__(256) sconv_fimg_kernel(const float* __restrict__ w, bf16_t* __restrict__ img, int Cout,
+                                                         int Cg, int ks, int Kp) {
+  const long tot = (long)Cout * Kp;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < tot; i += (long)gridDim.x * 256) {
+    const int o = (int)(i / Kp), k = (int)(i - (long)o * Kp);
+    float v = 0.f;
+    if (k < ks * Cg) {
+      const int j = k / Cg, c = k - j * Cg;
+      v = w[((long)o * Cg + c) * ks + j];
+    }
+    img[i] = f2bf(v);
+  }
+}
+
+__global__ void __launch_bounds__(256) sconv_dimg_kernel(const float* __restrict__ w, bf16_t* __restrict__ img, int G,
+                                                         int Cg, int Ng, int ks, int s, int U, int UNp) {
+  const long tot = (long)G * Cg * s * UNp;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < tot; i += (long)gridDim.x * 256) {
+    const int col = (int)(i % UNp);
+    const long rowr = i / UNp;
+    const int r = (int)(rowr % s);
+    const int gc = (int)(rowr / s);
+    const int g = gc / Cg, c = gc - g * Cg;
+    float v = 0.f;
+    if (col < U * Ng) {
+      const int u = col / Ng, n = col - u * Ng;
+      const int j = r + s * u;
+      if (j < ks) v = w[((long)(g * Ng + n) * Cg + c) * ks + j];
+    }
+    img[i] = f2bf(v);
+  }
+}
+
 int grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -725,24 +786,25 @@ SSAMD_API int ssamd_sconv_dgrad(const bf16_t* dz, const bf16_t* wdimg, void* dx,
 SSAMD_API long ssamd_sconv_wgrad_ws(int B, int Tin, int Cin, int Cout, int G, int ks, int s, int d, int p) {
   SConvGeom q;
   if (!make_geom(q, B, Tin, Cin, Cout, G, ks, s, d, p)) return -1;
-  return (long)wgrad_splits(q) * Cout * q.K;
+  return (long)wgrad_splits(q) * Cout * (q.K + 1);  // weight slabs + bias slabs
 }
 
-// Weight gradient: dz [B, Tout, Cout], x [B, Tin, Cin] -> dW fp32 [Cout][Cin / G][ks] (torch layout), through
-// ws (>= ssamd_sconv_wgrad_ws floats).  The bias gradient is a column sum of dz (ssamd_colsum).
-SSAMD_API int ssamd_sconv_wgrad(const bf16_t* dz, const bf16_t* x, float* ws, long ws_floats, float* dW, int B, int Tin,
-                                int Cin, int Cout, int G, int ks, int s, int d, int p, hipStream_t st) {
+// Weight gradient: dz [B, Tout, Cout], x [B, Tin, Cin] -> dW fp32 [Cout][Cin / G][ks] (torch layout) and (db non-null)
+// the bias gradient db [Cout] = column sums of dz, through ws (>= ssamd_sconv_wgrad_ws floats).
+SSAMD_API int ssamd_sconv_wgrad(const bf16_t* dz, const bf16_t* x, float* ws, long ws_floats, float* dW, float* db,
+                                int B, int Tin, int Cin, int Cout, int G, int ks, int s, int d, int p, hipStream_t st) {
   SConvGeom q;
   if (!make_geom(q, B, Tin, Cin, Cout, G, ks, s, d, p)) return -2;
   const int sp = wgrad_splits(q);
-  if ((long)sp * Cout * q.K > ws_floats) return -3;
+  if ((long)sp * Cout * (q.K + 1) > ws_floats) return -3;
+  float* bws = db ? ws + (long)sp * Cout * q.K : nullptr;
   const int M = B * q.Tout;
   int rps = (M + sp - 1) / sp;
   rps = (rps + 63) / 64 * 64;
   const int ktiles = (q.K + 63) / 64;
   dim3 grid(((q.Ng + 63) / 64) * ktiles, G, sp);
   const bool vz = q.Ng % 8 == 0, vx = q.Cg % 8 == 0;
-#define SW_L(A, Bv) hipLaunchKernelGGL((sconv_wgrad_kernel<A, Bv>), grid, dim3(SC_NT), 0, st, dz, x, ws, q, rps, ktiles)
+#define SW_L(A, Bv) hipLaunchKernelGGL((sconv_wgrad_kernel<A, Bv>), grid, dim3(SC_NT), 0, st, dz, x, ws, bws, q, rps, ktiles)
   if (vz && vx) SW_L(true, true);
   else if (vz) SW_L(true, false);
   else if (vx) SW_L(false, true);
@@ -750,7 +812,8 @@ SSAMD_API int ssamd_sconv_wgrad(const bf16_t* dz, const bf16_t* x, float* ws, lo
 #undef SW_L
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  hipLaunchKernelGGL(sconv_wreduce_kernel, dim3(grid_for((long)Cout * q.K)), dim3(256), 0, st, ws, dW, sp, Cout, q.Cg, ks);
+  hipLaunchKernelGGL(sconv_wreduce_kernel, dim3(grid_for((long)Cout * q.K + Cout)), dim3(256), 0, st, ws, dW, bws, db, sp,
+                     Cout, q.Cg, ks);
   return (int)hipGetLastError();
 }
 
@@ -855,5 +918,23 @@ SSAMD_API int ssamd_mel_l1(const float* spec, int ldspec, const float* basis, in
   const size_t sh = (size_t)(NB + NM) * sizeof(float);
   hipLaunchKernelGGL(mel_l1_kernel, dim3(R * F), dim3(256), sh, st, spec, ldspec, basis, NB, NM, target, Ft, F, Fv, scale,
                      part, dspec, ldd);
+  return (int)hipGetLastError();
+}
+
+// bf16 images of an fp32 weight [Cout][Cin / G][ks] (either pointer nullable): forward [Cout][round8(ks * Cg)] and
+// data gradient [Cin][s][round8(ceil(ks / s) * Cout / G)]
+SSAMD_API int ssamd_sconv_images(const float* w, bf16_t* fimg, bf16_t* dimg, int Cout, int Cin, int G, int ks, int s,
+                                 hipStream_t st) {
+  if (G <= 0 || Cin % G || Cout % G || ks <= 0 || s <= 0) return -2;
+  const int Cg = Cin / G, Ng = Cout / G;
+  if (fimg) {
+    const int Kp = (ks * Cg + 7) / 8 * 8;
+    hipLaunchKernelGGL(sconv_fimg_kernel, dim3(grid_for((long)Cout * Kp)), dim3(256), 0, st, w, fimg, Cout, Cg, ks, Kp);
+  }
+  if (dimg) {
+    const int U = (ks + s - 1) / s, UNp = (U * Ng + 7) / 8 * 8;
+    hipLaunchKernelGGL(sconv_dimg_kernel, dim3(grid_for((long)Cin * s * UNp)), dim3(256), 0, st, w, dimg, G, Cg, Ng, ks, s,
+                       U, UNp);
+  }
   return (int)hipGetLastError();
 }

@@ -99,7 +99,8 @@ _SIGS.update({
     "ssamd_sconv_tout": [I, I, I, I, I],
     "ssamd_sconv_dgrad": [P, P, P, I, I, I, I, I, I, I, I, I, I, I, P],
     "ssamd_sconv_wgrad_ws": [I, I, I, I, I, I, I, I, I],
-    "ssamd_sconv_wgrad": [P, P, P, L_, P, I, I, I, I, I, I, I, I, I, P],
+    "ssamd_sconv_wgrad": [P, P, P, L_, P, P, I, I, I, I, I, I, I, I, I, P],
+    "ssamd_sconv_images": [P, P, P, I, I, I, I, I, P],
     "ssamd_act_bwd": [P, P, P, F, P, L_, I, F, P],
     "ssamd_tanh_bwd_f32": [P, P, P, L_, P],
     "ssamd_ew": [I, P, P, P, P, L_, F, P],

@@ -56,28 +56,33 @@ def _chk(rc, name):
 
 
 # ------------------------------------------------------------------------------------------- weight images
-def fwd_image(w: torch.Tensor) -> torch.Tensor:
+def fwd_image(w: torch.Tensor, G: int = 1) -> torch.Tensor:
     """[Cout, Cg, ks] -> bf16 [Cout, Kp]: row o = W[o, c, j] at column j * Cg + c (Kp = round8(ks * Cg))."""
-    Cout, Cg, ks = w.shape
-    K = ks * Cg
-    img = w.detach().permute(0, 2, 1).reshape(Cout, K)
-    Kp = (K + 7) // 8 * 8
-    if Kp != K:
-        img = F.pad(img, (0, Kp - K))
-    return img.to(torch.bfloat16).contiguous()
+    Cout, Cg, ks = w.shape[:3]
+    Kp = (ks * Cg + 7) // 8 * 8
+    if w.is_cuda:
+        wf = w.detach().float().contiguous()
+        img = torch.empty(Cout, Kp, device=w.device, dtype=torch.bfloat16)
+        _chk(_lib().ssamd_sconv_images(_P(wf), _P(img), None, Cout, Cg * G, G, ks, 1, _s()), "ssamd_sconv_images")
+        return img
+    img = w.detach().float().reshape(Cout, Cg, ks).permute(0, 2, 1).reshape(Cout, ks * Cg)
+    return F.pad(img, (0, Kp - ks * Cg)).to(torch.bfloat16).contiguous()
 
 
 def dgrad_image(w: torch.Tensor, G: int, s: int) -> torch.Tensor:
     """[Cout, Cg, ks] -> bf16 [G*Cg, s, UNp]: row g*Cg + c, residue r, column u*Ng + n = W[g*Ng + n, c, r + s*u]."""
-    Cout, Cg, ks = w.shape
+    Cout, Cg, ks = w.shape[:3]
     Ng = Cout // G
     U = -(-ks // s)
     UNp = (U * Ng + 7) // 8 * 8
-    wp = F.pad(w.detach(), (0, U * s - ks)).view(G, Ng, Cg, U, s)
+    if w.is_cuda:
+        wf = w.detach().float().contiguous()
+        img = torch.empty(G * Cg, s, UNp, device=w.device, dtype=torch.bfloat16)
+        _chk(_lib().ssamd_sconv_images(_P(wf), None, _P(img), Cout, Cg * G, G, ks, s, _s()), "ssamd_sconv_images")
+        return img
+    wp = F.pad(w.detach().float().reshape(Cout, Cg, ks), (0, U * s - ks)).view(G, Ng, Cg, U, s)
     img = wp.permute(0, 2, 4, 3, 1).reshape(G * Cg, s, U * Ng)
-    if UNp != U * Ng:
-        img = F.pad(img, (0, UNp - U * Ng))
-    return img.to(torch.bfloat16).contiguous()
+    return F.pad(img, (0, UNp - U * Ng)).to(torch.bfloat16).contiguous()
 
 
 # ------------------------------------------------------------------------------------------- raw launches
@@ -118,8 +123,8 @@ def sconv_dgrad(dz, wdimg, Tin, Cin, G, ks, s, d, p, out_f32=False, out=None):
     return out
 
 
-def sconv_wgrad(dz, x, G, ks, s, d, p):
-    """-> dW fp32 [Cout, Cin/G, ks] (torch layout)."""
+def sconv_wgrad(dz, x, G, ks, s, d, p, with_bias=False):
+    """-> dW fp32 [Cout, Cin/G, ks] (torch layout) [, db fp32 [Cout] = column sums of dz]."""
     hip._need(dz, torch.bfloat16, "sconv_wgrad.dz")
     hip._need(x, torch.bfloat16, "sconv_wgrad.x")
     B, Tin, Cin = x.shape
@@ -128,9 +133,10 @@ def sconv_wgrad(dz, x, G, ks, s, d, p):
     n_ws = int(_lib().ssamd_sconv_wgrad_ws(B, Tin, Cin, Cout, G, ks, s, d, p))
     ws = hip._workspace(x.device, n_ws)
     dW = torch.empty(Cout, Cin // G, ks, device=x.device, dtype=torch.float32)
-    _chk(_lib().ssamd_sconv_wgrad(_P(dz), _P(x), _P(ws), ws.numel(), _P(dW), B, Tin, Cin, Cout, G, ks, s, d, p, _s()),
-         "ssamd_sconv_wgrad")
-    return dW
+    db = torch.empty(Cout, device=x.device, dtype=torch.float32) if with_bias else None
+    _chk(_lib().ssamd_sconv_wgrad(_P(dz), _P(x), _P(ws), ws.numel(), _P(dW), _P(db), B, Tin, Cin, Cout, G, ks, s, d, p,
+                                  _s()), "ssamd_sconv_wgrad")
+    return (dW, db) if with_bias else dW
 
 
 def act_bwd(dy, y, act=1, slope=LRELU, r=None, fm_scale=0.0, out=None):
@@ -201,7 +207,7 @@ class _Disc:
         self.layers = [_layer_geom(c) for c in d.convs]
         self.post = _layer_geom(d.conv_post)
         for L in self.layers + [self.post]:
-            L["img"] = fwd_image(L["w"])
+            L["img"] = fwd_image(L["w"], L["G"])
         self.period = getattr(d, "period", None)
 
     def dimg(self, L):
@@ -259,13 +265,14 @@ def _disc_d(d, u, loss, ws, gs):
         if li < len(layers) - 1:
             dz = act_bwd(dx, xs[li + 1], 1, LRELU)
         x_in = xs[li]
-        dW = sconv_wgrad(dz, x_in, L["G"], L["ks"], L["s"], L["d"], L["p"])
+        has_b = convs[li].bias is not None
+        dW, db = sconv_wgrad(dz, x_in, L["G"], L["ks"], L["s"], L["d"], L["p"], with_bias=True)
         w_eff = convs[li].weight
         ws.append(w_eff)
         gs.append(dW.view(w_eff.shape).to(w_eff.dtype))
-        if convs[li].bias is not None:
+        if has_b:
             ws.append(convs[li].bias)
-            gs.append(hip.colsum_raw(dz, dz.shape[-1]).to(convs[li].bias.dtype))
+            gs.append(db.to(convs[li].bias.dtype))
         if li > 0:
             dx = sconv_dgrad(dz, disc.dimg(L), x_in.shape[1], x_in.shape[2], L["G"], L["ks"], L["s"], L["d"], L["p"])
 
@@ -506,9 +513,8 @@ class _ConvPostTanhFn(torch.autograd.Function):
         dz = torch.empty(y.shape, device=y.device, dtype=torch.bfloat16)
         _chk(_lib().ssamd_tanh_bwd_f32(_P(dyc), _P(y), _P(dz), y.numel(), _s()), "ssamd_tanh_bwd_f32")
         da = sconv_dgrad(dz, dgrad_image(w.float(), 1, 1), a.shape[1], a.shape[2], 1, ks, 1, 1, ctx.pad)
-        dW = sconv_wgrad(dz, a, 1, ks, 1, 1, ctx.pad).view_as(w)
-        db = hip.colsum_raw(dz, 1)
-        return da, dW.to(w.dtype), db.to(w.dtype), None
+        dW, db = sconv_wgrad(dz, a, 1, ks, 1, 1, ctx.pad, with_bias=True)
+        return da, dW.view_as(w).to(w.dtype), db.to(w.dtype), None
 
 
 def lrelu(x, slope=LRELU):

@@ -120,3 +120,41 @@ def test_dp2_matches_single_process():
         loss.backward()
         arena.finalize_grads()
     torch.testing.assert_close(res[0][0], arena.grad, rtol=1e-4, atol=1e-6)
+
+
+def _flat_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from speakingstyle_amd.parallel import ddp
+
+    ddp.init_distributed("gloo")
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.zeros(n)) for n in (5, 300, 7, 1000)]
+    ps.append(torch.nn.Parameter(torch.zeros(3)))  # no grad: skipped
+    for i, p in enumerate(ps[:-1]):
+        p.grad = torch.full_like(p, float(rank + 1) * (i + 1)) + torch.arange(p.numel()).float() * rank
+    ddp.allreduce_grads_flat(ps, bucket_mb=1e-3)  # ~262 floats per bucket: several buckets, one oversized
+    q.put((rank, [p.grad.clone() if p.grad is not None else None for p in ps]))
+    torch.distributed.destroy_process_group()
+
+
+def test_allreduce_grads_flat_averages_over_ranks():
+    """The HiFi-GAN HIP path's discriminator-gradient all-reduce (vocoder/train.py:hip_step): flat buckets,
+    the rank average, grads without .grad skipped."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_flat_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i, n in enumerate((5, 300, 7, 1000)):
+        want = (torch.full((n,), 1.0 * (i + 1)) + torch.full((n,), 2.0 * (i + 1)) + torch.arange(n).float()) / 2
+        torch.testing.assert_close(res[0][i], want)
+        torch.testing.assert_close(res[1][i], want)
+    assert res[0][4] is None

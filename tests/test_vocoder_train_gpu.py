@@ -79,6 +79,11 @@ def test_sconv_fwd_dgrad_wgrad_vs_torch(case):
 
     db = hip.colsum_raw(dz, Cout)
     assert _rel(db, br.grad) < 2e-2
+    dW2, db2 = HT.sconv_wgrad(dz, x.to(torch.bfloat16).contiguous(), G, ks, s, d, p, with_bias=True)
+    assert torch.equal(dW2, dW) and _rel(db2, br.grad) < 2e-2
+    # the HIP image kernels vs the torch construction
+    assert torch.equal(HT.fwd_image(w, G), HT.fwd_image(w.cpu(), G).cuda())
+    assert torch.equal(HT.dgrad_image(w, G, s), HT.dgrad_image(w.cpu(), G, s).cuda())
 
 
 def test_sconv_dgrad_accumulates_fp32():

@@ -45,7 +45,7 @@ def full_step(use_hip, B, frames, iters=5, warm=2):
         loss_g, loss_mel = step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1000
-    return ms, float(loss_g), float(loss_mel)
+    return ms, float(loss_g.detach()), float(loss_mel.detach())
 
 
 def gen_only(hip_on, B, frames, iters=10):
@@ -77,6 +77,9 @@ if __name__ == "__main__":
                 res[key + "_loss_g"] = round(lg, 4)
                 res[key + "_loss_mel"] = round(lm, 4)
             print(json.dumps(res), flush=True)
+    if which == "hip":  # profiling: the HIP step only
+        ms, lg, lm = full_step(True, 16, 32, iters=3, warm=2)
+        print(json.dumps({"what": "hifigan train step (HIP)", "batch": 16, "hip_ms": round(ms, 2)}), flush=True)
     if which in ("gen", "all"):
         for B, frames in ((16, 32),):
             res = {"what": "generator fwd + L1 + bwd", "batch": B, "frames": frames}
