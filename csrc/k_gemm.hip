@@ -958,7 +958,8 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
   // EPI_BNH: the BatchNorm input h of this thread's 16 epilogue rows.  The first BNH_PRE rows (4 VGPRs each)
   // are loaded now and land under the main loop; the rest (register budget: the whole 16 would push the
   // epilogue past 256 VGPRs) are issued right after the accumulator staging, before its barrier
-  constexpr int BNH_PRE = 16;
+  // (STG: its fragment ring holds 16 more VGPRs -- half the rows prefetched, the rest after the main loop)
+  constexpr int BNH_PRE = STG ? 8 : 16;
   short8 hpre[16];
   auto load_h = [&](int it0, int it1) {
     const int c = tid & 31, r0 = tid >> 5;
@@ -2487,6 +2488,8 @@ SSAMD_API void ssamd_gemm_set_buf(int v) { g_gemm_buf = v; }
 // the k9 convs and K = 1024, +2 % PostNet k5, -1..4 % at K = 256 where the prologue / epilogue dominate)
 static int g_gemm_stg = 1;
 static int g_gemm_mask_pre = 1;  // EPI_MASK for the ReLU-mask data gradient (0: the generic epilogue, A/B)
+static int g_gemm_bnh_stg = 1;   // the BatchNorm-backward-head data gradient on the staggered main loop (0: A/B)
+SSAMD_API void ssamd_gemm_set_bnh_stg(int v) { g_gemm_bnh_stg = v; }
 SSAMD_API void ssamd_gemm_set_mask_pre(int v) { g_gemm_mask_pre = v; }
 SSAMD_API void ssamd_gemm_set_stg(int v) { g_gemm_stg = v; }
 
@@ -2613,6 +2616,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       allow_lds(conv_gemm_big64_kernel<true, true, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, true, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_BNH>, B64_LDS);
+      allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_BNH, true>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, false, false, EPI_BNH>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, false, false, false, EPI_BNH>, B64_LDS);
       allow_lds(conv_gemm_big64_kernel<false, true, false, true, EPI_GEN, true>, B64_LDS);
@@ -2643,6 +2647,9 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
         if (stg_ && !bnh)                                                                                \
           kfn = g.rinfo ? conv_gemm_big64_kernel<F32, true, true, true, EPI_GEN, true>                   \
                         : conv_gemm_big64_kernel<F32, true, false, true, EPI_GEN, true>;                 \
+        if constexpr (!F32) {                                                                            \
+          if (stg_ && bnh && g_gemm_bnh_stg) kfn = conv_gemm_big64_kernel<false, true, false, true, EPI_BNH, true>; \
+        }                                                                                                \
         if constexpr (!F32) {                                                                            \
           if (g_gemm_mask_pre && mask_pre)                                                               \
             kfn = stg_ ? (g.rinfo ? conv_gemm_big64_kernel<false, true, true, true, EPI_MASK, true>       \

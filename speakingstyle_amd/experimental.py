@@ -10,7 +10,8 @@ silently selecting a default (or an untested path).
 ``mi355x.experimental: {wgrad_first: "0"}`` in train.yaml does the same for ``train.py`` (the trainer
 calls ``configure`` with it; the environment wins on conflicts).
 
-Two switches select kernel-library variants (``KERNEL_SWITCHES``: ``gemm_stg``, ``gemm_mask_pre``).
+Three switches select kernel-library variants (``KERNEL_SWITCHES``: ``gemm_stg``, ``gemm_mask_pre``,
+``gemm_bnh_stg``).
 ``apply_kernel_switches()`` pushes their current values into the library; it runs when the library
 is first loaded (``ops/hip.py:lib``), after ``configure()`` and on entry to / exit from ``overrides``,
 so every path -- training, synthesis, kernel tests -- sees the same values.  The library's other
@@ -72,6 +73,7 @@ KNOBS: Dict[str, tuple] = {
                                    "only -- main-stream weight gradients then reduce in a different order)"),
     "gemm_stg": (True, _bool, "staggered 8-phase main loop of the 256x256 GEMM for K >= 512 (+0.7 % LJSpeech)"),
     "gemm_mask_pre": (True, _bool, "ReLU-mask data gradient with its mask bytes prefetched before the main loop"),
+    "gemm_bnh_stg": (True, _bool, "PostNet BatchNorm-backward-head data gradient on the staggered main loop"),
     "bn_fuse": (True, _bool, "PostNet BatchNorm backward started in the data-gradient GEMM's epilogue"),
     "defer_release": (False, _bool, "hand the side-stream weight-gradient inputs back to the trainer, freed "
                                     "during the next forward (holds a step's activations into it)"),
@@ -84,7 +86,8 @@ KNOBS: Dict[str, tuple] = {
 }
 
 # switch -> kernel-library setter it drives (applied by apply_kernel_switches)
-KERNEL_SWITCHES = {"gemm_stg": "ssamd_gemm_set_stg", "gemm_mask_pre": "ssamd_gemm_set_mask_pre"}
+KERNEL_SWITCHES = {"gemm_stg": "ssamd_gemm_set_stg", "gemm_mask_pre": "ssamd_gemm_set_mask_pre",
+                   "gemm_bnh_stg": "ssamd_gemm_set_bnh_stg"}
 
 _values: Dict[str, Any] = {}
 _parsed = [False]

@@ -50,6 +50,7 @@ _SIGS = {
     "ssamd_gemm_set_buf": [I],
     "ssamd_gemm_set_stg": [I],
     "ssamd_gemm_set_mask_pre": [I],
+    "ssamd_gemm_set_bnh_stg": [I],
     "ssamd_bn_set_dz_cfg": [I, I],
     "ssamd_wgrad_set_pp": [I],
     "ssamd_wgrad_set_prio": [I],

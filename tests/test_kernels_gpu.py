@@ -651,12 +651,21 @@ def test_bn_dropout_rate():
     assert 0.47 < frac < 0.53
 
 
+@pytest.mark.parametrize("bnh_stg", [True, False])
 @pytest.mark.parametrize("N,training,R", [(512, True, (5, 93)), (80, True, (3, 700)), (512, False, (4, 61)),
                                           (512, True, (2, 1)), (512, True, (1, 300))])
-def test_bn_act_conv_fused(N, training, R):
+def test_bn_act_conv_fused(N, training, R, bnh_stg):
     """One PostNet link conv(tanh(BN(h))) with the BatchNorm backward started in the data-gradient GEMM's
     epilogue (dz + per-tile column partials) vs fp32 torch: BN running stats, h / gamma / beta / W / bias
-    gradients.  Row counts that are not a multiple of the 256-row tile and a single-row batch included."""
+    gradients.  Row counts that are not a multiple of the 256-row tile and a single-row batch included.
+    ``bnh_stg``: that data gradient on the staggered 8-phase main loop (K = 5 * 512 >= 512) or the plain one."""
+    from speakingstyle_amd import experimental
+
+    with experimental.overrides(gemm_bnh_stg=bnh_stg):
+        _bn_act_conv_fused(N, training, R)
+
+
+def _bn_act_conv_fused(N, training, R):
     torch.manual_seed(21)
     B, L = R
     C, ks, pad = 512, 5, 2
