@@ -189,13 +189,30 @@ __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int ro
   // the caller's next phase re-uses the ring / tiles only after its own __syncthreads
 }
 
-template <int C, int K>
+// PROF (diagnostic instantiation, ssamd_resblock_layer_prof): wave 0 stamps s_memtime at the phase
+// boundaries (start, x staged, conv1 done, t1 staged, conv2 done, output tile staged, stores issued) into
+// prof[block][8]; the production instantiation compiles no stamp.
+template <bool PROF>
+__device__ __forceinline__ void rb_stamp(unsigned long long* st, int i) {
+  if constexpr (PROF) {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    st[i] = t;
+  }
+}
+
+template <int C, int K, bool PROF = false>
 __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
                                                             const float* __restrict__ b1, const bf16_t* __restrict__ w2,
                                                             const float* __restrict__ b2, const bf16_t* acc_in,
                                                             bf16_t* out, int T, int tiles, int d, float slope,
-                                                            float out_scale, int post_lrelu) {
+                                                            float out_scale, int post_lrelu,
+                                                            unsigned long long* __restrict__ prof = nullptr) {
   using R = RB<C, K>;
+  unsigned long long st[8];
+  rb_stamp<PROF>(st, 0);
   constexpr int NT = R::NT;
   constexpr int CH = C / 8;                                  // 16-B chunks per row
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -250,11 +267,13 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     }
   }
   __syncthreads();
+  rb_stamp<PROF>(st, 1);
 
   // 2. conv1 (dilation d): t1 row i <- x rows i + tap*d
   float4v acc[R::MAXRB][R::NSW];
   const int wr = wave % R::WR, wc = wave / R::WR;
   conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
+  rb_stamp<PROF>(st, 2);
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
     const int rb = wr + R::WR * r;
@@ -274,9 +293,11 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     }
   }
   __syncthreads();  // t1 complete; the x tile is dead from here on (os aliases it)
+  rb_stamp<PROF>(st, 3);
 
   // 3. conv2 (dilation 1): out row j <- t1 rows j + tap
   conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
+  rb_stamp<PROF>(st, 4);
 #pragma unroll
   for (int r = 0; r < R::MAXRB; ++r) {
     const int rb = wr + R::WR * r;
@@ -291,6 +312,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     }
   }
   __syncthreads();
+  rb_stamp<PROF>(st, 5);
 
   // 4. + residual (+ MRF accumulator), scale, coalesced 16-B stores (loads batched first)
   {
@@ -326,6 +348,14 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
         o[i] = (short)f2bf(v);
       }
       *reinterpret_cast<short8*>(ob + (long)t * C + c0) = o;
+    }
+  }
+  if constexpr (PROF) {
+    rb_stamp<PROF>(st, 6);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) prof[(long)blockIdx.x * 8 + i] = st[i];
+      prof[(long)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
     }
   }
 }
@@ -796,6 +826,33 @@ SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16
 
 // x / out / acc_in [B, T, C] bf16 (acc_in may alias out, or be null); w1 / w2 bf16 [C][K][C] (the
 // implicit-GEMM forward image); b1 / b2 fp32 [C].  C in {32, 64, 128}, K in {3, 7, 11}, 1 <= d <= 5.
+// Diagnostic: the per-layer kernel with phase stamps (see rb_stamp); prof >= 8 * B * ceil(T / BM) words.
+SSAMD_API int ssamd_resblock_layer_prof(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
+                                        const float* b2, const bf16_t* acc_in, bf16_t* out, int B, int T, int C, int K,
+                                        int d, float slope, float out_scale, int post_lrelu, unsigned long long* prof,
+                                        hipStream_t s) {
+#define RBP_CASE(CC, KK)                                                                                      \
+  if (C == CC && K == KK) {                                                                                   \
+    using R = RB<CC, KK>;                                                                                     \
+    allow_lds(resblock_layer_kernel<CC, KK, true>, R::LDS);                                                   \
+    const int tiles = (T + R::BM - 1) / R::BM;                                                                \
+    hipLaunchKernelGGL((resblock_layer_kernel<CC, KK, true>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, \
+                       w1, b1, w2, b2, acc_in, out, T, tiles, d, slope, out_scale, post_lrelu, prof);          \
+    return (int)hipGetLastError();                                                                            \
+  }
+  if (d < 1 || d > MAXD) return -2;
+  RBP_CASE(128, 11) RBP_CASE(128, 7) RBP_CASE(64, 11)
+#undef RBP_CASE
+  return -2;
+}
+
+SSAMD_API int ssamd_resblock_layer_tile(int C, int K) {
+  if (C == 128 && K == 11) return RB<128, 11>::BM;
+  if (C == 128 && K == 7) return RB<128, 7>::BM;
+  if (C == 64 && K == 11) return RB<64, 11>::BM;
+  return 0;
+}
+
 SSAMD_API int ssamd_resblock_layer(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
                                    const float* b2, const bf16_t* acc_in, bf16_t* out, int B, int T, int C, int K,
                                    int d, float slope, float out_scale, int post_lrelu, hipStream_t s) {
