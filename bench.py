@@ -129,9 +129,9 @@ def run(args):
 
         hip._USE_FAST[0] = False
     if args.no_side_wgrad and torch.cuda.is_available():
-        from speakingstyle_amd.ops import hip
+        from speakingstyle_amd import experimental
 
-        hip.set_wgrad_stream(False)
+        experimental.set_value("side_wgrad", "0", "bench --no-side-wgrad")
     if args.ln_reduce_main and torch.cuda.is_available():
         from speakingstyle_amd.ops import hip
 

@@ -68,6 +68,11 @@ KNOBS: Dict[str, tuple] = {
                     "issue a layer's weight gradient (side stream) before its data gradient: 0 never, 1 always, "
                     "auto when the data-gradient GEMMs have fewer row tiles than wgrad_first_waves x CUs"),
     "wgrad_first_waves": (1.25, float, "auto threshold of wgrad_first, in waves of 256-row tiles per CU"),
+    "side_wgrad": ("auto", _tristate,
+                   "weight gradients (and LayerNorm weight reductions) on the side stream: 0 never, 1 always, auto "
+                   "when the step has >= side_wgrad_min_frames valid mel frames (a small step is host-bound: the "
+                   "side stream's event record / wait per launch costs more host time than its overlap saves)"),
+    "side_wgrad_min_frames": (20000, _pos_int, "auto threshold of side_wgrad (valid mel frames per step and GPU)"),
     "wgrad_cu_frac": (0.75, _frac, "fraction of the CUs the side-stream weight-gradient split plan is sized for"),
     "wgrad_cus_all": (True, _bool, "apply the reduced weight-gradient CU plan to every stream (0: side stream "
                                    "only -- main-stream weight gradients then reduce in a different order)"),
@@ -125,6 +130,14 @@ def _ensure():
         for k, v in _parse_env().items():
             _set(k, v, "SSAMD_EXPERIMENTAL")
         _parsed[0] = True
+
+
+def set_value(name: str, value, source: str = "set_value"):
+    """Set a switch for the rest of the process (a CLI flag's programmatic equivalent); later ``configure``
+    calls do not reset it (they replace only their own block's values)."""
+    _ensure()
+    _set(name, value, source)
+    apply_kernel_switches()
 
 
 def configure(block: Optional[dict]):

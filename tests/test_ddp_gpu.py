@@ -15,6 +15,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _side_stream_on():
+    """These tests are about buckets behind queued side-stream weight gradients: force the side stream on
+    (the automatic policy turns it off for steps this small, experimental.side_wgrad)."""
+    from speakingstyle_amd import experimental
+
+    with experimental.overrides(side_wgrad="1"):
+        yield
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

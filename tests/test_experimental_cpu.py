@@ -63,3 +63,25 @@ def test_configure_replaces_previous_block_and_applies_kernel_switches(monkeypat
     with experimental.overrides(gemm_mask_pre=False):
         assert ("mask_pre", 0) in calls
     assert calls[-1] == ("mask_pre", 1) or ("mask_pre", 1) in calls[-2:]
+
+
+def test_side_wgrad_policy_threshold():
+    """Automatic side-stream weight gradients (experimental.side_wgrad): on for steps with >= the frame
+    threshold, off below it, forced by 0 / 1, undecided (None) without host lengths."""
+    import numpy as np
+
+    from speakingstyle_amd import experimental
+    from speakingstyle_amd.train.trainer import side_wgrad_wanted
+
+    small = np.full(16, 560)        # LibriTTS batch 16: ~9k frames
+    big = np.full(200, 570)         # LJSpeech batch 200: ~114k frames
+    capped = np.full(30, 5000)      # lengths past max_seq_len count as max_seq_len
+    with experimental.overrides(side_wgrad="auto", side_wgrad_min_frames=20000):
+        assert side_wgrad_wanted(small, 1000) is False
+        assert side_wgrad_wanted(big, 1000) is True
+        assert side_wgrad_wanted(capped, 600) is False   # 30 * 600 = 18000
+        assert side_wgrad_wanted(None, 1000) is None
+    with experimental.overrides(side_wgrad="1"):
+        assert side_wgrad_wanted(small, 1000) is True
+    with experimental.overrides(side_wgrad="0"):
+        assert side_wgrad_wanted(big, 1000) is False

@@ -97,19 +97,16 @@ def test_trainer_save_restore_continuation(tmp_path):
 def test_side_stream_weight_gradients_bitwise(name):
     """Weight gradients on the side stream (default) == on the main stream, bitwise: same kernels,
     same reduction order; the joins before the optimizer order everything."""
-    from speakingstyle_amd.ops import hip
+    from speakingstyle_amd import experimental
 
     cfg = _setup(name)
     bs = _batches(3, seed=8)
     res = []
-    for side in (True, False):
-        hip.set_wgrad_stream(side)
-        try:
+    for side in ("1", "0"):
+        with experimental.overrides(side_wgrad=side):
             m, t = _fresh(cfg)
             l = _run(t, bs)
             res.append((l, t.opt.arena.data.clone(), float(t.opt.last_grad_norm)))
-        finally:
-            hip.set_wgrad_stream(True)
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
     assert res[0][2] == res[1][2]
