@@ -816,6 +816,16 @@ __device__ __forceinline__ void pp_barrier() {
 //             epilogue (one exposed memory round trip per 8 rows with nothing else in flight).
 // STG (BUF only): the staggered 8-phase main loop -- see the comment at its loop below.
 constexpr int EPI_GEN = 0, EPI_BNH = 1, EPI_MASK = 2;
+
+// Epilogue staging tile (bf16, 528-B rows = 132 dwords): the accumulator staging writes 4-column (8-B) pieces with
+// ds_write_b64, whose 16-lane groups are 16 consecutive rows of one piece; at a 132-dword pitch rows r and r + 8
+// share banks (4 r mod 32), so rows with bit 3 set store the two 8-B halves of each 16-B chunk swapped (their
+// pieces land 2 dwords over: 32 distinct banks per group).  The 16-B chunk reads undo the swap in registers.
+__device__ __forceinline__ int ct_woff(int ml, int nl) { return ml * 528 + ((nl * 2) ^ (((ml >> 3) & 1) << 3)); }
+__device__ __forceinline__ short8 ct_read(const char* Ct, int r, int c16) {
+  const short8 v = *reinterpret_cast<const short8*>(Ct + r * 528 + c16 * 16);
+  return ((r >> 3) & 1) ? __builtin_shufflevector(v, v, 4, 5, 6, 7, 0, 1, 2, 3) : v;
+}
 // One 256x256 output tile (block vb) of the big64 GEMM.
 template <bool OUT_F32, bool FASTK, bool PACKED, bool BUF, int EPIM, bool STG>
 __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
@@ -1149,8 +1159,7 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
       // (528-B padded rows: conflict-free both ways) turns that into 16-B-per-lane stores of whole
       // 512-B rows, and the aux / residual operands are read the same coalesced way.
       // (Measured: the direct register stores cost up to 55 % of a K = 256 GEMM.)
-      constexpr int RSB = 528;
-      char* Ct = smem;
+      char* Ct = smem;  // [BG][528 B] staging tile (ct_woff / ct_read)
       // bias and activation are compile-time branches of the staging loop: as runtime checks inside the
       // unrolled 8 x 4 loop they cost ~350 scalar branches per tile, and the bias float4 was re-loaded
       // (behind a full vmcnt wait) for every (i, j) -- 32 serialised L2 round trips per tile
@@ -1188,7 +1197,7 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
             short4v o;
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = (short)f2bf(v[q]);
-            *reinterpret_cast<short4v*>(Ct + ml * RSB + nl * 2) = o;
+            *reinterpret_cast<short4v*>(Ct + ct_woff(ml, nl)) = o;
           }
         }
       };
@@ -1247,7 +1256,7 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
           for (int it = 0; it < EPI; ++it) {
             const int r = r0 + 16 * it;
             const int m = m0 + r;
-            const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
+            const short8 v = ct_read(Ct, r, c);
             const long off = (long)m * ldy + n;
             float ks[8];
             drop_scales<8>(ex.bn_seed, (uint64_t)off, ex.bn_p, ks);
@@ -1313,7 +1322,7 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
           const int r = e >> 5, cc = e & 31;
           const int m = m0 + r, nn = n0 + cc * 8;
           if (m >= g.M || nn >= g.N) continue;
-          const short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + cc * 16);
+          const short8 v = ct_read(Ct, r, cc);
           if (ex.mask_out) {
             unsigned bits = 0;
 #pragma unroll
@@ -1352,7 +1361,7 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
           const int r = r0 + 16 * (g0 + u);
           const int m = m0 + r;
           if (m >= g.M || !col_ok) continue;
-          short8 v = *reinterpret_cast<const short8*>(Ct + r * RSB + c * 16);
+          short8 v = ct_read(Ct, r, c);
           const bool valid = loads ? vv[u] : true;
           const long off = (long)m * ldy + n;
           if (ex.mask_out) {  // ReLU output > 0  <=>  its bf16 bits are a positive non-zero value
