@@ -1,6 +1,7 @@
 #!/usr/bin/env python
-"""A/B of the 256x256 weight-gradient main loops (ssamd_wgrad_set_pp: 0 double buffer, 1 ping-pong,
-2 staggered 8-phase with the bias summed by colsum) on the training step's weight-gradient shapes: dW must be
+"""A/B of the 256x256 weight-gradient main loops (ssamd_wgrad_set_pp: 0 double buffer, 1 ping-pong; 2 was
+the staggered 8-phase loop of the measurement in profiles/r5_exp_wgrad_staggered.txt -- rejected, so in the
+current library 2 selects the ping-pong loop again) on the training step's weight-gradient shapes: dW must be
 bitwise equal across loops (same per-accumulator row order), db within fp32 rounding of an fp32 column sum;
 then time each (kernel + reduce (+ colsum), warm, alternating).  JSON per shape.
 Usage (GPU): python tools/exp_wgrad_stg.py [--iters 20]"""
