@@ -1,5 +1,5 @@
 """Host-side (Python) cost of a training step: cProfile over N steady-state Trainer steps (GPU box).
-Usage: python tools/host_profile.py [config] [steps]"""
+Usage: python tools/host_profile.py [config] [steps] [batch]   (prints the unprofiled host ms/step first)"""
 import cProfile
 import io
 import os
@@ -20,11 +20,21 @@ pp, mc, tc = load_named(cfg)
 torch.manual_seed(0)
 model = FastSpeech2(pp, mc).to("cuda").set_compute_dtype(torch.bfloat16)
 tr = Trainer(model, (pp, mc, tc), seed=1)
-gen = SyntheticBatches(int(tc["optimizer"]["batch_size"]), device="cuda", max_seq_len=mc["max_seq_len"], seed=5)
+bs = int(sys.argv[3]) if len(sys.argv) > 3 else int(tc["optimizer"]["batch_size"])
+gen = SyntheticBatches(bs, device="cuda", max_seq_len=mc["max_seq_len"], seed=5)
 b = gen.make_batch()
 for _ in range(3):
     tr.train_step(b)
 torch.cuda.synchronize()
+import time  # noqa: E402
+
+t0 = time.perf_counter()
+for _ in range(20):
+    tr.train_step(b)
+t1 = time.perf_counter()
+torch.cuda.synchronize()
+t2 = time.perf_counter()
+print(f"{cfg} batch {bs}: host {1e3 * (t1 - t0) / 20:.2f} ms/step, wall {1e3 * (t2 - t0) / 20:.2f} ms/step", flush=True)
 if os.environ.get("SAME_THREAD_BWD", "1") == "1":  # backward on this thread so cProfile sees it
     torch.autograd.set_multithreading_enabled(False)
 pr = cProfile.Profile()
