@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
 //   part[blk][2C..3C) S1[b]     part[blk][3C..4C) S2[b]       (FiLM: S1 = sum_t dout*yd, S2 = sum_t dout)
 // (blk = b * gridDim.x + blockIdx.x) and the host finishes them with fixed-order column sums
 // (k_reduce.hip) -- no float atomics.
-template <int EPL, int LPR, bool RELU = false>
+template <int EPL, int LPR, bool RELU, bool RES, bool DA>
 __global__ void __launch_bounds__(256) addln_bwd_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ a, const bf16_t* __restrict__ res,
     const float* __restrict__ w, const float* __restrict__ bias, const float* __restrict__ fg,
@@ -233,20 +233,34 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     acc_w[i] = acc_b[i] = acc_s1[i] = acc_s2[i] = 0.f;
   }
   const float invC = 1.f / C;
-  for (int r = 0; r < ROWS_PER_WAVE / RPW; ++r) {
-    const int t = blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub;
-    if (t >= Lb) continue;
-    const long row = rowb + t;
-    float dh[EPL];
-    if (t >= len) {  // masked row: zero gradient flows back
+  // Rows software-pipelined one ahead, as in the forward: row r+1's a / res / dout / statistics loads are
+  // issued before row r's math and stores, in straight-line code (a half-wave past the block's rows
+  // recomputes and rewrites the last row -- identical bytes -- and adds nothing to the partial sums), so
+  // each row no longer waits out a full memory round trip (the kernel was 70 % s_waitcnt).
+  constexpr int NR = ROWS_PER_WAVE / RPW;
+  RawRow<EPL> ra[2], rr[2], rg[2];
+  float mun[2], rsn[2];
+  auto t_raw = [&](int r) { return blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub; };
+  auto fetch = [&](int r, int q) {
+    const long row = rowb + min(t_raw(r), Lb - 1);
+    load_raw<EPL>(a + row * lda + c0, ra[q]);
+    if constexpr (RES) load_raw<EPL>(res + row * C + c0, rr[q]);
+    load_raw<EPL>(dout + row * C + c0, rg[q]);
+    mun[q] = mean_in[row];
+    rsn[q] = rstd_in[row];
+  };
+  fetch(0, 0);
 #pragma unroll
-      for (int i = 0; i < EPL; ++i) dh[i] = 0.f;
-      store_row<EPL>(dh_out + row * lda + c0, dh);
-      if (da_out) store_row<EPL>(da_out + row * C + c0, dh);
-      continue;
-    }
+  for (int r = 0; r < NR; ++r) {
+    const int cur = r & 1;
+    if (r + 1 < NR) fetch(r + 1, cur ^ 1);
+    const int tr = t_raw(r);
+    const int t = min(tr, Lb - 1);
+    const long row = rowb + t;
+    const bool valid = t < len;     // masked (padding) row: zero gradient flows back
+    const bool count = tr < len;    // contributes to the parameter sums (the clamped repeats do not)
     float h[EPL], m1[EPL];
-    load_row<EPL>(a + row * lda + c0, h);
+    raw_to_f<EPL>(ra[cur], h);
     // RELU: a is a ReLU output and its producer's backward leaves the ReLU mask to this kernel (it
     // reads a anyway): d a = dh * (a > 0) -- no residual, no pre-dropout (host check).  Its own
     // instantiation, the mask as bits: the common kernel keeps its register count (occupancy).
@@ -258,15 +272,15 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     drop_scales<EPL>(seed, (uint64_t)row * C + c0, pre_p, m1);
 #pragma unroll
     for (int i = 0; i < EPL; ++i) h[i] *= m1[i];
-    if (res) {
+    if constexpr (RES) {
       float rv[EPL];
-      load_row<EPL>(res + row * C + c0, rv);
+      raw_to_f<EPL>(rr[cur], rv);
 #pragma unroll
       for (int i = 0; i < EPL; ++i) h[i] += rv[i];
     }
     float go[EPL];
-    load_row<EPL>(dout + row * C + c0, go);
-    const float mu = mean_in[row], rs = rstd_in[row];
+    raw_to_f<EPL>(rg[cur], go);
+    const float mu = mun[cur], rs = rsn[cur];
     float xh[EPL], dx[EPL], m2v[EPL];
     float sum1 = 0.f, sum2 = 0.f;
     drop_scales<EPL>(seed ^ 0x5bd1e9955bd1e995ULL, (uint64_t)row * C + c0, post_p, m2v);
@@ -275,25 +289,28 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
       xh[i] = (h[i] - mu) * rs;
       const float m2 = m2v[i];
       const float y = xh[i] * wv[i] + bv[i];
-      acc_s1[i] += go[i] * y * m2;
-      acc_s2[i] += go[i];
       const float dy = go[i] * G[i] * m2;
-      acc_w[i] += dy * xh[i];
-      acc_b[i] += dy;
+      if (count) {
+        acc_s1[i] += go[i] * y * m2;
+        acc_s2[i] += go[i];
+        acc_w[i] += dy * xh[i];
+        acc_b[i] += dy;
+      }
       dx[i] = dy * wv[i];
       sum1 += dx[i];
       sum2 += dx[i] * xh[i];
     }
     sum1 = row_sum<EPL, LPR>(sum1) * invC;
     sum2 = row_sum<EPL, LPR>(sum2) * invC;
+    float dh[EPL];
 #pragma unroll
-    for (int i = 0; i < EPL; ++i) dh[i] = rs * (dx[i] - sum1 - xh[i] * sum2);
-    if constexpr (RELU) {
-#pragma unroll
-      for (int i = 0; i < EPL; ++i) dh[i] = (pos >> i) & 1u ? dh[i] : 0.f;
+    for (int i = 0; i < EPL; ++i) {
+      float v = rs * (dx[i] - sum1 - xh[i] * sum2);
+      if constexpr (RELU) v = (pos >> i) & 1u ? v : 0.f;
+      dh[i] = valid ? v : 0.f;
     }
     store_row<EPL>(dh_out + row * lda + c0, dh);
-    if (da_out) {
+    if constexpr (DA) {
 #pragma unroll
       for (int i = 0; i < EPL; ++i) dh[i] *= m1[i];
       store_row<EPL>(da_out + row * C + c0, dh);
@@ -372,15 +389,22 @@ SSAMD_API int ssamd_addln_bwd(const bf16_t* dout, const bf16_t* a, const bf16_t*
   if (ws_floats < ssamd_addln_bwd_ws(B, L, C, film)) return -3;
   dim3 grid(gx, B);
   size_t lds = (size_t)WAVES * 2 * (C + C / 32) * sizeof(float);  // [WAVES * rows per wave][C padded]
+#define ADDLN_BWD(RELU_, RES_, DA_)                                                                          \
+  DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR, RELU_, RES_, DA_>), grid, dim3(256), lds, stream, \
+                                     dout, a, res, w, bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C,  \
+                                     pre_p, post_p, (uint64_t)seed, lda))
   if (relu_in) {
-    DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR, true>), grid, dim3(256), lds, stream, dout, a, res,
-                                       w, bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
-                                       (uint64_t)seed, lda));
+    ADDLN_BWD(true, false, false);
+  } else if (res && da) {
+    ADDLN_BWD(false, true, true);
+  } else if (res) {
+    ADDLN_BWD(false, true, false);
+  } else if (da) {
+    ADDLN_BWD(false, false, true);
   } else {
-    DISPATCH_EPL(C, hipLaunchKernelGGL((addln_bwd_kernel<EPL, LPR>), grid, dim3(256), lds, stream, dout, a, res, w,
-                                       bias, fg, s_g, lens, cu, mean, rstd, dh, da, ws, film, L, C, pre_p, post_p,
-                                       (uint64_t)seed, lda));
+    ADDLN_BWD(false, false, false);
   }
+#undef ADDLN_BWD
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   float* scratch = ws + nblk * nk * C;
