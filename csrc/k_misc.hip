@@ -57,6 +57,11 @@ __global__ void __launch_bounds__(256) lr_fwd_kernel(const bf16_t* __restrict__ 
 }
 
 // dx[b, p] = sum over the frames f in [cum[p-1], cum[p]) with f < M of dout[b, f]
+// LRB_ROWS phonemes per block (a thread per 16-B chunk of one phoneme at C = 256): the per-phoneme frame
+// sums are short dependent chains, so the grid is made wide (64 phonemes per block left 200-400 blocks
+// each walking 8 chunks x ~8 frames serially: 70 us for the LJSpeech batch) and each thread issues four
+// frames' loads before adding them in frame order (the same sums, bit for bit).
+constexpr int LRB_ROWS = 8;
 __global__ void __launch_bounds__(256) lr_bwd_kernel(const bf16_t* __restrict__ dout, const int64_t* __restrict__ dur,
                                                      bf16_t* __restrict__ dx, const int64_t* __restrict__ cu,
                                                      const int64_t* __restrict__ plen, int T, int M, int C) {
@@ -66,15 +71,26 @@ __global__ void __launch_bounds__(256) lr_bwd_kernel(const bf16_t* __restrict__ 
   const long obase = cu ? (long)cu[b] : (long)b * M;
   block_prefix_durations(dur + (long)b * T, T, cum);
   const int vec = C / 8;
-  for (int e = threadIdx.x; e < LR_ROWS * vec; e += blockDim.x) {
+  for (int e = threadIdx.x; e < LRB_ROWS * vec; e += blockDim.x) {
     const int r = e / vec, c8 = e % vec;
-    const int p = blockIdx.x * LR_ROWS + r;
+    const int p = blockIdx.x * LRB_ROWS + r;
     if (p >= T) break;
     const int f0 = p ? cum[p - 1] : 0;
     const int f1 = min(cum[p], Mb);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int f = f0; f < f1; ++f) {
-      short8 v = *reinterpret_cast<const short8*>(dout + (obase + f) * C + c8 * 8);
+    const bf16_t* src = dout + obase * C + c8 * 8;
+    int f = f0;
+    for (; f + 4 <= f1; f += 4) {
+      short8 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const short8*>(src + (long)(f + j) * C);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += bf2f((bf16_t)v[j][i]);
+    }
+    for (; f < f1; ++f) {
+      short8 v = *reinterpret_cast<const short8*>(src + (long)f * C);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += bf2f((bf16_t)v[i]);
     }
@@ -344,7 +360,7 @@ SSAMD_API int ssamd_lr_bwd(const bf16_t* dout, const int64_t* dur, bf16_t* dx, c
                            int B, int T, int M, int C, hipStream_t s) {
   if (C % 8) return -1;
   if (B == 0 || T == 0) return 0;
-  hipLaunchKernelGGL(lr_bwd_kernel, dim3(cdiv(T, LR_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, dout, dur, dx, cu,
+  hipLaunchKernelGGL(lr_bwd_kernel, dim3(cdiv(T, LRB_ROWS), B), dim3(256), (size_t)T * 4 + 16, s, dout, dur, dx, cu,
                      plen, T, M, C);
   return (int)hipGetLastError();
 }
@@ -1124,10 +1140,19 @@ __global__ void __launch_bounds__(256) pad_colsum_kernel(const T* __restrict__ d
   const int c = blockIdx.x * 64 + cl;
   const long r0 = (long)blockIdx.y * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
   float s = 0.f;
-  if (c < C) {
-    for (long row = r0 + rl; row < r1; row += 4) {
-      const int b = (int)(row / M), t = (int)(row - (long)b * M);
-      if (t >= lens[b]) s += ld_as_f<T>(dout + row * C + c);
+  if (c < C && r0 + rl < r1) {
+    // (sequence, position) of the first row once, then stepped: no 64-bit division per row
+    long row = r0 + rl;
+    int b = (int)(row / M), t = (int)(row - (long)b * M);
+    int lb = (int)lens[b];
+    for (; row < r1; row += 4) {
+      if (t >= lb) s += ld_as_f<T>(dout + row * C + c);
+      t += 4;
+      while (t >= M) {
+        t -= M;
+        ++b;
+        if (row + 4 < r1) lb = (int)lens[b];
+      }
     }
   }
   red[rl][cl] = s;

@@ -252,11 +252,11 @@ def test_add_layernorm_dropout_consistency():
     torch.testing.assert_close(bb.grad, kept, rtol=1e-3, atol=1e-2)
 
 
-def test_length_regulator():
+@pytest.mark.parametrize("B,T,C,dmax", [(3, 21, 256, 9), (40, 150, 512, 15)])
+def test_length_regulator(B, T, C, dmax):
     torch.manual_seed(4)
-    B, T, C = 3, 21, 256
     x = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
-    d = torch.randint(0, 9, (B, T), device=DEV)
+    d = torch.randint(0, dmax, (B, T), device=DEV)
     d[1, 10:] = 0
     M = int(d.sum(1).max().item()) - 5  # also exercise truncation
     xh = x.clone().requires_grad_(True)
@@ -1321,6 +1321,28 @@ def test_duration_round_seq_mean_add_rowvec():
     y.backward(gy)
     yr.backward(gy.float())
     assert _rel(v.grad, vr.grad) < 1e-3
+
+
+def test_unpack_fill_grad_many_rows():
+    """Gradient of the unpack fill row (sum of the padded rows) over many 256-row chunks, rows of a chunk
+    spanning several sequences, fp32 and bf16 gradients, vs torch."""
+    from speakingstyle_amd.ops import packing
+
+    torch.manual_seed(33)
+    B, M, C = 50, 611, 80
+    lens = torch.randint(0, M + 1, (B,), device=DEV)
+    lens[0] = M
+    R = int(lens.sum())
+    pk = packing.PackInfo.build(lens, M, R)
+    pad = ~(torch.arange(M, device=DEV)[None] < lens[:, None])
+    for dtype in (torch.float32, torch.bfloat16):
+        z = torch.randn(1, R, C, device=DEV).to(dtype).requires_grad_(True)
+        fill = torch.randn(C, device=DEV, requires_grad=True)
+        u = hip.unpack_rows(z, pk, fill)
+        gu = torch.randn(B, M, C, device=DEV).to(dtype)
+        u.backward(gu)
+        dfill_ref = (gu.float() * pad[..., None]).sum((0, 1))
+        assert _rel(fill.grad, dfill_ref) < 1e-5, dtype
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
