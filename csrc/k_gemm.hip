@@ -1627,6 +1627,14 @@ __device__ __forceinline__ short4v ds_read_tr_asm(const char* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
   return r;
 }
+// ... with a DS immediate offset: fragments that differ by a constant (the +4-row half, the k-half, the stage
+// buffer) share one address register -- no per-read v_add in the read segment
+template <int OFF>
+__device__ __forceinline__ short4v ds_read_tr_off(unsigned addr) {
+  short4v r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
 // s_waitcnt lgkmcnt(0) that the fragments data-depend on (MFMAs cannot be hoisted above it)
 __device__ __forceinline__ void lgkm_wait_tie(short8 (&fa)[4], short8 (&fb)[4]) {
   asm volatile("s_waitcnt lgkmcnt(0)"
@@ -1862,24 +1870,42 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
             acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[kk][j], acc[i0 + i][j0 + j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     };
-    auto rd = [&](const char* base, int rbase, int cb) {
-      const short4v v0 = ds_read_tr_asm(base + swz_tr512(rbase, cb));
-      const short4v v1 = ds_read_tr_asm(base + swz_tr512(rbase + 4, cb));
+    // per-lane fragment bases (stage 0, k-half 0): dY columns of the wave's 8 16-col blocks, X columns of
+    // its 4; the +4-row half (2 KiB), the k-half (16 KiB) and the stage (32 KiB) are DS immediates
+    unsigned fab[8], fbb[4];
+    {
+      const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)smem;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fab[i] = lds0 + swz_tr512(grp * 8 + q, (wn * 128 + i * 16) / 4 + p);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fbb[j] = lds0 + 65536 + swz_tr512(grp * 8 + q, (wk * 64 + j * 16) / 4 + p);
+    }
+    auto rd = [&](unsigned base, auto offc) {
+      constexpr int O = decltype(offc)::value;
+      const short4v v0 = ds_read_tr_off<O>(base);
+      const short4v v1 = ds_read_tr_off<O + 2048>(base);
       return (short8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     };
-    for (int st = 0; st < nsteps; ++st) {
-      const int buf = st & 1;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 16384>;
+    using I2 = std::integral_constant<int, 32768>;
+    using I3 = std::integral_constant<int, 32768 + 16384>;
+    auto step = [&](int st, auto bufc) {
+      constexpr int buf = decltype(bufc)::value;
+      using K0 = std::conditional_t<buf == 0, I0, I2>;  // k-half 0 / 1 of this stage
+      using K1 = std::conditional_t<buf == 0, I1, I3>;
       const char* Ys = smem + buf * 32768;
-      const char* Xs = smem + 65536 + buf * 32768;
       const bool more = st + 1 < nsteps;
       // phase 0: n rows 0-63 of the wave's half, k columns 0-31
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int rbase = kk * 32 + grp * 8 + q;
+      for (int j = 0; j < 2; ++j) {
+        fb0[0][j] = rd(fbb[j], K0{});
+        fb0[1][j] = rd(fbb[j], K1{});
+      }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb0[kk][j] = rd(Xs, rbase, (wk * 64 + j * 16) / 4 + p);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[kk][i] = rd(Ys, rbase, (wn * 128 + i * 16) / 4 + p);
+      for (int i = 0; i < 4; ++i) {
+        fa[0][i] = rd(fab[i], K0{});
+        fa[1][i] = rd(fab[i], K1{});
       }
       if (more) stage_y(r_begin + (st + 1) * 64, buf ^ 1);
       pp_barrier();
@@ -1889,10 +1915,9 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
       pp_barrier();
       // phase 1: n rows 0-63, k columns 32-63
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int rbase = kk * 32 + grp * 8 + q;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb1[kk][j] = rd(Xs, rbase, (wk * 64 + 32 + j * 16) / 4 + p);
+      for (int j = 0; j < 2; ++j) {
+        fb1[0][j] = rd(fbb[2 + j], K0{});
+        fb1[1][j] = rd(fbb[2 + j], K1{});
       }
       if (more) {
         stage_x(r_begin + (st + 1) * 64, buf ^ 1);
@@ -1904,10 +1929,9 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
       pp_barrier();
       // phase 2: n rows 64-127, k columns 32-63
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int rbase = kk * 32 + grp * 8 + q;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[kk][i] = rd(Ys, rbase, (wn * 128 + 64 + i * 16) / 4 + p);
+      for (int i = 0; i < 4; ++i) {
+        fa[0][i] = rd(fab[4 + i], K0{});
+        fa[1][i] = rd(fab[4 + i], K1{});
       }
       pp_barrier();
       lgkm_tie(fa);
@@ -1933,9 +1957,15 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
         // the rinfo rows of step st+2 are retired by the vmcnt(0) above; re-define them through an
         // empty asm so the compiler's waitcnt pass (which cannot see that wait) does not make the
         // next step's X stage wait for the dY DMA issued just before it
+        int2* rn = ri_nxt;  // (named here: an asm operand alone does not capture it in the generic lambda)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(ri_nxt[i].x), "+v"(ri_nxt[i].y));
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(rn[i].x), "+v"(rn[i].y));
       }
+    };
+    // two steps per iteration: the stage buffer is a compile-time immediate in each body
+    for (int st = 0; st < nsteps; st += 2) {
+      step(st, std::integral_constant<int, 0>{});
+      if (st + 1 < nsteps) step(st + 1, std::integral_constant<int, 1>{});
     }
     if (wn == 0) pp_barrier();
   } else {
