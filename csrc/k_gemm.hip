@@ -2025,15 +2025,30 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
       step(st, std::integral_constant<int, 0>{});
       if (st + 1 < nsteps) step(st + 1, std::integral_constant<int, 1>{});
     }
-  } else {  // all 24 fragment reads of a k-half issued, one wait, 32 MFMAs (runtime stage base)
-    for (int st = 0; st < nsteps; ++st) {
-      const int buf = st & 1;
+  } else {  // all 24 fragment reads of a k-half issued, one wait, 32 MFMAs
+    // fragment reads from per-block base registers + DS immediates (+4 rows, k-half, stage buffer), the
+    // loop unrolled over the two stage buffers (as in the ping-pong loop: no v_add per read)
+    unsigned fab[8], fbb[4];
+    {
+      const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)smem;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fab[i] = lds0 + swz_tr512(grp * 8 + q, (wn * 128 + i * 16) / 4 + p);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fbb[j] = lds0 + 65536 + swz_tr512(grp * 8 + q, (wk * 64 + j * 16) / 4 + p);
+    }
+    auto rd = [&](unsigned base, auto offc) {
+      constexpr int O = decltype(offc)::value;
+      const short4v v0 = ds_read_tr_off<O>(base);
+      const short4v v1 = ds_read_tr_off<O + 2048>(base);
+      return (short8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    };
+    auto step = [&](int st, auto bufc) {
+      constexpr int buf = decltype(bufc)::value;
       if (st + 1 < nsteps) {
         stage(r_begin + (st + 1) * 64, buf ^ 1);
         if constexpr (PACKED) load_ri(r_begin + (st + 2) * 64);
       }
       const char* Ys = smem + buf * 32768;
-      const char* Xs = smem + 65536 + buf * 32768;
       if (do_bias) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -2044,24 +2059,12 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
           for (int t = 0; t < 8; ++t) bsum[t] += bf2f((bf16_t)v[t]);
         }
       }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int rbase = kk * 32 + grp * 8 + q;
+      auto khalf = [&](auto offc) {
         short8 fa[8], fb[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cb = (wk * 64 + j * 16) / 4 + p;
-          short4v b0 = ds_read_tr_asm(Xs + swz_tr512(rbase, cb));
-          short4v b1 = ds_read_tr_asm(Xs + swz_tr512(rbase + 4, cb));
-          fb[j] = (short8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-        }
+        for (int j = 0; j < 4; ++j) fb[j] = rd(fbb[j], offc);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int ca = (wn * 128 + i * 16) / 4 + p;
-          short4v a0 = ds_read_tr_asm(Ys + swz_tr512(rbase, ca));
-          short4v a1 = ds_read_tr_asm(Ys + swz_tr512(rbase + 4, ca));
-          fa[i] = (short8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        }
+        for (int i = 0; i < 8; ++i) fa[i] = rd(fab[i], offc);
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
                        "+v"(fa[7]), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
@@ -2070,9 +2073,15 @@ __global__ void __launch_bounds__(NT3, 1) conv_wgrad_big64_kernel(const bf16_t* 
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
+      };
+      khalf(std::integral_constant<int, buf * 32768>{});
+      khalf(std::integral_constant<int, buf * 32768 + 16384>{});
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+    };
+    for (int st = 0; st < nsteps; st += 2) {
+      step(st, std::integral_constant<int, 0>{});
+      if (st + 1 < nsteps) step(st + 1, std::integral_constant<int, 1>{});
     }
   }
   }
