@@ -89,8 +89,13 @@ __global__ void __launch_bounds__(CP_T) conv_post_kernel(const bf16_t* __restric
                                                          const float* __restrict__ b, int T, float slope,
                                                          float scale, float* __restrict__ outf,
                                                          int16_t* __restrict__ outi) {
-  __shared__ float xs[(CP_T + 6) * (C + 1)];
-  __shared__ float ws[7 * C];
+  // rows staged with 16-B loads (8 channels per lane) into fp32 rows of RS = C + 4 floats (16-B aligned; the
+  // 36-dword pitch at C = 32 spreads a 16-lane group's ds_read_b128 over all 64 banks), the 7 x C dot
+  // product read back 4 channels per ds_read_b128 in the same tap / channel order as a scalar loop
+  constexpr int RS = C + 4;
+  constexpr int CH = C / 8;  // 16-B chunks per input row
+  __shared__ __attribute__((aligned(16))) float xs[(CP_T + 6) * RS];
+  __shared__ __attribute__((aligned(16))) float ws[7 * C];
   const int bb = blockIdx.y;
   const int t0 = blockIdx.x * CP_T;
   const bf16_t* xb = x + (long)bb * T * C;
@@ -98,15 +103,21 @@ __global__ void __launch_bounds__(CP_T) conv_post_kernel(const bf16_t* __restric
     const int c = e / 7, tap = e % 7;
     ws[tap * C + c] = w[e];
   }
-  for (int e = threadIdx.x; e < (CP_T + 6) * C; e += CP_T) {
-    const int rr = e / C, c = e % C;
+  for (int e = threadIdx.x; e < (CP_T + 6) * CH; e += CP_T) {
+    const int rr = e / CH, q = e % CH;
     const int t = t0 - 3 + rr;
-    float v = 0.f;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (t >= 0 && t < T) {
-      v = bf2f(xb[(long)t * C + c]);
-      v = v > 0.f ? v : slope * v;  // fused pre-activation
+      const short8 raw = *reinterpret_cast<const short8*>(xb + (long)t * C + q * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float f = bf2f((bf16_t)raw[i]);
+        v[i] = f > 0.f ? f : slope * f;  // fused pre-activation
+      }
     }
-    xs[rr * (C + 1) + c] = v;
+    float4* dst = reinterpret_cast<float4*>(xs + rr * RS + q * 8);
+    dst[0] = make_float4(v[0], v[1], v[2], v[3]);
+    dst[1] = make_float4(v[4], v[5], v[6], v[7]);
   }
   __syncthreads();
   const int t = t0 + threadIdx.x;
@@ -114,10 +125,16 @@ __global__ void __launch_bounds__(CP_T) conv_post_kernel(const bf16_t* __restric
   float s = b ? *b : 0.f;
 #pragma unroll
   for (int tap = 0; tap < 7; ++tap) {
-    const float* xr = xs + (threadIdx.x + tap) * (C + 1);
-    const float* wr = ws + tap * C;
+    const float4* xr = reinterpret_cast<const float4*>(xs + (threadIdx.x + tap) * RS);
+    const float4* wr = reinterpret_cast<const float4*>(ws + tap * C);
 #pragma unroll
-    for (int c = 0; c < C; ++c) s += xr[c] * wr[c];
+    for (int c4 = 0; c4 < C / 4; ++c4) {
+      const float4 xv = xr[c4], wv = wr[c4];
+      s += xv.x * wv.x;
+      s += xv.y * wv.y;
+      s += xv.z * wv.z;
+      s += xv.w * wv.w;
+    }
   }
   const float y = tanhf(s);
   const long o = (long)bb * T + t;
