@@ -109,9 +109,11 @@ __device__ __forceinline__ short8 pack8(const float4v& a, const float4v& b) {
 // loop is VALU-issue bound (MI355X_MICROARCH: 4 cycles per VALU, 8 per v_exp beside 16-cycle
 // MFMAs): raw v_exp_f32 (no denormal-range fix-up: softmax terms below 2^-126 are 0 anyway),
 // the key mask only on the one tile that straddles len, scale and max folded into one FMA,
-// the O rescale skipped when no lane's running max moved, and l kept as a per-lane partial
+// the running max deferred (moved only by jumps > kMaxSlack, so the O rescale is rare), and l kept as a
+// per-lane partial
 // (the 4 lane groups of a query share m, so the cross-group sum is deferred to the end).
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+constexpr float kMaxSlack = 8.f;
 
 template <int NF, int D>
 __device__ __forceinline__ void online_softmax(float4v (&st)[NF][4], float (&m)[NF], float (&l)[NF],
@@ -136,9 +138,14 @@ __device__ __forceinline__ void online_softmax(float4v (&st)[NF][4], float (&m)[
       mx = fmaxf(mx, fmaxf(fmaxf(st[f][kf][0], st[f][kf][1]), fmaxf(st[f][kf][2], st[f][kf][3])));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m[f], mx * scale_log2);  // the tile always holds a valid key: mn finite
-    alpha[f] = fast_exp2(m[f] - mn);                 // m = -inf on the first tile -> 0
-    rescale |= m[f] != mn;
+    // deferred max: the running max moves only when a tile's max exceeds it by more than kMaxSlack (log2
+    // units), so the O rescale runs on the first tile and on rare jumps instead of whenever any query's max
+    // creeps up; unnormalised p stay <= 2^kMaxSlack (exact in fp32 / bf16 range), l and O share the factor
+    const float cand = mx * scale_log2;               // the tile always holds a valid key: cand finite
+    const bool up = cand > m[f] + kMaxSlack;          // m = -inf on the first tile -> up
+    const float mn = up ? cand : m[f];
+    alpha[f] = fast_exp2(m[f] - mn);                  // 1 when the max stays, 0 on the first tile
+    rescale |= up;
     const float nb = -mn;
     float ls = 0.f;
 #pragma unroll
