@@ -72,6 +72,7 @@ for task in "$@"; do
       t=$(find gpurun_out/${TAG}_synth -name "*kernel_trace.csv" | head -1)
       f=$(find gpurun_out/${TAG}_synth -name "*kernel_stats.csv" | head -1)
       python tools/prof_summary.py "$f" "$t" > gpurun_out/${TAG}_synth_summary.txt
+      python tools/grid_census.py "$t" --all --top 60 > gpurun_out/${TAG}_synth_grid.txt 2>&1 || true
       rm -rf gpurun_out/${TAG}_synth
       head -30 gpurun_out/${TAG}_synth_summary.txt ;;
     pmc)

@@ -12,10 +12,11 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--match", default="")
+    ap.add_argument("--all", action="store_true", help="the whole trace (synthesis: no optimizer-step marker)")
     a = ap.parse_args()
     kt = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     ends = [i for i, r in enumerate(kt) if re.search(r"adam(_img)?_kernel", r["Kernel_Name"])]
-    step = kt[ends[-2] + 1: ends[-1] + 1]
+    step = kt if (a.all or len(ends) < 2) else kt[ends[-2] + 1: ends[-1] + 1]
     agg = defaultdict(lambda: [0, 0.0])
     for r in step:
         n = r["Kernel_Name"]
@@ -29,7 +30,7 @@ def main():
         e[0] += 1
         e[1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     tot = sum(v[1] for v in agg.values())
-    print(f"last step: {len(step)} kernels, {tot:.1f} us kernel time (both streams)")
+    print(f"{'whole trace' if step is kt else 'last step'}: {len(step)} kernels, {tot:.1f} us kernel time (both streams)")
     print(f"{'us':>9} {'n':>4} {'us/launch':>9}  q  gridX x gridY  lds  kernel")
     for (n, gx, gy, lds, q), (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"{t:9.1f} {c:4d} {t / c:9.1f}  {q}  {gx:>7} x {gy:<3} {lds:>6}  {n}")
