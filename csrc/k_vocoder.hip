@@ -203,16 +203,21 @@ __device__ __forceinline__ void rb_stamp(unsigned long long* st, int i) {
   }
 }
 
+// Persistent over tiles (tile = blockIdx.x + k * gridDim.x; the grid is the resident-block count): at C = 128
+// one 150-KiB block owns a CU, so nothing hid the x tile's global round trip (12 % of a block,
+// profiles/r5_resblock_phases.txt).  The next tile's x rows are fetched into registers right after conv2
+// (no DMA of conv_tile is in flight any more), under the output staging and the epilogue's own loads, and
+// the barriers of that span order LDS only (__syncthreads would drain the fetch: vmcnt counts it).
+// Synthesis RTF -1.2..-2.8 % same-box (profiles/r5_ab_rb_persistent.txt).
 template <int C, int K, bool PROF = false>
 __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
                                                             const float* __restrict__ b1, const bf16_t* __restrict__ w2,
                                                             const float* __restrict__ b2, const bf16_t* acc_in,
-                                                            bf16_t* out, int T, int tiles, int d, float slope,
+                                                            bf16_t* out, int T, int tiles, int ntiles, int d, float slope,
                                                             float out_scale, int post_lrelu,
                                                             unsigned long long* __restrict__ prof = nullptr) {
   using R = RB<C, K>;
   unsigned long long st[8];
-  rb_stamp<PROF>(st, 0);
   constexpr int NT = R::NT;
   constexpr int CH = C / 8;                                  // 16-B chunks per row
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -220,32 +225,26 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   float* os = reinterpret_cast<float*>(lds);                 // [NRB2*16][OSP] conv2 + b2 (after conv1)
   bf16_t* t1 = reinterpret_cast<bf16_t*>(lds + R::R0_BYTES);  // [R1P][LDC]  lrelu(conv1 + b1)
   char* bring = reinterpret_cast<char*>(lds + R::R0_BYTES + R::T1_BYTES);  // 3 x [C][32] weight slices
-  const int b = blockIdx.x / tiles, t0 = (blockIdx.x - b * tiles) * R::BM;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row-block tests are scalar
-  const int col = lane & 15, quad = lane >> 4;
+  const int tid0 = threadIdx.x;
   const int h1 = d * (K - 1) / 2;
-  const bf16_t* xb = x + (long)b * T * C;
   // both convs' bias columns of this lane (they depend on the sub-tile s only): loaded up front, not as
   // one exposed L2 round trip per (row block, sub-tile) between the two convolutions
   float bias1[R::NSW], bias2[R::NSW];
-  {
-    const int wc0 = wave / R::WR;
 #pragma unroll
-    for (int s = 0; s < R::NSW; ++s) {
-      const int ch = (wc0 * R::NSW + s) * 16 + col;
-      bias1[s] = b1[ch];
-      bias2[s] = b2[ch];
-    }
+  for (int s = 0; s < R::NSW; ++s) {
+    const int ch = ((tid0 >> 6) / R::WR * R::NSW + s) * 16 + (tid0 & 15);
+    bias1[s] = b1[ch];
+    bias2[s] = b2[ch];
   }
-
-  // 1. lrelu(x) rows [t0 - h1 - H2, ...) -- all global loads of the thread first, then convert + store
-  {
-    constexpr int IT = (R::RX * CH + NT - 1) / NT;
-    const int rows_x = R::R1P + (K - 1) * d;
-    short8 v[IT];
+  constexpr int IX = (R::RX * CH + NT - 1) / NT;
+  const int rows_x = R::R1P + (K - 1) * d;
+  short8 v[IX];
+  // x rows [t0 - h1 - H2, ...) of a tile into v (zero outside [0, T))
+  auto fetch_x = [&](int tile, int tid) {
+    const int b = tile / tiles, t0 = (tile - b * tiles) * R::BM;
+    const bf16_t* xb = x + (long)b * T * C;
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int it = 0; it < IX; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
       const int t = t0 - h1 - R::H2 + r;
       if (r < rows_x && t >= 0 && t < T) {
@@ -255,8 +254,28 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
         for (int i = 0; i < 8; ++i) v[it][i] = 0;
       }
     }
+  };
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  fetch_x(blockIdx.x, tid0);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // the thread index re-derived opaquely per tile: otherwise both unrolled convolutions' per-lane address
+    // terms are hoisted out of the tile loop and stay live across it (256 VGPRs + spills vs 152)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, col = lane & 15, quad = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row-block tests are scalar
+    const int wr = wave % R::WR, wc = wave / R::WR;
+    const int b = tile / tiles, t0 = (tile - b * tiles) * R::BM;
+    const bf16_t* xb = x + (long)b * T * C;
+    rb_stamp<PROF>(st, 0);
+
+    // 1. lrelu(x) -> LDS
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int it = 0; it < IX; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
       if (r < rows_x) {
         short8 o;
@@ -265,64 +284,47 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
         *reinterpret_cast<short8*>(xs + r * R::LDC + c0) = o;
       }
     }
-  }
-  __syncthreads();
-  rb_stamp<PROF>(st, 1);
+    __syncthreads();
+    rb_stamp<PROF>(st, 1);
 
-  // 2. conv1 (dilation d): t1 row i <- x rows i + tap*d
-  float4v acc[R::MAXRB][R::NSW];
-  const int wr = wave % R::WR, wc = wave / R::WR;
-  conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
-  rb_stamp<PROF>(st, 2);
+    // 2. conv1 (dilation d): t1 row i <- x rows i + tap*d
+    float4v acc[R::MAXRB][R::NSW];
+    conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
+    rb_stamp<PROF>(st, 2);
 #pragma unroll
-  for (int r = 0; r < R::MAXRB; ++r) {
-    const int rb = wr + R::WR * r;
-    if (rb < R::NRB1) {
+    for (int r = 0; r < R::MAXRB; ++r) {
+      const int rb = wr + R::WR * r;
+      if (rb < R::NRB1) {
 #pragma unroll
-      for (int s = 0; s < R::NSW; ++s) {
-        const int ch = (wc * R::NSW + s) * 16 + col;
-        const float bias = bias1[s];
+        for (int s = 0; s < R::NSW; ++s) {
+          const int ch = (wc * R::NSW + s) * 16 + col;
+          const float bias = bias1[s];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = rb * 16 + 4 * quad + i;
-          const int t = t0 - R::H2 + row;
-          const float v = (row < R::R1 && t >= 0 && t < T) ? lrelu(acc[r][s][i] + bias, slope) : 0.f;
-          t1[row * R::LDC + ch] = f2bf(v);
+          for (int i = 0; i < 4; ++i) {
+            const int row = rb * 16 + 4 * quad + i;
+            const int t = t0 - R::H2 + row;
+            const float v1 = (row < R::R1 && t >= 0 && t < T) ? lrelu(acc[r][s][i] + bias, slope) : 0.f;
+            t1[row * R::LDC + ch] = f2bf(v1);
+          }
         }
       }
     }
-  }
-  __syncthreads();  // t1 complete; the x tile is dead from here on (os aliases it)
-  rb_stamp<PROF>(st, 3);
+    __syncthreads();  // t1 complete; the x tile is dead from here on (os aliases it)
+    rb_stamp<PROF>(st, 3);
 
-  // 3. conv2 (dilation 1): out row j <- t1 rows j + tap
-  conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
-  rb_stamp<PROF>(st, 4);
-#pragma unroll
-  for (int r = 0; r < R::MAXRB; ++r) {
-    const int rb = wr + R::WR * r;
-    if (rb < R::NRB2) {
-#pragma unroll
-      for (int s = 0; s < R::NSW; ++s) {
-        const int ch = (wc * R::NSW + s) * 16 + col;
-        const float bias = bias2[s];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + ch] = acc[r][s][i] + bias;
-      }
-    }
-  }
-  __syncthreads();
-  rb_stamp<PROF>(st, 5);
-
-  // 4. + residual (+ MRF accumulator), scale, coalesced 16-B stores (loads batched first)
-  {
+    // 3. conv2 (dilation 1): out row j <- t1 rows j + tap
+    conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
+    rb_stamp<PROF>(st, 4);
+    const int nxt = tile + gridDim.x;
+    if (nxt < ntiles) fetch_x(nxt, tid);
+    // the epilogue's residual / accumulator rows, issued before the output staging
     constexpr int BM = R::BM;
-    constexpr int IT = (BM * CH + NT - 1) / NT;
+    constexpr int IE = (BM * CH + NT - 1) / NT;
     bf16_t* ob = out + (long)b * T * C;
     const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
-    short8 xr[IT], ar[IT];
+    short8 xr[IE], ar[IE];
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int it = 0; it < IE; ++it) {
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
       const int t = t0 + j;
       if (j < BM && t < T) {
@@ -331,7 +333,24 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
       }
     }
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
+    for (int r = 0; r < R::MAXRB; ++r) {
+      const int rb = wr + R::WR * r;
+      if (rb < R::NRB2) {
+#pragma unroll
+        for (int s = 0; s < R::NSW; ++s) {
+          const int ch = (wc * R::NSW + s) * 16 + col;
+          const float bias = bias2[s];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + ch] = acc[r][s][i] + bias;
+        }
+      }
+    }
+    lds_barrier();
+    rb_stamp<PROF>(st, 5);
+
+    // 4. + residual (+ MRF accumulator), scale, coalesced 16-B stores
+#pragma unroll
+    for (int it = 0; it < IE; ++it) {
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
       const int t = t0 + j;
       if (j >= BM || t >= T) continue;
@@ -341,22 +360,23 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
       short8 o;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float v = ov[i] + bf2f((bf16_t)xr[it][i]);
-        if (ab) v += bf2f((bf16_t)ar[it][i]);
-        v *= out_scale;
-        if (post_lrelu) v = lrelu(v, slope);  // the next upsampling conv's pre-activation
-        o[i] = (short)f2bf(v);
+        float y = ov[i] + bf2f((bf16_t)xr[it][i]);
+        if (ab) y += bf2f((bf16_t)ar[it][i]);
+        y *= out_scale;
+        if (post_lrelu) y = lrelu(y, slope);  // the next upsampling conv's pre-activation
+        o[i] = (short)f2bf(y);
       }
       *reinterpret_cast<short8*>(ob + (long)t * C + c0) = o;
     }
-  }
-  if constexpr (PROF) {
-    rb_stamp<PROF>(st, 6);
-    if (threadIdx.x == 0) {
+    if constexpr (PROF) {
+      rb_stamp<PROF>(st, 6);
+      if (threadIdx.x == 0) {
 #pragma unroll
-      for (int i = 0; i < 7; ++i) prof[(long)blockIdx.x * 8 + i] = st[i];
-      prof[(long)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+        for (int i = 0; i < 7; ++i) prof[(long)tile * 8 + i] = st[i];
+        prof[(long)tile * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+      }
     }
+    lds_barrier();  // every os read done before the next tile's x lands in the same LDS
   }
 }
 
@@ -371,9 +391,21 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
     allow_lds(resblock_layer_kernel<C, K>, R::LDS);
     lds_set = true;
   }
+  static int resident = 0;  // co-resident blocks on the whole device (LDS / register limited)
+  if (!resident) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resblock_layer_kernel<C, K>, R::NT, R::LDS) !=
+            hipSuccess || per_cu <= 0)
+      per_cu = 1;
+    resident = cus * per_cu;
+  }
   const int tiles = (T + R::BM - 1) / R::BM;
-  hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
-                     acc_in, out, T, tiles, d, slope, out_scale, post_lrelu);
+  const long ntiles = (long)B * tiles;
+  const int grid = (int)(ntiles < resident ? ntiles : resident);
+  hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3(grid), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
+                     acc_in, out, T, tiles, (int)ntiles, d, slope, out_scale, post_lrelu);
   return (int)hipGetLastError();
 }
 
@@ -827,17 +859,19 @@ SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16
 // x / out / acc_in [B, T, C] bf16 (acc_in may alias out, or be null); w1 / w2 bf16 [C][K][C] (the
 // implicit-GEMM forward image); b1 / b2 fp32 [C].  C in {32, 64, 128}, K in {3, 7, 11}, 1 <= d <= 5.
 // Diagnostic: the per-layer kernel with phase stamps (see rb_stamp); prof >= 8 * B * ceil(T / BM) words.
+// grid > 0 caps the workgroup count (the persistent tile loop of the production launch); 0 = one tile per block.
 SSAMD_API int ssamd_resblock_layer_prof(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
                                         const float* b2, const bf16_t* acc_in, bf16_t* out, int B, int T, int C, int K,
                                         int d, float slope, float out_scale, int post_lrelu, unsigned long long* prof,
-                                        hipStream_t s) {
+                                        int grid, hipStream_t s) {
 #define RBP_CASE(CC, KK)                                                                                      \
   if (C == CC && K == KK) {                                                                                   \
     using R = RB<CC, KK>;                                                                                     \
     allow_lds(resblock_layer_kernel<CC, KK, true>, R::LDS);                                                   \
     const int tiles = (T + R::BM - 1) / R::BM;                                                                \
-    hipLaunchKernelGGL((resblock_layer_kernel<CC, KK, true>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, \
-                       w1, b1, w2, b2, acc_in, out, T, tiles, d, slope, out_scale, post_lrelu, prof);          \
+    const int g = grid > 0 && grid < B * tiles ? grid : B * tiles;                                            \
+    hipLaunchKernelGGL((resblock_layer_kernel<CC, KK, true>), dim3(g), dim3(R::NT), R::LDS, s, x,              \
+                       w1, b1, w2, b2, acc_in, out, T, tiles, B * tiles, d, slope, out_scale, post_lrelu, prof); \
     return (int)hipGetLastError();                                                                            \
   }
   if (d < 1 || d > MAXD) return -2;

@@ -2116,7 +2116,7 @@ def token_bank(E, Wk, Wv, n_head):
 
 
 # ------------------------------------------------------------------------ vocoder (inference)
-_SIGS.update({"ssamd_resblock_layer_prof": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P, P],
+_SIGS.update({"ssamd_resblock_layer_prof": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P, I, P],
               "ssamd_resblock_layer_tile": [I, I]})
 _SIGS.update({"ssamd_resblock_layer": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P],
               "ssamd_conv_gemm_ex": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, F, I, P]})

@@ -1214,6 +1214,40 @@ def test_resblock_layer_fused(C, K, d, T):
         assert _rel(out, expect) < 1e-2
 
 
+@pytest.mark.parametrize("C,K,d,B,T", [(128, 11, 5, 6, 11000), (128, 7, 3, 5, 13000), (64, 11, 3, 8, 8200)])
+def test_resblock_layer_persistent_many_tiles(C, K, d, B, T):
+    """The per-layer kernel loops over tiles when they outnumber the resident blocks (256 / 512 here), fetching
+    the next tile's x under the current epilogue: bitwise equal to the one-tile-per-block launch (the phase-stamp
+    instantiation, full grid), and vs fp32 torch, with the in-place MRF accumulator."""
+    from speakingstyle_amd.models.hifigan import LRELU_SLOPE
+
+    torch.manual_seed(25)
+    BM = hip.lib().ssamd_resblock_layer_tile(C, K)
+    tiles = (T + BM - 1) // BM
+    assert B * tiles > 512
+    c1 = torch.nn.Conv1d(C, C, K, dilation=d, padding=d * (K - 1) // 2).to(DEV)
+    c2 = torch.nn.Conv1d(C, C, K, padding=(K - 1) // 2).to(DEV)
+    for c in (c1, c2):
+        c.weight.data.normal_(0, 0.5 / math.sqrt(C * K))
+        c.weight.data = c.weight.data.to(torch.bfloat16).float()
+    x = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    acc = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    acc0 = acc.clone()
+    with torch.no_grad():
+        xr = x.float().transpose(1, 2)
+        yr = (xr + c2(F.leaky_relu(c1(F.leaky_relu(xr, LRELU_SLOPE)), LRELU_SLOPE))).transpose(1, 2)
+        out = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE, acc=acc, out_scale=1 / 3)
+        assert _rel(out, (acc0.float() + yr) * (1 / 3)) < 1e-2
+        one = acc0.clone()
+        prof = torch.zeros(B * tiles * 8, dtype=torch.int64, device=DEV)
+        w1, w2 = hip.weight_fwd(c1.weight), hip.weight_fwd(c2.weight)
+        b1, b2 = c1.bias.detach().float().contiguous(), c2.bias.detach().float().contiguous()
+        hip._check(hip.lib().ssamd_resblock_layer_prof(
+            hip._ptr(x), hip._ptr(w1), hip._ptr(b1), hip._ptr(w2), hip._ptr(b2), hip._ptr(one), hip._ptr(one),
+            B, T, C, K, d, LRELU_SLOPE, 1 / 3, 0, hip._ptr(prof), 0, hip._stream()), "resblock prof")
+        assert torch.equal(out, one)
+
+
 @pytest.mark.parametrize("C,K,T", [(32, 3, 1500), (32, 7, 700), (32, 11, 1100), (32, 11, 9), (64, 3, 900),
                                    (64, 3, 5), (64, 7, 1000), (128, 3, 700), (128, 3, 40)])
 def test_resblock_whole_block_fused(C, K, T):

@@ -1,7 +1,8 @@
 """Phase timing of the fused HiFi-GAN ResBlock layer kernel (csrc/k_vocoder.hip resblock_layer_kernel, the
 diagnostic PROF instantiation): per workgroup s_memtime stamps at the phase boundaries -- x staged (global ->
 lrelu -> LDS), conv1, t1 epilogue, conv2, output-tile staging, epilogue (residual / acc loads, stores).
-Prints median cycles per phase and the share of the block's lifetime (GPU box).
+Prints median cycles per phase and the share of a tile's time, for one tile per workgroup and for the
+persistent grid of the production launch (GPU box).
 Usage: python tools/exp_rb_phases.py"""
 import json
 import os
@@ -28,14 +29,17 @@ for C, K, d, acc in ((128, 11, 1, False), (128, 11, 5, True), (128, 7, 3, False)
     prof = torch.zeros(B * tiles * 8, dtype=torch.int64, device="cuda")
 
     def run(p):
+        # p = 0: production launch; 1: stamped, one tile per workgroup; 2: stamped, the production launch's
+        # persistent grid (resident workgroups)
         f = hip.lib().ssamd_resblock_layer_prof if p else hip.lib().ssamd_resblock_layer
         args = [hip._ptr(x), hip._ptr(w1), hip._ptr(b1), hip._ptr(w2), hip._ptr(b2), hip._ptr(a),
                 hip._ptr(out if a is None else a), B, T, C, K, d, 0.1, 1.0, 0]
         if p:
-            args.append(hip._ptr(prof))
+            args += [hip._ptr(prof), 0 if p == 1 else (256 if C == 128 else 512)]
         hip._check(f(*args, hip._stream()), "resblock")
 
-    for p in (False, True):
+    ms = {}
+    for p in (0, 1, 2):
         for _ in range(3):
             run(p)
         torch.cuda.synchronize()
@@ -45,15 +49,16 @@ for C, K, d, acc in ((128, 11, 1, False), (128, 11, 5, True), (128, 7, 3, False)
             run(p)
         e1.record()
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 5
-        if not p:
-            ms_plain = ms
-    st = prof.view(-1, 8).cpu().double()
-    d_ = st[:, 1:7] - st[:, 0:6]
-    tot = (st[:, 6] - st[:, 0])
-    med = d_.median(0).values
-    rec = {"C": C, "K": K, "d": d, "acc": acc, "rows": B * T, "blocks": B * tiles, "us_plain": round(ms_plain * 1000, 1),
-           "us_prof": round(ms * 1000, 1), "block_cycles_med": int(tot.median()),
-           "phase_cycles_med": {k: int(v) for k, v in zip(PH, med.tolist())},
-           "phase_share": {k: round(float(v) / float(med.sum()), 3) for k, v in zip(PH, med.tolist())}}
-    print(json.dumps(rec), flush=True)
+        ms[p] = e0.elapsed_time(e1) / 5
+        if p == 0:
+            continue
+        st = prof.view(-1, 8).cpu().double()
+        d_ = st[:, 1:7] - st[:, 0:6]
+        tot = (st[:, 6] - st[:, 0])
+        med = d_.median(0).values
+        rec = {"C": C, "K": K, "d": d, "acc": acc, "grid": "one_tile_per_block" if p == 1 else "persistent",
+               "rows": B * T, "tiles": B * tiles, "us_plain": round(ms[0] * 1000, 1),
+               "us_prof": round(ms[p] * 1000, 1), "tile_cycles_med": int(tot.median()),
+               "phase_cycles_med": {k: int(v) for k, v in zip(PH, med.tolist())},
+               "phase_share": {k: round(float(v) / float(med.sum()), 3) for k, v in zip(PH, med.tolist())}}
+        print(json.dumps(rec), flush=True)
