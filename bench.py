@@ -190,6 +190,8 @@ def run(args):
         rec["host_lead_ms"] = tr["host_lead_ms"]
     if tr.get("host_tail_ms"):
         rec["host_tail_ms"] = tr["host_tail_ms"]
+    if tr.get("tail_events_ms"):
+        rec["tail_events_ms"] = tr["tail_events_ms"]
     if tr.get("graphs"):
         rec["graphs"] = tr["graphs"]
     if tr.get("phases"):

@@ -182,6 +182,43 @@ def train_phase(args, rank, world, device):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev0.record()
         evs, hts = [], []
+    # diagnostics: device events at the step tail, in stream order -- after the joined backward + gradient
+    # finalisation, before / after the clip + Adam launch: GPU time of the tail incl. any idle, free of the
+    # host slowdown a kernel tracer adds (its traces show a ~0.8 ms step-end bubble)
+    tail_ev = cuda and experimental.get("tail_events")
+    if tail_ev:
+        tail_recs = []
+        fin0, opt0 = trainer.opt.arena.finalize_grads, trainer.opt.step_and_update_lr
+
+        def _ev():
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+
+        from .ops import hip as _hip
+
+        join0 = _hip.join_side_streams
+
+        def join(*a, **k):
+            tail_recs.append({"bwd": _ev()})  # backward() returned: every main-stream backward kernel enqueued
+            r = join0(*a, **k)
+            tail_recs[-1]["joined"] = _ev()
+            return r
+
+        def fin(*a, **k):
+            r = fin0(*a, **k)
+            tail_recs[-1]["fin"] = _ev()
+            return r
+
+        _hip.join_side_streams = join
+
+        def opt(*a, **k):
+            tail_recs[-1]["opt0"] = _ev()
+            r = opt0(*a, **k)
+            tail_recs[-1]["opt1"] = _ev()
+            return r
+
+        trainer.opt.arena.finalize_grads, trainer.opt.step_and_update_lr = fin, opt
     for i in range(args.steps):
         h0 = time.perf_counter()
         frames += step(warm + i)
@@ -210,6 +247,18 @@ def train_phase(args, rank, world, device):
     if lead:
         # GPU finish time of step i minus the host time its enqueue ended (both from t0; ev0 recorded ~t0)
         info["host_lead_ms"] = [round(ev0.elapsed_time(e) - 1e3 * h, 2) for e, h in zip(evs, hts)]
+    if tail_ev:
+        trainer.opt.arena.finalize_grads, trainer.opt.step_and_update_lr = fin0, opt0
+        _hip.join_side_streams = join0
+        rec = [r for r in tail_recs if "opt1" in r]
+        mean = lambda xs: round(sum(xs) / max(1, len(xs)), 3)  # noqa: E731
+        info["tail_events_ms"] = {
+            "bwd_return->joined": mean([r["bwd"].elapsed_time(r["joined"]) for r in rec]),
+            "joined->finalized": mean([r["joined"].elapsed_time(r["fin"]) for r in rec]),
+            "finalized->opt_launch": mean([r["fin"].elapsed_time(r["opt0"]) for r in rec]),
+            "opt_launch->opt_done": mean([r["opt0"].elapsed_time(r["opt1"]) for r in rec]),
+            "step (opt_done->opt_done)": mean([a["opt1"].elapsed_time(b["opt1"]) for a, b in zip(rec, rec[1:])]),
+        }
     tail = trainer.host_tail_summary()
     if tail is not None:
         info["host_tail_ms"] = tail

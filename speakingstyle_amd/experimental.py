@@ -87,6 +87,7 @@ KNOBS: Dict[str, tuple] = {
     "phase_timing": (False, _bool, "per-phase host/device step times (Perf/phase_* scalars)"),
     "host_tail": (False, _bool, "host timestamps of the step tail (backward return .. optimizer launch)"),
     "host_lead": (False, _bool, "bench: how far the host enqueue runs ahead of the GPU per step"),
+    "tail_events": (False, _bool, "bench: device-side event timing of the step tail (joined backward .. Adam)"),
     "fail_rank": (None, int, "fault injection: this rank raises in its second timed bench step"),
 }
 
