@@ -2134,6 +2134,8 @@ def resblock_layer(x, c1, c2, d, slope, acc=None, out_scale=1.0, post_lrelu=Fals
     w1, w2 = weight_fwd(c1.weight), weight_fwd(c2.weight)
     b1 = c1.bias.detach().float().contiguous()
     b2 = c2.bias.detach().float().contiguous()
+    for t, nm in ((w1, "resblock.w1"), (w2, "resblock.w2"), (b1, "resblock.b1"), (b2, "resblock.b2")):
+        _need(t, t.dtype, nm)  # a host tensor here (e.g. a weight-norm .weight left on the CPU) would fault the GPU
     if acc is not None:
         _need(acc, torch.bfloat16, "resblock.acc")
         assert acc.shape == x.shape and acc.data_ptr() != x.data_ptr(), "acc must be a separate [B, T, C] buffer"
@@ -2169,6 +2171,8 @@ def resblock_fused(x, convs1, convs2, dilations, slope, acc=None, out_scale=1.0,
             assert tuple(c.weight.shape) == (C, C, K)
             ws.append(weight_fwd(c.weight))
             bs.append(c.bias.detach().float().contiguous())
+            _need(ws[-1], torch.bfloat16, "resblock.w")  # host weights (weight-norm .weight on the CPU) would fault
+            _need(bs[-1], torch.float32, "resblock.b")
     if acc is not None:
         _need(acc, torch.bfloat16, "resblock.acc")
         assert acc.shape == x.shape and acc.data_ptr() != x.data_ptr(), "acc must be a separate [B, T, C] buffer"
