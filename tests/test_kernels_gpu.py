@@ -1248,6 +1248,21 @@ def test_resblock_layer_persistent_many_tiles(C, K, d, B, T):
         assert torch.equal(out, one)
 
 
+def test_resblock_rejects_host_weights():
+    """A ResBlock1 moved with .cuda() while weight norm is still applied keeps its computed .weight on the host:
+    the wrappers must raise before any launch (a host address in the kernel faults the GPU)."""
+    from speakingstyle_amd.models import hifigan as H
+
+    blk = H.ResBlock1(64, 7, (1, 3, 5)).to(DEV)
+    assert not blk.convs1[0].weight.is_cuda
+    x = torch.randn(1, 64, 64, device=DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        with pytest.raises(ValueError, match="GPU"):
+            hip.resblock_fused(x, blk.convs1, blk.convs2, blk.dilation, H.LRELU_SLOPE)
+        with pytest.raises(ValueError, match="GPU"):
+            hip.resblock_layer(x, blk.convs1[0], blk.convs2[0], 1, H.LRELU_SLOPE)
+
+
 @pytest.mark.parametrize("C,K,T", [(32, 3, 1500), (32, 7, 700), (32, 11, 1100), (32, 11, 9), (64, 3, 900),
                                    (64, 3, 5), (64, 7, 1000), (128, 3, 700), (128, 3, 40)])
 def test_resblock_whole_block_fused(C, K, T):
