@@ -410,6 +410,136 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Square 3-tap conv (pad 1, dilation 1, N = Cin = C), y = conv(x) + b: the HiFi-GAN upsamplers whose
+// 3-tap implicit-GEMM form (convT_as_conv3: N = stride * Cout) is square -- ups 3 (128 -> 2 x 64) and
+// ups 4 (64 -> 2 x 32) of V1 -- over 64x / 128x the mel rate.  As a generic GEMM they are short-K
+// (K = 3C = 384 / 192) tiles of N <= 128 on a 256 x 128 tile (13.9 % MFMA busy, 4.6 % of synthesis,
+// profiles/r5_vocoder_pmc_summary_persistent.txt).  Here the resblock layer machinery does it: the x
+// tile (128 + 2 rows) is staged once and read at the three tap offsets (no per-tap re-read of A),
+// weights stream through the LDS-DMA ring (conv_tile), + bias into an fp32 LDS tile, coalesced 16-B
+// stores; persistent over tiles with the next tile's x fetched under the epilogue.
+template <int C>
+struct C3 {
+  using R = RB<C, 3>;
+  static constexpr int BM = R::R1P;                               // output rows per tile (all row blocks)
+  static constexpr int RXS = BM + 2;                              // staged x rows (1-row halo per side)
+  static constexpr int XS_BYTES = (RXS * R::LDC * 2 + 15) / 16 * 16;
+  static constexpr int OS_BYTES = BM * R::OSP * 4;
+  static constexpr int LDS = XS_BYTES + OS_BYTES + 3 * R::SLOT;
+  static_assert(LDS <= 160 * 1024, "conv3 tile");
+};
+
+template <int C>
+__global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                                   const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                                   int T, int tiles, int ntiles) {
+  using R = RB<C, 3>;
+  using G = C3<C>;
+  constexpr int NT = R::NT;
+  constexpr int CH = C / 8;
+  constexpr int BM = G::BM;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(lds);                  // [RXS][LDC]: x rows t0 - 1 ..
+  float* os = reinterpret_cast<float*>(lds + G::XS_BYTES);       // [BM][OSP]
+  char* bring = reinterpret_cast<char*>(lds + G::XS_BYTES + G::OS_BYTES);
+  const int tid0 = threadIdx.x;
+  float bv[R::NSW];
+#pragma unroll
+  for (int s = 0; s < R::NSW; ++s) bv[s] = bias[((tid0 >> 6) / R::WR * R::NSW + s) * 16 + (tid0 & 15)];
+  constexpr int IX = (G::RXS * CH + NT - 1) / NT;
+  short8 v[IX];
+  auto fetch_x = [&](int tile, int tid) {
+    const int b = tile / tiles, t0 = (tile - b * tiles) * BM;
+    const bf16_t* xb = x + (long)b * T * C;
+#pragma unroll
+    for (int it = 0; it < IX; ++it) {
+      const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
+      const int t = t0 - 1 + r;
+      if (r < G::RXS && t >= 0 && t < T) {
+        v[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[it][i] = 0;
+      }
+    }
+  };
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  fetch_x(blockIdx.x, tid0);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int tid = tid0;  // opaque per tile: keeps the unrolled conv's per-lane address terms inside the loop
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, col = lane & 15, quad = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave % R::WR, wc = wave / R::WR;
+    const int b = tile / tiles, t0 = (tile - b * tiles) * BM;
+#pragma unroll
+    for (int it = 0; it < IX; ++it) {
+      const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
+      if (r < G::RXS) *reinterpret_cast<short8*>(xs + r * R::LDC + c0) = v[it];
+    }
+    __syncthreads();
+    float4v acc[R::MAXRB][R::NSW];
+    conv_tile<C, 3>(xs, 1, w, bring, R::NRB1, wave, tid, acc);
+    const int nxt = tile + gridDim.x;
+    if (nxt < ntiles) fetch_x(nxt, tid);  // no DMA of conv_tile in flight any more
+#pragma unroll
+    for (int r = 0; r < R::MAXRB; ++r) {
+      const int rb = wr + R::WR * r;
+#pragma unroll
+      for (int s = 0; s < R::NSW; ++s) {
+        const int ch = (wc * R::NSW + s) * 16 + col;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + ch] = acc[r][s][i] + bv[s];
+      }
+    }
+    lds_barrier();
+    constexpr int IE = (BM * CH + NT - 1) / NT;
+    bf16_t* ob = out + (long)b * T * C;
+#pragma unroll
+    for (int it = 0; it < IE; ++it) {
+      const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+      const int t = t0 + j;
+      if (j >= BM || t >= T) continue;
+      const float4 o0 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0);
+      const float4 o1 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0 + 4);
+      const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+      short8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (short)f2bf(ov[i]);
+      *reinterpret_cast<short8*>(ob + (long)t * C + c0) = o;
+    }
+    lds_barrier();  // os read and xs / ring free before the next tile writes them
+  }
+}
+
+template <int C>
+int launch_c3(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* out, int B, int T, hipStream_t s) {
+  using G = C3<C>;
+  static int resident = 0;
+  if (!resident) {
+    allow_lds(conv3_sq_kernel<C>, G::LDS);
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv3_sq_kernel<C>, RB<C, 3>::NT, G::LDS) != hipSuccess ||
+        per_cu <= 0)
+      per_cu = 1;
+    resident = cus * per_cu;
+  }
+  const int tiles = (T + G::BM - 1) / G::BM;
+  const long ntiles = (long)B * tiles;
+  if (ntiles > 0x7fffffffL) return -2;
+  const int grid = (int)(ntiles < resident ? ntiles : resident);
+  hipLaunchKernelGGL((conv3_sq_kernel<C>), dim3(grid), dim3(RB<C, 3>::NT), G::LDS, s, x, w, bias, out, T, tiles,
+                     (int)ntiles);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Whole ResBlock1 in one kernel (reference hifigan/models.py:20-44, the three (c1_d, c2) layer
 // pairs, dilations d0 / d1 / d2):
 //
@@ -877,6 +1007,17 @@ SSAMD_API int ssamd_resblock_layer_prof(const bf16_t* x, const bf16_t* w1, const
   if (d < 1 || d > MAXD) return -2;
   RBP_CASE(128, 11) RBP_CASE(128, 7) RBP_CASE(64, 11)
 #undef RBP_CASE
+  return -2;
+}
+
+// Square 3-tap conv (pad 1): x / out [B, T, C] bf16 (out must not alias x), w bf16 [C][3][C] (implicit-GEMM
+// forward image), bias fp32 [C].  C in {64, 128}.
+SSAMD_API int ssamd_conv3_sq(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* out, int B, int T, int C,
+                             hipStream_t s) {
+  if ((long)B * T == 0) return 0;
+  if (x == out || !x || !w || !bias || !out) return -2;
+  if (C == 128) return launch_c3<128>(x, w, bias, out, B, T, s);
+  if (C == 64) return launch_c3<64>(x, w, bias, out, B, T, s);
   return -2;
 }
 

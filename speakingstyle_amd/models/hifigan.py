@@ -413,7 +413,9 @@ class Generator(nn.Module):
                 y = conv_transpose_polyphase(x, _w(up), up.bias, s, up.padding[0])
             else:
                 wu, wimg, bt = img
-                if fused:
+                if fused and _CONV3_SQ[0] and bt is not None and wu.shape[0] == wu.shape[1] in (64, 128):
+                    y = hip.conv3_sq(x, wimg, bt)  # N = stride * Cout = Cin: the staged-tile kernel
+                elif fused:
                     y = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg)
                 else:
                     y, x_act = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, dual_lrelu=True)
@@ -442,6 +444,10 @@ class Generator(nn.Module):
         return self
 
     remove_weight_norm = fold_weight_norm
+
+
+# square upsamplers (N = stride * Cout = Cin in {64, 128}) on ``hip.conv3_sq`` instead of the generic GEMM
+_CONV3_SQ = [True]
 
 
 def ref_conv_post(x, w, b):

@@ -2116,6 +2116,7 @@ def token_bank(E, Wk, Wv, n_head):
 
 
 # ------------------------------------------------------------------------ vocoder (inference)
+_SIGS.update({"ssamd_conv3_sq": [P, P, P, P, I, I, I, P]})
 _SIGS.update({"ssamd_resblock_layer_prof": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P, I, P],
               "ssamd_resblock_layer_tile": [I, I]})
 _SIGS.update({"ssamd_resblock_layer": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P],
@@ -2155,6 +2156,20 @@ _SIGS.update({"ssamd_resblock_fused": [P] * 15 + [I, I, I, I, I, I, I, F, F, I, 
 def resblock_fusable(C: int, K: int) -> bool:
     """Geometry with a whole-ResBlock kernel instance (``ssamd_resblock_fused``)."""
     return bool(lib().ssamd_resblock_fusable(int(C), int(K)))
+
+
+def conv3_sq(x, wimg, bias):
+    """Square 3-tap conv (pad 1), channel-last bf16, no autograd: ``y = conv(x) + bias`` with ``wimg`` the bf16
+    [C][3][C] implicit-GEMM image (csrc/k_vocoder.hip ``conv3_sq_kernel``: the upsamplers whose
+    ``convT_as_conv3`` form has N = stride * Cout = Cin).  C in {64, 128}."""
+    _need(x, torch.bfloat16, "conv3_sq.x")
+    _need(wimg, torch.bfloat16, "conv3_sq.w")
+    _need(bias, torch.float32, "conv3_sq.bias")
+    B, T, C = x.shape
+    assert tuple(wimg.shape) == (C, 3, C) and bias.numel() == C, "conv3_sq: weight / bias shape"
+    out = torch.empty_like(x)
+    _check(lib().ssamd_conv3_sq(_ptr(x), _ptr(wimg), _ptr(bias), _ptr(out), B, T, C, _stream()), "ssamd_conv3_sq")
+    return out
 
 
 def resblock_fused(x, convs1, convs2, dilations, slope, acc=None, out_scale=1.0, post_lrelu=False):

@@ -1248,6 +1248,24 @@ def test_resblock_layer_persistent_many_tiles(C, K, d, B, T):
         assert torch.equal(out, one)
 
 
+@pytest.mark.parametrize("C,B,T", [(128, 3, 1000), (64, 3, 1000), (128, 2, 5), (64, 1, 129), (128, 4, 40000),
+                                   (64, 4, 40000)])
+def test_conv3_sq(C, B, T):
+    """Square 3-tap conv kernel of the upsamplers (N = stride * Cout = Cin) vs fp32 torch conv1d (pad 1) and vs the
+    generic implicit-GEMM path; the large cases loop the persistent grid over more tiles than resident blocks."""
+    torch.manual_seed(26)
+    w = (torch.randn(C, C, 3, device=DEV) / math.sqrt(3 * C)).to(torch.bfloat16).float()
+    b = torch.randn(C, device=DEV) * 0.1
+    x = torch.randn(B, T, C, device=DEV).to(torch.bfloat16)
+    wimg = w.permute(0, 2, 1).to(torch.bfloat16).contiguous()
+    with torch.no_grad():
+        y = hip.conv3_sq(x, wimg, b)
+        yr = F.conv1d(x.float().transpose(1, 2), w, b, padding=1).transpose(1, 2)
+        assert _rel(y, yr) < 1e-2
+        yg = hip.conv1d_infer(x, w, b, 1, 1, None, wimg=wimg)
+        assert _rel(y, yg) < 1e-2
+
+
 def test_resblock_rejects_host_weights():
     """A ResBlock1 moved with .cuda() while weight norm is still applied keeps its computed .weight on the host:
     the wrappers must raise before any launch (a host address in the kernel faults the GPU)."""
