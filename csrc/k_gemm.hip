@@ -45,6 +45,10 @@ struct ConvGeom {
   // XCD's contiguous range of remapped ids covers nN / ngrp N tiles of more M tiles (its B slice
   // stays L2-resident instead of the whole weight image streaming through every XCD's L2)
   int ngrp;
+  // 3-tap ConvTranspose form (convT_as_conv3 with K = 2s, pad = s/2; 0 = off): output columns below ksplit are
+  // the phases r < s/2, which read taps {0, 1} only, the rest taps {1, 2} -- a 256-column big64 tile (never
+  // straddling ksplit) skips the k slabs of its all-zero tap: 2/3 of the MFMA work, bitwise the same result
+  int ksplit;
 };
 
 // (tm, tn) of remapped block id T (bijective over nM * nN; ngrp must divide nN)
@@ -993,6 +997,11 @@ __device__ __forceinline__ void big64_tile(const bf16_t* __restrict__ X, const b
     kt0 = blockIdx.y * per;
     nk = min(nk_all, kt0 + per);
     Yv = reinterpret_cast<float*>(Yv) + (long)blockIdx.y * g.M * ldy;
+  }
+  if (g.ksplit > 0 && gridDim.y == 1) {  // ConvTranspose 3-tap form: skip the tile's all-zero tap (see ConvGeom)
+    const int kc = g.Cin / 64;
+    if (n0 < g.ksplit) nk = 2 * kc;
+    else kt0 = kc;
   }
   if constexpr (STG) {
     // Staggered 8-phase main loop (MI355X: one wave of each group per SIMD, so one wave's MFMA cluster runs
@@ -2553,6 +2562,7 @@ static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N
   g.rinfo = nullptr;
   g.cu = nullptr;
   g.nseq = 0;
+  g.ksplit = 0;
   g.prio = g_gemm_prio < 0 ? (N >= 1024 && ks > 1) : g_gemm_prio;
   const int nN = (N + 255) / 256;
   g.ngrp = (g_gemm_ngrp > 1 && nN % g_gemm_ngrp == 0) ? g_gemm_ngrp : 1;
@@ -2562,11 +2572,12 @@ static ConvGeom make_geom(int B, int L, int Cin, int ks, int dil, int pad, int N
 static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* aux,
                           const bf16_t* resid, const int64_t* lens, void* Y, int out_f32, int B, int L, int Cin,
                           int ks, int dil, int pad, int N, int act, int ldy, const int* rinfo, EpiX ex, hipStream_t s,
-                          bool bnh = false) {
+                          bool bnh = false, int ksplit = 0) {
   if (Cin % 8 != 0) return -2;
   if ((long)B * L == 0 || N == 0) return 0;
   ConvGeom g = make_geom(B, L, Cin, ks, dil, pad, N);
   g.rinfo = reinterpret_cast<const int2*>(rinfo);
+  if (ksplit > 0 && ks == 3 && Cin % 64 == 0 && ksplit % 256 == 0 && ksplit < N) g.ksplit = ksplit;
   const int nwg = ((g.M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const size_t lds = (size_t)BM * CSTRIDE * 4;  // >= 2 stages x (A+B) = 64 KiB
   static bool lds_set = false;
@@ -2797,6 +2808,21 @@ SSAMD_API int ssamd_conv_gemm_ex(const bf16_t* X, const bf16_t* W, const float* 
   ex.scale = scale;
   ex.post_act = post_act;
   return conv_gemm_impl(X, W, bias, nullptr, resid, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, nullptr, ex, s);
+}
+
+// ssamd_conv_gemm_ex for the 3-tap ConvTranspose form (hifigan convT_as_conv3): ksplit = (stride / 2) * Cout,
+// the first output column of the phases that read taps {1, 2} (see ConvGeom::ksplit); ignored unless ks == 3,
+// Cin % 64 == 0 and ksplit % 256 == 0 (the weights' zero tap is then skipped per 256-column tile).
+SSAMD_API int ssamd_conv_gemm_ex2(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* resid, void* Y,
+                                  int B, int L, int Cin, int ks, int dil, int pad, int N, int act, const bf16_t* acc,
+                                  bf16_t* y2, float scale, int post_act, int ksplit, hipStream_t s) {
+  EpiX ex{};
+  ex.acc = acc;
+  ex.y2 = y2;
+  ex.scale = scale;
+  ex.post_act = post_act;
+  return conv_gemm_impl(X, W, bias, nullptr, resid, nullptr, Y, 0, B, L, Cin, ks, dil, pad, N, act, N, nullptr, ex, s,
+                        false, ksplit);
 }
 
 // Data gradient of a conv whose input came out of BatchNorm (+act, dropout): Y = dz (see EpiX.bn_*) and the

@@ -415,10 +415,15 @@ class Generator(nn.Module):
                 wu, wimg, bt = img
                 if fused and _CONV3_SQ[0] and bt is not None and wu.shape[0] == wu.shape[1] in (64, 128):
                     y = hip.conv3_sq(x, wimg, bt)  # N = stride * Cout = Cin: the staged-tile kernel
-                elif fused:
-                    y = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg)
                 else:
-                    y, x_act = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, dual_lrelu=True)
+                    # the 3-tap form's zero tap per phase half (K = 2s, pad = s/2): skipped per 256-column tile
+                    cout = wu.shape[0] // s
+                    ks_ = (s // 2) * cout if (_CONVT_KSPLIT[0] and up.kernel_size[0] == 2 * s
+                                              and up.padding[0] * 2 == s) else 0
+                    if fused:
+                        y = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, ksplit=ks_)
+                    else:
+                        y, x_act = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, dual_lrelu=True, ksplit=ks_)
                 y = y.view(B, T * s, -1)
                 if x_act is not None:
                     x_act = x_act.view(B, T * s, -1)
@@ -448,6 +453,8 @@ class Generator(nn.Module):
 
 # square upsamplers (N = stride * Cout = Cin in {64, 128}) on ``hip.conv3_sq`` instead of the generic GEMM
 _CONV3_SQ = [True]
+# the other upsamplers' 3-tap GEMM skips each 256-column tile's all-zero tap (ConvGeom::ksplit in csrc/k_gemm.hip)
+_CONVT_KSPLIT = [True]
 
 
 def ref_conv_post(x, w, b):

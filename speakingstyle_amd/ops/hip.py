@@ -2120,7 +2120,8 @@ _SIGS.update({"ssamd_conv3_sq": [P, P, P, P, I, I, I, P]})
 _SIGS.update({"ssamd_resblock_layer_prof": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P, I, P],
               "ssamd_resblock_layer_tile": [I, I]})
 _SIGS.update({"ssamd_resblock_layer": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P],
-              "ssamd_conv_gemm_ex": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, F, I, P]})
+              "ssamd_conv_gemm_ex": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, F, I, P],
+              "ssamd_conv_gemm_ex2": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, F, I, I, P]})
 
 
 def resblock_layer(x, c1, c2, d, slope, acc=None, out_scale=1.0, post_lrelu=False):
@@ -2203,18 +2204,20 @@ def resblock_fused(x, convs1, convs2, dilations, slope, acc=None, out_scale=1.0,
 
 
 def conv1d_infer(x, w, b, pad, dil, act=None, resid=None, acc=None, scale=1.0, post_act=None, dual_lrelu=False,
-                 wimg=None):
+                 wimg=None, ksplit=0):
     """Inference conv (no autograd), channel-last bf16, everything in the GEMM epilogue:
     ``v = act(conv(x) + b) [+ resid]``; ``v = (v [+ acc]) * scale``; returns ``post_act(v)``
     (and ``lrelu(v)`` as a second output when ``dual_lrelu``).  ``acc`` may be the output
     buffer itself (in-place accumulation; it is then returned).  ``wimg``: a prepared bf16
-    [N][ks][Cin] operand image (with ``w`` the fp32 [N, Cin, ks] it came from, for shapes)."""
+    [N][ks][Cin] operand image (with ``w`` the fp32 [N, Cin, ks] it came from, for shapes).  ``ksplit``: the
+    weights are the 3-tap ConvTranspose form (hifigan ``convT_as_conv3``) and output columns >= ksplit read
+    taps {1, 2} only, the others taps {0, 1} -- each 256-column tile skips its all-zero tap."""
     B, L, Cin = x.shape
     ks = 1 if w.dim() == 2 else w.shape[2]
     N = w.shape[0]
     bf = None if b is None else b.detach().float().contiguous()
     wi = weight_fwd(w) if wimg is None else wimg
-    if acc is None and scale == 1.0 and post_act is None and not dual_lrelu:
+    if acc is None and scale == 1.0 and post_act is None and not dual_lrelu and not ksplit:
         return conv_gemm_raw(x.contiguous(), wi, bf, B, L, Cin, ks, dil, pad, N, _ACT[act],
                              resid=None if resid is None else resid.contiguous())
     xc = x.contiguous()
@@ -2229,8 +2232,13 @@ def conv1d_infer(x, w, b, pad, dil, act=None, resid=None, acc=None, scale=1.0, p
             assert t.numel() == B * L * N, "conv_ex: operand shape"
     y = acc if acc is not None else torch.empty(B, L, N, device=x.device, dtype=torch.bfloat16)
     y2 = torch.empty_like(y) if dual_lrelu else None
-    rc = lib().ssamd_conv_gemm_ex(_ptr(xc), _ptr(wi), _ptr(bf), _ptr(resid), _ptr(y), B, L, Cin, ks, dil, pad, N,
-                                  _ACT[act], _ptr(acc), _ptr(y2), float(scale), _ACT[post_act], _stream())
+    if ksplit:
+        rc = lib().ssamd_conv_gemm_ex2(_ptr(xc), _ptr(wi), _ptr(bf), _ptr(resid), _ptr(y), B, L, Cin, ks, dil, pad,
+                                       N, _ACT[act], _ptr(acc), _ptr(y2), float(scale), _ACT[post_act], int(ksplit),
+                                       _stream())
+    else:
+        rc = lib().ssamd_conv_gemm_ex(_ptr(xc), _ptr(wi), _ptr(bf), _ptr(resid), _ptr(y), B, L, Cin, ks, dil, pad,
+                                      N, _ACT[act], _ptr(acc), _ptr(y2), float(scale), _ACT[post_act], _stream())
     _check(rc, "ssamd_conv_gemm_ex")
     return (y, y2) if dual_lrelu else y
 

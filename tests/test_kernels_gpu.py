@@ -1266,6 +1266,32 @@ def test_conv3_sq(C, B, T):
         assert _rel(y, yg) < 1e-2
 
 
+@pytest.mark.parametrize("Cin,Cout,s,B,T", [(512, 256, 8, 2, 300), (256, 128, 8, 3, 257)])
+def test_convT_gemm_zero_tap_skip(Cin, Cout, s, B, T):
+    """The upsamplers' 3-tap GEMM with each 256-column tile's all-zero tap skipped (ConvGeom::ksplit) is bitwise equal
+    to the full 3-tap GEMM (also with the dual lrelu output) and matches fp32 torch conv_transpose1d."""
+    from speakingstyle_amd.models.hifigan import convT_as_conv3
+
+    torch.manual_seed(27)
+    pad = s // 2
+    w = (torch.randn(Cin, Cout, 2 * s, device=DEV) / math.sqrt(Cin * 2)).to(torch.bfloat16).float()
+    b = torch.randn(Cout, device=DEV) * 0.1
+    x = torch.randn(B, T, Cin, device=DEV).to(torch.bfloat16)
+    wu = convT_as_conv3(w, s, pad)
+    wimg = wu.permute(0, 2, 1).to(torch.bfloat16).contiguous()
+    bt = b.repeat(s).contiguous()
+    ks = (s // 2) * Cout
+    with torch.no_grad():
+        full = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg)
+        y = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, ksplit=ks)
+        assert torch.equal(y, full)
+        y1, y2 = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, dual_lrelu=True, ksplit=ks)
+        f1, f2 = hip.conv1d_infer(x, wu, bt, 1, 1, None, wimg=wimg, dual_lrelu=True)
+        assert torch.equal(y1, f1) and torch.equal(y2, f2)
+        ref = F.conv_transpose1d(x.float().transpose(1, 2), w, b, stride=s, padding=pad).transpose(1, 2)
+        assert _rel(y.view(B, T * s, Cout), ref) < 1e-2
+
+
 def test_resblock_rejects_host_weights():
     """A ResBlock1 moved with .cuda() while weight norm is still applied keeps its computed .weight on the host:
     the wrappers must raise before any launch (a host address in the kernel faults the GPU)."""
