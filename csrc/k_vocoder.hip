@@ -442,6 +442,10 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
   bf16_t* xs = reinterpret_cast<bf16_t*>(lds);                  // [RXS][LDC]: x rows t0 - 1 ..
   float* os = reinterpret_cast<float*>(lds + G::XS_BYTES);       // [BM][OSP]
   char* bring = reinterpret_cast<char*>(lds + G::XS_BYTES + G::OS_BYTES);
+  // fp32 output tile column swizzle (C = 128): the epilogue's 16-B reads of lanes 0-15 step 32 B through a row, so
+  // chunks 2k and 2k + 16 shared banks (2-way); XOR-ing the chunk index with bit 4 moves the upper half by one chunk
+  constexpr bool SW = C == 128;
+  auto osw = [](int ch) { return SW ? ch ^ (((ch >> 6) & 1) << 2) : ch; };
   const int tid0 = threadIdx.x;
   float bv[R::NSW];
 #pragma unroll
@@ -493,7 +497,7 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
       for (int s = 0; s < R::NSW; ++s) {
         const int ch = (wc * R::NSW + s) * 16 + col;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + ch] = acc[r][s][i] + bv[s];
+        for (int i = 0; i < 4; ++i) os[(rb * 16 + 4 * quad + i) * R::OSP + osw(ch)] = acc[r][s][i] + bv[s];
       }
     }
     lds_barrier();
@@ -504,8 +508,9 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
       const int t = t0 + j;
       if (j >= BM || t >= T) continue;
-      const float4 o0 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0);
-      const float4 o1 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0 + 4);
+      const int f = SW ? (c0 >> 6) & 1 : 0;  // the pair of 16-B chunks is stored swapped when f (see osw)
+      const float4 o0 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0 + 4 * f);
+      const float4 o1 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0 + 4 - 4 * f);
       const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
       short8 o;
 #pragma unroll
