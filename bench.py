@@ -114,8 +114,6 @@ def main():
 
 
 def run(args):
-    # variable-shape batches: let the caching allocator grow segments instead of re-mallocing
-    os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
     import torch
 
     from speakingstyle_amd import benchmark as B

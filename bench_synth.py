@@ -34,7 +34,6 @@ def parse():
 
 
 def run(args):
-    os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
     import torch
 
     from speakingstyle_amd import benchmark as B

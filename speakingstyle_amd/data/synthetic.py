@@ -66,6 +66,7 @@ class SyntheticBatches:
         self.group = group_size
         self.fpp = frames_per_phone
         self.vocab = vocab
+        self.seed = int(seed)
         self.rng = np.random.default_rng(seed)
         self.gen = torch.Generator(device="cpu").manual_seed(seed)
         pc = phone_counts if phone_counts is not None else ljspeech_phone_counts()
@@ -117,6 +118,15 @@ class SyntheticBatches:
             self._queue.append({"T": Ts[cur], "d": [ds[j] for j in cur]})
         perm = self.rng.permutation(len(self._queue))
         self._queue = [self._queue[i] for i in perm]
+
+    def seek(self, index: int):
+        """Re-seed both generators from (seed, ``index``) and drop queued plans: batch ``index`` of a
+        seeked stream depends on nothing drawn before it, so a resumed run (``train/loop.py``, the
+        checkpoint's data position) regenerates exactly the batches an uninterrupted run would."""
+        ss = np.random.SeedSequence([self.seed, int(index)])
+        self.rng = np.random.default_rng(ss)
+        self.gen = torch.Generator(device="cpu").manual_seed(int(ss.generate_state(1, np.uint64)[0] >> 1))
+        self._queue = []
 
     def next_plan(self):
         if not self._queue:

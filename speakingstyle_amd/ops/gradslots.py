@@ -94,8 +94,24 @@ def unregister(p: torch.nn.Parameter):
     _slots.pop(id(p), None)
 
 
+_side_issued = set()  # ids of parameters whose weight gradient went to the side stream this step (hip.wgrad_async)
+
+
+def mark_side(params):
+    for p in params:
+        if p is not None:
+            _side_issued.add(id(p))
+
+
+def side_issued(p) -> bool:
+    """True when ``p``'s weight gradient was issued on the side stream since the last reset: only then can a
+    second, main-stream contribution have raced the slot write."""
+    return p is not None and id(p) in _side_issued
+
+
 def reset():
     _claimed.clear()
+    _side_issued.clear()
     for h in _film_holders.values():  # no L2 gradient / site registration survives into the next step
         h.reset()
         h.pending.clear()

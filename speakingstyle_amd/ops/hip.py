@@ -107,7 +107,7 @@ _SIGS.update({
     "ssamd_ew": [I, P, P, P, P, L_, F, P],
     "ssamd_l1_sum": [P, P, L_, I, F, P, P, I, P],
     "ssamd_sum_parts": [P, I, F, P, I, P],
-    "ssamd_lsgan": [P, I, F, F, P, P, P],
+    "ssamd_lsgan": [P, I, F, F, P, F, P, P, P],
     "ssamd_avgpool4": [P, P, I, I, P],
     "ssamd_avgpool4_bwd": [P, P, I, I, I, P],
     "ssamd_mpd_fold": [P, P, I, I, I, P],
@@ -395,6 +395,11 @@ def weight_dgrad(w: torch.Tensor, owner: Optional[torch.Tensor] = None) -> torch
 _ACT = {None: 0, "relu": 1, "lrelu": 2, "tanh": 3, "relu_ln": 1}  # relu_ln: ReLU, mask left to the consumer LN
 
 _ws = {}
+# HIP graphs (train/graphs.py) bake the workspace address into their kernels: once one has been captured, a
+# workspace that grows is retired here instead of freed, so a later replay of an older graph never writes
+# into memory the caching allocator has handed to another tensor
+_GRAPHS_LIVE = [False]
+_ws_retired = []
 
 
 def _workspace(device, nfloats: int) -> torch.Tensor:
@@ -403,6 +408,8 @@ def _workspace(device, nfloats: int) -> torch.Tensor:
     key = (device, _stream())
     cur = _ws.get(key)
     if cur is None or cur.numel() < nfloats:
+        if cur is not None and (_GRAPHS_LIVE[0] or torch.cuda.is_current_stream_capturing()):
+            _ws_retired.append(cur)
         side = _side_by_handle.get(key[1])
         if side is not None:
             with torch.cuda.stream(side):
@@ -490,6 +497,7 @@ def wgrad_async(launch, inputs, slots_ok: bool, params=()):
     if not (_SIDE_WGRAD[0] and slots_ok and all(gradslots.single_contribution(p) for p in params)):
         return launch()
     dev = inputs[0].device
+    gradslots.mark_side(params)
     sh = _side_stream(dev).cuda_stream
     _check(lib().ssamd_stream_wait(sh, _stream()), "ssamd_stream_wait")
     _stream_override[0] = sh

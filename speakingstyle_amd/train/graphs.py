@@ -68,7 +68,10 @@ class GraphedSteps:
         texts = F.pad(texts, (0, dT)) if dT else texts
         dur = F.pad(dur, (0, dT)) if dT else dur
         mels = F.pad(mels, (0, 0, 0, dM)) if dM else mels
-        frame_level = pitch.shape[1] == M and pitch.shape[1] != T
+        # the feature level comes from the preprocess config (a shape test cannot tell when M == T)
+        pre = self.tr.configs[0]["preprocessing"]
+        frame_level = pre["pitch"]["feature"] == "frame_level"
+        assert pre["energy"]["feature"] == pre["pitch"]["feature"], "graph steps: mixed pitch / energy levels"
         dp = dM if frame_level else dT
         if dp:
             pitch, energy = F.pad(pitch, (0, dp)), F.pad(energy, (0, dp))
@@ -104,7 +107,10 @@ class GraphedSteps:
         ent["graph"].replay()
         self.replays += 1
         lr = tr.step_tail(batch, True, graphed=True)
-        return ent["losses"], ent["output"], lr
+        # the static outputs live in the graph pool and the next replay of this bucket overwrites them: callers
+        # get clones (a few small tensors) so nothing they keep aliases graph memory
+        clone = lambda t: t.clone() if isinstance(t, torch.Tensor) else t  # noqa: E731
+        return [clone(t) for t in ent["losses"]], [clone(t) for t in ent["output"]], lr
 
     def _capture(self, ent, pb):
         tr = self.tr
@@ -113,6 +119,9 @@ class GraphedSteps:
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         stream = getattr(tr, "compute_stream", None)  # None: torch's own capture stream
+        from ..ops import hip
+
+        hip._GRAPHS_LIVE[0] = True  # from now on grown workspaces are retired, never freed (ops/hip.py)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         # the capture stream is the trainer's compute stream (priority, side-stream forks / joins)

@@ -55,8 +55,11 @@ def _batches(configs, device, rank, world, synthetic: bool, seed: int, pos=None)
         gen = SyntheticBatches(per_rank, device=device, max_seq_len=max_len, seed=seed + rank,
                                n_speakers=_n_speakers(preprocess_config), frames_per_batch=budget or None,
                                frame_level=preprocess_config["preprocessing"]["pitch"]["feature"] == "frame_level")
-        gi = 0
+        # one group = one batch; every group re-seeds the stream from (seed + rank, group index), so a
+        # resume at the checkpoint's data position continues with exactly the batches that were next
+        gi = int(pos[1]) if pos else 0
         while True:
+            gen.seek(gi)
             yield 0, gi, [gen.make_batch()]
             gi += 1
     from ..data.dataset import FrameBudgetSampler, ShardedGroupSampler

@@ -103,13 +103,15 @@ class FlatArena:
     def ensure_slot(self, p, i=None):
         """Make ``p.grad`` the arena slot (copying a gradient produced outside it).
 
-        A parameter whose weight gradient may have been written by the side stream this step
-        (``gradslots.single_contribution``) but that arrives here with a gradient that is NOT its slot
-        view received a second contribution summed on the main stream -- possibly while the side stream
-        was still writing the slot.  Its slot is poisoned with NaN instead: the global-norm guard of the
-        fused clip + Adam kernel then skips this step on the device (on every rank under DP: the slot is
-        poisoned before its bucket is all-reduced), and the flag flip in ``note_contributions`` keeps the
-        parameter on the main stream from the next step on."""
+        A parameter whose weight gradient WAS written by the side stream this step
+        (``gradslots.side_issued``, recorded by ``hip.wgrad_async``) but that arrives here with a gradient
+        that is NOT its slot view received a second contribution summed on the main stream -- possibly
+        while the side stream was still writing the slot.  Its slot is poisoned with NaN instead: the
+        global-norm guard of the fused clip + Adam kernel then skips this step on the device (on every rank
+        under DP: the slot is poisoned before its bucket is all-reduced), and the flag flip in
+        ``note_contributions`` keeps the parameter on the main stream from the next step on.  A parameter
+        whose gradient stayed on the main stream cannot have raced: its gradient is copied.  The race path
+        inside a HIP-graph capture is an error (the poison would be baked into every replay)."""
         from ..ops import gradslots
 
         g = p.grad
@@ -118,7 +120,10 @@ class FlatArena:
         if i is None:
             i = next(j for j, q in enumerate(self.params) if q is p)
         slot = self.grad_view(i)
-        if gradslots.single_contribution(p):
+        if gradslots.side_issued(p):
+            if g.is_cuda and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"gradslots: parameter {i} raced the weight-gradient side stream during a HIP-graph "
+                                   "capture; capture only after eager warm-up steps have settled the side-stream flags")
             slot.fill_(float("nan"))
             gradslots.report_race(i)
         else:

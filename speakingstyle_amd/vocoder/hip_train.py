@@ -162,9 +162,13 @@ def l1_sum_into(loss, a, b, scale, part):
          "ssamd_l1_sum")
 
 
-def lsgan_into(loss, s, target, gscale=1.0, ds=None):
-    """loss[0] += mean((target - s)^2); ds = d/ds * gscale (bf16) when given."""
-    _chk(_lib().ssamd_lsgan(_P(s), s.numel(), float(target), float(gscale), _P(ds), _P(loss), _s()), "ssamd_lsgan")
+def lsgan_into(loss, s, target, gscale=1.0, ds=None, r=None, fm_scale=0.0):
+    """loss[0] += mean((target - s)^2) [+ fm_scale * sum |s - r|]; ds = d/ds * gscale (bf16) when given.
+    s (and r) fp32 contiguous."""
+    if r is not None:
+        assert r.dtype == torch.float32 and r.is_contiguous() and r.numel() == s.numel(), "lsgan_into: r"
+    _chk(_lib().ssamd_lsgan(_P(s), s.numel(), float(target), float(gscale), _P(r), float(fm_scale), _P(ds), _P(loss),
+                            _s()), "ssamd_lsgan")
 
 
 def avgpool4(x):
@@ -296,12 +300,15 @@ def d_step(mpd, msd, y, y_hat):
 
 def _disc_g(d, u, loss, part, out0=None):
     """G step of one discriminator on u = [y; y_hat]: loss[0] += mean((1 - D(y_hat))^2) + 2 sum_l mean|fmap_l(y_hat)
-    - fmap_l(y)|; returns d loss / d (fake half of the layer-0 input), fp32 [B*, T*, 1]."""
+    - fmap_l(y)| over every feature map -- the post-lrelu conv outputs AND the conv_post score map (the reference
+    ``DiscriminatorP/S.forward`` appends the score to ``fmap``, hifigan/models.py:193-198); returns d loss / d (fake
+    half of the layer-0 input), fp32 [B*, T*, 1]."""
     disc = _Disc(d, hook_times=2 if _has_sn(d) else 1)
     xs, fmaps, score = disc.forward(disc.prep(u))
-    _, sg = _half(score)
+    sr, sg = _half(score)
     ds = torch.empty(sg.shape, device=u.device, dtype=torch.bfloat16)
-    lsgan_into(loss, sg, 1.0, 1.0, ds)
+    # adversarial term + the score map's feature-matching term 2 * mean|D(y_hat) - D(y)| in one kernel
+    lsgan_into(loss, sg, 1.0, 1.0, ds, r=sr, fm_scale=2.0 / sg.numel())
     fm = []
     for f in fmaps:
         fr, fg = _half(f)

@@ -135,7 +135,8 @@ def _flat_worker(rank, world, port, q):
     for i, p in enumerate(ps[:-1]):
         p.grad = torch.full_like(p, float(rank + 1) * (i + 1)) + torch.arange(p.numel()).float() * rank
     ddp.allreduce_grads_flat(ps, bucket_mb=1e-3)  # ~262 floats per bucket: several buckets, one oversized
-    q.put((rank, [p.grad.clone() if p.grad is not None else None for p in ps]))
+    # numpy copies: torch CPU tensors travel by fd passing, which breaks once this process has exited
+    q.put((rank, [p.grad.numpy().copy() if p.grad is not None else None for p in ps]))
     torch.distributed.destroy_process_group()
 
 
@@ -153,6 +154,7 @@ def test_allreduce_grads_flat_averages_over_ranks():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    res = {r: [None if g is None else torch.from_numpy(g) for g in gs] for r, gs in res.items()}
     for i, n in enumerate((5, 300, 7, 1000)):
         want = (torch.full((n,), 1.0 * (i + 1)) + torch.full((n,), 2.0 * (i + 1)) + torch.arange(n).float()) / 2
         torch.testing.assert_close(res[0][i], want)

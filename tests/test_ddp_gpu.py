@@ -8,6 +8,7 @@ The multi-rank launcher / gloo path is covered on the CPU (tests/test_bench_cpu.
 tests/test_ddp_cpu.py, tests/test_ddp_slots_cpu.py)."""
 import os
 import socket
+import warnings
 
 import pytest
 import torch
@@ -141,7 +142,21 @@ class _StreamWork:
         torch.cuda.current_stream().wait_event(self.ev)
 
 
-def test_rccl_bucket_order_non_idempotent_with_late_side_stream():
+class _GatherX2Work:
+    """wait(): the caller's stream waits for the ProcessGroup's all_gather, then t = 2 * (what RCCL read)."""
+
+    def __init__(self, work, out, t):
+        self.work, self.out, self.t = work, out, t
+
+    def wait(self):
+        self.work.wait()
+        torch.mul(self.out, 2.0, out=self.t)
+
+    def is_completed(self):
+        return self.work.is_completed()
+
+
+def test_rccl_bucket_order_non_idempotent_with_late_side_stream(record_property):
     """The 1-rank RCCL bucket path with a reduction that is NOT an identity (x2: RCCL PREMUL_SUM, or -- if
     this RCCL lacks it -- an in-place x2 on the same stream the collective would use) and a ~20 ms spin
     injected on the weight-gradient side stream ahead of a step's side-stream launches.  A bucket reduced
@@ -178,11 +193,22 @@ def test_rccl_bucket_order_non_idempotent_with_late_side_stream():
         except Exception:  # noqa: BLE001 -- RCCL without ncclRedOpCreatePreMulSum
             premul = False
 
+        branch = "premul_sum" if premul else "all_gather_x2"
+        # which branch ran goes into the test log (warnings summary) and the junit properties
+        warnings.warn(f"RCCL non-idempotent bucket reduction branch: {branch}", UserWarning)
+        print(f"RCCL non-idempotent bucket reduction branch: {branch}", flush=True)
+        record_property("rccl_branch", branch)
+
         def doubled(t):
             if premul:
                 return dist.all_reduce(t, op=dist._make_nccl_premul_sum(2.0), async_op=True)
-            t.mul_(2.0)  # same stream the collective would be issued on
-            return _StreamWork()
+            # no PREMUL_SUM: still a collective of the ProcessGroup, on its internal stream -- a 1-rank
+            # all_gather copies t as the RCCL kernel sees it (ordered exactly like the real all-reduce), and the
+            # x2 write-back happens after the work's wait(): a bucket read before its last side-stream weight
+            # gradient landed would be written back doubled from the partial slot
+            out = torch.empty_like(t)
+            w = dist.all_gather_into_tensor(out, t, async_op=True)
+            return _GatherX2Work(w, out, t)
 
         tr.buckets.collective = doubled
         g = _capture(tr, step=False)

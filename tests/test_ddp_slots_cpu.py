@@ -26,6 +26,9 @@ def _free_port():
     return p
 
 
+SIDE = [False]  # simulate the side-stream weight-gradient path (hip.wgrad_async) in SlotMatmul
+
+
 class SlotMatmul(torch.autograd.Function):
     """y = x @ w.T with the weight gradient written into w's arena slot when claimable."""
 
@@ -45,6 +48,8 @@ class SlotMatmul(torch.autograd.Function):
         if slot is not None:
             slot.copy_(gw)  # "kernel" writes in place
             gw = slot
+            if SIDE[0] and gradslots.single_contribution(ctx.w):
+                gradslots.mark_side([ctx.w])  # what hip.wgrad_async records when it takes the side stream
         return gy @ w, gw
 
 
@@ -240,7 +245,23 @@ def test_race_suspect_poisons_slot_and_adam_skips():
     assert gradslots.single_contribution(w)
     arena.zero_grad()
     before = gradslots.race_suspects[0]
+    # the side stream was off this step (e.g. the side_wgrad auto policy): nothing can have raced -> copied
     backward(True)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        arena.finalize_grads()
+    assert gradslots.race_suspects[0] == before and torch.isfinite(arena.grad[: w.numel()]).all()
+    arena.zero_grad()
+    # single flag restored, side stream on: the slot was written on the side stream -> poisoned
+    backward(False)
+    arena.finalize_grads()
+    gradslots.note_contributions(arena)
+    arena.zero_grad()
+    SIDE[0] = True
+    try:
+        backward(True)
+    finally:
+        SIDE[0] = False
     with pytest.warns(RuntimeWarning, match="skipped"):
         arena.finalize_grads()
     assert gradslots.race_suspects[0] == before + 1

@@ -81,6 +81,22 @@ def test_train_save_resume(tmp_path, style):
     assert {"Loss/total_loss", "Loss/mel_loss", "Weight/learning_rate"} <= tags
 
 
+def _losses(out):
+    return {int(l.split("Step ")[1].split("/")[0]): l.split(", ", 1)[1] for l in out.splitlines()
+            if l.startswith("Step ")}
+
+
+def test_synthetic_resume_is_exact(tmp_path):
+    """The synthetic stream honours the checkpoint's data position: resuming at step 4 logs the same
+    step-6 losses as the uninterrupted run (weights, Adam state, LR schedule, dropout RNG and data)."""
+    p, m, t = _tiny_configs(tmp_path)
+    full = _losses(_run(["train.py", "-p", p, "-m", m, "-t", t, "--synthetic", "--cpu", "--no_vocoder",
+                         "--max_steps", "6"]))
+    res = _losses(_run(["train.py", "-p", p, "-m", m, "-t", t, "--synthetic", "--cpu", "--no_vocoder",
+                        "--restore_step", "4", "--max_steps", "6"]))
+    assert 6 in full and res[6] == full[6], (full, res)
+
+
 def test_sigterm_checkpoint_and_fault_injection(tmp_path):
     p, m, t = _tiny_configs(tmp_path)
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")

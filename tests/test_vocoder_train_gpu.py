@@ -150,10 +150,18 @@ def test_d_step_loss_and_grads_vs_torch():
     assert (num / den) ** 0.5 < 3e-2 and worst < 0.12, ((num / den) ** 0.5, worst)
 
 
-def test_g_adv_grad_vs_torch():
+@pytest.mark.parametrize("post_gain", [1.0, 30.0])
+def test_g_adv_grad_vs_torch(post_gain):
+    """post_gain > 1 scales every weight-normed discriminator's conv_post, so D(y) and D(y_hat) differ widely and the
+    score map's feature-matching term (part of the reference's fmap lists) dominates loss and gradient: a G step
+    that dropped it fails here."""
     from speakingstyle_amd.vocoder import hip_train as HT
 
     H, mpd, msd = _discs()
+    if post_gain != 1.0:
+        with torch.no_grad():
+            for d in list(mpd.discriminators) + list(msd.discriminators)[1:]:
+                d.conv_post.weight_g.mul_(post_gain)
     B, T = 2, 4096
     y, yh0 = _wave(B, T, 4), _wave(B, T, 5)
     yh = yh0.clone().requires_grad_(True)

@@ -21,6 +21,10 @@ tail -3 $OUT/train.log
 ls $CK
 timeout -k 10 400 python train.py -p $P -m $M -t $T --synthetic --restore_step 20 --max_steps 40 > $OUT/resume.log 2>&1 || { tail -30 $OUT/resume.log; exit 1; }
 tail -2 $OUT/resume.log
+# the resumed run's step-30 losses must equal the uninterrupted run's (weights, Adam, LR, data position)
+a=$(grep '^Step 30/' $OUT/train.log | cut -d, -f2-); b=$(grep '^Step 30/' $OUT/resume.log | cut -d, -f2-)
+[ -n "$a" ] && [ "$a" = "$b" ] || { echo "RESUME MISMATCH at step 30: [$a] vs [$b]"; exit 1; }
+echo "resume exact at step 30:$a"
 timeout -k 10 300 python synthesize.py --mode single --text "Printing, in the only sense with which we are at present concerned." --restore_step 40 -p $P -m $M -t $T > $OUT/synth.log 2>&1 || { tail -30 $OUT/synth.log; exit 1; }
 tail -2 $OUT/synth.log
 find $OUT/result -name "*.wav"
