@@ -30,6 +30,10 @@ def parse():
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--tiny", action="store_true")
     ap.add_argument("--synth-serial", action="store_true", help="one stream (A/B of the two-stream pipeline)")
+    ap.add_argument("--b1-runs", type=int, default=0, dest="synth_b1_runs", help="batch-1 latency runs (0: off)")
+    ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
+    ap.add_argument("--bucketed", action="store_true",
+                    help="length-bucketed vocoding instead of the packed length-exact path (A/B)")
     return ap.parse_args()
 
 
@@ -44,9 +48,16 @@ def run(args):
     dev = torch.device("cuda", local_rank) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(dev)
+    if args.bucketed:
+        from speakingstyle_amd.models import hifigan
+
+        hifigan._PACKED[0] = False
     sy = B.synth_phase(args, rank, world, dev)
     if rank == 0:
+        b1 = sy.get("b1")
         B.report({
+            "b1_ms": None if b1 is None else round(1e3 * b1["median_s"], 3),
+            "b1_rtf": None if b1 is None else b1["rtf"], "vocoder": "bucketed" if args.bucketed else "packed",
             "metric": "synth RTF (FastSpeech2 + style + HiFi-GAN, text ids -> int16 wav)",
             "value": sy["rtf"], "unit": "s wall / s audio", "higher_is_better": False, "n_gpus": world,
             "steps": args.synth_steps, "warmup": args.synth_warmup, "audio_seconds": round(sy["audio_s"], 2),

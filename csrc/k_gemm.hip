@@ -2825,6 +2825,21 @@ SSAMD_API int ssamd_conv_gemm_ex2(const bf16_t* X, const bf16_t* W, const float*
                         false, ksplit);
 }
 
+// ssamd_conv_gemm_ex2 on packed rows (B = 1, L = R): rinfo [R] int2 {position, length} zero-pads every conv at its
+// own sequence's ends (the length-exact vocoder's GEMM stages, k_vocoder.hip ssamd_voc_rinfo).
+SSAMD_API int ssamd_conv_gemm_ex3(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* resid, void* Y,
+                                  int R, int Cin, int ks, int dil, int pad, int N, int act, const bf16_t* acc,
+                                  bf16_t* y2, float scale, int post_act, int ksplit, const int* rinfo, hipStream_t s) {
+  if (!rinfo) return -2;
+  EpiX ex{};
+  ex.acc = acc;
+  ex.y2 = y2;
+  ex.scale = scale;
+  ex.post_act = post_act;
+  return conv_gemm_impl(X, W, bias, nullptr, resid, nullptr, Y, 0, 1, R, Cin, ks, dil, pad, N, act, N, rinfo, ex, s,
+                        false, ksplit);
+}
+
 // Data gradient of a conv whose input came out of BatchNorm (+act, dropout): Y = dz (see EpiX.bn_*) and the
 // per-M-tile column partials bn_part [2][ceil(M/256)][N] of dz and dz * (h - mean) (ssamd_bn_bwd_dz applies rstd).
 SSAMD_API int ssamd_conv_gemm_bnbwd(const bf16_t* X, const bf16_t* W, void* Y, int B, int L, int Cin, int ks, int dil,

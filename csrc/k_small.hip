@@ -86,9 +86,10 @@ constexpr int CP_T = 256;
 
 template <int C>
 __global__ void __launch_bounds__(CP_T) conv_post_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
-                                                         const float* __restrict__ b, int T, float slope,
+                                                         const float* __restrict__ b, int Tp, float slope,
                                                          float scale, float* __restrict__ outf,
-                                                         int16_t* __restrict__ outi) {
+                                                         int16_t* __restrict__ outi, const int4* __restrict__ tt,
+                                                         long ostride) {
   // rows staged with 16-B loads (8 channels per lane) into fp32 rows of RS = C + 4 floats (16-B aligned; the
   // 36-dword pitch at C = 32 spreads a 16-lane group's ds_read_b128 over all 64 banks), the 7 x C dot
   // product read back 4 channels per ds_read_b128 in the same tap / channel order as a scalar loop
@@ -96,9 +97,24 @@ __global__ void __launch_bounds__(CP_T) conv_post_kernel(const bf16_t* __restric
   constexpr int CH = C / 8;  // 16-B chunks per input row
   __shared__ __attribute__((aligned(16))) float xs[(CP_T + 6) * RS];
   __shared__ __attribute__((aligned(16))) float ws[7 * C];
-  const int bb = blockIdx.y;
-  const int t0 = blockIdx.x * CP_T;
-  const bf16_t* xb = x + (long)bb * T * C;
+  // padded: block (x, y) = samples [x * CP_T, ...) of row y of [B, Tp]; packed (tt: the length-exact vocoder,
+  // k_vocoder.hip TileGeo): tt[block] = {first row of the sequence in x, its length, t0, sequence}, the output
+  // row of sequence u at out + u * ostride
+  int T, t0;
+  long xo, oo;
+  if (tt) {
+    const int4 e = tt[blockIdx.x];
+    xo = e.x;
+    T = e.y;
+    t0 = e.z;
+    oo = (long)e.w * ostride;
+  } else {
+    T = Tp;
+    t0 = blockIdx.x * CP_T;
+    xo = (long)blockIdx.y * Tp;
+    oo = xo;
+  }
+  const bf16_t* xb = x + xo * C;
   for (int e = threadIdx.x; e < 7 * C; e += CP_T) {  // w[0][c][tap] -> ws[tap][c]
     const int c = e / 7, tap = e % 7;
     ws[tap * C + c] = w[e];
@@ -137,7 +153,7 @@ __global__ void __launch_bounds__(CP_T) conv_post_kernel(const bf16_t* __restric
     }
   }
   const float y = tanhf(s);
-  const long o = (long)bb * T + t;
+  const long o = oo + t;
   if (outi) {
     float v = y * scale;
     v = fminf(fmaxf(v, -32768.f), 32767.f);
@@ -186,9 +202,30 @@ SSAMD_API int ssamd_conv_post(const bf16_t* x, const float* w, const float* b, i
   if ((long)B * T == 0) return 0;
   dim3 grid(cdiv(T, CP_T), B);
   switch (C) {
-    case 32: hipLaunchKernelGGL(conv_post_kernel<32>, grid, dim3(CP_T), 0, s, x, w, b, T, slope, scale, outf, outi); break;
-    case 8: hipLaunchKernelGGL(conv_post_kernel<8>, grid, dim3(CP_T), 0, s, x, w, b, T, slope, scale, outf, outi); break;
+    case 32: hipLaunchKernelGGL(conv_post_kernel<32>, grid, dim3(CP_T), 0, s, x, w, b, T, slope, scale, outf, outi,
+                                (const int4*)nullptr, 0L); break;
+    case 8: hipLaunchKernelGGL(conv_post_kernel<8>, grid, dim3(CP_T), 0, s, x, w, b, T, slope, scale, outf, outi,
+                               (const int4*)nullptr, 0L); break;
     default: return -1;
   }
   return (int)hipGetLastError();
 }
+
+// Packed rows (length-exact vocoder): x [R, C], tt = ntt tiles of CP_T rows (k_vocoder.hip TileGeo layout), sample t
+// of sequence u written to out[u * ostride + t] (the caller zero-fills the samples past each length).
+SSAMD_API int ssamd_conv_post_pk(const bf16_t* x, const float* w, const float* b, const int* tt, int ntt, int C,
+                                 float slope, float scale, float* outf, int16_t* outi, long ostride, hipStream_t s) {
+  if (ntt <= 0) return 0;
+  if (!tt) return -2;
+  const int4* t4 = reinterpret_cast<const int4*>(tt);
+  switch (C) {
+    case 32: hipLaunchKernelGGL(conv_post_kernel<32>, dim3(ntt), dim3(CP_T), 0, s, x, w, b, 0, slope, scale, outf, outi,
+                                t4, ostride); break;
+    case 8: hipLaunchKernelGGL(conv_post_kernel<8>, dim3(ntt), dim3(CP_T), 0, s, x, w, b, 0, slope, scale, outf, outi,
+                               t4, ostride); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_conv_post_tile_rows() { return CP_T; }

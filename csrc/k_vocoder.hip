@@ -97,6 +97,33 @@ __device__ __forceinline__ void wait_vm_lgkm0() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
 }
 
+// Where a tile's rows live.  Padded batches [B, Tp, C]: tile = b * tiles + i, rows [i * BM, ...) of sequence b.
+// Packed batches (the length-exact vocoder path, models/hifigan.py ``Generator.infer_packed``): every sequence's
+// rows are contiguous in one [R, C] buffer and the host-built tile table tt[tile] = {first row of the sequence,
+// its length, t0, sequence index} -- tiles never straddle two sequences, and every conv zero-pads at the
+// sequence's own ends exactly as it does at the ends of a padded row.
+struct TileGeo {
+  long off;  // first row of the tile's sequence
+  int T;     // rows of the sequence
+  int t0;    // first output row of the tile within the sequence
+};
+
+__device__ __forceinline__ TileGeo tile_geo(const int4* __restrict__ tt, int tile, int tiles, int Tp, int BM) {
+  TileGeo g;
+  if (tt) {
+    const int4 e = tt[tile];
+    g.off = e.x;
+    g.T = e.y;
+    g.t0 = e.z;
+  } else {
+    const int b = tile / tiles;
+    g.off = (long)b * Tp;
+    g.T = Tp;
+    g.t0 = (tile - b * tiles) * BM;
+  }
+  return g;
+}
+
 template <int C, int K>
 __device__ __forceinline__ void stage_b(const bf16_t* __restrict__ w, int step, char* slot, int tid, int wave) {
   using R = RB<C, K>;
@@ -213,8 +240,9 @@ template <int C, int K, bool PROF = false>
 __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
                                                             const float* __restrict__ b1, const bf16_t* __restrict__ w2,
                                                             const float* __restrict__ b2, const bf16_t* acc_in,
-                                                            bf16_t* out, int T, int tiles, int ntiles, int d, float slope,
+                                                            bf16_t* out, int Tp, int tiles, int ntiles, int d, float slope,
                                                             float out_scale, int post_lrelu,
+                                                            const int4* __restrict__ tt,
                                                             unsigned long long* __restrict__ prof = nullptr) {
   using R = RB<C, K>;
   unsigned long long st[8];
@@ -241,8 +269,9 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
   short8 v[IX];
   // x rows [t0 - h1 - H2, ...) of a tile into v (zero outside [0, T))
   auto fetch_x = [&](int tile, int tid) {
-    const int b = tile / tiles, t0 = (tile - b * tiles) * R::BM;
-    const bf16_t* xb = x + (long)b * T * C;
+    const TileGeo gq = tile_geo(tt, tile, tiles, Tp, R::BM);
+    const int T = gq.T, t0 = gq.t0;
+    const bf16_t* xb = x + gq.off * C;
 #pragma unroll
     for (int it = 0; it < IX; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
@@ -269,8 +298,9 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     const int lane = tid & 63, col = lane & 15, quad = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row-block tests are scalar
     const int wr = wave % R::WR, wc = wave / R::WR;
-    const int b = tile / tiles, t0 = (tile - b * tiles) * R::BM;
-    const bf16_t* xb = x + (long)b * T * C;
+    const TileGeo gt = tile_geo(tt, tile, tiles, Tp, R::BM);
+    const int T = gt.T, t0 = gt.t0;
+    const bf16_t* xb = x + gt.off * C;
     rb_stamp<PROF>(st, 0);
 
     // 1. lrelu(x) -> LDS
@@ -320,8 +350,8 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     // the epilogue's residual / accumulator rows, issued before the output staging
     constexpr int BM = R::BM;
     constexpr int IE = (BM * CH + NT - 1) / NT;
-    bf16_t* ob = out + (long)b * T * C;
-    const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
+    bf16_t* ob = out + gt.off * C;
+    const bf16_t* ab = acc_in ? acc_in + gt.off * C : nullptr;
     short8 xr[IE], ar[IE];
 #pragma unroll
     for (int it = 0; it < IE; ++it) {
@@ -384,7 +414,7 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
 template <int C, int K>
 int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
               const bf16_t* acc_in, bf16_t* out, int B, int T, int d, float slope, float out_scale, int post_lrelu,
-              hipStream_t s) {
+              hipStream_t s, const int4* tt = nullptr, int ntt = 0) {
   using R = RB<C, K>;
   static bool lds_set = false;
   if (!lds_set) {
@@ -401,11 +431,13 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
       per_cu = 1;
     resident = cus * per_cu;
   }
-  const int tiles = (T + R::BM - 1) / R::BM;
-  const long ntiles = (long)B * tiles;
+  const int tiles = tt ? 1 : (T + R::BM - 1) / R::BM;
+  const long ntiles = tt ? (long)ntt : (long)B * tiles;
+  if (ntiles > 0x7fffffffL) return -2;
+  if (ntiles == 0) return 0;
   const int grid = (int)(ntiles < resident ? ntiles : resident);
   hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3(grid), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
-                     acc_in, out, T, tiles, (int)ntiles, d, slope, out_scale, post_lrelu);
+                     acc_in, out, T, tiles, (int)ntiles, d, slope, out_scale, post_lrelu, tt);
   return (int)hipGetLastError();
 }
 
@@ -432,7 +464,8 @@ struct C3 {
 template <int C>
 __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                                    const float* __restrict__ bias, bf16_t* __restrict__ out,
-                                                                   int T, int tiles, int ntiles) {
+                                                                   int Tp, int tiles, int ntiles,
+                                                                   const int4* __restrict__ tt) {
   using R = RB<C, 3>;
   using G = C3<C>;
   constexpr int NT = R::NT;
@@ -453,8 +486,9 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
   constexpr int IX = (G::RXS * CH + NT - 1) / NT;
   short8 v[IX];
   auto fetch_x = [&](int tile, int tid) {
-    const int b = tile / tiles, t0 = (tile - b * tiles) * BM;
-    const bf16_t* xb = x + (long)b * T * C;
+    const TileGeo gq = tile_geo(tt, tile, tiles, Tp, BM);
+    const int T = gq.T, t0 = gq.t0;
+    const bf16_t* xb = x + gq.off * C;
 #pragma unroll
     for (int it = 0; it < IX; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
@@ -479,7 +513,8 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
     const int lane = tid & 63, col = lane & 15, quad = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave % R::WR, wc = wave / R::WR;
-    const int b = tile / tiles, t0 = (tile - b * tiles) * BM;
+    const TileGeo gt = tile_geo(tt, tile, tiles, Tp, BM);
+    const int T = gt.T, t0 = gt.t0;
 #pragma unroll
     for (int it = 0; it < IX; ++it) {
       const int q = tid + it * NT, r = q / CH, c0 = (q - r * CH) * 8;
@@ -502,7 +537,7 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
     }
     lds_barrier();
     constexpr int IE = (BM * CH + NT - 1) / NT;
-    bf16_t* ob = out + (long)b * T * C;
+    bf16_t* ob = out + gt.off * C;
 #pragma unroll
     for (int it = 0; it < IE; ++it) {
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
@@ -522,7 +557,8 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
 }
 
 template <int C>
-int launch_c3(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* out, int B, int T, hipStream_t s) {
+int launch_c3(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* out, int B, int T, hipStream_t s,
+              const int4* tt = nullptr, int ntt = 0) {
   using G = C3<C>;
   static int resident = 0;
   if (!resident) {
@@ -535,12 +571,13 @@ int launch_c3(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* out, 
       per_cu = 1;
     resident = cus * per_cu;
   }
-  const int tiles = (T + G::BM - 1) / G::BM;
-  const long ntiles = (long)B * tiles;
+  const int tiles = tt ? 1 : (T + G::BM - 1) / G::BM;
+  const long ntiles = tt ? (long)ntt : (long)B * tiles;
   if (ntiles > 0x7fffffffL) return -2;
+  if (ntiles == 0) return 0;
   const int grid = (int)(ntiles < resident ? ntiles : resident);
   hipLaunchKernelGGL((conv3_sq_kernel<C>), dim3(grid), dim3(RB<C, 3>::NT), G::LDS, s, x, w, bias, out, T, tiles,
-                     (int)ntiles);
+                     (int)ntiles, tt);
   return (int)hipGetLastError();
 }
 
@@ -723,9 +760,10 @@ __device__ __forceinline__ void conv_rf_ring(const bf16_t* __restrict__ src, int
 
 template <int C, int K>
 __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fused_kernel(const bf16_t* __restrict__ x, RFW p,
-                                                                        const bf16_t* acc_in, bf16_t* out, int T,
+                                                                        const bf16_t* acc_in, bf16_t* out, int Tp,
                                                                         int tiles, int HT, float slope,
-                                                                        float out_scale, int post_lrelu) {
+                                                                        float out_scale, int post_lrelu,
+                                                                        const int4* __restrict__ tt) {
   using R = RF<C, K>;
   constexpr int NT = R::NT;
   constexpr int CH = C / 8;
@@ -735,13 +773,14 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
   char* Ws = reinterpret_cast<char*>(lds + 2 * R::BUF);
   float* Os = reinterpret_cast<float*>(lds);                               // final fp32 tile (aliases A / T)
   const int BM = R::R0 - 2 * HT;
-  const int b = blockIdx.x / tiles, t0 = (blockIdx.x - b * tiles) * BM;
+  const TileGeo gt = tile_geo(tt, blockIdx.x, tiles, Tp, BM);
+  const int T = gt.T, t0 = gt.t0;
   const int tb = t0 - HT;  // sequence position of absolute row 0
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave % R::WR, wc = wave / R::WR;
   const int col = lane & 15, quad = lane >> 4;
-  const bf16_t* xb = x + (long)b * T * C;
+  const bf16_t* xb = x + gt.off * C;
 
   // Weight images go global -> registers -> LDS.  Two register sets: the load of conv c+2's image is
   // issued at the start of conv c (two convs of latency cover), conv c+1's image is written to LDS
@@ -813,7 +852,7 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
 
   // the final epilogue's acc_in rows, loaded during the last conv
   constexpr int ITMAX = (R::R0 * CH + NT - 1) / NT;
-  const bf16_t* ab = acc_in ? acc_in + (long)b * T * C : nullptr;
+  const bf16_t* ab = acc_in ? acc_in + gt.off * C : nullptr;
   short8 ar[ITMAX];
 
   float4v acc[R::MAXRB][R::NSW];
@@ -917,7 +956,7 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
   }
   __syncthreads();
   {
-    bf16_t* ob = out + (long)b * T * C;
+    bf16_t* ob = out + gt.off * C;
 #pragma unroll
     for (int it = 0; it < ITMAX; ++it) {
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
@@ -943,7 +982,7 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
 
 template <int C, int K>
 int launch_rf(const bf16_t* x, const RFW& p, const bf16_t* acc_in, bf16_t* out, int B, int T, float slope,
-              float out_scale, int post_lrelu, hipStream_t s) {
+              float out_scale, int post_lrelu, hipStream_t s, const int4* tt = nullptr, int ntt = 0) {
   using R = RF<C, K>;
   const int HT = R::H2 * (p.d[0] + p.d[1] + p.d[2] + 3);
   const int BM = R::R0 - 2 * HT;
@@ -953,13 +992,128 @@ int launch_rf(const bf16_t* x, const RFW& p, const bf16_t* acc_in, bf16_t* out, 
     allow_lds(resblock_fused_kernel<C, K>, R::LDS);
     lds_set = true;
   }
-  const int tiles = (T + BM - 1) / BM;
-  hipLaunchKernelGGL((resblock_fused_kernel<C, K>), dim3((long)B * tiles), dim3(R::NT), R::LDS, s, x, p, acc_in,
-                     out, T, tiles, HT, slope, out_scale, post_lrelu);
+  const int tiles = tt ? 1 : (T + BM - 1) / BM;
+  const long nblk = tt ? (long)ntt : (long)B * tiles;
+  if (nblk > 0x7fffffffL) return -2;
+  if (nblk == 0) return 0;
+  hipLaunchKernelGGL((resblock_fused_kernel<C, K>), dim3(nblk), dim3(R::NT), R::LDS, s, x, p, acc_in,
+                     out, T, tiles, HT, slope, out_scale, post_lrelu, tt);
   return (int)hipGetLastError();
 }
 
+// rinfo[m] = {position in its sequence, sequence length} of the packed rows at `rate` rows per frame (cu: int32
+// frame offsets [B + 1]): the implicit-GEMM convs' per-row zero-padding table (ConvGeom::rinfo) for the packed
+// vocoder stages that run on the generic GEMM (conv_pre, the C = 256 MRF, the first two upsamplers)
+__global__ void __launch_bounds__(256) voc_rinfo_kernel(const int* __restrict__ cu, int rate, int2* __restrict__ rinfo) {
+  const int b = blockIdx.y;
+  const long r0 = (long)cu[b] * rate;
+  const int n = (cu[b + 1] - cu[b]) * rate;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) rinfo[r0 + i] = make_int2((int)i, n);
+}
+
+// dst [R, C] bf16 <- the valid rows of src [B, M, C] (fp32 or bf16): sequence b's cu[b+1] - cu[b] rows at cu[b]
+template <typename TS>
+__global__ void __launch_bounds__(256) voc_pack_kernel(const TS* __restrict__ src, const int* __restrict__ cu, int M,
+                                                       int C, bf16_t* __restrict__ dst) {
+  const int b = blockIdx.y;
+  const long n = (long)(cu[b + 1] - cu[b]) * C;
+  const TS* sb = src + (long)b * M * C;
+  bf16_t* db = dst + (long)cu[b] * C;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    if constexpr (sizeof(TS) == 4) db[i] = f2bf(sb[i]);
+    else db[i] = sb[i];
+  }
+}
+
 }  // namespace
+
+
+// ------------------------------------------------------------------------------- packed (length-exact) vocoder
+// Tile height (output rows per tile) of each tiled vocoder kernel, for the host-built packed tile tables:
+// kind 0 = resblock_layer (C, K), 1 = resblock_fused (C, K, dilations), 2 = conv3_sq (C).  0 = no such instance.
+SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2) {
+#define VT_RB(CC, KK) \
+  if (C == CC && K == KK) return RB<CC, KK>::BM;
+#define VT_RF(CC, KK) \
+  if (C == CC && K == KK) return RF<CC, KK>::R0 - 2 * (RF<CC, KK>::H2 * (d0 + d1 + d2 + 3));
+  if (kind == 0) {
+    VT_RB(32, 3) VT_RB(32, 7) VT_RB(32, 11) VT_RB(64, 3) VT_RB(64, 7) VT_RB(64, 11) VT_RB(128, 3) VT_RB(128, 7)
+    VT_RB(128, 11)
+  } else if (kind == 1) {
+    VT_RF(32, 3) VT_RF(32, 7) VT_RF(32, 11) VT_RF(64, 3) VT_RF(64, 7) VT_RF(128, 3)
+  } else if (kind == 2) {
+    if (C == 128) return C3<128>::BM;
+    if (C == 64) return C3<64>::BM;
+  }
+#undef VT_RB
+#undef VT_RF
+  return 0;
+}
+
+SSAMD_API int ssamd_voc_rinfo(const int* cu, int B, int rate, int max_rows, int* rinfo, hipStream_t s) {
+  if (B <= 0 || max_rows <= 0) return 0;
+  const int gx = max_rows / 256 + 1 < 64 ? max_rows / 256 + 1 : 64;
+  hipLaunchKernelGGL(voc_rinfo_kernel, dim3(gx, B), dim3(256), 0, s, cu, rate, reinterpret_cast<int2*>(rinfo));
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_voc_pack(const void* src, int src_f32, const int* cu, int B, int M, int C, bf16_t* dst,
+                             hipStream_t s) {
+  if (B <= 0 || M <= 0) return 0;
+  const long n = (long)M * C;
+  const int gx = (int)(n / 2048 + 1 < 32 ? n / 2048 + 1 : 32);
+  if (src_f32)
+    hipLaunchKernelGGL(voc_pack_kernel<float>, dim3(gx, B), dim3(256), 0, s, (const float*)src, cu, M, C, dst);
+  else
+    hipLaunchKernelGGL(voc_pack_kernel<bf16_t>, dim3(gx, B), dim3(256), 0, s, (const bf16_t*)src, cu, M, C, dst);
+  return (int)hipGetLastError();
+}
+
+SSAMD_API int ssamd_resblock_layer_pk(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
+                                      const float* b2, const bf16_t* acc_in, bf16_t* out, const int* tt, int ntt, int C,
+                                      int K, int d, float slope, float out_scale, int post_lrelu, hipStream_t s) {
+  if (d < 1 || d > MAXD || !tt) return -2;
+  if (ntt <= 0) return 0;
+  const int4* t4 = reinterpret_cast<const int4*>(tt);
+#define RBK_CASE(CC, KK) \
+  if (C == CC && K == KK) \
+    return launch_rb<CC, KK>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, ntt);
+  RBK_CASE(32, 3) RBK_CASE(32, 7) RBK_CASE(32, 11)
+  RBK_CASE(64, 3) RBK_CASE(64, 7) RBK_CASE(64, 11)
+  RBK_CASE(128, 3) RBK_CASE(128, 7) RBK_CASE(128, 11)
+#undef RBK_CASE
+  return -2;
+}
+
+SSAMD_API int ssamd_resblock_fused_pk(const bf16_t* x, const bf16_t* w0, const bf16_t* w1, const bf16_t* w2,
+                                      const bf16_t* w3, const bf16_t* w4, const bf16_t* w5, const float* b0,
+                                      const float* b1, const float* b2, const float* b3, const float* b4,
+                                      const float* b5, const bf16_t* acc_in, bf16_t* out, const int* tt, int ntt, int C,
+                                      int K, int d0, int d1, int d2, float slope, float out_scale, int post_lrelu,
+                                      hipStream_t s) {
+  const int dd[3] = {d0, d1, d2};
+  for (int i = 0; i < 3; ++i)
+    if (dd[i] < 1 || dd[i] > MAXD) return -2;
+  if (x == out || !tt) return -2;
+  if (ntt <= 0) return 0;
+  const int4* t4 = reinterpret_cast<const int4*>(tt);
+  RFW p = {{w0, w1, w2, w3, w4, w5}, {b0, b1, b2, b3, b4, b5}, {d0, d1, d2}};
+#define RFK_CASE(CC, KK) \
+  if (C == CC && K == KK) return launch_rf<CC, KK>(x, p, acc_in, out, 1, 1, slope, out_scale, post_lrelu, s, t4, ntt);
+  RFK_CASE(32, 3) RFK_CASE(32, 7) RFK_CASE(32, 11) RFK_CASE(64, 3) RFK_CASE(64, 7) RFK_CASE(128, 3)
+#undef RFK_CASE
+  return -2;
+}
+
+SSAMD_API int ssamd_conv3_sq_pk(const bf16_t* x, const bf16_t* w, const float* bias, bf16_t* out, const int* tt, int ntt,
+                                int C, hipStream_t s) {
+  if (x == out || !x || !w || !bias || !out || !tt) return -2;
+  if (ntt <= 0) return 0;
+  const int4* t4 = reinterpret_cast<const int4*>(tt);
+  if (C == 128) return launch_c3<128>(x, w, bias, out, 1, 0, s, t4, ntt);
+  if (C == 64) return launch_c3<64>(x, w, bias, out, 1, 0, s, t4, ntt);
+  return -2;
+}
 
 
 // Whole ResBlock1 (see resblock_fused_kernel).  x / out / acc_in [B, T, C] bf16 (out must not alias x;
@@ -1006,7 +1160,8 @@ SSAMD_API int ssamd_resblock_layer_prof(const bf16_t* x, const bf16_t* w1, const
     const int tiles = (T + R::BM - 1) / R::BM;                                                                \
     const int g = grid > 0 && grid < B * tiles ? grid : B * tiles;                                            \
     hipLaunchKernelGGL((resblock_layer_kernel<CC, KK, true>), dim3(g), dim3(R::NT), R::LDS, s, x,              \
-                       w1, b1, w2, b2, acc_in, out, T, tiles, B * tiles, d, slope, out_scale, post_lrelu, prof); \
+                       w1, b1, w2, b2, acc_in, out, T, tiles, B * tiles, d, slope, out_scale, post_lrelu,      \
+                       (const int4*)nullptr, prof);                                                           \
     return (int)hipGetLastError();                                                                            \
   }
   if (d < 1 || d > MAXD) return -2;

@@ -315,8 +315,8 @@ def synth_phase(args, rank, world, device):
         out = model(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
         mel, mel_len = out[1], out[9]
         lens = mel_len.cpu()  # host lengths: the vocoder runs length-bucketed (exact on valid samples)
-        if cuda:  # int16 conversion fused into the vocoder's conv_post kernel
-            mel_b = mel.to(torch.bfloat16).contiguous()
+        if cuda:  # int16 conversion fused into the vocoder's conv_post kernel; the pack kernel casts fp32 -> bf16
+            mel_b = mel.contiguous()
             if stream is not None:
                 stream.wait_stream(torch.cuda.current_stream())
                 mel_b.record_stream(stream)  # the main stream's allocator must not recycle it early

@@ -193,6 +193,43 @@ class ResBlock1(nn.Module):
         return _lrelu(x) if post_lrelu else x
 
 
+    def forward_packed(self, x, vp, rate, acc=None, out_scale=1.0, x_act=None, post_lrelu=False):
+        """``forward_cl`` on packed rows x [R*rate, C] (``hip.VocPack``: every conv zero-pads at its own
+        utterance's ends, so each utterance is vocoded exactly as alone, with no padded rows)."""
+        hip = ops._hip()
+        k = self.kernel_size
+        n = len(self.convs1)
+        C = x.shape[-1]
+        if self.fusable(C):
+            if _WHOLE_BLOCK[0] and n == 3 and hip.resblock_fusable(C, k):
+                return hip.resblock_fused_packed(x, vp, rate, self.convs1, self.convs2, self.dilation, LRELU_SLOPE,
+                                                 acc=acc, out_scale=out_scale, post_lrelu=post_lrelu)
+            for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
+                last = i == n - 1
+                x = hip.resblock_layer_packed(x, vp, rate, c1, c2, d, LRELU_SLOPE, acc=acc if last else None,
+                                              out_scale=out_scale if last else 1.0, post_lrelu=post_lrelu and last)
+            return x
+        a = x_act if x_act is not None else _lrelu(x)
+        for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
+            t = hip.conv1d_infer_packed(a, vp, rate, _w(c1), c1.bias, get_padding(k, d), d, "lrelu")
+            if i < n - 1:
+                x, a = hip.conv1d_infer_packed(t, vp, rate, _w(c2), c2.bias, get_padding(k, 1), 1, None, resid=x,
+                                               dual_lrelu=True)
+            else:
+                x = hip.conv1d_infer_packed(t, vp, rate, _w(c2), c2.bias, get_padding(k, 1), 1, None, resid=x, acc=acc,
+                                            scale=out_scale, post_act="lrelu" if post_lrelu else None)
+        return x
+
+    def packed_tiles(self, C: int, rate: int):
+        """(rate, tile rows) pairs of this block's tiled kernels at channel width C."""
+        hip = ops._hip()
+        if not self.fusable(C):
+            return []
+        if _WHOLE_BLOCK[0] and len(self.convs1) == 3 and hip.resblock_fusable(C, self.kernel_size):
+            return [(rate, hip.voc_tile_rows(1, C, self.kernel_size, self.dilation))]
+        return [(rate, hip.voc_tile_rows(0, C, self.kernel_size))]
+
+
 def _lrelu(x, slope=LRELU_SLOPE):
     return F.leaky_relu(x, slope)
 
@@ -336,7 +373,16 @@ class Generator(nn.Module):
         ``max_len + receptive_radius()`` frames, instead of the whole padded batch.  Exact for the
         valid samples ``[0, lengths[b] * hop)``: their dependency cone never reaches the truncation
         point (``tests/test_vocoder_buckets_cpu.py``); samples past a group's width are zero.  The
-        reference vocodes the padded batch and trims (``utils/model.py:97-115``)."""
+        reference vocodes the padded batch and trims (``utils/model.py:97-115``).
+
+        On the GPU with ``lengths`` the batch is vocoded PACKED instead (``infer_packed``, ``_PACKED``): every
+        utterance exactly as if alone, no padded rows; its samples past ``lengths[b] * hop`` are zero."""
+        if (lengths is not None and _PACKED[0] and mel_cl.is_cuda and ops.use_hip(mel_cl)
+                and mel_cl.dtype in (torch.float32, torch.bfloat16) and self.packable()):
+            hop = 1
+            for u in self.h.upsample_rates:
+                hop *= u
+            return self.infer_packed(mel_cl, lengths, int16_scale, width=mel_cl.shape[1] * hop)
         if lengths is not None and mel_cl.shape[0] > 1:
             B, T, _ = mel_cl.shape
             groups = self.length_buckets([int(v) for v in lengths], T, self.receptive_radius(), max_buckets,
@@ -442,6 +488,87 @@ class Generator(nn.Module):
             y = (y * int16_scale).clamp(-32768, 32767).to(torch.int16)
         return y
 
+    # ------------------------------------------------------------------ packed (length-exact) inference
+    def packable(self) -> bool:
+        """Every upsampler has the 3-tap form and conv_post the VALU kernel: ``infer_packed`` applies."""
+        c_last = self.h.upsample_initial_channel // 2 ** self.num_upsamples
+        return c_last in (8, 32) and all(self._ups_image(i) is not None for i in range(self.num_upsamples))
+
+    @torch.no_grad()
+    def infer_packed(self, mel: torch.Tensor, lengths, int16_scale=None, width=None) -> torch.Tensor:
+        """mel [B, M, n_mel] (padded, channel-last, fp32 / bf16) + host frame ``lengths`` -> wav [B, W] (W = ``width``
+        or max(lengths) * hop; int16 when ``int16_scale``), samples past ``lengths[b] * hop`` zero.
+
+        The utterances' valid frames are packed back to back ([R, C] rows per stage, ``hip.VocPack``) and every
+        kernel zero-pads each conv at the utterance's own ends (the GEMM stages through a per-row position table,
+        the tiled ResBlock / upsampler / conv_post kernels through per-tile tables whose tiles never straddle two
+        utterances), so each utterance is vocoded exactly as if alone -- the reference vocodes the padded batch
+        and trims (``utils/model.py:97-115``) -- with no padded rows at any stage and one launch per layer for the
+        whole batch (the length-bucketed ``infer`` pads each bucket to its longest utterance + the receptive radius:
+        ~10 % extra rows at 8 buckets, and 8x the launches)."""
+        hip = ops._hip()
+        dev = mel.device
+        B = mel.shape[0]
+        lens = [max(0, min(int(v), mel.shape[1])) for v in lengths]
+        hop = 1
+        for u in self.h.upsample_rates:
+            hop *= u
+        W = int(width) if width is not None else max(lens) * hop
+        nk = self.num_kernels
+        # every (rate, tile height) the tiled kernels will ask for: one host-built table buffer, one H2D copy
+        geoms, rate = [], 1
+        for i in range(self.num_upsamples):
+            up = self.ups[i]
+            s = up.stride[0]
+            blocks = [self.resblocks[i * nk + j] for j in range(nk)]
+            wu, _, bt = self._ups_image(i)
+            cout = wu.shape[0] // s
+            if blocks[0].fusable(cout) and _CONV3_SQ[0] and bt is not None and wu.shape[0] == wu.shape[1] in (64, 128):
+                geoms.append((rate, hip.voc_tile_rows(2, wu.shape[1])))
+            rate *= s
+            for blk in blocks:
+                geoms.extend(blk.packed_tiles(cout, rate))
+        c_last = self.h.upsample_initial_channel // 2 ** self.num_upsamples
+        geoms.append((rate, hip.voc_tile_rows(3, c_last)))
+        vp = hip.VocPack(lens, dev, geoms)
+        out = torch.zeros(B, W, device=dev, dtype=torch.int16 if int16_scale is not None else torch.float32)
+        if vp.R == 0:
+            return out
+        x = hip.voc_pack(mel, vp)
+        x = hip.conv1d_infer_packed(x, vp, 1, _w(self.conv_pre), self.conv_pre.bias, 3, 1, "lrelu")
+        rate = 1
+        for i in range(self.num_upsamples):
+            up = self.ups[i]
+            s = up.stride[0]
+            blocks = [self.resblocks[i * nk + j] for j in range(nk)]
+            wu, wimg, bt = self._ups_image(i)
+            cout = wu.shape[0] // s
+            fused = blocks[0].fusable(cout)
+            x_act = None
+            if fused and _CONV3_SQ[0] and bt is not None and wu.shape[0] == wu.shape[1] in (64, 128):
+                y = hip.conv3_sq_packed(x, vp, rate, wimg, bt)
+            else:
+                ks_ = (s // 2) * cout if (_CONVT_KSPLIT[0] and up.kernel_size[0] == 2 * s
+                                          and up.padding[0] * 2 == s) else 0
+                if fused:
+                    y = hip.conv1d_infer_packed(x, vp, rate, wu, bt, 1, 1, None, wimg=wimg, ksplit=ks_)
+                else:
+                    y, x_act = hip.conv1d_infer_packed(x, vp, rate, wu, bt, 1, 1, None, wimg=wimg, dual_lrelu=True,
+                                                       ksplit=ks_)
+            # [R*rate, s*Cout] rows ARE the interleaved [R*rate*s, Cout] rows (each utterance's block stays whole)
+            rate *= s
+            y = y.view(vp.R * rate, cout)
+            if x_act is not None:
+                x_act = x_act.view(vp.R * rate, cout)
+            post = i < self.num_upsamples - 1
+            xs = None
+            for j, blk in enumerate(blocks):
+                last = j == nk - 1
+                xs = blk.forward_packed(y, vp, rate, acc=xs, out_scale=(1.0 / nk) if last else 1.0, x_act=x_act,
+                                        post_lrelu=post and last)
+            x = xs
+        return hip.conv_post_packed(x, vp, rate, _w(self.conv_post), self.conv_post.bias, out, 0.01, int16_scale)
+
     def fold_weight_norm(self):
         for m in self.modules():
             if isinstance(m, (nn.Conv1d, nn.ConvTranspose1d)) and hasattr(m, "weight_g"):
@@ -451,6 +578,8 @@ class Generator(nn.Module):
     remove_weight_norm = fold_weight_norm
 
 
+# GPU inference with host lengths: the packed, length-exact path (infer_packed) instead of length buckets
+_PACKED = [True]
 # square upsamplers (N = stride * Cout = Cin in {64, 128}) on ``hip.conv3_sq`` instead of the generic GEMM
 _CONV3_SQ = [True]
 # the other upsamplers' 3-tap GEMM skips each 256-column tile's all-zero tap (ConvGeom::ksplit in csrc/k_gemm.hip)

@@ -2211,6 +2211,186 @@ def resblock_fused(x, convs1, convs2, dilations, slope, acc=None, out_scale=1.0,
     return out
 
 
+# ------------------------------------------------------------------------ packed (length-exact) vocoder
+_SIGS.update({"ssamd_voc_tile_rows": [I, I, I, I, I, I],
+              "ssamd_voc_rinfo": [P, I, I, I, P, P],
+              "ssamd_voc_pack": [P, I, P, I, I, I, P, P],
+              "ssamd_resblock_layer_pk": [P, P, P, P, P, P, P, P, I, I, I, I, F, F, I, P],
+              "ssamd_resblock_fused_pk": [P] * 16 + [I, I, I, I, I, I, F, F, I, P],
+              "ssamd_conv3_sq_pk": [P, P, P, P, P, I, I, P],
+              "ssamd_conv_post_pk": [P, P, P, P, I, I, F, F, P, P, L_, P],
+              "ssamd_conv_post_tile_rows": [],
+              "ssamd_conv_gemm_ex3": [P, P, P, P, P, I, I, I, I, I, I, I, P, P, F, I, I, P, P]})
+
+
+class VocPack:
+    """Row layout of a packed vocoder batch: sequence b's frames at rows ``cu[b] .. cu[b+1]-1`` of every stage
+    (times the stage's rate), no padding.  ``tiles(kind, rate, BM)`` returns (device int32 [n, 4] table, n) of the
+    tiled kernels' work items -- {first row of the sequence, its rows, t0, sequence} per tile of BM rows at that
+    rate, tiles never straddling two sequences -- and ``rinfo(rate)`` the per-row {position, length} table of the
+    GEMM stages; both are built once per batch and cached per key.  The host knows the lengths (they sized the
+    batch), so the tables cost no device sync: all of them go up in ONE pinned host-to-device copy."""
+
+    def __init__(self, lens, device, rate_tiles):
+        import numpy as np
+
+        self.lens = np.asarray([int(v) for v in lens], dtype=np.int64)
+        self.B = len(self.lens)
+        self.R = int(self.lens.sum())
+        self.device = device
+        cu = np.zeros(self.B + 1, dtype=np.int64)
+        cu[1:] = np.cumsum(self.lens)
+        self.cu_host = cu
+        # every (rate, BM) tile table the caller will ask for, laid out back to back in one int32 buffer
+        parts, self._off = [cu.astype(np.int32)], {}
+        o = self.B + 1
+        for rate, bm in rate_tiles:
+            key = (int(rate), int(bm))
+            if key in self._off or bm <= 0:
+                continue
+            L = self.lens * rate
+            cnt = (L + bm - 1) // bm
+            n = int(cnt.sum())
+            u = np.repeat(np.arange(self.B), cnt)
+            first = np.zeros(self.B, dtype=np.int64)
+            first[1:] = np.cumsum(cnt)[:-1]
+            t0 = (np.arange(n) - first[u]) * bm
+            tab = np.stack([cu[u] * rate, L[u], t0, u], axis=1).astype(np.int32)
+            assert (cu[-1] * rate) < 2 ** 31, "packed vocoder: row offsets exceed int32"
+            parts.append(tab.reshape(-1))
+            self._off[key] = (o, n)
+            o += 4 * n
+        host = torch.from_numpy(np.concatenate(parts)).pin_memory() if device.type == "cuda" else \
+            torch.from_numpy(np.concatenate(parts))
+        self.buf = host.to(device, non_blocking=True)
+        self.cu = self.buf[: self.B + 1]
+        self._rinfo = {}
+
+    def tiles(self, rate, bm):
+        o, n = self._off[(int(rate), int(bm))]
+        return self.buf[o: o + 4 * n], n
+
+    def rinfo(self, rate):
+        r = self._rinfo.get(rate)
+        if r is None:
+            rows = int(self.lens.max()) * rate if self.B else 0
+            r = torch.empty(self.R * rate, 2, device=self.device, dtype=torch.int32)
+            _check(lib().ssamd_voc_rinfo(_ptr(self.cu), self.B, int(rate), rows, _ptr(r), _stream()), "ssamd_voc_rinfo")
+            self._rinfo[rate] = r
+        return r
+
+
+def voc_tile_rows(kind: int, C: int, K: int = 0, dil=(0, 0, 0)) -> int:
+    """Tile height of a tiled vocoder kernel (0 resblock_layer, 1 resblock_fused, 2 conv3_sq, 3 conv_post)."""
+    if kind == 3:
+        return int(lib().ssamd_conv_post_tile_rows())
+    d0, d1, d2 = (int(v) for v in dil)
+    return int(lib().ssamd_voc_tile_rows(int(kind), int(C), int(K), d0, d1, d2))
+
+
+def voc_pack(mel, vp: "VocPack"):
+    """[B, M, C] (fp32 / bf16) -> [R, C] bf16 valid rows in the VocPack order."""
+    B, M, C = mel.shape
+    src = mel.contiguous()
+    f32 = src.dtype == torch.float32
+    if not f32:
+        _need(src, torch.bfloat16, "voc_pack.src")
+    out = torch.empty(vp.R, C, device=mel.device, dtype=torch.bfloat16)
+    _check(lib().ssamd_voc_pack(_ptr(src), int(f32), _ptr(vp.cu), B, M, C, _ptr(out), _stream()), "ssamd_voc_pack")
+    return out
+
+
+def conv1d_infer_packed(x, vp, rate, w, b, pad, dil, act=None, resid=None, acc=None, scale=1.0, post_act=None,
+                        dual_lrelu=False, wimg=None, ksplit=0):
+    """``conv1d_infer`` on packed rows x [R*rate, Cin]: every conv zero-pads at its own sequence's ends."""
+    Rr, Cin = x.shape
+    ks = 1 if w.dim() == 2 else w.shape[2]
+    N = w.shape[0]
+    bf = None if b is None else b.detach().float().contiguous()
+    wi = weight_fwd(w) if wimg is None else wimg
+    xc = x.contiguous()
+    _need(xc, torch.bfloat16, "conv_pk.x")
+    _need(wi, torch.bfloat16, "conv_pk.w")
+    assert Rr == vp.R * rate and wi.numel() == N * ks * Cin and N % 8 == 0 and Cin % 8 == 0, "conv_pk: shape"
+    for t in (resid, acc):
+        if t is not None:
+            _need(t, torch.bfloat16, "conv_pk.operand")
+            assert t.numel() == Rr * N, "conv_pk: operand shape"
+    y = acc if acc is not None else torch.empty(Rr, N, device=x.device, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y) if dual_lrelu else None
+    ri = vp.rinfo(rate)
+    rc = lib().ssamd_conv_gemm_ex3(_ptr(xc), _ptr(wi), _ptr(bf), _ptr(resid), _ptr(y), Rr, Cin, ks, dil, pad, N,
+                                   _ACT[act], _ptr(acc), _ptr(y2), float(scale), _ACT[post_act], int(ksplit), _ptr(ri),
+                                   _stream())
+    _check(rc, "ssamd_conv_gemm_ex3")
+    return (y, y2) if dual_lrelu else y
+
+
+def resblock_layer_packed(x, vp, rate, c1, c2, d, slope, acc=None, out_scale=1.0, post_lrelu=False):
+    """``resblock_layer`` on packed rows x [R*rate, C]."""
+    _need(x, torch.bfloat16, "resblock.x")
+    Rr, C = x.shape
+    K = c1.weight.shape[2]
+    w1, w2 = weight_fwd(c1.weight), weight_fwd(c2.weight)
+    b1 = c1.bias.detach().float().contiguous()
+    b2 = c2.bias.detach().float().contiguous()
+    out = acc if acc is not None else torch.empty_like(x)
+    tt, n = vp.tiles(rate, voc_tile_rows(0, C, K))
+    rc = lib().ssamd_resblock_layer_pk(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(acc), _ptr(out), _ptr(tt),
+                                       n, C, K, int(d), float(slope), float(out_scale), int(bool(post_lrelu)), _stream())
+    _check(rc, "ssamd_resblock_layer_pk")
+    return out
+
+
+def resblock_fused_packed(x, vp, rate, convs1, convs2, dilations, slope, acc=None, out_scale=1.0, post_lrelu=False):
+    """``resblock_fused`` on packed rows x [R*rate, C]."""
+    _need(x, torch.bfloat16, "resblock.x")
+    Rr, C = x.shape
+    K = convs1[0].weight.shape[2]
+    ws, bs = [], []
+    for c1, c2 in zip(convs1, convs2):
+        for c in (c1, c2):
+            ws.append(weight_fwd(c.weight))
+            bs.append(c.bias.detach().float().contiguous())
+    out = acc if acc is not None else torch.empty_like(x)
+    d0, d1, d2 = (int(v) for v in dilations)
+    tt, n = vp.tiles(rate, voc_tile_rows(1, C, K, (d0, d1, d2)))
+    rc = lib().ssamd_resblock_fused_pk(_ptr(x), *[_ptr(w) for w in ws], *[_ptr(b) for b in bs], _ptr(acc), _ptr(out),
+                                       _ptr(tt), n, C, K, d0, d1, d2, float(slope), float(out_scale),
+                                       int(bool(post_lrelu)), _stream())
+    _check(rc, "ssamd_resblock_fused_pk")
+    return out
+
+
+def conv3_sq_packed(x, vp, rate, wimg, bias):
+    Rr, C = x.shape
+    out = torch.empty_like(x)
+    tt, n = vp.tiles(rate, voc_tile_rows(2, C))
+    _check(lib().ssamd_conv3_sq_pk(_ptr(x), _ptr(wimg), _ptr(bias), _ptr(out), _ptr(tt), n, C, _stream()),
+           "ssamd_conv3_sq_pk")
+    return out
+
+
+def conv_post_packed(x, vp, rate, w, b, out, slope=0.01, int16_scale=None):
+    """conv_post on packed rows x [R*rate, C] into out [B, W] (sample t of sequence u at out[u, t]; the caller
+    zero-fills out)."""
+    Rr, C = x.shape
+    wf = w.detach().reshape(-1).float().contiguous()
+    bf = None if b is None else b.detach().reshape(-1).float().contiguous()
+    tt, n = vp.tiles(rate, voc_tile_rows(3, C))
+    assert out.shape[0] == vp.B and out.shape[1] >= int(vp.lens.max()) * rate, "conv_post_packed: output shape"
+    if int16_scale is None:
+        assert out.dtype == torch.float32
+        rc = lib().ssamd_conv_post_pk(_ptr(x), _ptr(wf), _ptr(bf), _ptr(tt), n, C, float(slope), 1.0, _ptr(out), None,
+                                      out.stride(0), _stream())
+    else:
+        assert out.dtype == torch.int16
+        rc = lib().ssamd_conv_post_pk(_ptr(x), _ptr(wf), _ptr(bf), _ptr(tt), n, C, float(slope), float(int16_scale),
+                                      None, _ptr(out), out.stride(0), _stream())
+    _check(rc, "ssamd_conv_post_pk")
+    return out
+
+
 def conv1d_infer(x, w, b, pad, dil, act=None, resid=None, acc=None, scale=1.0, post_act=None, dual_lrelu=False,
                  wimg=None, ksplit=0):
     """Inference conv (no autograd), channel-last bf16, everything in the GEMM epilogue:

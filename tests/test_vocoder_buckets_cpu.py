@@ -69,3 +69,29 @@ def test_bucket_dp_is_optimal_small():
             edges = (0,) + cuts + (9,)
             best = min(best, sum((edges[j + 1] - edges[j]) * min(T, s[edges[j + 1] - 1] + halo) + c for j in range(m)))
     assert got == best
+
+
+def test_vocpack_tile_tables_cover_each_utterance_exactly():
+    """hip.VocPack (the packed vocoder's work tables): per (rate, tile rows) every utterance's rows [0, L*rate) are
+    covered by consecutive tiles of its own (t0 = 0, BM, 2BM, ...; never straddling two utterances), row offsets are
+    the packed prefix sums, and the whole set lives in one buffer (one host-to-device copy)."""
+    import numpy as np
+    import torch
+
+    from speakingstyle_amd.ops.hip import VocPack
+
+    lens = [300, 41, 0, 170, 1, 90]
+    geoms = [(1, 256), (64, 118), (256, 408), (64, 118)]  # duplicate key: built once
+    vp = VocPack(lens, torch.device("cpu"), geoms)
+    assert vp.R == sum(lens) and vp.cu.tolist() == [0, 300, 341, 341, 511, 512, 602]
+    for rate, bm in geoms:
+        tab, n = vp.tiles(rate, bm)
+        t = tab.view(n, 4).numpy()
+        assert n == sum(-(-L * rate // bm) for L in lens)
+        for u, L in enumerate(lens):
+            mine = t[t[:, 3] == u]
+            assert len(mine) == -(-L * rate // bm)
+            if L:
+                assert (mine[:, 0] == vp.cu_host[u] * rate).all() and (mine[:, 1] == L * rate).all()
+                assert mine[:, 2].tolist() == list(range(0, L * rate, bm))
+        assert np.all(np.diff(t[:, 3]) >= 0)  # utterance-major

@@ -105,21 +105,24 @@ def test_bc2013_fs2_vocoder_int16_e2e_vs_fp32_oracle():
         model.set_compute_dtype(torch.bfloat16)
         out = model(*args)
         mel_hip, len_hip = out[1], out[9]
-        # the bench's synthesis path: length-bucketed vocoding (forced to split even this small batch)
-        pcm_hip = voc.infer(mel_hip.to(torch.bfloat16).contiguous(), int16_scale=mx, lengths=len_hip.tolist(),
-                            max_buckets=4, bucket_cost=0)
+        # the bench's synthesis path: the packed, length-exact vocoder (each utterance vocoded as if alone)
+        pcm_hip = voc.infer(mel_hip, int16_scale=mx, lengths=len_hip.tolist())
+    lens = len_hip.tolist()
+    # fp32 oracle per utterance, alone (the reference's batch-1 synthesis: synthesize.py single mode)
+    one = lambda m, i: m[i:i + 1, : lens[i]]  # noqa: E731
     with torch_fp32_only(), torch.no_grad():
         model.set_compute_dtype(torch.float32)
         out_r = model(*args)
         mel_ref, len_ref = out_r[1], out_r[9]
-        wav_ref = voc(mel_ref.transpose(1, 2)).squeeze(1)
-        pcm_ref = (wav_ref * mx).clamp(-32768, 32767).to(torch.int16)
+        wav_ref = [voc(one(mel_ref, i).transpose(1, 2)).reshape(-1) for i in range(len(lens))]
+        pcm_ref = [(w * mx).clamp(-32768, 32767).to(torch.int16) for w in wav_ref]
         # the FS2 error propagated through the fp32 generator
-        wav_prop = voc(mel_hip.float().transpose(1, 2)).squeeze(1)
+        wav_prop = [voc(one(mel_hip, i).float().transpose(1, 2)).reshape(-1) for i in range(len(lens))]
     with torch.no_grad():
-        wav_voc = voc.infer(mel_ref.to(torch.bfloat16).contiguous()).float()
+        wav_voc = [voc.infer(one(mel_ref, i).to(torch.bfloat16).contiguous()).float().reshape(-1)
+                   for i in range(len(lens))]
     assert torch.equal(len_hip.cpu(), len_ref.cpu())
-    assert pcm_hip.shape == pcm_ref.shape
+    assert pcm_hip.shape == (len(lens), mel_hip.shape[1] * 256)
     # Error budget per utterance (relative L2 over its valid samples).  By the triangle inequality
     #   e_total = |pcm_hip - pcm_ref| <= e_voc + e_prop + e_q (+ the vocoder's error difference between
     #   its two inputs, second order), with
@@ -136,11 +139,12 @@ def test_bc2013_fs2_vocoder_int16_e2e_vs_fp32_oracle():
     report = []
     for i, n in enumerate(len_ref.tolist()):
         a = pcm_hip[i, : n * hop].float()
-        r = pcm_ref[i, : n * hop].float()
+        r = pcm_ref[i].float()
+        assert not pcm_hip[i, n * hop:].any()  # past its length: zero
         e_total = _rel(a, r)
-        e_voc = _rel(wav_voc[i, : n * hop], wav_ref[i, : n * hop])
-        e_prop = _rel(wav_prop[i, : n * hop], wav_ref[i, : n * hop])
-        rms = wav_ref[i, : n * hop].float().pow(2).mean().sqrt().item()
+        e_voc = _rel(wav_voc[i], wav_ref[i])
+        e_prop = _rel(wav_prop[i], wav_ref[i])
+        rms = wav_ref[i].float().pow(2).mean().sqrt().item()
         e_q = (2 * 0.5 / mx) / max(rms, 1e-12) / (12 ** 0.5)
         report.append((round(e_total, 4), round(e_voc, 4), round(e_prop, 4), round(e_q, 6)))
         assert e_voc < 5e-2, report
@@ -149,10 +153,45 @@ def test_bc2013_fs2_vocoder_int16_e2e_vs_fp32_oracle():
         assert e_total < 8e-2, report
 
 
+def test_packed_vocoding_equals_each_utterance_alone():
+    """The packed, length-exact vocoder (``Generator.infer_packed``: all utterances' rows back to back, every conv
+    zero-padding at its own utterance's ends through row / tile tables) against each utterance vocoded ALONE on the
+    padded HIP path (B = 1, no lengths): the same samples up to fp32 summation order (the GEMM stages may pick a
+    different tile / split-K variant for the smaller M; the tiled ResBlock kernels start their tiles at each
+    utterance's row 0 in both) -- and zeros past each length; plus the fp32 oracle per utterance."""
+    from speakingstyle_amd.models import hifigan as H
+
+    g = _generator(9)
+    assert g.packable()
+    lengths = [300, 41, 170, 90, 260, 12, 1, 333]
+    B, T = len(lengths), max(lengths) + 7
+    torch.manual_seed(5)
+    mel = torch.randn(B, T, 80, device=DEV) * 2 - 5  # fp32 in: packed to bf16 rows by the pack kernel
+    with torch.no_grad():
+        pk = g.infer(mel, int16_scale=32768.0, lengths=lengths)
+        pkf = g.infer_packed(mel, lengths)
+        assert pk.shape == (B, T * 256) and pk.dtype == torch.int16 and pkf.shape == (B, max(lengths) * 256)
+        for i, n in enumerate(lengths):
+            alone = g.infer(mel[i:i + 1, :n].to(torch.bfloat16).contiguous(), int16_scale=32768.0)[0]
+            assert _rel(pk[i, : n * 256], alone) < 1e-2, (i, _rel(pk[i, : n * 256], alone))
+            assert not pk[i, n * 256:].any()
+            alone_f = g.infer(mel[i:i + 1, :n].to(torch.bfloat16).contiguous())[0]
+            assert _rel(pkf[i, : n * 256], alone_f) < 1e-2, (i, _rel(pkf[i, : n * 256], alone_f))
+    with torch_fp32_only(), torch.no_grad():
+        refs = [g(mel[i:i + 1, :n].transpose(1, 2)).reshape(-1) for i, n in enumerate(lengths)]
+    for i, n in enumerate(lengths):
+        if n >= 8:
+            assert _rel(pkf[i, : n * 256], refs[i]) < 5e-2, (i, _rel(pkf[i, : n * 256], refs[i]))
+    # the bucketed path stays available (reference padded-batch semantics) behind the switch
+    assert H._PACKED[0]
+
+
 def test_bucketed_vocoding_matches_padded_batch():
     """Length buckets (each group truncated at max_len + receptive radius) vs the padded batch on
     the same HIP kernels: the valid samples agree (the GEMMs are row-independent; only a different
     tile / split choice for the smaller M may reorder fp32 sums)."""
+    from speakingstyle_amd.models import hifigan as H
+
     g = _generator(3)
     lengths = [300, 41, 170, 90, 260, 12]
     B, T = len(lengths), max(lengths)
@@ -160,7 +199,11 @@ def test_bucketed_vocoding_matches_padded_batch():
     mel = (torch.randn(B, T, 80, device=DEV) * 2 - 5).to(torch.bfloat16)
     with torch.no_grad():
         pad = g.infer(mel, int16_scale=32768.0)
-        buck = g.infer(mel, int16_scale=32768.0, lengths=lengths, max_buckets=4, bucket_cost=0)
+        H._PACKED[0] = False  # the bucketed path (packed vocoding has per-utterance semantics instead)
+        try:
+            buck = g.infer(mel, int16_scale=32768.0, lengths=lengths, max_buckets=4, bucket_cost=0)
+        finally:
+            H._PACKED[0] = True
     assert len(g.length_buckets(lengths, T, g.receptive_radius(), 4, 0)) == 4
     assert buck.shape == pad.shape and buck.dtype == torch.int16
     for i, n in enumerate(lengths):

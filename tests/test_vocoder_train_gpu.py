@@ -168,11 +168,20 @@ def test_g_adv_grad_vs_torch(post_gain):
     _, g_, fr, fg = mpd(y.unsqueeze(1), yh.unsqueeze(1))
     _, g2, fr2, fg2 = msd(y.unsqueeze(1), yh.unsqueeze(1))
     loss_ref = H.generator_loss(g_)[0] + H.generator_loss(g2)[0] + H.feature_loss(fr, fg) + H.feature_loss(fr2, fg2)
-    (dref,) = torch.autograd.grad(loss_ref, [yh])
+    (dref,) = torch.autograd.grad(loss_ref, [yh], retain_graph=post_gain != 1.0)
     dy = torch.zeros(B, T, device="cuda")
     loss = HT.g_adv(mpd, msd, y, yh0, dy)
     assert abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()) < 2e-2, (loss.item(), loss_ref.item())
-    assert _rel(dy, dref) < 5e-2, _rel(dy, dref)
+    # the boosted score term's gradient runs back through every discriminator layer in bf16: ~8 % vs fp32 torch
+    tol = 5e-2 if post_gain == 1.0 else 0.12
+    assert _rel(dy, dref) < tol, _rel(dy, dref)
+    if post_gain != 1.0:
+        # discriminating power: the objective WITHOUT the score-map feature term is far from both
+        no_score = (H.generator_loss(g_)[0] + H.generator_loss(g2)[0] + H.feature_loss([f[:-1] for f in fr],
+                    [f[:-1] for f in fg]) + H.feature_loss([f[:-1] for f in fr2], [f[:-1] for f in fg2]))
+        (dref_ns,) = torch.autograd.grad(no_score, [yh])
+        assert _rel(dref_ns, dref) > 3 * tol and _rel(dy, dref_ns) > 3 * tol, (_rel(dref_ns, dref), _rel(dy, dref_ns))
+        assert abs(no_score.item() - loss_ref.item()) / abs(loss_ref.item()) > 0.1
 
 
 @pytest.mark.parametrize("T", [8192, 8192 + 512])
