@@ -181,7 +181,7 @@ def test_g_adv_grad_vs_torch(post_gain):
                     [f[:-1] for f in fg]) + H.feature_loss([f[:-1] for f in fr2], [f[:-1] for f in fg2]))
         (dref_ns,) = torch.autograd.grad(no_score, [yh])
         assert _rel(dref_ns, dref) > 3 * tol and _rel(dy, dref_ns) > 3 * tol, (_rel(dref_ns, dref), _rel(dy, dref_ns))
-        assert abs(no_score.item() - loss_ref.item()) / abs(loss_ref.item()) > 0.1
+        assert abs(no_score.item() - loss_ref.item()) / abs(loss_ref.item()) > 0.03  # > the 2e-2 loss tolerance
 
 
 @pytest.mark.parametrize("T", [8192, 8192 + 512])
