@@ -530,7 +530,7 @@ class Generator(nn.Module):
                 geoms.extend(blk.packed_tiles(cout, rate))
         c_last = self.h.upsample_initial_channel // 2 ** self.num_upsamples
         geoms.append((rate, hip.voc_tile_rows(3, c_last)))
-        vp = hip.VocPack(lens, dev, geoms)
+        vp = hip.voc_pack_for(lens, dev, geoms)
         out = torch.zeros(B, W, device=dev, dtype=torch.int16 if int16_scale is not None else torch.float32)
         if vp.R == 0:
             return out

@@ -12,6 +12,7 @@ once per optimizer step and cached on the parameter's version counter.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import sysconfig
 import math
@@ -2280,12 +2281,39 @@ class VocPack:
         return r
 
 
+_VOC_PACKS = collections.OrderedDict()  # (device, lengths, geometries) -> VocPack: tables of a repeated length set
+
+
+def voc_pack_for(lens, device, rate_tiles, cache: int = 32) -> "VocPack":
+    """A VocPack for these lengths, reused when the same length set comes back (batch-1 serving repeats lengths;
+    the tables depend on the lengths only, never on the data, and are never written after they are built)."""
+    key = (str(device), tuple(int(v) for v in lens), tuple(rate_tiles))
+    vp = _VOC_PACKS.get(key)
+    if vp is not None:
+        _VOC_PACKS.move_to_end(key)
+        return vp
+    vp = VocPack(lens, device, rate_tiles)
+    _VOC_PACKS[key] = vp
+    while len(_VOC_PACKS) > cache:
+        _VOC_PACKS.popitem(last=False)
+    return vp
+
+
+_TILE_ROWS = {}
+
+
 def voc_tile_rows(kind: int, C: int, K: int = 0, dil=(0, 0, 0)) -> int:
     """Tile height of a tiled vocoder kernel (0 resblock_layer, 1 resblock_fused, 2 conv3_sq, 3 conv_post)."""
-    if kind == 3:
-        return int(lib().ssamd_conv_post_tile_rows())
-    d0, d1, d2 = (int(v) for v in dil)
-    return int(lib().ssamd_voc_tile_rows(int(kind), int(C), int(K), d0, d1, d2))
+    key = (kind, C, K, tuple(dil))
+    v = _TILE_ROWS.get(key)
+    if v is None:
+        if kind == 3:
+            v = int(lib().ssamd_conv_post_tile_rows())
+        else:
+            d0, d1, d2 = (int(x) for x in dil)
+            v = int(lib().ssamd_voc_tile_rows(int(kind), int(C), int(K), d0, d1, d2))
+        _TILE_ROWS[key] = v
+    return v
 
 
 def voc_pack(mel, vp: "VocPack"):
