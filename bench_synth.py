@@ -33,7 +33,9 @@ def parse():
     ap.add_argument("--b1-runs", type=int, default=0, dest="synth_b1_runs", help="batch-1 latency runs (0: off)")
     ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
     ap.add_argument("--bucketed", action="store_true",
-                    help="length-bucketed vocoding instead of the packed length-exact path (A/B)")
+                    help="padded FS2 + length-bucketed vocoding instead of the packed length-exact path (A/B)")
+    ap.add_argument("--padded-fs2", action="store_false", dest="packed_fs2",
+                    help="padded FS2 decoder / PostNet, packed vocoder (A/B)")
     return ap.parse_args()
 
 
@@ -52,12 +54,14 @@ def run(args):
         from speakingstyle_amd.models import hifigan
 
         hifigan._PACKED[0] = False
+        args.packed_fs2 = False
     sy = B.synth_phase(args, rank, world, dev)
     if rank == 0:
         b1 = sy.get("b1")
         B.report({
             "b1_ms": None if b1 is None else round(1e3 * b1["median_s"], 3),
             "b1_rtf": None if b1 is None else b1["rtf"], "vocoder": "bucketed" if args.bucketed else "packed",
+            "fs2": "packed" if getattr(args, "packed_fs2", True) else "padded",
             "metric": "synth RTF (FastSpeech2 + style + HiFi-GAN, text ids -> int16 wav)",
             "value": sy["rtf"], "unit": "s wall / s audio", "higher_is_better": False, "n_gpus": world,
             "steps": args.synth_steps, "warmup": args.synth_warmup, "audio_seconds": round(sy["audio_s"], 2),

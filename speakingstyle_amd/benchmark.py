@@ -308,10 +308,25 @@ def synth_phase(args, rank, world, device):
     # work; the RTF is wall time over all audio of the timed batches (--synth-serial: one stream, A/B).
     voc_stream = torch.cuda.Stream(device=device) if (cuda and not getattr(args, "synth_serial", False)) else None
 
+    packed = cuda and getattr(args, "packed_fs2", True)
+
     @torch.no_grad()
     def synth(b, stream=voc_stream, host_wav=False):
         speakers, texts, src_lens, max_src = b[2], b[3], b[4], b[5]
         ref_mels, ref_lens, ref_max = b[6], b[7], b[8]
+        if packed and model.packed_inference_ok(texts):
+            # decoder / PostNet / vocoder on the valid frames only (FastSpeech2.infer_packed -> Generator.infer_packed)
+            rows, lens_l, _ = model.infer_packed(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
+            if stream is not None:
+                stream.wait_stream(torch.cuda.current_stream())
+                rows.record_stream(stream)
+                with torch.cuda.stream(stream):
+                    pcm = voc.infer_packed(rows, lens_l, int16_scale=mx)
+            else:
+                pcm = voc.infer_packed(rows, lens_l, int16_scale=mx)
+            if host_wav:
+                pcm = pcm.cpu()
+            return pcm, torch.tensor(lens_l)
         out = model(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
         mel, mel_len = out[1], out[9]
         lens = mel_len.cpu()  # host lengths: the vocoder runs length-bucketed (exact on valid samples)

@@ -438,3 +438,40 @@ class FastSpeech2(nn.Module):
         src_masks = ops.lengths_to_mask(src_lens, texts.shape[1])
         mel_masks = ops.lengths_to_mask(dec_lens, mel.shape[1])
         return (mel, post, p_pred, e_pred, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_lens_out)
+
+    def packed_inference_ok(self, texts) -> bool:
+        return (not self.training and ops.use_hip(texts) and self.variance_adaptor.packable()
+                and self.compute_dtype == torch.bfloat16)
+
+    @torch.no_grad()
+    def infer_packed(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None, max_mel_len=None,
+                     p_control=1.0, e_control=1.0, d_control=1.0, style_weights=None):
+        """Synthesis with predicted durations, the length-regulated half on PACKED rows: the decoder, mel_linear
+        and the PostNet run on the R = sum(mel lengths) valid frames only (``Decoder.forward_packed``,
+        ``PostNet.forward_packed``) instead of B x max(mel length) padded rows -- at batch 256 of LJSpeech-like
+        lengths ~45 % of the padded rows.  Each utterance's frames are exactly its batch-1 synthesis (every conv
+        zero-pads at its own ends; the padded reference path lets the padded frames' mel_linear bias leak into the
+        last PostNet frames of shorter utterances).  The one host sync is the same as the padded path's (the mel
+        lengths, which size the length regulator): here all B lengths come back at once.
+        Returns (post-net mel [R, n_mel] fp32 rows of utterance b at cu[b].., host lengths (list), device mel_len)."""
+        cd = self.compute_dtype
+        dev = texts.device
+        if mels is not None and max_mel_len is None:
+            max_mel_len = mels.shape[1]
+        style = self.compute_style(mels, mel_lens, max_mel_len, texts.shape[0], dev, style_weights)
+        x = self.encoder(texts, src_lens, style, cd)
+        if self.speaker_emb is not None:
+            if self.spker_embed_proj is None:
+                x = ops.add_table_rows(x, self.speaker_emb.weight, speakers)
+            else:
+                spk = self.speaker_emb(speakers) + self.spker_embed_proj(self.spker_table[speakers])
+                x = ops.add_rowvec(x, spk)
+        x, _, _, log_d, _, _ = self.variance_adaptor(x, src_lens, None, None, None, None, None, p_control,
+                                                     e_control, d_control, style, regulate=False)
+        d_rounded, mel_len = ops.duration_round(log_d, src_lens, d_control)
+        lens = [int(v) for v in mel_len.cpu().tolist()]  # the one D2H: sizes the packed decoder
+        M, R = max(lens) if lens else 0, sum(lens)
+        x, dec_lens, pk = self.decoder.forward_packed(x, d_rounded, mel_len, M, R, style)
+        mel = ops.linear(x, self.mel_linear.weight, self.mel_linear.bias).float()
+        post = self.postnet.forward_packed(mel.to(cd), pk).float() + mel
+        return post.reshape(R, -1), lens, mel_len

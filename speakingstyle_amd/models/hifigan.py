@@ -508,8 +508,11 @@ class Generator(nn.Module):
         ~10 % extra rows at 8 buckets, and 8x the launches)."""
         hip = ops._hip()
         dev = mel.device
-        B = mel.shape[0]
-        lens = [max(0, min(int(v), mel.shape[1])) for v in lengths]
+        rows_in = mel.dim() == 2  # already packed [R, n_mel] rows in ``lengths`` order (FastSpeech2.infer_packed)
+        B = len(lengths) if rows_in else mel.shape[0]
+        lens = [max(0, int(v)) for v in lengths] if rows_in else [max(0, min(int(v), mel.shape[1])) for v in lengths]
+        if rows_in:
+            assert mel.shape[0] == sum(lens), "infer_packed: packed rows vs lengths"
         hop = 1
         for u in self.h.upsample_rates:
             hop *= u
@@ -534,7 +537,7 @@ class Generator(nn.Module):
         out = torch.zeros(B, W, device=dev, dtype=torch.int16 if int16_scale is not None else torch.float32)
         if vp.R == 0:
             return out
-        x = hip.voc_pack(mel, vp)
+        x = mel.to(torch.bfloat16).contiguous() if rows_in else hip.voc_pack(mel, vp)
         x = hip.conv1d_infer_packed(x, vp, 1, _w(self.conv_pre), self.conv_pre.bias, 3, 1, "lrelu")
         rate = 1
         for i in range(self.num_upsamples):

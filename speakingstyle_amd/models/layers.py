@@ -165,3 +165,17 @@ class PostNet(nn.Module):
             bn, nxt = self.convolutions[i][1], self.convolutions[i + 1][0]
             h = ops.bn_act_conv(h, bn, self.training, True, self.dropout, nxt.conv.weight, nxt.conv.bias, nxt.pad)
         return ops.bn_act(h, self.convolutions[last][1], self.training, act_tanh=False, p=self.dropout, out_f32=True)
+
+    def forward_packed(self, x, pack):
+        """Inference on packed rows [1, R, C] (``ops/packing.py``): eval-mode BatchNorm is a per-channel affine of
+        the running statistics (row-independent) and every conv zero-pads at its own sequence's ends -- each
+        utterance's PostNet output exactly as when it is synthesized alone."""
+        assert not self.training, "PostNet.forward_packed: inference only (training BatchNorm needs the padded rows)"
+        last = len(self.convolutions) - 1
+        c0 = self.convolutions[0][0]
+        h = ops.conv1d(x, c0.conv.weight, c0.conv.bias, c0.pad, c0.dil, pack=pack)
+        for i in range(last):
+            bn, nxt = self.convolutions[i][1], self.convolutions[i + 1][0]
+            h = ops.conv1d(ops.bn_act(h, bn, False, True, 0.0), nxt.conv.weight, nxt.conv.bias, nxt.pad, nxt.dil,
+                           pack=pack)
+        return ops.bn_act(h, self.convolutions[last][1], False, act_tanh=False, p=0.0, out_f32=True)
