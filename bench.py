@@ -73,6 +73,8 @@ def parse(argv=None):
     ap.add_argument("--synth-b1-runs", type=int, default=30,
                     help="batch-1 latency runs (one ~113-frame utterance, text -> int16 wav on the host; 0 disables)")
     ap.add_argument("--synth-b1-phones", type=int, default=14, help="phonemes of the batch-1 utterance")
+    ap.add_argument("--no-synth-graphs", action="store_false", dest="synth_graphs",
+                    help="batch-1 synthesis launched eagerly instead of replayed from HIP graphs (A/B)")
     ap.add_argument("--synth-warmup", type=int, default=1)
     ap.add_argument("--frames-per-phone", type=float, default=8.1)
     ap.add_argument("--vocoder-buckets", type=int, default=8,
@@ -218,6 +220,7 @@ def run(args):
                                   "median_ms": round(1e3 * b1["median_s"], 3), "min_ms": round(1e3 * b1["min_s"], 3),
                                   "max_ms": round(1e3 * b1["max_s"], 3), "runs": b1["runs"],
                                   "mel_frames": b1["mel_frames"], "audio_seconds": round(b1["audio_s"], 4),
+                                  "hip_graphs": b1.get("graphs"),
                                   "baseline": "RTF 1.33: 113 frames, batch 1 (notebooks/control.ipynb:778)"}
         if sy2 is not None:
             rec["synth"]["rtf_also"] = {"model": f"FastSpeech2 ({args.synth_also}) + HiFi-GAN V1", "rtf": sy2["rtf"],

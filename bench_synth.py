@@ -32,6 +32,7 @@ def parse():
     ap.add_argument("--synth-serial", action="store_true", help="one stream (A/B of the two-stream pipeline)")
     ap.add_argument("--b1-runs", type=int, default=0, dest="synth_b1_runs", help="batch-1 latency runs (0: off)")
     ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
+    ap.add_argument("--no-graphs", action="store_false", dest="synth_graphs", help="eager batch-1 synthesis (A/B)")
     ap.add_argument("--bucketed", action="store_true",
                     help="padded FS2 + length-bucketed vocoding instead of the packed length-exact path (A/B)")
     ap.add_argument("--padded-fs2", action="store_false", dest="packed_fs2",

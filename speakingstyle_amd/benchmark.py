@@ -380,20 +380,36 @@ def synth_phase(args, rank, world, device):
         g1 = SyntheticBatches(1, device=device, seed=17 + rank, max_seq_len=mc["max_seq_len"],
                               phone_counts=np.array([int(getattr(args, "synth_b1_phones", 14))]))
         b1 = g1.make_batch()
+        # serving path: the packed synthesis replayed from HIP graphs (infer/graphs.py; every replay recomputes
+        # text -> wav from the inputs, only the ~350 launches' host cost goes)
+        sg = None
+        if packed and getattr(args, "synth_graphs", True):
+            from .infer.graphs import SynthGraphs
+
+            sg = SynthGraphs(model, voc, int16_scale=mx)
+            if not sg.supported(b1[3]):
+                sg = None
+
+        def one():
+            if sg is None:
+                return synth(b1, stream=None, host_wav=True)
+            pcm_d, lens_l = sg(b1[2], b1[3], b1[4], b1[5], b1[6], b1[7], b1[8])
+            return pcm_d.cpu(), torch.tensor(lens_l)
+
         for _ in range(max(3, args.synth_warmup)):
-            synth(b1, stream=None, host_wav=True)
+            one()
         times, frames = [], 0
         for _ in range(runs):
             _sync(cuda)
             t1 = time.perf_counter()
-            pcm, mel_len = synth(b1, stream=None, host_wav=True)
+            pcm, mel_len = one()
             times.append(time.perf_counter() - t1)
             frames = int(mel_len.sum())
         med = float(np.median(times))
         audio1 = frames * hop / sr
         info["b1"] = {"median_s": med, "min_s": float(min(times)), "max_s": float(max(times)), "runs": runs,
                       "mel_frames": frames, "audio_s": audio1, "rtf": med / max(audio1, 1e-12),
-                      "samples": int(pcm.numel())}
+                      "samples": int(pcm.numel()), "graphs": None if sg is None else dict(sg.stats)}
     del model, voc
     if cuda:
         torch.cuda.empty_cache()

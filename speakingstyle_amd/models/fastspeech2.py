@@ -454,6 +454,16 @@ class FastSpeech2(nn.Module):
         last PostNet frames of shorter utterances).  The one host sync is the same as the padded path's (the mel
         lengths, which size the length regulator): here all B lengths come back at once.
         Returns (post-net mel [R, n_mel] fp32 rows of utterance b at cu[b].., host lengths (list), device mel_len)."""
+        front = self.infer_front(speakers, texts, src_lens, max_src_len, mels, mel_lens, max_mel_len, p_control,
+                                 e_control, d_control, style_weights)
+        lens = [int(v) for v in front[2].cpu().tolist()]  # the one D2H: sizes the packed decoder
+        return self.infer_back(front, lens), lens, front[2]
+
+    @torch.no_grad()
+    def infer_front(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None, max_mel_len=None,
+                    p_control=1.0, e_control=1.0, d_control=1.0, style_weights=None):
+        """``infer_packed`` up to the durations (no host sync, fixed shapes: HIP-graph capturable,
+        ``infer/graphs.py``) -> (x [B, T, d], rounded durations [B, T], mel_len [B], style)."""
         cd = self.compute_dtype
         dev = texts.device
         if mels is not None and max_mel_len is None:
@@ -469,9 +479,15 @@ class FastSpeech2(nn.Module):
         x, _, _, log_d, _, _ = self.variance_adaptor(x, src_lens, None, None, None, None, None, p_control,
                                                      e_control, d_control, style, regulate=False)
         d_rounded, mel_len = ops.duration_round(log_d, src_lens, d_control)
-        lens = [int(v) for v in mel_len.cpu().tolist()]  # the one D2H: sizes the packed decoder
+        return x, d_rounded, mel_len, style
+
+    @torch.no_grad()
+    def infer_back(self, front, lens):
+        """``infer_packed`` after the durations, for host mel lengths ``lens`` (fixed shapes given lens:
+        capturable) -> post-net mel rows [R, n_mel] fp32."""
+        x, d_rounded, mel_len, style = front
         M, R = max(lens) if lens else 0, sum(lens)
         x, dec_lens, pk = self.decoder.forward_packed(x, d_rounded, mel_len, M, R, style)
         mel = ops.linear(x, self.mel_linear.weight, self.mel_linear.bias).float()
-        post = self.postnet.forward_packed(mel.to(cd), pk).float() + mel
-        return post.reshape(R, -1), lens, mel_len
+        post = self.postnet.forward_packed(mel.to(self.compute_dtype), pk).float() + mel
+        return post.reshape(R, -1)

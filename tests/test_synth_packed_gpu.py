@@ -66,3 +66,43 @@ def test_fs2_infer_packed_equals_each_utterance_alone(config):
             m = (n - 16) * 256
             assert _rel(w_rows[i, :m], w_pad[i, :m]) < 5e-2
         assert not w_rows[i, n * 256:].any()
+
+
+def test_synth_graphs_replay_equals_eager():
+    """infer/graphs.SynthGraphs: the captured packed synthesis (graph 1: style + encoder + variance adaptor +
+    durations; graph 2: decoder + PostNet + vocoder for the returned lengths) replays bitwise the eager packed
+    synthesis -- for new inputs of the same shapes too (replays read the static inputs) -- and new length sets
+    warm / capture their own graph 2."""
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.data.synthetic import SyntheticBatches
+    from speakingstyle_amd.infer.graphs import SynthGraphs
+    from speakingstyle_amd.models.fastspeech2 import FastSpeech2
+    from speakingstyle_amd.models.hifigan import Generator, default_config
+
+    dev = torch.device("cuda", 0)
+    pp, mc, tc = load_named("BC2013_GST")
+    torch.manual_seed(0)
+    model = FastSpeech2(pp, mc).to(dev)
+    with torch.no_grad():
+        lin = model.variance_adaptor.duration_predictor.linear_layer
+        lin.weight.normal_(0.0, 0.005)
+        lin.bias.fill_(math.log(9.1))
+    model.eval().set_compute_dtype(torch.bfloat16)
+    model.requires_grad_(False)
+    torch.manual_seed(1)
+    g = Generator(default_config()).eval().fold_weight_norm().to(dev)
+    sg = SynthGraphs(model, g, int16_scale=32768.0, warm=1)
+    import numpy as np
+
+    for B in (1, 3):
+        gen = SyntheticBatches(B, device=dev, seed=11 + B, max_seq_len=mc["max_seq_len"],
+                               phone_counts=np.array([14, 14]))
+        batches = [gen.make_batch() for _ in range(4)]
+        r = batches[0]  # one reference mel (fixed shape), different texts
+        for k, b in enumerate(batches + batches[:2]):
+            args = (b[2], b[3], b[4], b[5], r[6], r[7], r[8])
+            wav, lens = sg(*args)
+            rows, lens_e, _ = model.infer_packed(*args)
+            ref = g.infer_packed(rows, lens_e, int16_scale=32768.0)
+            assert lens == lens_e and torch.equal(wav, ref), (B, k)
+    assert sg.stats["captures"] >= 2 and sg.stats["replays"] >= 4, sg.stats
