@@ -2512,6 +2512,10 @@ static std::mutex g_splitk_mu;
 // Workspace of >= need bytes for (current device, s), or nullptr.  Sized once to 64 MiB (S * tiles <=
 // 256 CUs bounds every split-K workspace by 256 tiles x 256 KiB): a regrow would hipFree, a device-wide
 // synchronisation in the middle of a training step.
+static bool g_ws_retain = false;
+static hipStreamCaptureStatus g_cap_status;
+SSAMD_API void ssamd_gemm_retain_workspaces(int v) { g_ws_retain = v != 0; }
+
 static void* splitk_workspace(hipStream_t s, size_t need) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
@@ -2526,7 +2530,14 @@ static void* splitk_workspace(hipStream_t s, size_t need) {
   }
   if (need > e->bytes) {
     const size_t want = need > ((size_t)64 << 20) ? need : ((size_t)64 << 20);
-    if (e->p) (void)hipFree(e->p);
+    // a captured HIP graph holds the old address: once graphs exist (ssamd_gemm_retain_workspaces) the old buffer
+    // is kept (leaked) instead of freed; during a capture no allocation is legal at all (-4: warm the shape first)
+    if (g_ws_retain) {
+      if (hipStreamIsCapturing(s, &g_cap_status) == hipSuccess && g_cap_status != hipStreamCaptureStatusNone)
+        return nullptr;
+    } else if (e->p) {
+      (void)hipFree(e->p);
+    }
     e->p = nullptr;
     e->bytes = 0;
     if (hipMalloc(&e->p, want) != hipSuccess) return nullptr;

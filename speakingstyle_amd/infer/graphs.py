@@ -33,6 +33,8 @@ class SynthGraphs:
         self.g1 = collections.OrderedDict()
         self.g2 = collections.OrderedDict()
         self.pool = None
+        self.stream = None  # warm-up AND capture run on this one stream: the stream-keyed workspaces of the kernel
+        #                     library (split-K partials) are allocated by the warm-up, never inside a capture
         self.stats = {"captures": 0, "replays": 0, "eager": 0, "capture_s": 0.0}
 
     def supported(self, texts) -> bool:
@@ -51,13 +53,13 @@ class SynthGraphs:
     def _capture(self, fn):
         from ..ops import hip
 
-        hip._GRAPHS_LIVE[0] = True  # grown workspaces are retired from now on (graphs hold their addresses)
+        hip.graphs_live()  # grown workspaces are retired from now on (graphs hold their addresses)
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         t0 = time.perf_counter()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
+        with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
             out = fn()
         torch.cuda.synchronize()
         self.stats["captures"] += 1
@@ -71,7 +73,19 @@ class SynthGraphs:
     # ------------------------------------------------------------------ synthesis
     @torch.no_grad()
     def __call__(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None, max_mel_len=None):
-        """-> (wav [B, max(lens) * hop] (int16 when int16_scale), host mel lengths).  The wav is a fresh tensor."""
+        """-> (wav [B, max(lens) * hop] (int16 when int16_scale), host mel lengths).  The wav is a fresh tensor,
+        ordered on the caller's stream."""
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=texts.device)
+        cur = torch.cuda.current_stream(texts.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            wav, lens = self._run(speakers, texts, src_lens, max_src_len, mels, mel_lens, max_mel_len)
+        cur.wait_stream(self.stream)
+        wav.record_stream(cur)
+        return wav, lens
+
+    def _run(self, speakers, texts, src_lens, max_src_len, mels, mel_lens, max_mel_len):
         inp = (speakers, texts, src_lens, int(max_src_len), mels, mel_lens,
                None if max_mel_len is None else int(max_mel_len))
         if not self.supported(texts):

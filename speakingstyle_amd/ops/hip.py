@@ -403,6 +403,14 @@ _GRAPHS_LIVE = [False]
 _ws_retired = []
 
 
+def graphs_live():
+    """Called before the first HIP-graph capture: from now on no workspace a graph may hold is ever freed (the
+    Python scratch buffers here, the split-K workspaces of the GEMM library)."""
+    if not _GRAPHS_LIVE[0]:
+        _GRAPHS_LIVE[0] = True
+        lib().ssamd_gemm_retain_workspaces(1)
+
+
 def _workspace(device, nfloats: int) -> torch.Tensor:
     """Scratch buffer of the current stream (the weight-gradient side stream has its own, allocated
     under that stream so the caching allocator orders its reuse after the side-stream kernels)."""
@@ -2213,7 +2221,8 @@ def resblock_fused(x, convs1, convs2, dilations, slope, acc=None, out_scale=1.0,
 
 
 # ------------------------------------------------------------------------ packed (length-exact) vocoder
-_SIGS.update({"ssamd_voc_tile_rows": [I, I, I, I, I, I],
+_SIGS.update({"ssamd_gemm_retain_workspaces": [I],
+              "ssamd_voc_tile_rows": [I, I, I, I, I, I],
               "ssamd_voc_rinfo": [P, I, I, I, P, P],
               "ssamd_voc_pack": [P, I, P, I, I, I, P, P],
               "ssamd_resblock_layer_pk": [P, P, P, P, P, P, P, P, I, I, I, I, F, F, I, P],

@@ -121,7 +121,7 @@ class GraphedSteps:
         stream = getattr(tr, "compute_stream", None)  # None: torch's own capture stream
         from ..ops import hip
 
-        hip._GRAPHS_LIVE[0] = True  # from now on grown workspaces are retired, never freed (ops/hip.py)
+        hip.graphs_live()  # from now on grown workspaces are retired, never freed (ops/hip.py)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         # the capture stream is the trainer's compute stream (priority, side-stream forks / joins)
