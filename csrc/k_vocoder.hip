@@ -31,13 +31,21 @@ constexpr int MAXD = 5;
 // (Measured and lost: C = 128 at one wave per SIMD with a 64 x 64 wave tile -- 8 fragment reads per 16
 // MFMAs instead of 6 per 8 -- K = 7 5.25 -> 5.85 ms, K = 3 3.47 -> 4.00 ms: the second wave per SIMD
 // hides more than the saved LDS reads.)
-template <int C, int K>
+// BIG_ (the "tall" per-layer tile, resblock_layer_tall_kernel): 8 waves of 64 x 64 (RPW_ = 4 row blocks x 4
+// sub-tiles), 8 fragment reads per 16 MFMAs instead of 6 per 8 -- the LDS-read-bound conv loop moves 1/3 fewer bytes
+// per MFMA and the weight slices are staged once per 256 (C = 128) / 512 (C = 64) rows instead of per 128 / 64.  The
+// x tile, the t1 tile and the fp32 output tile share one LDS region (each is dead before the next is written:
+// extra barriers after each conv), the weight ring sits behind the x tile.
+template <int C_, int K_, int RPW_ = 2, bool BIG_ = false>
 struct RB {
-  static constexpr int NW = C >= 128 ? 8 : 4;       // waves per block
+  static constexpr int C = C_;
+  static constexpr int K = K_;
+  static constexpr bool BIG = BIG_;
+  static constexpr int NW = BIG ? 8 : (C >= 128 ? 8 : 4);  // waves per block
   static constexpr int NT = 64 * NW;
   static constexpr int WC = C >= 128 ? 2 : 1;       // column groups
   static constexpr int WR = NW / WC;                // row groups
-  static constexpr int RPW = 2;                     // row blocks per wave
+  static constexpr int RPW = RPW_;                  // row blocks per wave
   static constexpr int H2 = (K - 1) / 2;
   static constexpr int NRB1 = RPW * WR;             // conv1 row blocks
   static constexpr int R1P = NRB1 * 16;             // t1 rows (= R1: no padding)
@@ -54,17 +62,26 @@ struct RB {
   static constexpr int NS = C / 16;                // 16-wide output sub-tiles
   static constexpr int NSW = NS / WC;              // sub-tiles per wave
   static constexpr int KC = C / 32;                // 32-deep K chunks per tap
-  static constexpr int KC2 = KC >= 2 ? 2 : 1;      // 32-deep chunks per pipeline step (one barrier each)
+  // 32-deep chunks per pipeline step (one barrier each); the tall tile keeps one (its 64 x 64 wave tile already
+  // holds 64 accumulator VGPRs and 8 fragments per chunk and buffer)
+  static constexpr int KC2 = (KC >= 2 && !BIG) ? 2 : 1;
   static constexpr int SLOT = KC2 * C * 64;        // ring slot: KC2 sub-slices [C][32] bf16
   static constexpr int XS_BYTES = RX * LDC * 2;
   static constexpr int OSP = C + 4;                // fp32 output-tile pitch (skewed banks)
   static constexpr int OUT_BYTES = NRB2 * 16 * OSP * 4;
   static constexpr int R0_BYTES = ((XS_BYTES > OUT_BYTES ? XS_BYTES : OUT_BYTES) + 15) / 16 * 16;
   static constexpr int T1_BYTES = R1P * LDC * 2;
-  static constexpr int LDS = R0_BYTES + T1_BYTES + 3 * SLOT;  // + the weight-slice ring
+  // BIG: x / t1 / fp32 output alias one region, the ring behind the x tile
+  static constexpr int XS16 = (XS_BYTES + 15) / 16 * 16;
+  static constexpr int RING_OFF = BIG ? XS16 : R0_BYTES + T1_BYTES;
+  static constexpr int LDS_BIG = (XS16 + 3 * SLOT > OUT_BYTES ? XS16 + 3 * SLOT : OUT_BYTES);
+  static constexpr int LDS = BIG ? LDS_BIG : R0_BYTES + T1_BYTES + 3 * SLOT;  // + the weight-slice ring
   static constexpr int MAXRB = RPW;
   static_assert(NRB2 <= NRB1 && LDS <= 160 * 1024, "resblock tile");
+  static_assert(!BIG || T1_BYTES <= XS16, "t1 aliases the x tile");
 };
+template <int C, int K>
+using RBT = RB<C, K, 4, true>;  // the tall tile
 
 __device__ __forceinline__ float lrelu(float v, float s) { return v >= 0.f ? v : v * s; }
 
@@ -83,9 +100,9 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
 }
 
 // DMA pieces per thread and pipeline step (vmcnt bookkeeping of conv_tile)
-template <int C, int K>
+template <class R>
 constexpr int rb_dps() {
-  return RB<C, K>::KC2 * (C * 4 > RB<C, K>::NT ? C * 4 / RB<C, K>::NT : 1);
+  return R::KC2 * (R::C * 4 > R::NT ? R::C * 4 / R::NT : 1);
 }
 
 template <int N>
@@ -124,9 +141,9 @@ __device__ __forceinline__ TileGeo tile_geo(const int4* __restrict__ tt, int til
   return g;
 }
 
-template <int C, int K>
+template <class R>
 __device__ __forceinline__ void stage_b(const bf16_t* __restrict__ w, int step, char* slot, int tid, int wave) {
-  using R = RB<C, K>;
+  constexpr int C = R::C, K = R::K;
   constexpr int CHUNKS = C * 4;  // 16-B chunks per [C][32] sub-slice
   constexpr int REP = CHUNKS > R::NT ? CHUNKS / R::NT : 1;
   static_assert(CHUNKS <= R::NT || CHUNKS % R::NT == 0, "slice chunks over the block");
@@ -144,11 +161,11 @@ __device__ __forceinline__ void stage_b(const bf16_t* __restrict__ w, int step, 
   }
 }
 
-template <int C, int K>
+template <class R>
 __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int row_step, const bf16_t* __restrict__ w,
                                           char* bring, int nrb, int wave, int tid,
-                                          float4v (&acc)[RB<C, K>::MAXRB][RB<C, K>::NSW]) {
-  using R = RB<C, K>;
+                                          float4v (&acc)[R::MAXRB][R::NSW]) {
+  constexpr int C = R::C, K = R::K;
   constexpr int STEPS = K * R::KC / R::KC2;
   constexpr int SLOT = R::SLOT;
   const int lane = tid & 63, col = lane & 15, quad = lane >> 4;
@@ -160,11 +177,11 @@ __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int ro
   // Ring: slot j % 3 holds step j.  DMA runs three steps ahead of the MFMAs and the fragments of
   // step+1 are read into registers while step's MFMAs run, so one barrier per step only has to
   // cover "slot step+1 landed" and "everyone is done reading slot step" (re-filled with step+3).
-  stage_b<C, K>(w, 0, bring, tid, wave);
-  if (STEPS > 1) stage_b<C, K>(w, 1, bring + SLOT, tid, wave);
-  if (STEPS > 2) stage_b<C, K>(w, 2, bring + 2 * SLOT, tid, wave);
+  stage_b<R>(w, 0, bring, tid, wave);
+  if (STEPS > 1) stage_b<R>(w, 1, bring + SLOT, tid, wave);
+  if (STEPS > 2) stage_b<R>(w, 2, bring + 2 * SLOT, tid, wave);
   // (vmcnt counts this thread's DMA pieces: DPS per step)
-  constexpr int DPS = rb_dps<C, K>();
+  constexpr int DPS = rb_dps<R>();
   if constexpr (STEPS > 2) wait_vm<2 * DPS>();
   else if constexpr (STEPS > 1) wait_vm<DPS>();
   else wait_vm<0>();
@@ -199,7 +216,7 @@ __device__ __forceinline__ void conv_tile(const bf16_t* __restrict__ src, int ro
       if (step + 2 < STEPS) wait_vm_lgkm0<DPS>();
       else wait_vm_lgkm0<0>();
       __builtin_amdgcn_s_barrier();
-      if (step + 3 < STEPS) stage_b<C, K>(w, step + 3, bring + (step % 3) * SLOT, tid, wave);
+      if (step + 3 < STEPS) stage_b<R>(w, step + 3, bring + (step % 3) * SLOT, tid, wave);
       load(step + 1, cur ^ 1);
     }
 #pragma unroll
@@ -236,23 +253,24 @@ __device__ __forceinline__ void rb_stamp(unsigned long long* st, int i) {
 // (no DMA of conv_tile is in flight any more), under the output staging and the epilogue's own loads, and
 // the barriers of that span order LDS only (__syncthreads would drain the fetch: vmcnt counts it).
 // Synthesis RTF -1.2..-2.8 % same-box (profiles/r5_ab_rb_persistent.txt).
-template <int C, int K, bool PROF = false>
-__global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
+template <class R, bool PROF = false>
+__global__ void __launch_bounds__((R::NT)) resblock_layer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
                                                             const float* __restrict__ b1, const bf16_t* __restrict__ w2,
                                                             const float* __restrict__ b2, const bf16_t* acc_in,
                                                             bf16_t* out, int Tp, int tiles, int ntiles, int d, float slope,
                                                             float out_scale, int post_lrelu,
                                                             const int4* __restrict__ tt,
                                                             unsigned long long* __restrict__ prof = nullptr) {
-  using R = RB<C, K>;
+  constexpr int C = R::C, K = R::K;
   unsigned long long st[8];
   constexpr int NT = R::NT;
   constexpr int CH = C / 8;                                  // 16-B chunks per row
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(lds);               // [RX][LDC]   lrelu(x) tile
   float* os = reinterpret_cast<float*>(lds);                 // [NRB2*16][OSP] conv2 + b2 (after conv1)
-  bf16_t* t1 = reinterpret_cast<bf16_t*>(lds + R::R0_BYTES);  // [R1P][LDC]  lrelu(conv1 + b1)
-  char* bring = reinterpret_cast<char*>(lds + R::R0_BYTES + R::T1_BYTES);  // 3 x [C][32] weight slices
+  // [R1P][LDC]  lrelu(conv1 + b1): its own region, or (BIG) over the dead x tile
+  bf16_t* t1 = reinterpret_cast<bf16_t*>(lds + (R::BIG ? 0 : R::R0_BYTES));
+  char* bring = reinterpret_cast<char*>(lds + R::RING_OFF);  // 3 x [C][32] weight slices
   const int tid0 = threadIdx.x;
   const int h1 = d * (K - 1) / 2;
   // both convs' bias columns of this lane (they depend on the sub-tile s only): loaded up front, not as
@@ -319,8 +337,9 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
 
     // 2. conv1 (dilation d): t1 row i <- x rows i + tap*d
     float4v acc[R::MAXRB][R::NSW];
-    conv_tile<C, K>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
+    conv_tile<R>(xs, d, w1, bring, R::NRB1, wave, tid, acc);
     rb_stamp<PROF>(st, 2);
+    if constexpr (R::BIG) __syncthreads();  // every wave done reading x: t1 overwrites it
 #pragma unroll
     for (int r = 0; r < R::MAXRB; ++r) {
       const int rb = wr + R::WR * r;
@@ -343,23 +362,31 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
     rb_stamp<PROF>(st, 3);
 
     // 3. conv2 (dilation 1): out row j <- t1 rows j + tap
-    conv_tile<C, K>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
+    conv_tile<R>(t1, 1, w2, bring, R::NRB2, wave, tid, acc);
     rb_stamp<PROF>(st, 4);
     const int nxt = tile + gridDim.x;
     if (nxt < ntiles) fetch_x(nxt, tid);
+    // BIG: the output tile overwrites t1 and the ring -- wait for every wave's last conv2 reads (LDS order only:
+    // a full __syncthreads would also drain the next tile's fetch)
+    if constexpr (R::BIG) lds_barrier();
     // the epilogue's residual / accumulator rows, issued before the output staging
     constexpr int BM = R::BM;
     constexpr int IE = (BM * CH + NT - 1) / NT;
     bf16_t* ob = out + gt.off * C;
     const bf16_t* ab = acc_in ? acc_in + gt.off * C : nullptr;
-    short8 xr[IE], ar[IE];
+    // (BIG: the residual rows are read inside the store loop, after the staging -- the 64-VGPR accumulators, the
+    // next tile's x and a whole tile of residual rows do not fit in 256 registers together)
+    constexpr int IEP = R::BIG ? 1 : IE;
+    short8 xr[IEP], ar[IEP];
+    if constexpr (!R::BIG) {
 #pragma unroll
-    for (int it = 0; it < IE; ++it) {
-      const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
-      const int t = t0 + j;
-      if (j < BM && t < T) {
-        xr[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
-        if (ab) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
+      for (int it = 0; it < IE; ++it) {
+        const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
+        const int t = t0 + j;
+        if (j < BM && t < T) {
+          xr[it] = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
+          if (ab) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
+        }
       }
     }
 #pragma unroll
@@ -384,14 +411,22 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
       const int q = tid + it * NT, j = q / CH, c0 = (q - j * CH) * 8;
       const int t = t0 + j;
       if (j >= BM || t >= T) continue;
+      short8 xv, av;
+      if constexpr (R::BIG) {
+        xv = *reinterpret_cast<const short8*>(xb + (long)t * C + c0);
+        if (ab) av = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
+      } else {
+        xv = xr[it];
+        if (ab) av = ar[it];
+      }
       const float4 o0 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0);
       const float4 o1 = *reinterpret_cast<const float4*>(os + j * R::OSP + c0 + 4);
       const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
       short8 o;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float y = ov[i] + bf2f((bf16_t)xr[it][i]);
-        if (ab) y += bf2f((bf16_t)ar[it][i]);
+        float y = ov[i] + bf2f((bf16_t)xv[i]);
+        if (ab) y += bf2f((bf16_t)av[i]);
         y *= out_scale;
         if (post_lrelu) y = lrelu(y, slope);  // the next upsampling conv's pre-activation
         o[i] = (short)f2bf(y);
@@ -411,14 +446,21 @@ __global__ void __launch_bounds__((RB<C, K>::NT)) resblock_layer_kernel(const bf
 }
 
 
+// per-layer kernel variant: 1 = the tall tile (RBT) where it is instantiated, 0 = the 128-row tile (A/B switch)
+static int g_rb_tall = 1;
+SSAMD_API void ssamd_resblock_set_tall(int v) { g_rb_tall = v; }
 template <int C, int K>
+constexpr bool has_tall() {
+  return (C == 128 && (K == 7 || K == 11)) || (C == 64 && K == 11);
+}
+
+template <class R>
 int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
               const bf16_t* acc_in, bf16_t* out, int B, int T, int d, float slope, float out_scale, int post_lrelu,
               hipStream_t s, const int4* tt = nullptr, int ntt = 0) {
-  using R = RB<C, K>;
   static bool lds_set = false;
   if (!lds_set) {
-    allow_lds(resblock_layer_kernel<C, K>, R::LDS);
+    allow_lds(resblock_layer_kernel<R>, R::LDS);
     lds_set = true;
   }
   static int resident = 0;  // co-resident blocks on the whole device (LDS / register limited)
@@ -426,7 +468,7 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resblock_layer_kernel<C, K>, R::NT, R::LDS) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, resblock_layer_kernel<R>, R::NT, R::LDS) !=
             hipSuccess || per_cu <= 0)
       per_cu = 1;
     resident = cus * per_cu;
@@ -436,9 +478,28 @@ int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* 
   if (ntiles > 0x7fffffffL) return -2;
   if (ntiles == 0) return 0;
   const int grid = (int)(ntiles < resident ? ntiles : resident);
-  hipLaunchKernelGGL((resblock_layer_kernel<C, K>), dim3(grid), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
+  hipLaunchKernelGGL((resblock_layer_kernel<R>), dim3(grid), dim3(R::NT), R::LDS, s, x, w1, b1, w2, b2,
                      acc_in, out, T, tiles, (int)ntiles, d, slope, out_scale, post_lrelu, tt);
   return (int)hipGetLastError();
+}
+
+template <int C, int K>
+int launch_rb_any(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
+                  const bf16_t* acc_in, bf16_t* out, int B, int T, int d, float slope, float out_scale, int post_lrelu,
+                  hipStream_t s, const int4* tt = nullptr, int ntt = 0) {
+  if constexpr (has_tall<C, K>()) {
+    if (g_rb_tall)
+      return launch_rb<RBT<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
+  }
+  return launch_rb<RB<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
+}
+
+template <int C, int K>
+int rb_bm() {
+  if constexpr (has_tall<C, K>()) {
+    if (g_rb_tall) return RBT<C, K>::BM;
+  }
+  return RB<C, K>::BM;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -522,7 +583,7 @@ __global__ void __launch_bounds__((RB<C, 3>::NT)) conv3_sq_kernel(const bf16_t* 
     }
     __syncthreads();
     float4v acc[R::MAXRB][R::NSW];
-    conv_tile<C, 3>(xs, 1, w, bring, R::NRB1, wave, tid, acc);
+    conv_tile<R>(xs, 1, w, bring, R::NRB1, wave, tid, acc);
     const int nxt = tile + gridDim.x;
     if (nxt < ntiles) fetch_x(nxt, tid);  // no DMA of conv_tile in flight any more
 #pragma unroll
@@ -1033,7 +1094,7 @@ __global__ void __launch_bounds__(256) voc_pack_kernel(const TS* __restrict__ sr
 // kind 0 = resblock_layer (C, K), 1 = resblock_fused (C, K, dilations), 2 = conv3_sq (C).  0 = no such instance.
 SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2) {
 #define VT_RB(CC, KK) \
-  if (C == CC && K == KK) return RB<CC, KK>::BM;
+  if (C == CC && K == KK) return rb_bm<CC, KK>();
 #define VT_RF(CC, KK) \
   if (C == CC && K == KK) return RF<CC, KK>::R0 - 2 * (RF<CC, KK>::H2 * (d0 + d1 + d2 + 3));
   if (kind == 0) {
@@ -1077,7 +1138,7 @@ SSAMD_API int ssamd_resblock_layer_pk(const bf16_t* x, const bf16_t* w1, const f
   const int4* t4 = reinterpret_cast<const int4*>(tt);
 #define RBK_CASE(CC, KK) \
   if (C == CC && K == KK) \
-    return launch_rb<CC, KK>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, ntt);
+    return launch_rb_any<CC, KK>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, ntt);
   RBK_CASE(32, 3) RBK_CASE(32, 7) RBK_CASE(32, 11)
   RBK_CASE(64, 3) RBK_CASE(64, 7) RBK_CASE(64, 11)
   RBK_CASE(128, 3) RBK_CASE(128, 7) RBK_CASE(128, 11)
@@ -1156,10 +1217,10 @@ SSAMD_API int ssamd_resblock_layer_prof(const bf16_t* x, const bf16_t* w1, const
 #define RBP_CASE(CC, KK)                                                                                      \
   if (C == CC && K == KK) {                                                                                   \
     using R = RB<CC, KK>;                                                                                     \
-    allow_lds(resblock_layer_kernel<CC, KK, true>, R::LDS);                                                   \
+    allow_lds(resblock_layer_kernel<R, true>, R::LDS);                                                        \
     const int tiles = (T + R::BM - 1) / R::BM;                                                                \
     const int g = grid > 0 && grid < B * tiles ? grid : B * tiles;                                            \
-    hipLaunchKernelGGL((resblock_layer_kernel<CC, KK, true>), dim3(g), dim3(R::NT), R::LDS, s, x,              \
+    hipLaunchKernelGGL((resblock_layer_kernel<R, true>), dim3(g), dim3(R::NT), R::LDS, s, x,                   \
                        w1, b1, w2, b2, acc_in, out, T, tiles, B * tiles, d, slope, out_scale, post_lrelu,      \
                        (const int4*)nullptr, prof);                                                           \
     return (int)hipGetLastError();                                                                            \
@@ -1182,9 +1243,9 @@ SSAMD_API int ssamd_conv3_sq(const bf16_t* x, const bf16_t* w, const float* bias
 }
 
 SSAMD_API int ssamd_resblock_layer_tile(int C, int K) {
-  if (C == 128 && K == 11) return RB<128, 11>::BM;
-  if (C == 128 && K == 7) return RB<128, 7>::BM;
-  if (C == 64 && K == 11) return RB<64, 11>::BM;
+  if (C == 128 && K == 11) return rb_bm<128, 11>();
+  if (C == 128 && K == 7) return rb_bm<128, 7>();
+  if (C == 64 && K == 11) return rb_bm<64, 11>();
   return 0;
 }
 
@@ -1195,7 +1256,7 @@ SSAMD_API int ssamd_resblock_layer(const bf16_t* x, const bf16_t* w1, const floa
   if ((long)B * T == 0) return 0;
 #define RB_CASE(CC, KK) \
   if (C == CC && K == KK) \
-    return launch_rb<CC, KK>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s);
+    return launch_rb_any<CC, KK>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s);
   RB_CASE(32, 3) RB_CASE(32, 7) RB_CASE(32, 11)
   RB_CASE(64, 3) RB_CASE(64, 7) RB_CASE(64, 11)
   RB_CASE(128, 3) RB_CASE(128, 7) RB_CASE(128, 11)

@@ -1214,17 +1214,28 @@ def test_resblock_layer_fused(C, K, d, T):
         assert _rel(out, expect) < 1e-2
 
 
+@pytest.mark.parametrize("tall", [1, 0])
 @pytest.mark.parametrize("C,K,d,B,T", [(128, 11, 5, 6, 11000), (128, 7, 3, 5, 13000), (64, 11, 3, 8, 8200)])
-def test_resblock_layer_persistent_many_tiles(C, K, d, B, T):
-    """The per-layer kernel loops over tiles when they outnumber the resident blocks (256 / 512 here), fetching
-    the next tile's x under the current epilogue: bitwise equal to the one-tile-per-block launch (the phase-stamp
-    instantiation, full grid), and vs fp32 torch, with the in-place MRF accumulator."""
+def test_resblock_layer_persistent_many_tiles(C, K, d, B, T, tall):
+    """The per-layer kernel loops over tiles when they outnumber the resident blocks (256 here: one 136-150 KiB
+    block per CU), fetching the next tile's x under the current epilogue: bitwise equal to the one-tile-per-block
+    launch of the 128-row tile (the phase-stamp instantiation, full grid) -- for the tall 64 x 64-per-wave tile
+    (tall = 1, the production variant) too: every output element sums the same (tap, chunk) products in the same
+    order -- and vs fp32 torch, with the in-place MRF accumulator."""
     from speakingstyle_amd.models.hifigan import LRELU_SLOPE
 
+    hip.lib().ssamd_resblock_set_tall(tall)
+    try:
+        _persistent_case(C, K, d, B, T, LRELU_SLOPE)
+    finally:
+        hip.lib().ssamd_resblock_set_tall(1)
+
+
+def _persistent_case(C, K, d, B, T, LRELU_SLOPE):
     torch.manual_seed(25)
     BM = hip.lib().ssamd_resblock_layer_tile(C, K)
     tiles = (T + BM - 1) // BM
-    assert B * tiles > 512
+    assert B * tiles > 256
     c1 = torch.nn.Conv1d(C, C, K, dilation=d, padding=d * (K - 1) // 2).to(DEV)
     c2 = torch.nn.Conv1d(C, C, K, padding=(K - 1) // 2).to(DEV)
     for c in (c1, c2):
