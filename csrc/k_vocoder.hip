@@ -1213,12 +1213,13 @@ SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16
 SSAMD_API int ssamd_resblock_layer_prof(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
                                         const float* b2, const bf16_t* acc_in, bf16_t* out, int B, int T, int C, int K,
                                         int d, float slope, float out_scale, int post_lrelu, unsigned long long* prof,
-                                        int grid, hipStream_t s) {
+                                        long prof_words, int grid, hipStream_t s) {
 #define RBP_CASE(CC, KK)                                                                                      \
   if (C == CC && K == KK) {                                                                                   \
     using R = RB<CC, KK>;                                                                                     \
     allow_lds(resblock_layer_kernel<R, true>, R::LDS);                                                        \
     const int tiles = (T + R::BM - 1) / R::BM;                                                                \
+    if ((long)B * tiles * 8 > prof_words) return -3; /* stamp buffer too small for this tile height */       \
     const int g = grid > 0 && grid < B * tiles ? grid : B * tiles;                                            \
     hipLaunchKernelGGL((resblock_layer_kernel<R, true>), dim3(g), dim3(R::NT), R::LDS, s, x,                   \
                        w1, b1, w2, b2, acc_in, out, T, tiles, B * tiles, d, slope, out_scale, post_lrelu,      \

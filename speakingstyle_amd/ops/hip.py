@@ -2134,7 +2134,7 @@ def token_bank(E, Wk, Wv, n_head):
 
 # ------------------------------------------------------------------------ vocoder (inference)
 _SIGS.update({"ssamd_conv3_sq": [P, P, P, P, I, I, I, P]})
-_SIGS.update({"ssamd_resblock_layer_prof": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P, I, P],
+_SIGS.update({"ssamd_resblock_layer_prof": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P, L_, I, P],
               "ssamd_resblock_layer_tile": [I, I]})
 _SIGS.update({"ssamd_resblock_layer": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, I, P],
               "ssamd_conv_gemm_ex": [P, P, P, P, P, I, I, I, I, I, I, I, I, P, P, F, I, P],

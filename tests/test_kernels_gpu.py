@@ -1250,12 +1250,13 @@ def _persistent_case(C, K, d, B, T, LRELU_SLOPE):
         out = hip.resblock_layer(x, c1, c2, d, LRELU_SLOPE, acc=acc, out_scale=1 / 3)
         assert _rel(out, (acc0.float() + yr) * (1 / 3)) < 1e-2
         one = acc0.clone()
-        prof = torch.zeros(B * tiles * 8, dtype=torch.int64, device=DEV)
+        # the stamp instantiation runs the 128-row tile (its own, smaller BM): size its stamp buffer for any tile height
+        prof = torch.zeros(B * (T // 16 + 1) * 8, dtype=torch.int64, device=DEV)
         w1, w2 = hip.weight_fwd(c1.weight), hip.weight_fwd(c2.weight)
         b1, b2 = c1.bias.detach().float().contiguous(), c2.bias.detach().float().contiguous()
         hip._check(hip.lib().ssamd_resblock_layer_prof(
             hip._ptr(x), hip._ptr(w1), hip._ptr(b1), hip._ptr(w2), hip._ptr(b2), hip._ptr(one), hip._ptr(one),
-            B, T, C, K, d, LRELU_SLOPE, 1 / 3, 0, hip._ptr(prof), 0, hip._stream()), "resblock prof")
+            B, T, C, K, d, LRELU_SLOPE, 1 / 3, 0, hip._ptr(prof), prof.numel(), 0, hip._stream()), "resblock prof")
         assert torch.equal(out, one)
 
 
