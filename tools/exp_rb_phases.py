@@ -24,6 +24,8 @@ for C, K, d, acc in ((128, 11, 1, False), (128, 11, 5, True), (128, 7, 3, False)
     out = torch.empty_like(x)
     w1, w2 = hip.weight_fwd(c1.weight), hip.weight_fwd(c2.weight)
     b1, b2 = c1.bias.detach().float().contiguous(), c2.bias.detach().float().contiguous()
+    BM = hip.lib().ssamd_resblock_layer_tile(C, K)
+    tiles = (T + BM - 1) // BM
     prof = torch.zeros(B * (T // 16 + 1) * 8, dtype=torch.int64, device="cuda")  # any tile height
 
     def run(p):
