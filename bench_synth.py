@@ -33,6 +33,8 @@ def parse():
     ap.add_argument("--b1-runs", type=int, default=0, dest="synth_b1_runs", help="batch-1 latency runs (0: off)")
     ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
     ap.add_argument("--no-graphs", action="store_false", dest="synth_graphs", help="eager batch-1 synthesis (A/B)")
+    ap.add_argument("--rb-whole-extra", action="store_true",
+                    help="whole-ResBlock kernels also for C = 64 / K = 11 and C = 128 / K = 7 (A/B)")
     ap.add_argument("--rb-regular", action="store_true",
                     help="per-layer ResBlock kernel on the 128-row tile instead of the tall 64x64-per-wave tile (A/B)")
     ap.add_argument("--bucketed", action="store_true",
@@ -57,6 +59,10 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.lib().ssamd_resblock_set_tall(0)
+    if args.rb_whole_extra and cuda:
+        from speakingstyle_amd.ops import hip
+
+        hip.lib().ssamd_resblock_set_whole_extra(1)
     if args.bucketed:
         from speakingstyle_amd.models import hifigan
 

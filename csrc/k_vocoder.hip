@@ -1101,7 +1101,7 @@ SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2
     VT_RB(32, 3) VT_RB(32, 7) VT_RB(32, 11) VT_RB(64, 3) VT_RB(64, 7) VT_RB(64, 11) VT_RB(128, 3) VT_RB(128, 7)
     VT_RB(128, 11)
   } else if (kind == 1) {
-    VT_RF(32, 3) VT_RF(32, 7) VT_RF(32, 11) VT_RF(64, 3) VT_RF(64, 7) VT_RF(128, 3)
+    VT_RF(32, 3) VT_RF(32, 7) VT_RF(32, 11) VT_RF(64, 3) VT_RF(64, 7) VT_RF(128, 3) VT_RF(64, 11) VT_RF(128, 7)
   } else if (kind == 2) {
     if (C == 128) return C3<128>::BM;
     if (C == 64) return C3<64>::BM;
@@ -1162,6 +1162,7 @@ SSAMD_API int ssamd_resblock_fused_pk(const bf16_t* x, const bf16_t* w0, const b
 #define RFK_CASE(CC, KK) \
   if (C == CC && K == KK) return launch_rf<CC, KK>(x, p, acc_in, out, 1, 1, slope, out_scale, post_lrelu, s, t4, ntt);
   RFK_CASE(32, 3) RFK_CASE(32, 7) RFK_CASE(32, 11) RFK_CASE(64, 3) RFK_CASE(64, 7) RFK_CASE(128, 3)
+  RFK_CASE(64, 11) RFK_CASE(128, 7)
 #undef RFK_CASE
   return -2;
 }
@@ -1181,8 +1182,14 @@ SSAMD_API int ssamd_conv3_sq_pk(const bf16_t* x, const bf16_t* w, const float* b
 // acc_in may alias out, or be null); w: 6 bf16 [C][K][C] images (c1_0, c2_0, c1_1, c2_1, c1_2, c2_2);
 // b: 6 fp32 [C]; dilations 1 <= d <= 5.  Returns -2 for a geometry without a fused instance
 // (ssamd_resblock_fusable).
+// Whole-ResBlock instances for the long-kernel geometries the per-layer kernel serves by default (C = 64 / K = 11,
+// C = 128 / K = 7): the ring-fed fused kernel with their summed halo (60 / 36 rows per side on a 384 / 192-row tile,
+// BM = 264 / 120 output rows) -- switched on by ssamd_resblock_set_whole_extra (A/B against the tall per-layer tile).
+static int g_rf_extra = 0;
+SSAMD_API void ssamd_resblock_set_whole_extra(int v) { g_rf_extra = v; }
 SSAMD_API int ssamd_resblock_fusable(int C, int K) {
-  return (C == 32 && (K == 3 || K == 7 || K == 11)) || (C == 64 && (K == 3 || K == 7)) || (C == 128 && K == 3);
+  return (C == 32 && (K == 3 || K == 7 || K == 11)) || (C == 64 && (K == 3 || K == 7)) || (C == 128 && K == 3) ||
+         (g_rf_extra && ((C == 64 && K == 11) || (C == 128 && K == 7)));
 }
 
 SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16_t* w1, const bf16_t* w2,
@@ -1203,6 +1210,8 @@ SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16
   if (C == 64 && K == 3) return launch_rf<64, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
   if (C == 64 && K == 7) return launch_rf<64, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
   if (C == 128 && K == 3) return launch_rf<128, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 64 && K == 11) return launch_rf<64, 11>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 128 && K == 7) return launch_rf<128, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
   return -2;
 }
 

@@ -2223,6 +2223,7 @@ def resblock_fused(x, convs1, convs2, dilations, slope, acc=None, out_scale=1.0,
 # ------------------------------------------------------------------------ packed (length-exact) vocoder
 _SIGS.update({"ssamd_gemm_retain_workspaces": [I],
               "ssamd_resblock_set_tall": [I],
+              "ssamd_resblock_set_whole_extra": [I],
               "ssamd_voc_tile_rows": [I, I, I, I, I, I],
               "ssamd_voc_rinfo": [P, I, I, I, P, P],
               "ssamd_voc_pack": [P, I, P, I, I, I, P, P],

@@ -1320,8 +1320,21 @@ def test_resblock_rejects_host_weights():
 
 
 @pytest.mark.parametrize("C,K,T", [(32, 3, 1500), (32, 7, 700), (32, 11, 1100), (32, 11, 9), (64, 3, 900),
-                                   (64, 3, 5), (64, 7, 1000), (128, 3, 700), (128, 3, 40)])
+                                   (64, 3, 5), (64, 7, 1000), (128, 3, 700), (128, 3, 40),
+                                   (64, 11, 1300), (64, 11, 7), (128, 7, 600), (128, 7, 30)])
 def test_resblock_whole_block_fused(C, K, T):
+    """(C = 64 / K = 11 and C = 128 / K = 7: the whole-block instances behind ssamd_resblock_set_whole_extra.)"""
+    extra = (C, K) in ((64, 11), (128, 7))
+    if extra:
+        hip.lib().ssamd_resblock_set_whole_extra(1)
+    try:
+        _whole_block_case(C, K, T)
+    finally:
+        if extra:
+            hip.lib().ssamd_resblock_set_whole_extra(0)
+
+
+def _whole_block_case(C, K, T):
     """Whole ResBlock1 kernel (3 layer pairs, dilations 1/3/5, residual in fp32 registers) vs the fp32
     torch ResBlock1 (reference hifigan/models.py:20-44), with the MRF accumulate / scale / post-lrelu
     epilogue; several tiles per sequence (halo recompute at tile edges) and sequences shorter than one
