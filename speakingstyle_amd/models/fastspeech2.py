@@ -16,6 +16,7 @@ from __future__ import annotations
 import json
 import math
 import os
+import weakref
 from typing import Optional
 
 import torch
@@ -33,12 +34,23 @@ def _pe_param(n_position: int, d: int) -> nn.Parameter:
     return nn.Parameter(ops.sinusoid_table(n_position, d).unsqueeze(0), requires_grad=False)
 
 
-def positional_rows(pe_param: torch.Tensor, length: int, d: int, device) -> torch.Tensor:
+_PE_CAST = weakref.WeakKeyDictionary()  # positional table -> (dtype, version, address) key, cast copy
+
+
+def positional_rows(pe_param: torch.Tensor, length: int, d: int, device, dtype=None) -> torch.Tensor:
     """First ``length`` sinusoid rows; beyond the stored table (eval on long
-    inputs, reference ``transformer/Models.py:82-87``) they are generated."""
+    inputs, reference ``transformer/Models.py:82-87``) they are generated.  ``dtype``: the rows in that dtype,
+    from a per-dtype copy of the (constant, non-trainable) table made once."""
     if length <= pe_param.shape[1]:
-        return pe_param[0, :length]
-    return ops.sinusoid_table(length, d, device=device)
+        if dtype is None or dtype == pe_param.dtype:
+            return pe_param[0, :length]
+        hit = _PE_CAST.get(pe_param)
+        if hit is None or hit[0] != (dtype, pe_param._version, pe_param.data_ptr()):
+            hit = ((dtype, pe_param._version, pe_param.data_ptr()), pe_param.detach()[0].to(dtype).contiguous())
+            _PE_CAST[pe_param] = hit
+        return hit[1][:length]
+    t = ops.sinusoid_table(length, d, device=device)
+    return t if dtype is None else t.to(dtype)
 
 
 class Encoder(nn.Module):
@@ -60,7 +72,7 @@ class Encoder(nn.Module):
 
     def forward(self, texts, src_lens, style=None, compute_dtype=torch.float32):
         T = texts.shape[1]
-        pe = positional_rows(self.position_enc, T, self.d_model, texts.device).to(compute_dtype)
+        pe = positional_rows(self.position_enc, T, self.d_model, texts.device, compute_dtype)
         # the fp32 table itself: the HIP op reads its cached bf16 image and writes the gradient slot
         tab = self.src_word_emb.weight if ops.use_hip(texts) else self.src_word_emb.weight.to(compute_dtype)
         x = ops.embed_add_pe(texts, tab, pe)
@@ -92,7 +104,7 @@ class Decoder(nn.Module):
             M = self.max_seq_len
             x = x[:, :M]
             mel_lens = mel_lens.clamp(max=M)
-        pe = positional_rows(self.position_enc, M, self.d_model, x.device).to(x.dtype)
+        pe = positional_rows(self.position_enc, M, self.d_model, x.device, x.dtype)
         x = x + pe.unsqueeze(0)
         for layer in self.layer_stack:
             x = layer(x, mel_lens, style)
@@ -107,7 +119,7 @@ class Decoder(nn.Module):
             M = self.max_seq_len
         dec_lens = mel_lens.clamp(max=M)
         pk = ops.PackInfo.build(dec_lens, M, R)
-        pe = positional_rows(self.position_enc, M, self.d_model, x_phone.device).to(x_phone.dtype)
+        pe = positional_rows(self.position_enc, M, self.d_model, x_phone.device, x_phone.dtype)
         x = ops.length_regulate_packed(x_phone, durations, pk, pe)
         for layer in self.layer_stack:
             x = layer(x, dec_lens, style, pack=pk)
