@@ -18,20 +18,39 @@ def main():
     from speakingstyle_amd.train.trainer import Trainer
 
     cfg = sys.argv[1] if len(sys.argv) > 1 else "LJSpeech"
+    synth = cfg.startswith("synth:")  # synth:<config>: one batch-1 packed synthesis (eager) instead of a train step
+    cfg = cfg.split(":", 1)[1] if synth else cfg
     pp, mc, tc = load_named(cfg)
-    bs = int(sys.argv[2]) if len(sys.argv) > 2 else int(tc["optimizer"]["batch_size"])
+    bs = int(sys.argv[2]) if len(sys.argv) > 2 else (1 if synth else int(tc["optimizer"]["batch_size"]))
     torch.manual_seed(0)
     model = FastSpeech2(pp, mc).to("cuda").set_compute_dtype(torch.bfloat16)
-    tr = Trainer(model, (pp, mc, tc), seed=1)
-    tr.use_priority_stream(True)
     gen = SyntheticBatches(bs, device="cuda", max_seq_len=mc["max_seq_len"], seed=5,
                            frame_level=pp["preprocessing"]["pitch"]["feature"] == "frame_level")
     bats = [gen.make_batch() for _ in range(3)]
+    if synth:
+        import math
+
+        from speakingstyle_amd.utils.model import get_vocoder
+
+        with torch.no_grad():
+            lin = model.variance_adaptor.duration_predictor.linear_layer
+            lin.weight.normal_(0.0, 0.005)
+            lin.bias.fill_(math.log(9.1))
+        model.eval().requires_grad_(False)
+        voc = get_vocoder(mc, torch.device("cuda"))
+
+        def step(b):
+            rows, lens, _ = model.infer_packed(b[2], b[3], b[4], b[5], b[6], b[7], b[8])
+            voc.infer_packed(rows, lens, int16_scale=32768.0).cpu()
+    else:
+        tr = Trainer(model, (pp, mc, tc), seed=1)
+        tr.use_priority_stream(True)
+        step = tr.train_step
     for b in bats[:2]:
-        tr.train_step(b)
+        step(b)
     torch.cuda.synchronize()
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
-        tr.train_step(bats[2])
+        step(bats[2])
         torch.cuda.synchronize()
     sites, kinds = Counter(), Counter()
     total = Counter()
