@@ -16,7 +16,6 @@ from __future__ import annotations
 import json
 import math
 import os
-import weakref
 from typing import Optional
 
 import torch
@@ -34,7 +33,7 @@ def _pe_param(n_position: int, d: int) -> nn.Parameter:
     return nn.Parameter(ops.sinusoid_table(n_position, d).unsqueeze(0), requires_grad=False)
 
 
-_PE_CAST = weakref.WeakKeyDictionary()  # positional table -> (dtype, version, address) key, cast copy
+_PE_CAST = ops.IdCache()  # positional table -> ((dtype, version, address), cast copy)
 
 
 def positional_rows(pe_param: torch.Tensor, length: int, d: int, device, dtype=None) -> torch.Tensor:
@@ -47,7 +46,7 @@ def positional_rows(pe_param: torch.Tensor, length: int, d: int, device, dtype=N
         hit = _PE_CAST.get(pe_param)
         if hit is None or hit[0] != (dtype, pe_param._version, pe_param.data_ptr()):
             hit = ((dtype, pe_param._version, pe_param.data_ptr()), pe_param.detach()[0].to(dtype).contiguous())
-            _PE_CAST[pe_param] = hit
+            _PE_CAST.put(pe_param, hit)
         return hit[1][:length]
     t = ops.sinusoid_table(length, d, device=device)
     return t if dtype is None else t.to(dtype)

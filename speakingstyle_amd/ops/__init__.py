@@ -76,6 +76,25 @@ def linear_group(x, weights, biases, mailbox=None):
     return ref.linear(x, torch.cat(list(weights), 0), torch.cat(list(biases), 0))
 
 
+class IdCache:
+    """Values cached per tensor object (by identity, held weakly): ``WeakKeyDictionary`` compares tensor keys with
+    ``==`` (elementwise) and cannot be used for tensors."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, t):
+        e = self._d.get(id(t))
+        return e[1] if e is not None and e[0]() is t else None
+
+    def put(self, t, v):
+        import weakref
+
+        if len(self._d) > 256:  # drop entries whose tensor is gone
+            self._d = {k: e for k, e in self._d.items() if e[0]() is not None}
+        self._d[id(t)] = (weakref.ref(t), v)
+
+
 def conv1d(x, w, b=None, pad=0, dil=1, act=None, pack: Optional[PackInfo] = None):
     """``pack``: x is packed ``[1, R, C]``; the conv zero-pads at every sequence end."""
     if use_hip(x):

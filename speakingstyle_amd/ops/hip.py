@@ -815,7 +815,7 @@ class _GroupLinearFn(torch.autograd.Function):
         return (dx, None, None, None, None, *gradslots.split_rows(dw, ws), *gradslots.split_rows(db, bs))
 
 
-_GROUP_CAT = weakref.WeakKeyDictionary()  # first weight of a projection group -> (versions, fused weight, bias)
+_GROUP_CAT = None  # IdCache: first weight of a projection group -> (versions, fused weight, bias)
 
 
 def linear_group(x, weights, biases, mailbox=None):
@@ -829,11 +829,16 @@ def linear_group(x, weights, biases, mailbox=None):
         else:  # inference outside an arena: the concatenation cached per weight version, held as a Parameter so
             #     that its bf16 operand image is cached too (_cached); nothing is attached to the model's tensors
             key = tuple((t.data_ptr(), t._version) for t in weights + biases)
+            global _GROUP_CAT
+            if _GROUP_CAT is None:
+                from . import IdCache
+
+                _GROUP_CAT = IdCache()
             hit = _GROUP_CAT.get(weights[0])
             if hit is None or hit[0] != key:
                 wc = torch.nn.Parameter(torch.cat([t.detach() for t in weights], 0), requires_grad=False)
                 hit = (key, wc, torch.cat([t.detach().float() for t in biases], 0).contiguous())
-                _GROUP_CAT[weights[0]] = hit
+                _GROUP_CAT.put(weights[0], hit)
             w, b = hit[1], hit[2]
         return linear(x, w, b)
     shp = x.shape

@@ -73,3 +73,26 @@ def test_pack_info_cpu():
     mask = torch.arange(4)[None] < lens.clamp(max=4)[:, None]
     torch.testing.assert_close(y[mask], x[mask])
     assert (y[~mask] == torch.tensor([7.0, 8.0])).all()
+
+
+def test_positional_rows_cast_cache_and_idcache():
+    """The per-dtype positional table copy is made once and sliced (no cast per forward); IdCache is keyed by
+    tensor identity (a WeakKeyDictionary would compare tensor keys elementwise) and follows in-place updates."""
+    import torch
+
+    from speakingstyle_amd.models.fastspeech2 import positional_rows
+    from speakingstyle_amd.ops import IdCache
+
+    p = torch.nn.Parameter(torch.randn(1, 10, 4), requires_grad=False)
+    a = positional_rows(p, 5, 4, "cpu", torch.bfloat16)
+    b = positional_rows(p, 3, 4, "cpu", torch.bfloat16)
+    assert a.dtype == torch.bfloat16 and a.data_ptr() == b.data_ptr()
+    assert torch.equal(a, p[0, :5].to(torch.bfloat16))
+    with torch.no_grad():
+        p.add_(1.0)  # version bump -> fresh copy
+    c = positional_rows(p, 5, 4, "cpu", torch.bfloat16)
+    assert torch.equal(c, p[0, :5].to(torch.bfloat16))
+    cache = IdCache()
+    t1, t2 = torch.zeros(3), torch.zeros(3)
+    cache.put(t1, "one")
+    assert cache.get(t1) == "one" and cache.get(t2) is None
