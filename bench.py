@@ -95,9 +95,6 @@ def parse(argv=None):
                     help="launch kernels through ctypes instead of the generated native bindings (A/B)")
     ap.add_argument("--force-buckets", action="store_true",
                     help="1 GPU: run the DP gradient path (1-rank RCCL group, hooks, bucket all-reduces)")
-    ap.add_argument("--graphs", action="store_true",
-                    help="HIP-graph training steps (train/graphs.py): forward + backward captured per padded-shape "
-                         "bucket and replayed -- for host-bound small per-GPU batches (1 process)")
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
                     help="default: nccl (RCCL) on GPUs; gloo rehearses the multi-rank path on fewer GPUs")
     return ap.parse_args(argv)
@@ -192,8 +189,6 @@ def run(args):
         rec["host_tail_ms"] = tr["host_tail_ms"]
     if tr.get("tail_events_ms"):
         rec["tail_events_ms"] = tr["tail_events_ms"]
-    if tr.get("graphs"):
-        rec["graphs"] = tr["graphs"]
     if tr.get("phases"):
         rec["phase_ms"] = {k: {"host": round(v["host_ms"], 3), "device": round(v["device_ms"], 3)}
                            for k, v in tr["phases"].items()}

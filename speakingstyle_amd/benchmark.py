@@ -143,28 +143,15 @@ def train_phase(args, rank, world, device):
     from . import experimental
 
     fail_rank = experimental.get("fail_rank")  # fault injection (launcher failure-path test)
-    graphed = None
-    if getattr(args, "graphs", False) and cuda:
-        from .train.graphs import GraphedSteps
-
-        if GraphedSteps.supported(trainer):
-            graphed = GraphedSteps(trainer)
-
     def step(i):
         if fail_rank is not None and int(fail_rank) == rank and i == 1:
             raise RuntimeError(f"injected failure on rank {rank}")
         b, frames = pool[i % len(pool)]
-        if graphed is not None:
-            graphed.step(b)
-        else:
-            trainer.train_step(b)
+        trainer.train_step(b)
         return frames
 
-    # at least one untimed step under DP: the gradient-bucket calibration pass (ddp.GradBuckets); with HIP
-    # graphs every pool batch's bucket is warmed and captured before the timed steps
+    # at least one untimed step under DP: the gradient-bucket calibration pass (ddp.GradBuckets)
     warm = max(args.warmup, 1 if (world > 1 or trainer.buckets.active) else 0)
-    if graphed is not None:
-        warm = max(warm, (graphed.warm + 1) * len(pool))
     for i in range(warm):
         step(i)
     trainer.timer.summary()  # drop the warm-up phases
@@ -262,8 +249,6 @@ def train_phase(args, rank, world, device):
     tail = trainer.host_tail_summary()
     if tail is not None:
         info["host_tail_ms"] = tail
-    if graphed is not None:
-        info["graphs"] = graphed.stats()
     del trainer, model, pool
     if cuda:
         torch.cuda.empty_cache()

@@ -112,12 +112,6 @@ _TRAIN_DEFAULTS: Config = {
         "stream_priority": "high",
         # run backward on the calling thread (no autograd device worker thread): less host time per step
         "backward_same_thread": True,
-        # HIP-graph training steps (train/graphs.py): forward + backward captured once per padded-shape
-        # bucket (phonemes rounded up to graph_t_quant, frames to graph_m_quant) and replayed -- removes
-        # the ~12 ms of host launch work per step that bounds small per-GPU batches; one process only
-        "graph_steps": False,
-        "graph_t_quant": 16,
-        "graph_m_quant": 32,
         # (non-finite steps are always skipped on the device by the fused clip+Adam kernel: no knob)
         # validated experiment / diagnostic switches (speakingstyle_amd/experimental.py); empty = production
         "experimental": {},
@@ -210,9 +204,8 @@ def normalize_train_config(cfg: Config | None) -> Config:
     mi = out["mi355x"]
     _check_enum(mi["dtype"], ["bf16", "fp32"], "mi355x.dtype")
     _check_enum(mi.get("stream_priority", "high"), ["high", "normal"], "mi355x.stream_priority")
-    for q in ("graph_t_quant", "graph_m_quant"):
-        if int(mi.get(q, 16)) <= 0:
-            raise ConfigError(f"mi355x.{q} must be a positive multiple")
+    for k in ("graph_steps", "graph_t_quant", "graph_m_quant"):  # removed knobs (round 6: training graphs lost)
+        mi.pop(k, None)
     if mi.get("frames_per_gpu") is not None and int(mi["frames_per_gpu"]) <= 0:
         raise ConfigError("mi355x.frames_per_gpu must be a positive frame count (or null)")
     if "nan_guard" in mi:  # removed knob: the device-side non-finite skip is unconditional

@@ -396,7 +396,7 @@ def weight_dgrad(w: torch.Tensor, owner: Optional[torch.Tensor] = None) -> torch
 _ACT = {None: 0, "relu": 1, "lrelu": 2, "tanh": 3, "relu_ln": 1}  # relu_ln: ReLU, mask left to the consumer LN
 
 _ws = {}
-# HIP graphs (train/graphs.py) bake the workspace address into their kernels: once one has been captured, a
+# HIP graphs (infer/graphs.py) bake the workspace address into their kernels: once one has been captured, a
 # workspace that grows is retired here instead of freed, so a later replay of an older graph never writes
 # into memory the caching allocator has handed to another tensor
 _GRAPHS_LIVE = [False]

@@ -127,17 +127,6 @@ def train(args, configs):
     trainer.use_priority_stream(cuda and (train_config.get("mi355x", {}) or {}).get("stream_priority", "high") == "high")
     if ckpt is not None and "optimizer" in ckpt:
         trainer.opt.load_state_dict(ckpt["optimizer"])
-    # mi355x.graph_steps: HIP-graph steps per padded-shape bucket (train/graphs.py) -- for host-bound small
-    # per-GPU batches; single process only (multi-rank runs stay eager)
-    graphed = None
-    if cuda and mi.get("graph_steps", False):
-        from .graphs import GraphedSteps
-
-        if GraphedSteps.supported(trainer):
-            graphed = GraphedSteps(trainer, t_quant=int(mi.get("graph_t_quant", 16)),
-                                   m_quant=int(mi.get("graph_m_quant", 32)))
-        elif rank == 0:
-            print("mi355x.graph_steps: needs one process and grad_acc_step 1; running eager steps", flush=True)
     if ckpt is not None and isinstance(ckpt.get("rng"), torch.Tensor) and not cuda:
         torch.set_rng_state(ckpt["rng"])  # CPU dropout (torch RNG); the GPU masks are step-seeded
     if rank == 0:
@@ -207,7 +196,7 @@ def train(args, configs):
                     continue
                 if fail_at and step == fail_at:
                     raise RuntimeError(f"fault injection at step {step}")
-                losses, output, lr = (graphed.step(batch) if graphed is not None else trainer.train_step(batch))
+                losses, output, lr = trainer.train_step(batch)
                 if step == restore + 1:  # per-rank batch shape of the first step (DP batch semantics)
                     budget = (train_config.get("mi355x") or {}).get("frames_per_gpu")
                     rule = f"frames_per_gpu={budget}" if budget else f"batch_size/world={bs_global}/{world}"

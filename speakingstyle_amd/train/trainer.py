@@ -160,7 +160,7 @@ class Trainer:
         """Dropout randomness of this micro-step: the per-op seeds (host LCG) start from a per-(seed, rank)
         value that does not change between steps, and the step-dependent part -- (optimizer step, micro-step)
         -- is the device dropout salt (``hip.set_dropout_salt``), so a step captured in a HIP graph
-        (``train/graphs.py``) replays with the masks of the step it stands for, bit-identical to the eager
+        (a captured step) replays with the masks of the step it stands for, bit-identical to the eager
         step, and a resumed run reproduces the masks of an uninterrupted one."""
         if self.seed is None or not self.opt.arena.data.is_cuda:
             return
@@ -202,7 +202,7 @@ class Trainer:
     def forward_backward(self, batch, counts=None, work=None, last_micro=True):
         """Forward + loss + backward of one micro-step, every gradient in its arena slot at return (side
         streams joined).  Device work only after ``_step_seed``: the part a HIP graph captures
-        (``train/graphs.py``)."""
+        (a captured step)."""
         tm = self.timer
         if self.opt.arena.data.is_cuda and self.seed is not None:
             from ..ops import hip

@@ -17,6 +17,7 @@ from speakingstyle_amd.models.hifigan import LRELU_SLOPE, ResBlock1
 
 # (C, K) -> NB of struct RF (16-row blocks per tile)
 RF_NB = {(32, 3): 16, (32, 7): 40, (32, 11): 40, (64, 3): 24, (64, 7): 24, (128, 3): 12}
+RF_NB_EXTRA = {(64, 11): 24, (128, 7): 12}  # behind ssamd_resblock_set_whole_extra (measured slower, off)
 MAXD = 5
 
 
@@ -169,10 +170,12 @@ def test_tile_constants_mirror_the_kernel():
                 nest -= 1
         raise ValueError(e)
 
-    for (C, K), nb in RF_NB.items():
+    for (C, K), nb in list(RF_NB.items()) + list(RF_NB_EXTRA.items()):
         assert ev(expr, C, K) == nb, (C, K, expr)
     fus = re.search(r"int ssamd_resblock_fusable\(int C, int K\) \{\s*return (.+?);", src, re.S).group(1)
-    fus = fus.replace("&&", " and ").replace("||", " or ")
-    for C in (32, 64, 128, 256):
-        for K in (3, 7, 11):
-            assert bool(eval(fus, {"C": C, "K": K})) == ((C, K) in RF_NB), (C, K)
+    fus = " ".join(fus.replace("&&", " and ").replace("||", " or ").split())
+    for extra in (0, 1):  # g_rf_extra: the whole-block instances of ssamd_resblock_set_whole_extra
+        want = set(RF_NB) | (set(RF_NB_EXTRA) if extra else set())
+        for C in (32, 64, 128, 256):
+            for K in (3, 7, 11):
+                assert bool(eval(fus, {"C": C, "K": K, "g_rf_extra": extra})) == ((C, K) in want), (C, K, extra)
