@@ -43,7 +43,8 @@ struct RB {
   static constexpr bool BIG = BIG_;
   static constexpr int NW = BIG ? 8 : (C >= 128 ? 8 : 4);  // waves per block
   static constexpr int NT = 64 * NW;
-  static constexpr int WC = C >= 128 ? 2 : 1;       // column groups
+  // column groups: 64 columns per wave in the tall tile (C = 256: 4 x 2 waves), else 2 groups from C = 128 up
+  static constexpr int WC = BIG ? (C >= 64 ? C / 64 : 1) : (C >= 128 ? 2 : 1);
   static constexpr int WR = NW / WC;                // row groups
   static constexpr int RPW = RPW_;                  // row blocks per wave
   static constexpr int H2 = (K - 1) / 2;
@@ -451,7 +452,11 @@ static int g_rb_tall = 1;
 SSAMD_API void ssamd_resblock_set_tall(int v) { g_rb_tall = v; }
 template <int C, int K>
 constexpr bool has_tall() {
-  return (C == 128 && (K == 7 || K == 11)) || (C == 64 && K == 11);
+  return (C == 128 && (K == 7 || K == 11)) || (C == 64 && K == 11) || (C == 256 && K <= 7);
+}
+template <int C>
+constexpr bool tall_only() {  // C = 256: the 128-row tile does not fit the LDS -- the tall tile is the only one
+  return C == 256;
 }
 
 template <class R>
@@ -487,19 +492,27 @@ template <int C, int K>
 int launch_rb_any(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
                   const bf16_t* acc_in, bf16_t* out, int B, int T, int d, float slope, float out_scale, int post_lrelu,
                   hipStream_t s, const int4* tt = nullptr, int ntt = 0) {
-  if constexpr (has_tall<C, K>()) {
-    if (g_rb_tall)
-      return launch_rb<RBT<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
+  if constexpr (tall_only<C>()) {
+    return launch_rb<RBT<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
+  } else {
+    if constexpr (has_tall<C, K>()) {
+      if (g_rb_tall)
+        return launch_rb<RBT<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
+    }
+    return launch_rb<RB<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
   }
-  return launch_rb<RB<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
 }
 
 template <int C, int K>
 int rb_bm() {
-  if constexpr (has_tall<C, K>()) {
-    if (g_rb_tall) return RBT<C, K>::BM;
+  if constexpr (tall_only<C>()) {
+    return RBT<C, K>::BM;
+  } else {
+    if constexpr (has_tall<C, K>()) {
+      if (g_rb_tall) return RBT<C, K>::BM;
+    }
+    return RB<C, K>::BM;
   }
-  return RB<C, K>::BM;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1099,7 +1112,7 @@ SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2
   if (C == CC && K == KK) return RF<CC, KK>::R0 - 2 * (RF<CC, KK>::H2 * (d0 + d1 + d2 + 3));
   if (kind == 0) {
     VT_RB(32, 3) VT_RB(32, 7) VT_RB(32, 11) VT_RB(64, 3) VT_RB(64, 7) VT_RB(64, 11) VT_RB(128, 3) VT_RB(128, 7)
-    VT_RB(128, 11)
+    VT_RB(128, 11) VT_RB(256, 3) VT_RB(256, 7)
   } else if (kind == 1) {
     VT_RF(32, 3) VT_RF(32, 7) VT_RF(32, 11) VT_RF(64, 3) VT_RF(64, 7) VT_RF(128, 3) VT_RF(64, 11) VT_RF(128, 7)
   } else if (kind == 2) {
@@ -1142,6 +1155,7 @@ SSAMD_API int ssamd_resblock_layer_pk(const bf16_t* x, const bf16_t* w1, const f
   RBK_CASE(32, 3) RBK_CASE(32, 7) RBK_CASE(32, 11)
   RBK_CASE(64, 3) RBK_CASE(64, 7) RBK_CASE(64, 11)
   RBK_CASE(128, 3) RBK_CASE(128, 7) RBK_CASE(128, 11)
+  RBK_CASE(256, 3) RBK_CASE(256, 7)  // (C = 256 / K = 11 spills at 256 VGPRs: the GEMM path)
 #undef RBK_CASE
   return -2;
 }
@@ -1270,6 +1284,7 @@ SSAMD_API int ssamd_resblock_layer(const bf16_t* x, const bf16_t* w1, const floa
   RB_CASE(32, 3) RB_CASE(32, 7) RB_CASE(32, 11)
   RB_CASE(64, 3) RB_CASE(64, 7) RB_CASE(64, 11)
   RB_CASE(128, 3) RB_CASE(128, 7) RB_CASE(128, 11)
+  RB_CASE(256, 3) RB_CASE(256, 7)
 #undef RB_CASE
   return -2;
 }

@@ -143,8 +143,11 @@ class ResBlock1(nn.Module):
         return x
 
     def fusable(self, channels: int) -> bool:
-        """Geometry covered by the fused ResBlock1 layer kernel (csrc/k_vocoder.hip)."""
-        return channels in (32, 64, 128) and self.kernel_size in (3, 7, 11) and max(self.dilation) <= 5
+        """Geometry covered by the fused ResBlock1 layer kernel (csrc/k_vocoder.hip); C = 256 (K <= 7) on its
+        tall tile only, behind ``_RB256``."""
+        if max(self.dilation) > 5 or self.kernel_size not in (3, 7, 11):
+            return False
+        return channels in (32, 64, 128) or (_RB256[0] and channels == 256 and self.kernel_size <= 7)
 
     def fused_ok(self, x) -> bool:
         return x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16 and self.fusable(x.shape[-1])
@@ -453,7 +456,7 @@ class Generator(nn.Module):
             blocks = [self.resblocks[i * nk + j] for j in range(nk)]
             B, T, _ = x.shape
             img = self._ups_image(i)
-            fused = blocks[0].fusable(up.weight.shape[1])
+            fused = all(b.fusable(up.weight.shape[1]) for b in blocks)
             x_act = None
             if img is None:  # generic ConvTranspose geometry: polyphase fallback on the same GEMM kernel
                 y = conv_transpose_polyphase(x, _w(up), up.bias, s, up.padding[0])
@@ -526,7 +529,8 @@ class Generator(nn.Module):
             blocks = [self.resblocks[i * nk + j] for j in range(nk)]
             wu, _, bt = self._ups_image(i)
             cout = wu.shape[0] // s
-            if blocks[0].fusable(cout) and _CONV3_SQ[0] and bt is not None and wu.shape[0] == wu.shape[1] in (64, 128):
+            if all(b.fusable(cout) for b in blocks) and _CONV3_SQ[0] and bt is not None and \
+                    wu.shape[0] == wu.shape[1] in (64, 128):
                 geoms.append((rate, hip.voc_tile_rows(2, wu.shape[1])))
             rate *= s
             for blk in blocks:
@@ -546,7 +550,8 @@ class Generator(nn.Module):
             blocks = [self.resblocks[i * nk + j] for j in range(nk)]
             wu, wimg, bt = self._ups_image(i)
             cout = wu.shape[0] // s
-            fused = blocks[0].fusable(cout)
+            # lrelu(y) as a second GEMM output only when some branch runs on the GEMM path (it needs it as input)
+            fused = all(b.fusable(cout) for b in blocks)
             x_act = None
             if fused and _CONV3_SQ[0] and bt is not None and wu.shape[0] == wu.shape[1] in (64, 128):
                 y = hip.conv3_sq_packed(x, vp, rate, wimg, bt)
@@ -581,6 +586,8 @@ class Generator(nn.Module):
     remove_weight_norm = fold_weight_norm
 
 
+# the C = 256 MRF (K = 3 / 7 branches) on the tall per-layer ResBlock kernel instead of two GEMMs per layer pair
+_RB256 = [True]
 # GPU inference with host lengths: the packed, length-exact path (infer_packed) instead of length buckets
 _PACKED = [True]
 # square upsamplers (N = stride * Cout = Cin in {64, 128}) on ``hip.conv3_sq`` instead of the generic GEMM

@@ -1187,7 +1187,8 @@ def test_weight_prep_batched_refresh_exact():
 
 
 @pytest.mark.parametrize("C,K,d,T", [(32, 3, 1, 300), (32, 11, 5, 1000), (64, 7, 3, 129), (64, 11, 5, 40), (32, 7, 1, 5),
-                                     (128, 11, 5, 700), (128, 3, 3, 129)])
+                                     (128, 11, 5, 700), (128, 3, 3, 129), (256, 3, 5, 300), (256, 7, 3, 200),
+                                     (256, 7, 1, 9)])
 def test_resblock_layer_fused(C, K, d, T):
     """Fused HiFi-GAN ResBlock1 layer (lrelu -> dilated conv -> lrelu -> conv -> + x [+ acc, * scale])
     vs fp32 torch, incl. sequences shorter than the halo and the in-place MRF accumulation."""
