@@ -37,11 +37,28 @@ def cuda_any(a, k, r):
     return any(t.is_cuda for t in ts)
 
 
+def launched(a, k, r):
+    """A kernel (or runtime copy) ran: conversions / slicing count only when they made new storage."""
+    if not cuda_any(a, k, r):
+        return False
+    src = a[0] if a and isinstance(a[0], torch.Tensor) else None
+    if isinstance(r, torch.Tensor) and src is not None:
+        if r is src:
+            return False
+        try:
+            if r.untyped_storage().data_ptr() == src.untyped_storage().data_ptr():
+                return False  # a view
+        except Exception:  # noqa: BLE001
+            pass
+    return True
+
+
 def main():
     for n in ("copy_", "clone", "to", "contiguous", "float", "fill_", "zero_", "__add__", "__mul__", "__sub__",
-              "add_", "mul_", "masked_fill", "masked_fill_", "__getitem__", "sum", "clamp", "expand", "repeat"):
-        wrap(torch.Tensor, n, cuda_any)
-    for n in ("cat", "zeros", "full", "stack", "zeros_like", "ones", "arange", "tensor", "empty_like"):
+              "__truediv__", "__floordiv__", "__rshift__", "add_", "mul_", "masked_fill", "masked_fill_",
+              "__getitem__", "sum", "clamp", "repeat", "index_select", "long", "int"):
+        wrap(torch.Tensor, n, launched)
+    for n in ("cat", "zeros", "full", "stack", "zeros_like", "ones", "arange", "tensor"):
         wrap(torch, n, cuda_any)
     from speakingstyle_amd.config import load_named
     from speakingstyle_amd.data.synthetic import SyntheticBatches
