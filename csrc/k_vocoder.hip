@@ -1118,6 +1118,16 @@ SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2
   } else if (kind == 2) {
     if (C == 128) return C3<128>::BM;
     if (C == 64) return C3<64>::BM;
+  } else if (kind == 3 || kind == 4) {  // 3: the tall per-layer tile, 4: the 128-row one (0: no such instance)
+#define VT_RB2(CC, KK)                                                                  \
+  if (C == CC && K == KK) {                                                             \
+    if constexpr (has_tall<CC, KK>()) { if (kind == 3) return RBT<CC, KK>::BM; }        \
+    if constexpr (!tall_only<CC>()) { if (kind == 4) return RB<CC, KK>::BM; }           \
+    return 0;                                                                           \
+  }
+    VT_RB2(32, 3) VT_RB2(32, 7) VT_RB2(32, 11) VT_RB2(64, 3) VT_RB2(64, 7) VT_RB2(64, 11) VT_RB2(128, 3)
+    VT_RB2(128, 7) VT_RB2(128, 11) VT_RB2(256, 3) VT_RB2(256, 7)
+#undef VT_RB2
   }
 #undef VT_RB
 #undef VT_RF
@@ -1157,6 +1167,36 @@ SSAMD_API int ssamd_resblock_layer_pk(const bf16_t* x, const bf16_t* w1, const f
   RBK_CASE(128, 3) RBK_CASE(128, 7) RBK_CASE(128, 11)
   RBK_CASE(256, 3) RBK_CASE(256, 7)  // (C = 256 / K = 11 spills at 256 VGPRs: the GEMM path)
 #undef RBK_CASE
+  return -2;
+}
+
+// ssamd_resblock_layer_pk with the tile chosen by the caller (tall = 1: the tall tile, 0: the 128-row tile) -- the
+// packed vocoder picks per call from the tile count (ssamd_voc_tile_rows kinds 3 / 4): a batch-1 utterance gets
+// twice the workgroups from the shorter tile, a batch of 256 the tall tile's fewer LDS reads per MFMA
+SSAMD_API int ssamd_resblock_layer_pk2(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
+                                       const float* b2, const bf16_t* acc_in, bf16_t* out, const int* tt, int ntt, int C,
+                                       int K, int d, float slope, float out_scale, int post_lrelu, int tall,
+                                       hipStream_t s) {
+  if (d < 1 || d > MAXD || !tt) return -2;
+  if (ntt <= 0) return 0;
+  const int4* t4 = reinterpret_cast<const int4*>(tt);
+#define RBK2_CASE(CC, KK)                                                                                          \
+  if (C == CC && K == KK) {                                                                                        \
+    if constexpr (has_tall<CC, KK>()) {                                                                            \
+      if (tall)                                                                                                    \
+        return launch_rb<RBT<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, \
+                                      ntt);                                                                        \
+    }                                                                                                              \
+    if constexpr (!tall_only<CC>()) {                                                                              \
+      if (!tall)                                                                                                   \
+        return launch_rb<RB<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4,  \
+                                     ntt);                                                                         \
+    }                                                                                                              \
+    return -2;                                                                                                     \
+  }
+  RBK2_CASE(32, 3) RBK2_CASE(32, 7) RBK2_CASE(32, 11) RBK2_CASE(64, 3) RBK2_CASE(64, 7) RBK2_CASE(64, 11)
+  RBK2_CASE(128, 3) RBK2_CASE(128, 7) RBK2_CASE(128, 11) RBK2_CASE(256, 3) RBK2_CASE(256, 7)
+#undef RBK2_CASE
   return -2;
 }
 

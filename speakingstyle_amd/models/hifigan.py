@@ -142,12 +142,15 @@ class ResBlock1(nn.Module):
             x = glue.add(t, x)
         return x
 
-    def fusable(self, channels: int) -> bool:
+    def fusable(self, channels: int, rows=None) -> bool:
         """Geometry covered by the fused ResBlock1 layer kernel (csrc/k_vocoder.hip); C = 256 (K <= 7) on its
-        tall tile only, behind ``_RB256``."""
+        tall tile only, behind ``_RB256``, and (``rows`` given) only for >= ``_RB256_MIN_ROWS`` rows: a batch-1
+        utterance's few 128-row tiles leave the GPU idle where the GEMM path spreads the work over more blocks."""
         if max(self.dilation) > 5 or self.kernel_size not in (3, 7, 11):
             return False
-        return channels in (32, 64, 128) or (_RB256[0] and channels == 256 and self.kernel_size <= 7)
+        if channels == 256:
+            return bool(_RB256[0] and self.kernel_size <= 7 and (rows is None or rows >= _RB256_MIN_ROWS[0]))
+        return channels in (32, 64, 128)
 
     def fused_ok(self, x) -> bool:
         return x.is_cuda and ops.use_hip(x) and x.dtype == torch.bfloat16 and self.fusable(x.shape[-1])
@@ -203,7 +206,7 @@ class ResBlock1(nn.Module):
         k = self.kernel_size
         n = len(self.convs1)
         C = x.shape[-1]
-        if self.fusable(C):
+        if self.fusable(C, x.shape[0]):
             if _WHOLE_BLOCK[0] and n == 3 and hip.resblock_fusable(C, k):
                 return hip.resblock_fused_packed(x, vp, rate, self.convs1, self.convs2, self.dilation, LRELU_SLOPE,
                                                  acc=acc, out_scale=out_scale, post_lrelu=post_lrelu)
@@ -223,14 +226,15 @@ class ResBlock1(nn.Module):
                                             scale=out_scale, post_act="lrelu" if post_lrelu else None)
         return x
 
-    def packed_tiles(self, C: int, rate: int):
-        """(rate, tile rows) pairs of this block's tiled kernels at channel width C."""
+    def packed_tiles(self, C: int, rate: int, lens=()):
+        """(rate, tile rows) pairs of this block's tiled kernels at channel width C for a packed batch of
+        these frame lengths."""
         hip = ops._hip()
-        if not self.fusable(C):
+        if not self.fusable(C, sum(int(L) for L in lens) * rate):
             return []
         if _WHOLE_BLOCK[0] and len(self.convs1) == 3 and hip.resblock_fusable(C, self.kernel_size):
             return [(rate, hip.voc_tile_rows(1, C, self.kernel_size, self.dilation))]
-        return [(rate, hip.voc_tile_rows(0, C, self.kernel_size))]
+        return [(rate, hip.rb_layer_tile(C, self.kernel_size, lens, rate)[1])]
 
 
 def _lrelu(x, slope=LRELU_SLOPE):
@@ -529,14 +533,14 @@ class Generator(nn.Module):
             blocks = [self.resblocks[i * nk + j] for j in range(nk)]
             wu, _, bt = self._ups_image(i)
             cout = wu.shape[0] // s
-            if all(b.fusable(cout) for b in blocks) and _CONV3_SQ[0] and bt is not None and \
+            if all(b.fusable(cout, sum(lens) * rate * s) for b in blocks) and _CONV3_SQ[0] and bt is not None and \
                     wu.shape[0] == wu.shape[1] in (64, 128):
                 geoms.append((rate, hip.voc_tile_rows(2, wu.shape[1])))
             rate *= s
             for blk in blocks:
-                geoms.extend(blk.packed_tiles(cout, rate))
+                geoms.extend(blk.packed_tiles(cout, rate, lens))
         c_last = self.h.upsample_initial_channel // 2 ** self.num_upsamples
-        geoms.append((rate, hip.voc_tile_rows(3, c_last)))
+        geoms.append((rate, hip.voc_tile_rows("post", c_last)))
         vp = hip.voc_pack_for(lens, dev, geoms)
         out = torch.zeros(B, W, device=dev, dtype=torch.int16 if int16_scale is not None else torch.float32)
         if vp.R == 0:
@@ -551,7 +555,7 @@ class Generator(nn.Module):
             wu, wimg, bt = self._ups_image(i)
             cout = wu.shape[0] // s
             # lrelu(y) as a second GEMM output only when some branch runs on the GEMM path (it needs it as input)
-            fused = all(b.fusable(cout) for b in blocks)
+            fused = all(b.fusable(cout, vp.R * rate * s) for b in blocks)
             x_act = None
             if fused and _CONV3_SQ[0] and bt is not None and wu.shape[0] == wu.shape[1] in (64, 128):
                 y = hip.conv3_sq_packed(x, vp, rate, wimg, bt)
@@ -588,6 +592,7 @@ class Generator(nn.Module):
 
 # the C = 256 MRF (K = 3 / 7 branches) on the tall per-layer ResBlock kernel instead of two GEMMs per layer pair
 _RB256 = [True]
+_RB256_MIN_ROWS = [65536]  # (256 tiles of the 128-row tall tile at C = 256 -- one per CU -- is 32k rows)
 # GPU inference with host lengths: the packed, length-exact path (infer_packed) instead of length buckets
 _PACKED = [True]
 # square upsamplers (N = stride * Cout = Cin in {64, 128}) on ``hip.conv3_sq`` instead of the generic GEMM

@@ -2246,6 +2246,7 @@ _SIGS.update({"ssamd_gemm_retain_workspaces": [I],
               "ssamd_voc_rinfo": [P, I, I, I, P, P],
               "ssamd_voc_pack": [P, I, P, I, I, I, P, P],
               "ssamd_resblock_layer_pk": [P, P, P, P, P, P, P, P, I, I, I, I, F, F, I, P],
+              "ssamd_resblock_layer_pk2": [P, P, P, P, P, P, P, P, I, I, I, I, F, F, I, I, P],
               "ssamd_resblock_fused_pk": [P] * 16 + [I, I, I, I, I, I, F, F, I, P],
               "ssamd_conv3_sq_pk": [P, P, P, P, P, I, I, P],
               "ssamd_conv_post_pk": [P, P, P, P, I, I, F, F, P, P, L_, P],
@@ -2331,12 +2332,13 @@ def voc_pack_for(lens, device, rate_tiles, cache: int = 32) -> "VocPack":
 _TILE_ROWS = {}
 
 
-def voc_tile_rows(kind: int, C: int, K: int = 0, dil=(0, 0, 0)) -> int:
-    """Tile height of a tiled vocoder kernel (0 resblock_layer, 1 resblock_fused, 2 conv3_sq, 3 conv_post)."""
+def voc_tile_rows(kind, C: int, K: int = 0, dil=(0, 0, 0)) -> int:
+    """Tile height of a tiled vocoder kernel (0 resblock_layer (the global variant), 1 resblock_fused, 2 conv3_sq,
+    3 / 4 the tall / 128-row per-layer tile, "post" conv_post)."""
     key = (kind, C, K, tuple(dil))
     v = _TILE_ROWS.get(key)
     if v is None:
-        if kind == 3:
+        if kind == "post":
             v = int(lib().ssamd_conv_post_tile_rows())
         else:
             d0, d1, d2 = (int(x) for x in dil)
@@ -2383,8 +2385,28 @@ def conv1d_infer_packed(x, vp, rate, w, b, pad, dil, act=None, resid=None, acc=N
     return (y, y2) if dual_lrelu else y
 
 
+_TALL_MIN_TILES = [512]  # packed per-layer ResBlock: the tall tile only when it still yields >= this many tiles
+
+
+def rb_layer_tile(C: int, K: int, lens, rate: int):
+    """(tall, tile rows) of the per-layer ResBlock kernel for a packed batch: the tall tile (fewer LDS reads per
+    MFMA, ``csrc/k_vocoder.hip`` RBT) when the batch gives it at least ``_TALL_MIN_TILES`` tiles (two per CU),
+    else the 128-row tile (twice the workgroups: batch-1 latency).  Deterministic in (C, K, lengths, rate), so the
+    tile tables and the launch agree."""
+    bt, br = voc_tile_rows(3, C, K), voc_tile_rows(4, C, K)
+    if not br:
+        return True, bt
+    if not bt or not _TALL[0]:
+        return False, br
+    tiles = sum(-(-int(L) * rate // bt) for L in lens)
+    return (True, bt) if tiles >= _TALL_MIN_TILES[0] else (False, br)
+
+
+_TALL = [True]
+
+
 def resblock_layer_packed(x, vp, rate, c1, c2, d, slope, acc=None, out_scale=1.0, post_lrelu=False):
-    """``resblock_layer`` on packed rows x [R*rate, C]."""
+    """``resblock_layer`` on packed rows x [R*rate, C] (tile variant: ``rb_layer_tile``)."""
     _need(x, torch.bfloat16, "resblock.x")
     Rr, C = x.shape
     K = c1.weight.shape[2]
@@ -2392,10 +2414,12 @@ def resblock_layer_packed(x, vp, rate, c1, c2, d, slope, acc=None, out_scale=1.0
     b1 = c1.bias.detach().float().contiguous()
     b2 = c2.bias.detach().float().contiguous()
     out = acc if acc is not None else torch.empty_like(x)
-    tt, n = vp.tiles(rate, voc_tile_rows(0, C, K))
-    rc = lib().ssamd_resblock_layer_pk(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(acc), _ptr(out), _ptr(tt),
-                                       n, C, K, int(d), float(slope), float(out_scale), int(bool(post_lrelu)), _stream())
-    _check(rc, "ssamd_resblock_layer_pk")
+    tall, bm = rb_layer_tile(C, K, vp.lens, rate)
+    tt, n = vp.tiles(rate, bm)
+    rc = lib().ssamd_resblock_layer_pk2(_ptr(x), _ptr(w1), _ptr(b1), _ptr(w2), _ptr(b2), _ptr(acc), _ptr(out),
+                                        _ptr(tt), n, C, K, int(d), float(slope), float(out_scale),
+                                        int(bool(post_lrelu)), int(tall), _stream())
+    _check(rc, "ssamd_resblock_layer_pk2")
     return out
 
 
@@ -2434,7 +2458,7 @@ def conv_post_packed(x, vp, rate, w, b, out, slope=0.01, int16_scale=None):
     Rr, C = x.shape
     wf = w.detach().reshape(-1).float().contiguous()
     bf = None if b is None else b.detach().reshape(-1).float().contiguous()
-    tt, n = vp.tiles(rate, voc_tile_rows(3, C))
+    tt, n = vp.tiles(rate, voc_tile_rows("post", C))
     assert out.shape[0] == vp.B and out.shape[1] >= int(vp.lens.max()) * rate, "conv_post_packed: output shape"
     if int16_scale is None:
         assert out.dtype == torch.float32
