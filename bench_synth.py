@@ -33,6 +33,8 @@ def parse():
     ap.add_argument("--b1-runs", type=int, default=0, dest="synth_b1_runs", help="batch-1 latency runs (0: off)")
     ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
     ap.add_argument("--no-graphs", action="store_false", dest="synth_graphs", help="eager batch-1 synthesis (A/B)")
+    ap.add_argument("--whole-skip", default="",
+                    help="C:K,C:K whole-ResBlock geometries to run on the per-layer kernel instead (A/B)")
     ap.add_argument("--no-rb256", action="store_true",
                     help="C = 256 MRF on the GEMM path instead of the tall per-layer ResBlock kernel (A/B)")
     ap.add_argument("--rb-whole-extra", action="store_true",
@@ -61,6 +63,10 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.lib().ssamd_resblock_set_tall(0)
+    if args.whole_skip:
+        from speakingstyle_amd.models import hifigan as _H
+
+        _H._WHOLE_SKIP.update(tuple(int(v) for v in g.split(":")) for g in args.whole_skip.split(","))
     if args.no_rb256:
         from speakingstyle_amd.models import hifigan as _H
 

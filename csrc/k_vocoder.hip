@@ -452,7 +452,8 @@ static int g_rb_tall = 1;
 SSAMD_API void ssamd_resblock_set_tall(int v) { g_rb_tall = v; }
 template <int C, int K>
 constexpr bool has_tall() {
-  return (C == 128 && (K == 7 || K == 11)) || (C == 64 && K == 11) || (C == 256 && K <= 7);
+  return (C == 128 && (K == 7 || K == 11)) || (C == 64 && (K == 7 || K == 11)) || (C == 32 && K == 11) ||
+         (C == 256 && K <= 7);
 }
 template <int C>
 constexpr bool tall_only() {  // C = 256: the 128-row tile does not fit the LDS -- the tall tile is the only one
@@ -1103,6 +1104,19 @@ __global__ void __launch_bounds__(256) voc_pack_kernel(const TS* __restrict__ sr
 
 
 // ------------------------------------------------------------------------------- packed (length-exact) vocoder
+namespace {
+template <int C, int K>
+int rb_bm_kind(int kind) {  // 3: the tall per-layer tile's BM, 4: the 128-row tile's (0: no such instance)
+  if constexpr (has_tall<C, K>()) {
+    if (kind == 3) return RBT<C, K>::BM;
+  }
+  if constexpr (!tall_only<C>()) {
+    if (kind == 4) return RB<C, K>::BM;
+  }
+  return 0;
+}
+}  // namespace
+
 // Tile height (output rows per tile) of each tiled vocoder kernel, for the host-built packed tile tables:
 // kind 0 = resblock_layer (C, K), 1 = resblock_fused (C, K, dilations), 2 = conv3_sq (C).  0 = no such instance.
 SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2) {
@@ -1119,12 +1133,8 @@ SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2
     if (C == 128) return C3<128>::BM;
     if (C == 64) return C3<64>::BM;
   } else if (kind == 3 || kind == 4) {  // 3: the tall per-layer tile, 4: the 128-row one (0: no such instance)
-#define VT_RB2(CC, KK)                                                                  \
-  if (C == CC && K == KK) {                                                             \
-    if constexpr (has_tall<CC, KK>()) { if (kind == 3) return RBT<CC, KK>::BM; }        \
-    if constexpr (!tall_only<CC>()) { if (kind == 4) return RB<CC, KK>::BM; }           \
-    return 0;                                                                           \
-  }
+#define VT_RB2(CC, KK) \
+  if (C == CC && K == KK) return rb_bm_kind<CC, KK>(kind);
     VT_RB2(32, 3) VT_RB2(32, 7) VT_RB2(32, 11) VT_RB2(64, 3) VT_RB2(64, 7) VT_RB2(64, 11) VT_RB2(128, 3)
     VT_RB2(128, 7) VT_RB2(128, 11) VT_RB2(256, 3) VT_RB2(256, 7)
 #undef VT_RB2

@@ -35,6 +35,8 @@ from .. import ops
 LRELU_SLOPE = 0.1
 # whole-ResBlock kernel for the narrow stages (False: one fused kernel per layer pair; A/B + tests)
 _WHOLE_BLOCK = [True]
+# whole-block geometries routed to the per-layer kernel instead (A/B of halo recompute vs three launches)
+_WHOLE_SKIP = set()
 
 
 class AttrDict(dict):
@@ -207,7 +209,7 @@ class ResBlock1(nn.Module):
         n = len(self.convs1)
         C = x.shape[-1]
         if self.fusable(C, x.shape[0]):
-            if _WHOLE_BLOCK[0] and n == 3 and hip.resblock_fusable(C, k):
+            if _WHOLE_BLOCK[0] and n == 3 and hip.resblock_fusable(C, k) and (C, k) not in _WHOLE_SKIP:
                 return hip.resblock_fused_packed(x, vp, rate, self.convs1, self.convs2, self.dilation, LRELU_SLOPE,
                                                  acc=acc, out_scale=out_scale, post_lrelu=post_lrelu)
             for i, (c1, c2, d) in enumerate(zip(self.convs1, self.convs2, self.dilation)):
@@ -232,7 +234,8 @@ class ResBlock1(nn.Module):
         hip = ops._hip()
         if not self.fusable(C, sum(int(L) for L in lens) * rate):
             return []
-        if _WHOLE_BLOCK[0] and len(self.convs1) == 3 and hip.resblock_fusable(C, self.kernel_size):
+        if (_WHOLE_BLOCK[0] and len(self.convs1) == 3 and hip.resblock_fusable(C, self.kernel_size)
+                and (C, self.kernel_size) not in _WHOLE_SKIP):
             return [(rate, hip.voc_tile_rows(1, C, self.kernel_size, self.dilation))]
         return [(rate, hip.rb_layer_tile(C, self.kernel_size, lens, rate)[1])]
 
