@@ -33,6 +33,8 @@ def parse():
     ap.add_argument("--b1-runs", type=int, default=0, dest="synth_b1_runs", help="batch-1 latency runs (0: off)")
     ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
     ap.add_argument("--no-graphs", action="store_false", dest="synth_graphs", help="eager batch-1 synthesis (A/B)")
+    ap.add_argument("--no-synth-prio", action="store_false", dest="synth_prio",
+                    help="FastSpeech2 on the default-priority stream instead of a high-priority one (A/B)")
     ap.add_argument("--whole-skip", default="",
                     help="C:K,C:K whole-ResBlock geometries to run on the per-layer kernel instead (A/B)")
     ap.add_argument("--no-rb256", action="store_true",

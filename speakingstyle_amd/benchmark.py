@@ -292,6 +292,11 @@ def synth_phase(args, rank, world, device):
     # only, so the GPU is not drained between batches.  Every batch still does its full FS2 + vocoder
     # work; the RTF is wall time over all audio of the timed batches (--synth-serial: one stream, A/B).
     voc_stream = torch.cuda.Stream(device=device) if (cuda and not getattr(args, "synth_serial", False)) else None
+    # FastSpeech2 of batch i+1 on a HIGH-priority stream: its (short, latency-bound) kernels are dispatched as soon
+    # as the vocoder of batch i frees CUs, so the host's length sync -- and with it the next vocoder launch -- is not
+    # queued behind the whole vocoder (its persistent grids hold every CU)
+    fs2_stream = (torch.cuda.Stream(device=device, priority=-1)
+                  if (voc_stream is not None and getattr(args, "synth_prio", True)) else None)
 
     packed = cuda and getattr(args, "packed_fs2", True)
 
@@ -301,6 +306,18 @@ def synth_phase(args, rank, world, device):
         ref_mels, ref_lens, ref_max = b[6], b[7], b[8]
         if packed and model.packed_inference_ok(texts):
             # decoder / PostNet / vocoder on the valid frames only (FastSpeech2.infer_packed -> Generator.infer_packed)
+            if stream is not None and fs2_stream is not None:
+                fs2_stream.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(fs2_stream):
+                    rows, lens_l, _ = model.infer_packed(speakers, texts, src_lens, max_src, ref_mels, ref_lens,
+                                                         ref_max)
+                stream.wait_stream(fs2_stream)
+                rows.record_stream(stream)
+                with torch.cuda.stream(stream):
+                    pcm = voc.infer_packed(rows, lens_l, int16_scale=mx)
+                if host_wav:
+                    pcm = pcm.cpu()
+                return pcm, torch.tensor(lens_l)
             rows, lens_l, _ = model.infer_packed(speakers, texts, src_lens, max_src, ref_mels, ref_lens, ref_max)
             if stream is not None:
                 stream.wait_stream(torch.cuda.current_stream())
