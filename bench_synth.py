@@ -33,6 +33,7 @@ def parse():
     ap.add_argument("--b1-runs", type=int, default=0, dest="synth_b1_runs", help="batch-1 latency runs (0: off)")
     ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
     ap.add_argument("--no-graphs", action="store_false", dest="synth_graphs", help="eager batch-1 synthesis (A/B)")
+    ap.add_argument("--synth-lead", action="store_true", help="host-lead probe of the timed batches (diagnostic)")
     ap.add_argument("--no-synth-prio", action="store_false", dest="synth_prio",
                     help="FastSpeech2 on the default-priority stream instead of a high-priority one (A/B)")
     ap.add_argument("--whole-skip", default="",
@@ -88,6 +89,7 @@ def run(args):
         B.report({
             "b1_ms": None if b1 is None else round(1e3 * b1["median_s"], 3),
             "b1_rtf": None if b1 is None else b1["rtf"], "vocoder": "bucketed" if args.bucketed else "packed",
+            "lead": sy.get("lead"),
             "fs2": "packed" if getattr(args, "packed_fs2", True) else "padded",
             "metric": "synth RTF (FastSpeech2 + style + HiFi-GAN, text ids -> int16 wav)",
             "value": sy["rtf"], "unit": "s wall / s audio", "higher_is_better": False, "n_gpus": world,

@@ -359,11 +359,25 @@ def synth_phase(args, rank, world, device):
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)
+    # host-lead probe (``--synth-lead``): per timed batch, the time the host finished enqueueing it and the time the
+    # GPU finished its vocoder (an event on the vocoder stream), both from t0.  GPU-bound steady state: every batch
+    # completes on the GPU well after the host enqueued it (lead ~ one batch of vocoder work), and the host's own
+    # time per batch (enqueue + the one length sync) is a fraction of the GPU's
+    lead = cuda and voc_stream is not None and getattr(args, "synth_lead", False)
+    if lead:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        evs, hts = [], []
     t0 = time.perf_counter()
     samples = 0
     for i in range(args.synth_steps):
         pcm, mel_len = synth(batches[(args.synth_warmup + i) % len(batches)])
         samples += int(mel_len.sum()) * hop  # valid audio (the D2H of lengths is inside synth())
+        if lead:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(voc_stream)
+            evs.append(e)
+            hts.append(time.perf_counter() - t0)
     _sync(cuda)
     ddp.barrier()
     _sync(cuda)
@@ -372,6 +386,11 @@ def synth_phase(args, rank, world, device):
     info = {"wall": wall, "audio_s": audio_s, "rtf": wall / max(audio_s, 1e-12),
             "frames_per_utt": samples / hop / max(1, args.synth_steps * args.synth_batch),
             "distinct_batches": min(args.synth_steps, len(batches))}
+    if lead:
+        done = [ev0.elapsed_time(e) for e in evs]
+        info["lead"] = {"host_enqueued_ms": [round(1e3 * h, 2) for h in hts], "gpu_done_ms": [round(d, 2) for d in done],
+                        "gpu_minus_host_ms": [round(d - 1e3 * h, 2) for d, h in zip(done, hts)],
+                        "gpu_ms_per_batch": round((done[-1] - done[0]) / max(1, len(done) - 1), 2)}
     del batches
 
     # Batch-1 latency, like-for-like with the reference's only synthesis number (one utterance of 113 mel
