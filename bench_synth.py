@@ -34,8 +34,8 @@ def parse():
     ap.add_argument("--b1-phones", type=int, default=14, dest="synth_b1_phones")
     ap.add_argument("--no-graphs", action="store_false", dest="synth_graphs", help="eager batch-1 synthesis (A/B)")
     ap.add_argument("--synth-lead", action="store_true", help="host-lead probe of the timed batches (diagnostic)")
-    ap.add_argument("--no-synth-prio", action="store_false", dest="synth_prio",
-                    help="FastSpeech2 on the default-priority stream instead of a high-priority one (A/B)")
+    ap.add_argument("--synth-prio", action="store_true",
+                    help="FastSpeech2 on a high-priority stream instead of the default one (A/B)")
     ap.add_argument("--whole-skip", default="",
                     help="C:K,C:K whole-ResBlock geometries to run on the per-layer kernel instead (A/B)")
     ap.add_argument("--no-rb256", action="store_true",

@@ -295,8 +295,9 @@ def synth_phase(args, rank, world, device):
     # FastSpeech2 of batch i+1 on a HIGH-priority stream: its (short, latency-bound) kernels are dispatched as soon
     # as the vocoder of batch i frees CUs, so the host's length sync -- and with it the next vocoder launch -- is not
     # queued behind the whole vocoder (its persistent grids hold every CU)
+    # (measured neutral-to-slightly-worse, profiles/r6_ab_synth.txt: off unless --synth-prio)
     fs2_stream = (torch.cuda.Stream(device=device, priority=-1)
-                  if (voc_stream is not None and getattr(args, "synth_prio", True)) else None)
+                  if (voc_stream is not None and getattr(args, "synth_prio", False)) else None)
 
     packed = cuda and getattr(args, "packed_fs2", True)
 
