@@ -42,6 +42,8 @@ def parse():
                     help="C = 256 MRF on the GEMM path instead of the tall per-layer ResBlock kernel (A/B)")
     ap.add_argument("--rb-whole-extra", action="store_true",
                     help="whole-ResBlock kernels also for C = 64 / K = 11 and C = 128 / K = 7 (A/B)")
+    ap.add_argument("--rb-half", action="store_true",
+                    help="per-layer ResBlock kernel on the half tall block (4 waves, two blocks per CU) (A/B)")
     ap.add_argument("--rb-regular", action="store_true",
                     help="per-layer ResBlock kernel on the 128-row tile instead of the tall 64x64-per-wave tile (A/B)")
     ap.add_argument("--bucketed", action="store_true",
@@ -62,6 +64,10 @@ def run(args):
     dev = torch.device("cuda", local_rank) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(dev)
+    if args.rb_half and cuda:
+        from speakingstyle_amd.ops import hip
+
+        hip.lib().ssamd_resblock_set_tall(2)
     if args.rb_regular and cuda:
         from speakingstyle_amd.ops import hip
 

@@ -36,12 +36,14 @@ constexpr int MAXD = 5;
 // per MFMA and the weight slices are staged once per 256 (C = 128) / 512 (C = 64) rows instead of per 128 / 64.  The
 // x tile, the t1 tile and the fp32 output tile share one LDS region (each is dead before the next is written:
 // extra barriers after each conv), the weight ring sits behind the x tile.
-template <int C_, int K_, int RPW_ = 2, bool BIG_ = false>
+// NW_ (> 0): waves per block of a tall tile -- 4 gives the "half" tall block (the same 64 x 64 wave tile on half the
+// rows and LDS), two of which share a CU so one block's staging / epilogue phases run under the other's MFMAs
+template <int C_, int K_, int RPW_ = 2, bool BIG_ = false, int NW_ = 0>
 struct RB {
   static constexpr int C = C_;
   static constexpr int K = K_;
   static constexpr bool BIG = BIG_;
-  static constexpr int NW = BIG ? 8 : (C >= 128 ? 8 : 4);  // waves per block
+  static constexpr int NW = NW_ > 0 ? NW_ : (BIG ? 8 : (C >= 128 ? 8 : 4));  // waves per block
   static constexpr int NT = 64 * NW;
   // column groups: 64 columns per wave in the tall tile (C = 256: 4 x 2 waves), else 2 groups from C = 128 up
   static constexpr int WC = BIG ? (C >= 64 ? C / 64 : 1) : (C >= 128 ? 2 : 1);
@@ -83,6 +85,8 @@ struct RB {
 };
 template <int C, int K>
 using RBT = RB<C, K, 4, true>;  // the tall tile
+template <int C, int K>
+using RBH = RB<C, K, 4, true, 4>;  // the half tall block (two per CU)
 
 __device__ __forceinline__ float lrelu(float v, float s) { return v >= 0.f ? v : v * s; }
 
@@ -459,6 +463,10 @@ template <int C>
 constexpr bool tall_only() {  // C = 256: the 128-row tile does not fit the LDS -- the tall tile is the only one
   return C == 256;
 }
+template <int C, int K>
+constexpr bool has_half() {
+  return has_tall<C, K>() && C <= 128;
+}
 
 template <class R>
 int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
@@ -496,6 +504,10 @@ int launch_rb_any(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16
   if constexpr (tall_only<C>()) {
     return launch_rb<RBT<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
   } else {
+    if constexpr (has_half<C, K>()) {
+      if (g_rb_tall == 2)
+        return launch_rb<RBH<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
+    }
     if constexpr (has_tall<C, K>()) {
       if (g_rb_tall)
         return launch_rb<RBT<C, K>>(x, w1, b1, w2, b2, acc_in, out, B, T, d, slope, out_scale, post_lrelu, s, tt, ntt);
@@ -509,6 +521,9 @@ int rb_bm() {
   if constexpr (tall_only<C>()) {
     return RBT<C, K>::BM;
   } else {
+    if constexpr (has_half<C, K>()) {
+      if (g_rb_tall == 2) return RBH<C, K>::BM;
+    }
     if constexpr (has_tall<C, K>()) {
       if (g_rb_tall) return RBT<C, K>::BM;
     }
@@ -1107,6 +1122,9 @@ __global__ void __launch_bounds__(256) voc_pack_kernel(const TS* __restrict__ sr
 namespace {
 template <int C, int K>
 int rb_bm_kind(int kind) {  // 3: the tall per-layer tile's BM, 4: the 128-row tile's (0: no such instance)
+  if constexpr (has_half<C, K>()) {
+    if (kind == 3 && g_rb_tall == 2) return RBH<C, K>::BM;
+  }
   if constexpr (has_tall<C, K>()) {
     if (kind == 3) return RBT<C, K>::BM;
   }
@@ -1192,6 +1210,11 @@ SSAMD_API int ssamd_resblock_layer_pk2(const bf16_t* x, const bf16_t* w1, const 
   const int4* t4 = reinterpret_cast<const int4*>(tt);
 #define RBK2_CASE(CC, KK)                                                                                          \
   if (C == CC && K == KK) {                                                                                        \
+    if constexpr (has_half<CC, KK>()) {                                                                            \
+      if (tall && g_rb_tall == 2)                                                                                  \
+        return launch_rb<RBH<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, \
+                                      ntt);                                                                        \
+    }                                                                                                              \
     if constexpr (has_tall<CC, KK>()) {                                                                            \
       if (tall)                                                                                                    \
         return launch_rb<RBT<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, \

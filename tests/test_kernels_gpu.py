@@ -1215,7 +1215,7 @@ def test_resblock_layer_fused(C, K, d, T):
         assert _rel(out, expect) < 1e-2
 
 
-@pytest.mark.parametrize("tall", [1, 0])
+@pytest.mark.parametrize("tall", [1, 0, 2])
 @pytest.mark.parametrize("C,K,d,B,T", [(128, 11, 5, 6, 11000), (128, 7, 3, 5, 13000), (64, 11, 3, 8, 20000)])
 def test_resblock_layer_persistent_many_tiles(C, K, d, B, T, tall):
     """The per-layer kernel loops over tiles when they outnumber the resident blocks (256 here: one 136-150 KiB
