@@ -40,6 +40,9 @@ def parse():
                     help="C:K,C:K whole-ResBlock geometries to run on the per-layer kernel instead (A/B)")
     ap.add_argument("--no-rb256", action="store_true",
                     help="C = 256 MRF on the GEMM path instead of the tall per-layer ResBlock kernel (A/B)")
+    ap.add_argument("--rb256-min-rows", type=int, default=None,
+                    help="row count from which the C = 256 MRF uses the tall per-layer kernel (A/B; default 65536)")
+    ap.add_argument("--splitk", type=int, default=None, help="GEMM split-K: -1 auto, 0 off, S forced (A/B)")
     ap.add_argument("--rb-whole-extra", action="store_true",
                     help="whole-ResBlock kernels also for C = 64 / K = 11 and C = 128 / K = 7 (A/B)")
     ap.add_argument("--rb-half", action="store_true",
@@ -80,6 +83,14 @@ def run(args):
         from speakingstyle_amd.models import hifigan as _H
 
         _H._RB256[0] = False
+    if args.rb256_min_rows is not None:
+        from speakingstyle_amd.models import hifigan as _H
+
+        _H._RB256_MIN_ROWS[0] = args.rb256_min_rows
+    if args.splitk is not None and cuda:
+        from speakingstyle_amd.ops import hip
+
+        hip.lib().ssamd_gemm_set_splitk(args.splitk)
     if args.rb_whole_extra and cuda:
         from speakingstyle_amd.ops import hip
 

@@ -2320,14 +2320,17 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
 }
 
 // Split-K finish: out[m][n] = epilogue( sum_s P[s][m][n] ) in a fixed slice order, with the
-// epi_store4 semantics (bias, activation, ReLU-aux mask, residual, row validity).  8 columns per
-// thread (two float4 per slice).
+// epi_store4 semantics (bias, activation, ReLU-aux mask, residual, row validity) and, for bf16 output, the
+// big64 EpiX tail (accumulate, scale, leaky-ReLU copy y2, post activation).  8 columns per thread (two
+// float4 per slice).
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ P, int S, long M, int N,
                                                             const float* __restrict__ bias,
                                                             const bf16_t* __restrict__ aux,
                                                             const bf16_t* __restrict__ resid,
                                                             const int64_t* __restrict__ lens, int L, int act,
-                                                            int out_f32, void* __restrict__ Y) {
+                                                            int out_f32, void* Y,
+                                                            const bf16_t* xacc, bf16_t* y2,
+                                                            float scale, int post_act) {
   const int n8 = N >> 3;
   const long e = blockIdx.x * 256L + threadIdx.x;
   if (e >= M * n8) return;
@@ -2357,9 +2360,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] += bf2f((bf16_t)x[q]);
   }
+  bool valid = true;
   if (lens) {
     const long b = m / L;
-    if (m - b * L >= lens[b]) {
+    valid = m - b * L < lens[b];
+    if (!valid) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = 0.f;
     }
@@ -2369,6 +2374,23 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
     o[0] = make_float4(v[0], v[1], v[2], v[3]);
     o[1] = make_float4(v[4], v[5], v[6], v[7]);
   } else {
+    if (xacc) {
+      const short8 x = *reinterpret_cast<const short8*>(xacc + off);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += bf2f((bf16_t)x[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = valid ? v[q] * scale : 0.f;
+    if (y2) {
+      short8 o2;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o2[q] = (short)f2bf(v[q] > 0.f ? v[q] : 0.1f * v[q]);
+      *reinterpret_cast<short8*>(y2 + off) = o2;
+    }
+    if (post_act == ACT_LRELU) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : 0.1f * v[q];
+    }
     short8 o;
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = (short)f2bf(v[q]);
@@ -2617,7 +2639,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   {
     const int tiles = ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG);
     const int nk64 = (g.K + 63) / 64;
-    const bool plain = !(ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f || ex.mask_out || ex.mask_in || bnh);
+    // the reduce applies EpiX's accumulate / scale / y2 / post activation (bf16 output, as the big64 epilogue)
+    const bool xon = ex.acc || ex.y2 || ex.post_act || ex.scale != 1.f;
+    const bool plain = !(ex.mask_out || ex.mask_in || bnh) && (!xon || (!out_f32 && (ex.post_act == 0 ||
+                                                                                     ex.post_act == ACT_LRELU)));
     int S = 0;
     if (g_splitk > 0) S = g_splitk;
     else if (g_splitk < 0 && g_gemm_variant < 0 && tiles <= 128 && nk64 >= 16)
@@ -2648,7 +2673,7 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       const long nthr = (long)g.M * (N / 8);
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(nthr, 256)), dim3(256), 0, s,
                          reinterpret_cast<const float*>(ws), S, (long)g.M, N, bias, aux, resid, lens, g.L,
-                         act, out_f32, Y);
+                         act, out_f32, Y, ex.acc, ex.y2, ex.scale, ex.post_act);
       return (int)hipGetLastError();
     }
   }

@@ -281,33 +281,49 @@ __global__ void __launch_bounds__(gru_threads(GH)) gru_bwd_kernel(const float* _
 // tanh(token bank)); o [B, NH*D] = softmax(q_h K_h^T * scale) V_h, w [B, NH, N] = the weights.
 constexpr int NTOK_MAX = 32;
 
+// one wave per (utterance, head): the head's N key / value rows are loaded up front (independent loads in
+// flight together; a batch-1 synthesis is a chain of latency-bound launches), then N wave reductions
 __global__ void __launch_bounds__(64) token_attn_fwd_kernel(const float* __restrict__ q, const float* __restrict__ K,
                                                             const float* __restrict__ V, int NH, int N, int D,
                                                             float scale, float* __restrict__ o,
                                                             float* __restrict__ wout) {
-  const int b = blockIdx.x, l = threadIdx.x;
-  for (int hh = 0; hh < NH; ++hh) {
-    const float qv = l < D ? q[((long)b * NH + hh) * D + l] : 0.f;
-    float s[NTOK_MAX];
-    float mx = -INFINITY;
-    for (int n = 0; n < N; ++n) {
-      s[n] = wave_sum(l < D ? qv * K[((long)hh * N + n) * D + l] : 0.f) * scale;
+  const int b = blockIdx.x, hh = blockIdx.y, l = threadIdx.x;
+  const bool on = l < D;
+  const float qv = on ? q[((long)b * NH + hh) * D + l] : 0.f;
+  float kv[NTOK_MAX], vv[NTOK_MAX], s[NTOK_MAX];
+#pragma unroll
+  for (int n = 0; n < NTOK_MAX; ++n) {
+    const bool ok = on && n < N;
+    kv[n] = ok ? K[((long)hh * N + n) * D + l] : 0.f;
+    vv[n] = ok ? V[((long)hh * N + n) * D + l] : 0.f;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int n = 0; n < NTOK_MAX; ++n) {
+    if (n < N) {
+      s[n] = wave_sum(qv * kv[n]) * scale;
       mx = fmaxf(mx, s[n]);
     }
-    float den = 0.f;
-    for (int n = 0; n < N; ++n) {
+  }
+  float den = 0.f;
+#pragma unroll
+  for (int n = 0; n < NTOK_MAX; ++n) {
+    if (n < N) {
       s[n] = __expf(s[n] - mx);
       den += s[n];
     }
-    const float inv = 1.f / den;
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n) {
+  }
+  const float inv = 1.f / den;
+  float acc = 0.f;
+#pragma unroll
+  for (int n = 0; n < NTOK_MAX; ++n) {
+    if (n < N) {
       const float wn = s[n] * inv;
-      if (l < D) acc += wn * V[((long)hh * N + n) * D + l];
+      acc += wn * vv[n];
       if (l == n) wout[((long)b * NH + hh) * N + n] = wn;
     }
-    if (l < D) o[((long)b * NH + hh) * D + l] = acc;
   }
+  if (on) o[((long)b * NH + hh) * D + l] = acc;
 }
 
 // dq [B, NH*D]; part [B, 2, NH, N, D] = per-utterance (dK, dV) contributions.  dwts (optional):
@@ -469,7 +485,7 @@ SSAMD_API int ssamd_token_attn_fwd(const float* q, const float* K, const float* 
                                    float scale, float* o, float* w, hipStream_t s) {
   if (N > NTOK_MAX || D > 64) return -2;
   if (B == 0) return 0;
-  hipLaunchKernelGGL(token_attn_fwd_kernel, dim3(B), dim3(64), 0, s, q, K, V, NH, N, D, scale, o, w);
+  hipLaunchKernelGGL(token_attn_fwd_kernel, dim3(B, NH), dim3(64), 0, s, q, K, V, NH, N, D, scale, o, w);
   return (int)hipGetLastError();
 }
 

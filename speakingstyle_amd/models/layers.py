@@ -169,13 +169,40 @@ class PostNet(nn.Module):
     def forward_packed(self, x, pack):
         """Inference on packed rows [1, R, C] (``ops/packing.py``): eval-mode BatchNorm is a per-channel affine of
         the running statistics (row-independent) and every conv zero-pads at its own sequence's ends -- each
-        utterance's PostNet output exactly as when it is synthesized alone."""
+        utterance's PostNet output exactly as when it is synthesized alone.
+
+        The affine is folded into the conv it follows (``folded``): 5 GEMM launches (tanh in the epilogue, the
+        last one writing fp32) instead of 5 GEMMs + 5 BatchNorm finalize / apply pairs -- the batch-1 serving
+        path is launch-bound."""
         assert not self.training, "PostNet.forward_packed: inference only (training BatchNorm needs the padded rows)"
-        last = len(self.convolutions) - 1
-        c0 = self.convolutions[0][0]
-        h = ops.conv1d(x, c0.conv.weight, c0.conv.bias, c0.pad, c0.dil, pack=pack)
-        for i in range(last):
-            bn, nxt = self.convolutions[i][1], self.convolutions[i + 1][0]
-            h = ops.conv1d(ops.bn_act(h, bn, False, True, 0.0), nxt.conv.weight, nxt.conv.bias, nxt.pad, nxt.dil,
-                           pack=pack)
-        return ops.bn_act(h, self.convolutions[last][1], False, act_tanh=False, p=0.0, out_f32=True)
+        layers = self.folded()
+        h = x
+        for i, (w, b) in enumerate(layers):
+            c = self.convolutions[i][0]
+            last = i == len(layers) - 1
+            h = ops.conv1d(h, w, b, c.pad, c.dil, act=None if last else "tanh", pack=pack, out_f32=last)
+        return h
+
+    def folded(self):
+        """Per layer (W * s, b * s + t) with s = gamma / sqrt(running_var + eps), t = beta - running_mean * s:
+        conv followed by eval BatchNorm as one conv.  Cached per parameter / buffer version (not registered,
+        so never in the state dict)."""
+        ts = []
+        for conv, bn in self.convolutions:
+            ts += [conv.conv.weight, conv.conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+        key = tuple((t.data_ptr(), t._version) for t in ts if t is not None)
+        hit = self.__dict__.get("_fold")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        out = []
+        with torch.no_grad():
+            for conv, bn in self.convolutions:
+                w = conv.conv.weight.detach().float()
+                s = bn.weight.detach().float() * torch.rsqrt(bn.running_var.float() + bn.eps)
+                t = bn.bias.detach().float() - bn.running_mean.float() * s
+                b = conv.conv.bias.detach().float() if conv.conv.bias is not None else torch.zeros_like(s)
+                wf = nn.Parameter((w * s.view(-1, *([1] * (w.dim() - 1)))).to(conv.conv.weight.dtype),
+                                  requires_grad=False)
+                out.append((wf, (b * s + t).contiguous()))
+        self.__dict__["_fold"] = (key, out)
+        return out

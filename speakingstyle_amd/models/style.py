@@ -148,17 +148,44 @@ class GlobalStyleTokens(nn.Module):
         x = mel.unsqueeze(-1)
         if not ops.use_hip(x):
             x = x.float()
-        for conv, bn in zip(self.convs, self.bns):
-            y = ops.conv2d_s2(x, conv.weight, conv.bias)
-            B, Ho, Wo, C = y.shape
-            x = ops.bn_act(y.reshape(B, Ho * Wo, C), bn, self.training, "relu", 0.0).view(B, Ho, Wo, C)
-        # each stride-2 conv maps a length l to (l - 1) // 2 + 1 = ceil(l / 2), so n of them give ceil(l / 2^n):
-        # one expression instead of three tiny device ops per layer
+        if not self.training and not torch.is_grad_enabled():
+            # eval BatchNorm is a per-channel affine: folded into the conv, ReLU in its GEMM epilogue
+            for prep in self.folded_convs():
+                x = ops.conv2d_s2_infer(x, prep, "relu")
+        else:
+            for conv, bn in zip(self.convs, self.bns):
+                y = ops.conv2d_s2(x, conv.weight, conv.bias)
+                B, Ho, Wo, C = y.shape
+                x = ops.bn_act(y.reshape(B, Ho * Wo, C), bn, self.training, "relu", 0.0).view(B, Ho, Wo, C)
+        # each stride-2 conv maps a length l to (l - 1) // 2 + 1 = ceil(l / 2), so n of them give ceil(l / 2^n) and
+        # the last valid GRU step is ceil(l / 2^n) - 1 = (l - 1) >> n (-1 -> 0 for an empty mel): three tiny device
+        # ops instead of three per layer
         n = len(self.convs)
-        lens = (mel_lens + ((1 << n) - 1)) >> n
         B, T, Fq, C = x.shape
         x = x.permute(0, 1, 3, 2).reshape(B, T, C * Fq)
-        return ops.gru_last(x, self.gru, lens.clamp(min=1, max=T) - 1)
+        return ops.gru_last(x, self.gru, ((mel_lens - 1) >> n).clamp(0, T - 1))
+
+    def folded_convs(self):
+        """Per layer the ``ops.conv2d_s2_prepare`` operand of (W * s, b * s + t), s = gamma / sqrt(running_var +
+        eps), t = beta - running_mean * s: Conv2d + eval BatchNorm2d as one conv.  Cached per parameter / buffer
+        version (not registered: never in the state dict); on the GPU the weight images are built here once
+        instead of per call (batch-1 serving is launch-bound)."""
+        ts = []
+        for conv, bn in zip(self.convs, self.bns):
+            ts += [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+        key = tuple((t.data_ptr(), t._version, t.device) for t in ts if t is not None)
+        hit = self.__dict__.get("_fold")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        out = []
+        with torch.no_grad():
+            for conv, bn in zip(self.convs, self.bns):
+                s = bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)
+                t = bn.bias.float() - bn.running_mean.float() * s
+                b = conv.bias.float() if conv.bias is not None else torch.zeros_like(s)
+                out.append(ops.conv2d_s2_prepare(conv.weight.float() * s.view(-1, 1, 1, 1), b * s + t))
+        self.__dict__["_fold"] = (key, out)
+        return out
 
     def token_bank(self):
         """Keys / values of the style-token bank, [heads, n_tok, token_size/heads] each."""

@@ -95,13 +95,16 @@ class IdCache:
         self._d[id(t)] = (weakref.ref(t), v)
 
 
-def conv1d(x, w, b=None, pad=0, dil=1, act=None, pack: Optional[PackInfo] = None):
-    """``pack``: x is packed ``[1, R, C]``; the conv zero-pads at every sequence end."""
+def conv1d(x, w, b=None, pad=0, dil=1, act=None, pack: Optional[PackInfo] = None, out_f32: bool = False):
+    """``pack``: x is packed ``[1, R, C]``; the conv zero-pads at every sequence end.  ``out_f32``: fp32 output
+    (the GPU GEMM writes its fp32 accumulators)."""
     if use_hip(x):
-        return _hip().conv1d(x, w, b, pad, dil, act, pack=pack)
+        return _hip().conv1d(x, w, b, pad, dil, act, out_f32=out_f32, pack=pack)
     if pack is not None:
-        return pack_rows(ref.conv1d(unpack_rows(x, pack), w, b, pad, dil, act), pack)
-    return ref.conv1d(x, w, b, pad, dil, act)
+        y = pack_rows(ref.conv1d(unpack_rows(x, pack), w, b, pad, dil, act), pack)
+    else:
+        y = ref.conv1d(x, w, b, pad, dil, act)
+    return y.float() if out_f32 else y
 
 
 def conv_relu_layernorm(x, w, b, pad, dil, ln_w, ln_b, **kw):
@@ -298,6 +301,26 @@ def conv2d_s2(x, w, b=None):
         return _hip().conv2d_s2(x, w, b)
     y = F.conv2d(x.permute(0, 3, 1, 2), w.to(x.dtype), None if b is None else b.to(x.dtype), stride=2, padding=1)
     return y.permute(0, 2, 3, 1)
+
+
+def conv2d_s2_prepare(w, b):
+    """Inference operand of ``conv2d_s2_infer`` for weight w [Cout, Cin, 3, 3] / bias b (fp32): on the GPU the
+    bf16 im2col-order image, built once by the caller's cache instead of per call."""
+    b = b.detach().float().contiguous()
+    if use_hip(w):
+        return ("img", _hip().conv2d_s2_image(w), b)
+    return ("ref", w.detach(), b)
+
+
+def conv2d_s2_infer(x, prep, act=None):
+    """Forward-only Conv2d(3x3, s2, p1) (+ activation) with an operand from ``conv2d_s2_prepare``."""
+    kind, w, b = prep
+    if kind == "img" and use_hip(x):
+        return _hip().conv2d_s2_infer(x, w, b, act)
+    if kind == "img":
+        raise ValueError("conv2d_s2_infer: GPU weight image with a host input")
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.to(x.dtype), b.to(x.dtype), stride=2, padding=1).permute(0, 2, 3, 1)
+    return ref._act(y, act)
 
 
 def gru_last(x, gru, last):

@@ -852,7 +852,7 @@ class _FFNFn(torch.autograd.Function):
     data-gradient epilogue of the second conv (aux = h), so no extra pass."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, rinfo, mailbox):
+    def forward(ctx, x, w1, b1, w2, b2, rinfo, mailbox, need_mask=True):
         B, L, C = x.shape
         ctx.mailbox = mailbox
         k1, k2 = w1.shape[2], w2.shape[2]
@@ -863,8 +863,9 @@ class _FFNFn(torch.autograd.Function):
         r2 = rinfo if k2 > 1 else None
         ctx.cu = (cu if k1 > 1 else None, cu if k2 > 1 else None)
         mask = None
-        if H >= 256 and H % 8 == 0 and has("ssamd_conv_gemm_mask"):
-            # ReLU bitmask of h for the second conv's data gradient (M x H/8 bytes instead of h itself)
+        if H >= 256 and H % 8 == 0 and need_mask and has("ssamd_conv_gemm_mask"):
+            # ReLU bitmask of h for the second conv's data gradient (M x H/8 bytes instead of h itself); not
+            # in inference, where the plain epilogue keeps the split-K path open for tile-poor row counts
             mask = torch.empty(B * L, H // 8, device=x.device, dtype=torch.uint8)
             h = conv_gemm_mask_raw(xc, weight_fwd(w1), b1.detach().float(), B, L, C, k1, (k1 - 1) // 2, H, 1,
                                    rinfo=r1, mask_out=mask)
@@ -916,13 +917,14 @@ class _FFNFn(torch.autograd.Function):
                            resid=_resid_for(ctx.mailbox, xc))
         if not first:
             dw1, db1 = _wgrad1()
-        return dx, dw1, db1, dw2, db2, None, None
+        return dx, dw1, db1, dw2, db2, None, None, None
 
 
 def ffn(x, w1, b1, w2, b2, pack=None, mailbox=None):
     if pack is not None:
         assert x.shape[0] == 1 and x.shape[1] == pack.R, "packed FFN expects [1, R, C]"
-    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu), mailbox)
+    grad = torch.is_grad_enabled() and any(t.requires_grad for t in (x, w1, b1, w2, b2))
+    return _FFNFn.apply(x, w1, b1, w2, b2, None if pack is None else (pack.rinfo, pack.cu), mailbox, grad)
 
 
 # ------------------------------------------------------------------------ add + LayerNorm
@@ -2008,6 +2010,23 @@ class _Conv2dS2Fn(torch.autograd.Function):
 def conv2d_s2(x, w, b=None):
     """NHWC [B, H, W, Cin] -> [B, ceil(H/2), ceil(W/2), Cout] bf16 (Conv2d 3x3, stride 2, pad 1)."""
     return _Conv2dS2Fn.apply(x, w, b)
+
+
+def conv2d_s2_image(w):
+    """Inference operand of ``conv2d_s2_infer``: the bf16 [Cout, Kp] im2col-order weight image."""
+    return _conv2d_wimg(w, (9 * w.shape[1] + 7) // 8 * 8)
+
+
+def conv2d_s2_infer(x, wimg, bias, act=None):
+    """Forward-only conv2d_s2 on a prebuilt weight image (``conv2d_s2_image``) with the GEMM epilogue's
+    activation: im2col + one GEMM, nothing rebuilt per call."""
+    B, H, W, C = x.shape
+    Cout, Kp = wimg.shape
+    assert Kp == (9 * C + 7) // 8 * 8, "conv2d_s2_infer: weight image / input channel mismatch"
+    Ho, Wo = _s2(H), _s2(W)
+    col = im2col_s2(x.to(torch.bfloat16).contiguous(), Kp)
+    y = conv_gemm_raw(col, wimg, bias, 1, B * Ho * Wo, Kp, 1, 1, 0, Cout, _ACT[act])
+    return y.view(B, Ho, Wo, Cout)
 
 
 class _GRUFn(torch.autograd.Function):

@@ -1,0 +1,30 @@
+"""Eval-mode BatchNorm folded into the preceding conv for inference (GST reference encoder): the folded
+no-grad path equals the conv + BatchNorm + ReLU path on the CPU reference ops."""
+import torch
+
+
+def test_gst_folded_eval_matches_unfolded():
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.models.style import GlobalStyleTokens
+
+    pp, mc, _ = load_named("BC2013_GST")
+    torch.manual_seed(1)
+    m = GlobalStyleTokens(pp, mc)
+    for bn in m.bns:
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.data.uniform_(0.5, 1.5)
+    m.eval()
+    mel = torch.randn(2, 64, 80)
+    lens = torch.tensor([64, 37])
+    ref = m.reference_embedding(mel, lens)  # grad enabled: conv + BatchNorm path
+    with torch.no_grad():
+        got = m.reference_embedding(mel, lens)  # folded path
+        assert "_fold" in m.__dict__ and m.__dict__["_fold"][1][0][0] == "ref"
+        m.bns[1].running_var.mul_(1.5)  # in place: refolded
+        got2 = m.reference_embedding(mel, lens)
+    torch.testing.assert_close(got, ref.detach(), rtol=1e-4, atol=1e-5)
+    with torch.enable_grad():
+        ref2 = m.reference_embedding(mel, lens)
+    torch.testing.assert_close(got2, ref2.detach(), rtol=1e-4, atol=1e-5)
+    assert not any("_fold" in k for k in m.state_dict())

@@ -159,6 +159,31 @@ def test_gst_module_matches_cpu(filters):
     assert not bad, (bad, errs)
 
 
+def test_gst_eval_folded_matches_cpu():
+    """Inference (eval, no grad): the conv + BatchNorm2d stack runs folded (``folded_convs``: ReLU in the GEMM
+    epilogue, cached weight images) -- against the fp32 CPU module in eval, with non-trivial running stats."""
+    from speakingstyle_amd.config import load_named
+    from speakingstyle_amd.models.style import GlobalStyleTokens
+
+    pp, mc, _ = load_named("BC2013_GST")
+    torch.manual_seed(5)
+    cpu = GlobalStyleTokens(pp, mc)
+    for bn in cpu.bns:
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 2.0)
+    cpu.eval()
+    gpu = copy.deepcopy(cpu).to(DEV)
+    mel = torch.randn(3, 150, 80).to(torch.bfloat16)
+    lens = torch.tensor([150, 97, 41])
+    with torch.no_grad():
+        g_c, b_c = cpu(mel.float(), lens)
+        g_g, b_g = gpu(mel.to(DEV), lens.to(DEV))
+        assert "_fold" in gpu.__dict__ and gpu.__dict__["_fold"][1][0][0] == "img"
+        g_g2, _ = gpu(mel.to(DEV), lens.to(DEV))  # cached fold: same result
+    assert _rel(g_g, g_c) < 3e-2 and _rel(b_g, b_c) < 3e-2
+    assert torch.equal(g_g, g_g2)
+
+
 def test_style_tuner_gpu():
     """Style-token bank tuning on the GPU path (HIP encoder + token-attention backward)."""
     import numpy as np

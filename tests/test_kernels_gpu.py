@@ -1643,6 +1643,44 @@ def test_splitk_gemm_vs_reference(act, use_bias, use_res, packed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dual,post,inplace", [(False, None, True), (True, "lrelu", True), (False, "lrelu", False)])
+def test_splitk_gemm_epix_vs_reference(dual, post, inplace):
+    """Split-K with the inference EpiX tail in the reduce (accumulate in place, scale, leaky-ReLU copy, post
+    activation): a tile-poor vocoder conv (904 rows, C = 256, k = 11) vs fp32 torch, forced S = 3 and the auto
+    choice, and bitwise-equal slices order across two runs."""
+    torch.manual_seed(36)
+    L, C, ks, dil = 904, 256, 11, 3
+    pad = dil * (ks - 1) // 2
+    x = torch.randn(1, L, C, device=DEV).to(torch.bfloat16)
+    w = torch.randn(C, C, ks, device=DEV) / (ks * C) ** 0.5
+    b = torch.randn(C, device=DEV) * 0.1
+    a0 = torch.randn(1, L, C, device=DEV).to(torch.bfloat16)
+    wq = w.to(torch.bfloat16).float()
+    v = F.conv1d(x.float().transpose(1, 2), wq, b, padding=pad, dilation=dil).transpose(1, 2)
+    v = (v + a0.float()) * 0.5
+    y2_ref = F.leaky_relu(v, 0.1)
+    y_ref = F.leaky_relu(v, 0.1) if post else v
+    for S in (3, -1, 3):
+        hip.lib().ssamd_gemm_set_splitk(S)
+        try:
+            acc = a0.clone()
+            out = hip.conv1d_infer(x, w, b, pad, dil, acc=acc if inplace else a0.clone(), scale=0.5, post_act=post,
+                                   dual_lrelu=dual)
+        finally:
+            hip.lib().ssamd_gemm_set_splitk(-1)
+        y, y2 = out if dual else (out, None)
+        assert _rel(y, y_ref) < 1e-2, S
+        if dual:
+            assert _rel(y2, y2_ref) < 1e-2, S
+        if inplace:
+            assert y.data_ptr() == acc.data_ptr()
+        if S == 3:
+            if "first" in locals():
+                assert torch.equal(y, first)
+            first = y.clone()
+
+
+@pytest.mark.gpu
 def test_fused_adam_images_match_two_kernel_path():
     """clip+Adam that rewrites the bf16 images in the same launch (ssamd_clip_adam_img): parameters
     and Adam moments bitwise equal to adam_kernel, every cached image equal to a fresh cast of its

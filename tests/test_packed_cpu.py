@@ -96,3 +96,33 @@ def test_positional_rows_cast_cache_and_idcache():
     t1, t2 = torch.zeros(3), torch.zeros(3)
     cache.put(t1, "one")
     assert cache.get(t1) == "one" and cache.get(t2) is None
+
+
+def test_postnet_folded_batchnorm_packed_matches_eval():
+    """PostNet.forward_packed folds eval BatchNorm into the convs: same output as the eval forward on the padded
+    batch (valid frames), and the fold follows in-place updates of the running statistics."""
+    from speakingstyle_amd.models.layers import PostNet
+    from speakingstyle_amd.ops.packing import PackInfo, pack, unpack
+
+    torch.manual_seed(0)
+    pn = PostNet(n_mel_channels=16, emb=32, k=5, n=5)
+    for _, bn in pn.convolutions:
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.data.uniform_(0.5, 1.5)
+        bn.bias.data.uniform_(-0.2, 0.2)
+    pn.eval()
+    lens = torch.tensor([9, 4, 13])
+    L = 13
+    x = torch.randn(3, L, 16)
+    mask = torch.arange(L)[None] < lens[:, None]
+    pk = PackInfo.build(lens, L, int(lens.sum()))
+    for _ in range(2):
+        with torch.no_grad():
+            ref = torch.stack([pn(x[b:b + 1, : int(lens[b])]).squeeze(0).new_zeros(L, 16).index_copy(
+                0, torch.arange(int(lens[b])), pn(x[b:b + 1, : int(lens[b])]).squeeze(0)) for b in range(3)])
+            got = unpack(pn.forward_packed(pack(x, pk), pk), pk)
+        assert got.dtype == torch.float32
+        torch.testing.assert_close(got[mask], ref[mask], rtol=1e-5, atol=1e-5)
+        pn.convolutions[2][1].running_mean.add_(0.3)  # in place: the cached fold must be rebuilt
+    assert "_fold" not in pn.state_dict()

@@ -30,3 +30,12 @@ for s in big[-2:]:
         c[k] += 1
     for k, v in t.most_common(25):
         print(f"  {v:8.1f} us  n={c[k]:3d}  {k}")
+if len(sys.argv) > 2 and sys.argv[2] == "--seq":  # ordered kernel sequence of the last run (fusion census)
+    s = big[-1]
+    t0 = int(s[0]["Start_Timestamp"])
+    prev = t0
+    for r in s:
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:80]
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        print(f"{(st - t0) / 1e3:9.1f} {(en - st) / 1e3:7.1f} gap {(st - prev) / 1e3:6.1f}  {k}")
+        prev = en
