@@ -2524,6 +2524,7 @@ static int g_gemm_ngrp = 1;  // 256x256 tile order: N-tile groups (tile_of); exp
 SSAMD_API void ssamd_gemm_set_ngrp(int v) { g_gemm_ngrp = v; }
 SSAMD_API void ssamd_wgrad_set_prio(int v) { g_wgrad_prio = v; }
 static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 split-K + reduce)
+static int g_splitk_tiny = 3;    // min k-steps per slice for <= 8 tiles (0: the general rule only)
 static int g_num_cus_gemm = 256;
 // Split-K fp32 partials: one workspace per (device, stream).  A process-global buffer would hand a
 // foreign-device pointer to a second GPU and let GEMMs on two streams race on the same partials.
@@ -2568,6 +2569,7 @@ static void* splitk_workspace(hipStream_t s, size_t need) {
   return e->p;
 }
 SSAMD_API void ssamd_gemm_set_splitk(int v) { g_splitk = v; }
+SSAMD_API void ssamd_gemm_set_splitk_tiny(int v) { g_splitk_tiny = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
 SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
@@ -2649,6 +2651,12 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       // as many slices as keep the split grid within ONE wave of blocks (a second partial wave
       // costs more than it saves: M = 10800 / 43 tiles: S = 4 81 us, S = 6 111 us, unsplit 149 us)
       S = min(min(8, g_num_cus_gemm / tiles), nk64 / 6);
+    // a handful of tiles at <= 1024 rows (batch-1 inference: one utterance's phonemes / frames / first vocoder
+    // stages) is a serial chain of k-steps on a few CUs: shorter slices (>= g_splitk_tiny k-steps each), also
+    // for the shorter K of the k = 3 convs
+    if (g_splitk < 0 && g_gemm_variant < 0 && g_splitk_tiny > 0 && tiles <= 8 && g.M <= 1024 &&
+        nk64 >= 2 * g_splitk_tiny)
+      S = max(S, min(8, nk64 / g_splitk_tiny));
     if (S > 1 && plain && reg && N >= 256 && (N % 8) == 0 && ldy == N && act >= 0 && (ldy % 8) == 0) {
       void* ws = splitk_workspace(s, (size_t)S * g.M * N * sizeof(float));
       if (!ws) return -4;

@@ -1378,3 +1378,51 @@ SSAMD_API int ssamd_stream_wait(hipStream_t waiter, hipStream_t signaler) {
   if (hipEventRecord(e, signaler) != hipSuccess) return -4;
   return hipStreamWaitEvent(waiter, e, 0) == hipSuccess ? 0 : -5;
 }
+
+// ---------------------------------------------------------------- multi-tensor device copy
+// Up to 6 independent device-to-device copies in ONE launch (the static-input refresh of a HIP-graph replay:
+// a batch-1 synthesis is launch-bound, each torch copy_ is a launch of its own).  blockIdx.y = copy index;
+// 16-B vectors when source, destination and size are 16-B aligned, bytes otherwise.
+struct MCopy {
+  const unsigned char* s[6];
+  unsigned char* d[6];
+  long b[6];
+};
+
+__global__ void __launch_bounds__(256) multi_copy_kernel(MCopy m, int n) {
+  const int t = blockIdx.y;
+  if (t >= n) return;
+  const unsigned char* s = m.s[t];
+  unsigned char* d = m.d[t];
+  const long nb = m.b[t];
+  const long i0 = blockIdx.x * 256L + threadIdx.x, st = gridDim.x * 256L;
+  if ((((uintptr_t)s | (uintptr_t)d | (uintptr_t)nb) & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    for (long i = i0; i < nb / 16; i += st) d4[i] = s4[i];
+  } else {
+    for (long i = i0; i < nb; i += st) d[i] = s[i];
+  }
+}
+
+SSAMD_API int ssamd_multi_copy(int n, const void* s0, void* d0, long b0, const void* s1, void* d1, long b1,
+                               const void* s2, void* d2, long b2, const void* s3, void* d3, long b3, const void* s4,
+                               void* d4, long b4, const void* s5, void* d5, long b5, hipStream_t s) {
+  if (n < 0 || n > 6) return -2;
+  if (n == 0) return 0;
+  MCopy m;
+  const void* ss[6] = {s0, s1, s2, s3, s4, s5};
+  void* dd[6] = {d0, d1, d2, d3, d4, d5};
+  const long bb[6] = {b0, b1, b2, b3, b4, b5};
+  long mx = 0;
+  for (int i = 0; i < 6; ++i) {
+    m.s[i] = static_cast<const unsigned char*>(ss[i]);
+    m.d[i] = static_cast<unsigned char*>(dd[i]);
+    m.b[i] = i < n ? bb[i] : 0;
+    if (i < n && (bb[i] < 0 || (bb[i] > 0 && (!ss[i] || !dd[i])))) return -2;
+    if (i < n) mx = std::max(mx, bb[i]);
+  }
+  const int gx = (int)std::max<long>(1L, std::min<long>((long)cdiv(mx, 256L * 16), 64L));
+  hipLaunchKernelGGL(multi_copy_kernel, dim3(gx, n), dim3(256), 0, s, m, n);
+  return (int)hipGetLastError();
+}

@@ -25,6 +25,12 @@ import time
 import torch
 
 
+def _multi_copy(pairs) -> bool:
+    from ..ops import hip
+
+    return hip.multi_copy(pairs)
+
+
 class SynthGraphs:
     def __init__(self, model, vocoder, int16_scale=None, warm: int = 1, max_batch: int = 8, max_graphs: int = 64):
         self.model, self.voc = model, vocoder
@@ -110,8 +116,9 @@ class SynthGraphs:
             static = tuple(t.clone() if isinstance(t, torch.Tensor) else t for t in inp)
             e1["static"] = static
             e1["graph"], e1["out"] = self._capture(lambda: self._front(static))
-        for dst, src in zip(e1["static"], inp):
-            if isinstance(dst, torch.Tensor):
+        pairs = [(dst, src) for dst, src in zip(e1["static"], inp) if isinstance(dst, torch.Tensor)]
+        if not _multi_copy(pairs):  # one launch for all inputs when they are device tensors
+            for dst, src in pairs:
                 dst.copy_(src, non_blocking=True)
         e1["graph"].replay()
         self.stats["replays"] += 1

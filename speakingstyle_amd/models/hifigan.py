@@ -146,8 +146,8 @@ class ResBlock1(nn.Module):
 
     def fusable(self, channels: int, rows=None) -> bool:
         """Geometry covered by the fused ResBlock1 layer kernel (csrc/k_vocoder.hip); C = 256 (K <= 7) on its
-        tall tile only, behind ``_RB256``, and (``rows`` given) only for >= ``_RB256_MIN_ROWS`` rows: a batch-1
-        utterance's few 128-row tiles leave the GPU idle where the GEMM path spreads the work over more blocks."""
+        tall tile only, behind ``_RB256``, and (``rows`` given) only for >= ``_RB256_MIN_ROWS`` rows (an A/B knob:
+        0, every size, measured best -- even one utterance's few tiles beat the split-K GEMMs)."""
         if max(self.dilation) > 5 or self.kernel_size not in (3, 7, 11):
             return False
         if channels == 256:
@@ -595,7 +595,10 @@ class Generator(nn.Module):
 
 # the C = 256 MRF (K = 3 / 7 branches) on the tall per-layer ResBlock kernel instead of two GEMMs per layer pair
 _RB256 = [True]
-_RB256_MIN_ROWS = [65536]  # (256 tiles of the 128-row tall tile at C = 256 -- one per CU -- is 32k rows)
+# row count from which the C = 256 MRF takes the kernel path: every size since the split-K GEMM alternative measured
+# slower at batch 1 too (904 rows: b1 2.394 / 2.427 ms on the kernel vs 2.436 / 2.458 ms on split-K GEMMs,
+# profiles/r6_b1_latency.txt)
+_RB256_MIN_ROWS = [0]
 # GPU inference with host lengths: the packed, length-exact path (infer_packed) instead of length buckets
 _PACKED = [True]
 # square upsamplers (N = stride * Cout = Cin in {64, 128}) on ``hip.conv3_sq`` instead of the generic GEMM

@@ -45,6 +45,7 @@ _SIGS = {
     "ssamd_attn_set_nf32": [I, I],
     "ssamd_wgrad_set_imm": [I],
     "ssamd_gemm_set_splitk": [I],
+    "ssamd_gemm_set_splitk_tiny": [I],
     "ssamd_gemm_set_prio": [I],
     "ssamd_gemm_set_ngrp": [I],
     "ssamd_wgrad_set_buf": [I],
@@ -1770,6 +1771,27 @@ def stamp_images(entries):
         owner = e[2]()
         if owner is not None:
             e[0], e[1] = owner._version, g
+
+
+# ------------------------------------------------------------------------ multi-tensor copy
+_SIGS["ssamd_multi_copy"] = [I] + [P, P, L_] * 6 + [P]
+
+
+def multi_copy(pairs) -> bool:
+    """dst.copy_(src) for up to 6 (dst, src) pairs of contiguous same-size device tensors in ONE launch (the HIP-graph
+    replays' static-input refresh, ``infer/graphs.py``).  Returns False (nothing done) when the pairs do not qualify:
+    the caller copies them one by one."""
+    if not pairs or len(pairs) > 6 or not has("ssamd_multi_copy"):
+        return False
+    args = []
+    for d, s in pairs:
+        if not (d.is_cuda and s.is_cuda and d.device == s.device and d.is_contiguous() and s.is_contiguous()
+                and d.dtype == s.dtype and d.numel() == s.numel()):
+            return False
+        args += [_ptr(s), _ptr(d), d.numel() * d.element_size()]
+    args += [None, None, 0] * (6 - len(pairs))
+    _check(lib().ssamd_multi_copy(len(pairs), *args, _stream()), "ssamd_multi_copy")
+    return True
 
 
 # ------------------------------------------------------------------------ BatchNorm (+tanh, dropout)

@@ -1681,6 +1681,28 @@ def test_splitk_gemm_epix_vs_reference(dual, post, inplace):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("L,ks", [(14, 3), (113, 9), (904, 3)])
+def test_splitk_tiny_tiles_vs_reference(L, ks):
+    """The <= 8-tile split-K rule (batch-1 inference: short slices, k = 3 included) vs fp32 torch and vs the
+    unsplit kernel, bias + ReLU epilogue."""
+    torch.manual_seed(37)
+    Cin, N = 256, 256 if ks == 3 else 1024
+    pad = (ks - 1) // 2
+    x = torch.randn(1, L, Cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, Cin, ks, device=DEV) / (ks * Cin) ** 0.5
+    b = torch.randn(N, device=DEV) * 0.1
+    y_ref = torch.relu(F.conv1d(x.float().transpose(1, 2), w.to(torch.bfloat16).float(), b, padding=pad)).transpose(1, 2)
+    ys = {}
+    for tiny in (3, 0):
+        hip.lib().ssamd_gemm_set_splitk_tiny(tiny)
+        try:
+            ys[tiny] = hip.conv1d_infer(x, w, b, pad, 1, act="relu")
+        finally:
+            hip.lib().ssamd_gemm_set_splitk_tiny(3)
+        assert _rel(ys[tiny], y_ref) < 1e-2, tiny
+
+
+@pytest.mark.gpu
 def test_fused_adam_images_match_two_kernel_path():
     """clip+Adam that rewrites the bf16 images in the same launch (ssamd_clip_adam_img): parameters
     and Adam moments bitwise equal to adam_kernel, every cached image equal to a fresh cast of its
@@ -1773,3 +1795,19 @@ def test_hifigan_generator_hip_training_vs_torch():
         if _rel(grads[n], p.grad) > tol:
             bad.append((n, _rel(grads[n], p.grad)))
     assert len(grads) > 50 and not bad, bad
+
+
+@pytest.mark.gpu
+def test_multi_copy_one_launch():
+    """hip.multi_copy: up to 6 device copies in one launch, 16-B vector and byte paths (odd sizes / offsets)."""
+    torch.manual_seed(38)
+    srcs = [torch.randn(1, 203, 80, device=DEV), torch.randint(0, 300, (1, 14), device=DEV),
+            torch.randn(7, device=DEV).to(torch.bfloat16), torch.arange(5, device=DEV, dtype=torch.int64),
+            torch.randint(0, 255, (33,), device=DEV, dtype=torch.uint8)[1:]]
+    dsts = [torch.empty_like(s) for s in srcs]
+    assert hip.multi_copy(list(zip(dsts, srcs)))
+    torch.cuda.synchronize()
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s)
+    assert not hip.multi_copy([(torch.empty(3, device=DEV), torch.empty(4, device=DEV))])
+    assert not hip.multi_copy([(torch.empty(3), torch.empty(3))])
