@@ -2524,6 +2524,7 @@ static int g_gemm_ngrp = 1;  // 256x256 tile order: N-tile groups (tile_of); exp
 SSAMD_API void ssamd_gemm_set_ngrp(int v) { g_gemm_ngrp = v; }
 SSAMD_API void ssamd_wgrad_set_prio(int v) { g_wgrad_prio = v; }
 static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 split-K + reduce)
+static int g_ring_maxk = 0, g_ring_maxn = 256;  // 0: the 256x128 ring only for <= 64 big tiles (A/B knob)
 static int g_splitk_tiny = 3;    // min k-steps per slice for <= 8 tiles (0: the general rule only)
 static int g_num_cus_gemm = 256;
 // Split-K fp32 partials: one workspace per (device, stream).  A process-global buffer would hand a
@@ -2570,6 +2571,8 @@ static void* splitk_workspace(hipStream_t s, size_t need) {
 }
 SSAMD_API void ssamd_gemm_set_splitk(int v) { g_splitk = v; }
 SSAMD_API void ssamd_gemm_set_splitk_tiny(int v) { g_splitk_tiny = v; }
+SSAMD_API void ssamd_gemm_set_ring_maxk(int v) { g_ring_maxk = v; }
+SSAMD_API void ssamd_gemm_set_ring_maxn(int v) { g_ring_maxn = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
 SSAMD_API void ssamd_gemm_set_variant(int v) { g_gemm_variant = v; }
@@ -2635,6 +2638,10 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   // N = 256 shape (k9 dgrad 219 -> 141 us), while N >= 768 keeps the 256x256 tile.
   if (g_gemm_variant < 0 && N >= 256 && N <= 256 && ((g.M + BG - 1) / BG) * ((N + BG - 1) / BG) <= 64)
     variant = (Cin % BK == 0) ? 2 : 1;
+  // (A/B) the 256x128 ring also for short-K GEMMs with more tiles (K <= g_ring_maxk, N <= g_ring_maxn)
+  if (g_gemm_variant < 0 && g_ring_maxk > 0 && N >= 256 && N <= g_ring_maxn && g.K <= g_ring_maxk &&
+      Cin % BK == 0)
+    variant = 2;
   // Split-K for few 256x256 tiles with a long K (encoder-sized M, k = 9 data gradients, K = 9216):
   // S slices of the k range as extra blocks writing fp32 partials, one fixed-order reduce kernel
   // applies the epilogue.  Measured (tools/exp_splitk.py) on the tile-poor shapes only.

@@ -46,6 +46,8 @@ _SIGS = {
     "ssamd_wgrad_set_imm": [I],
     "ssamd_gemm_set_splitk": [I],
     "ssamd_gemm_set_splitk_tiny": [I],
+    "ssamd_gemm_set_ring_maxk": [I],
+    "ssamd_gemm_set_ring_maxn": [I],
     "ssamd_gemm_set_prio": [I],
     "ssamd_gemm_set_ngrp": [I],
     "ssamd_wgrad_set_buf": [I],
