@@ -2319,6 +2319,70 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
       }
 }
 
+// Skinny-M implicit-GEMM conv (M <= 64 rows: a batch-1 utterance's phonemes, per-utterance style vectors): the
+// tile machinery above pays a 256-row prologue / epilogue for a handful of rows and leaves most CUs idle.  Here a
+// 4-wave block owns a 16-row x 16-column output tile and splits the k-steps (32 deep) over its waves, operands
+// straight from global memory in the MFMA fragment layout (no LDS staging: the A rows are a few KiB, every weight
+// fragment is read once), the four partial tiles summed in LDS in a fixed order, then the conv_gemm epilogue
+// (bias, activation, ReLU-aux mask, residual, row validity, fp32 out, EpiX tail).  Grid = N/16 x M/16 blocks.
+// Requires Cin % 32 == 0 (a k-step never straddles a tap) and N % 16 == 0.
+__global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          const float* __restrict__ bias,
+                                                          const bf16_t* __restrict__ aux,
+                                                          const bf16_t* __restrict__ resid,
+                                                          const int64_t* __restrict__ lens, void* Y, int out_f32,
+                                                          ConvGeom g, int act, int ldy, EpiX ex) {
+  __shared__ float red[4][64][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int r = m0 + (lane & 15), ks8 = 8 * (lane >> 4);
+  const int K = g.K, nk = K / 32;
+  int2 rp = make_int2(0, 0);
+  if (r < g.M) rp = row_pos(g, r);
+  const bf16_t* wrow = W + (long)(n0 + (lane & 15)) * K + ks8;
+  float4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int st = wave; st < nk; st += 4) {
+    const int k0 = st * 32, tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
+    const int sp = rp.x + tap * g.dil - g.pad;  // source position in the row's sequence
+    short8 a = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < g.M && sp >= 0 && sp < rp.y)
+      a = *reinterpret_cast<const short8*>(X + (long)(r + sp - rp.x) * g.Cin + c0 + ks8);
+    const short8 b = *reinterpret_cast<const short8*>(wrow + k0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][lane][i] = acc[i];
+  __syncthreads();
+  // thread t: output (row 4 * (t >> 6) + (t & 3), col (t >> 2) & 15) -- i.e. lane L = (t >> 2) & 15 | (t >> 6) << 4
+  const int L = ((tid >> 2) & 15) | ((tid >> 6) << 4), i = tid & 3;
+  const int m = m0 + 4 * (L >> 4) + i, n = n0 + (L & 15);
+  if (m >= g.M) return;
+  float v = red[0][L][i] + red[1][L][i] + red[2][L][i] + red[3][L][i];
+  if (bias) v += bias[n];
+  if (act == ACT_RELU) v = fmaxf(v, 0.f);
+  else if (act == ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+  else if (act == ACT_TANH) v = tanhf(v);
+  const long off = (long)m * ldy + n;
+  if (aux) v = bf2f(aux[off]) > 0.f ? v : 0.f;
+  if (resid) v += bf2f(resid[off]);
+  bool valid = true;
+  if (lens) {
+    const int bb = m / g.L;
+    valid = m - bb * g.L < (int)lens[bb];
+  }
+  if (!valid) v = 0.f;
+  if (out_f32) {
+    reinterpret_cast<float*>(Y)[off] = v;
+    return;
+  }
+  if (ex.acc) v += bf2f(ex.acc[off]);
+  v = valid ? v * ex.scale : 0.f;
+  if (ex.y2) ex.y2[off] = f2bf(v > 0.f ? v : 0.1f * v);
+  if (ex.post_act == ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
+  reinterpret_cast<bf16_t*>(Y)[off] = f2bf(v);
+}
+
 // Split-K finish: out[m][n] = epilogue( sum_s P[s][m][n] ) in a fixed slice order, with the
 // epi_store4 semantics (bias, activation, ReLU-aux mask, residual, row validity) and, for bf16 output, the
 // big64 EpiX tail (accumulate, scale, leaky-ReLU copy y2, post activation).  8 columns per thread (two
@@ -2526,6 +2590,7 @@ SSAMD_API void ssamd_wgrad_set_prio(int v) { g_wgrad_prio = v; }
 static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 split-K + reduce)
 static int g_ring_maxk = 0, g_ring_maxn = 256;  // 0: the 256x128 ring only for <= 64 big tiles (A/B knob)
 static int g_splitk_tiny = 3;    // min k-steps per slice for <= 8 tiles (0: the general rule only)
+static int g_skinny = 1;         // skinny_gemm_kernel for M <= 64 rows (0: off, A/B)
 static int g_num_cus_gemm = 256;
 // Split-K fp32 partials: one workspace per (device, stream).  A process-global buffer would hand a
 // foreign-device pointer to a second GPU and let GEMMs on two streams race on the same partials.
@@ -2572,6 +2637,7 @@ static void* splitk_workspace(hipStream_t s, size_t need) {
 SSAMD_API void ssamd_gemm_set_splitk(int v) { g_splitk = v; }
 SSAMD_API void ssamd_gemm_set_splitk_tiny(int v) { g_splitk_tiny = v; }
 SSAMD_API void ssamd_gemm_set_ring_maxk(int v) { g_ring_maxk = v; }
+SSAMD_API void ssamd_gemm_set_skinny(int v) { g_skinny = v; }
 SSAMD_API void ssamd_gemm_set_ring_maxn(int v) { g_ring_maxn = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
@@ -2642,6 +2708,14 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   if (g_gemm_variant < 0 && g_ring_maxk > 0 && N >= 256 && N <= g_ring_maxn && g.K <= g_ring_maxk &&
       Cin % BK == 0)
     variant = 2;
+  // Skinny M (<= 64 rows): 16 x 16 output tiles, k split over the block's waves (skinny_gemm_kernel)
+  if (g_skinny && g.M <= 64 && Cin % 32 == 0 && N % 16 == 0 && !g.ksplit && !bnh && !ex.mask_out && !ex.mask_in &&
+      act >= 0 && (ex.post_act == 0 || ex.post_act == ACT_LRELU) && (!out_f32 || !(ex.acc || ex.y2 || ex.post_act ||
+      ex.scale != 1.f))) {
+    hipLaunchKernelGGL(skinny_gemm_kernel, dim3(N / 16, (g.M + 15) / 16), dim3(256), 0, s, X, W, bias, aux, resid,
+                       lens, Y, out_f32, g, act, ldy, ex);
+    return (int)hipGetLastError();
+  }
   // Split-K for few 256x256 tiles with a long K (encoder-sized M, k = 9 data gradients, K = 9216):
   // S slices of the k range as extra blocks writing fp32 partials, one fixed-order reduce kernel
   // applies the epilogue.  Measured (tools/exp_splitk.py) on the tile-poor shapes only.

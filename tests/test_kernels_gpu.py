@@ -1811,3 +1811,69 @@ def test_multi_copy_one_launch():
         assert torch.equal(d, s)
     assert not hip.multi_copy([(torch.empty(3, device=DEV), torch.empty(4, device=DEV))])
     assert not hip.multi_copy([(torch.empty(3), torch.empty(3))])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,Cin,ks,dil,N,act,res,f32,packed", [
+    (1, 14, 256, 9, 1, 1024, 1, False, False, False),
+    (2, 7, 256, 3, 1, 256, 0, True, False, False),
+    (1, 40, 512, 5, 2, 512, 3, False, False, True),
+    (4, 16, 512, 1, 1, 80, 0, False, True, False),
+    (1, 64, 1024, 1, 1, 256, 2, True, False, False),
+])
+def test_skinny_gemm_vs_reference(B, L, Cin, ks, dil, N, act, res, f32, packed):
+    """GEMMs of <= 64 rows on skinny_gemm_kernel (16 x 16 tiles, k split over the waves): conv taps / dilation,
+    per-sequence zero padding (padded with lengths, or packed rows), bias / activation / residual / fp32 output vs
+    fp32 torch, and against the tile kernels (skinny off)."""
+    from speakingstyle_amd.ops.packing import PackInfo
+
+    torch.manual_seed(39)
+    pad = dil * (ks - 1) // 2
+    x = torch.randn(B, L, Cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, Cin, ks, device=DEV) / (ks * Cin) ** 0.5
+    b = torch.randn(N, device=DEV) * 0.1
+    r = torch.randn(B, L, N, device=DEV).to(torch.bfloat16) if res else None
+    wq = w.to(torch.bfloat16).float()
+    ri, lens = None, None
+    if packed:
+        ln = torch.tensor([23, 17], device=DEV)
+        ri = PackInfo.build(ln, 23, L).rinfo
+        xs = [x[:, :23].float(), x[:, 23:].float()]
+    else:
+        lens = torch.tensor([L - (i % 3) for i in range(B)], device=DEV)
+        xs = [x.float()]
+    ys = [F.conv1d(t.transpose(1, 2), wq, b, padding=pad, dilation=dil).transpose(1, 2) for t in xs]
+    y_ref = torch.cat(ys, 1)
+    y_ref = {0: y_ref, 1: torch.relu(y_ref), 2: F.leaky_relu(y_ref, 0.1), 3: torch.tanh(y_ref)}[act]
+    if r is not None:
+        y_ref = y_ref + r.float()
+    if lens is not None:
+        y_ref = y_ref * (torch.arange(L, device=DEV)[None, :, None] < lens[:, None, None])
+    outs = []
+    for sk in (1, 0):
+        hip.lib().ssamd_gemm_set_skinny(sk)
+        try:
+            outs.append(hip.conv_gemm_raw(x, hip.weight_fwd(w), b, B, L, Cin, ks, dil, pad, N, act, resid=r,
+                                          lens=lens, out_f32=f32, rinfo=ri))
+        finally:
+            hip.lib().ssamd_gemm_set_skinny(1)
+    for y in outs:
+        assert _rel(y, y_ref) < 1e-2
+    assert _rel(outs[0], outs[1]) < 1e-2
+
+
+@pytest.mark.gpu
+def test_skinny_gemm_epix():
+    """The EpiX tail on the skinny kernel (in-place accumulate, scale, leaky-ReLU copy, post activation)."""
+    torch.manual_seed(40)
+    L, C, ks = 30, 256, 7
+    x = torch.randn(1, L, C, device=DEV).to(torch.bfloat16)
+    w = torch.randn(C, C, ks, device=DEV) / (ks * C) ** 0.5
+    b = torch.randn(C, device=DEV) * 0.1
+    a0 = torch.randn(1, L, C, device=DEV).to(torch.bfloat16)
+    v = (F.conv1d(x.float().transpose(1, 2), w.to(torch.bfloat16).float(), b, padding=3).transpose(1, 2)
+         + a0.float()) * 0.5
+    acc = a0.clone()
+    y, y2 = hip.conv1d_infer(x, w, b, 3, 1, acc=acc, scale=0.5, post_act="lrelu", dual_lrelu=True)
+    assert y.data_ptr() == acc.data_ptr()
+    assert _rel(y, F.leaky_relu(v, 0.1)) < 1e-2 and _rel(y2, F.leaky_relu(v, 0.1)) < 1e-2
