@@ -2325,7 +2325,8 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
 // straight from global memory in the MFMA fragment layout (no LDS staging: the A rows are a few KiB, every weight
 // fragment is read once), the four partial tiles summed in LDS in a fixed order, then the conv_gemm epilogue
 // (bias, activation, ReLU-aux mask, residual, row validity, fp32 out, EpiX tail).  Grid = N/16 x M/16 blocks.
-// Requires Cin % 32 == 0 (a k-step never straddles a tap) and N % 16 == 0.
+// Requires Cin % 32 == 0 (a k-step never straddles a tap) and N % 16 == 0.  A ConvTranspose 3-tap form (ksplit) is
+// computed in full: its zero tap adds exact zeros, so the result is bitwise the same with or without the skip.
 __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                           const float* __restrict__ bias,
                                                           const bf16_t* __restrict__ aux,
@@ -2590,7 +2591,8 @@ SSAMD_API void ssamd_wgrad_set_prio(int v) { g_wgrad_prio = v; }
 static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 split-K + reduce)
 static int g_ring_maxk = 0, g_ring_maxn = 256;  // 0: the 256x128 ring only for <= 64 big tiles (A/B knob)
 static int g_splitk_tiny = 3;    // min k-steps per slice for <= 8 tiles (0: the general rule only)
-static int g_skinny = 1;         // skinny_gemm_kernel for M <= 64 rows (0: off, A/B)
+static int g_skinny = 1;         // skinny_gemm_kernel for M <= g_skinny_maxm rows (0: off, A/B)
+static int g_skinny_maxm = 1024;  // measured at batch 1: 64 -> 2.19 ms, 128 -> 1.80, 1024 -> 1.76 (r6_b1_latency.txt)
 static int g_num_cus_gemm = 256;
 // Split-K fp32 partials: one workspace per (device, stream).  A process-global buffer would hand a
 // foreign-device pointer to a second GPU and let GEMMs on two streams race on the same partials.
@@ -2638,6 +2640,7 @@ SSAMD_API void ssamd_gemm_set_splitk(int v) { g_splitk = v; }
 SSAMD_API void ssamd_gemm_set_splitk_tiny(int v) { g_splitk_tiny = v; }
 SSAMD_API void ssamd_gemm_set_ring_maxk(int v) { g_ring_maxk = v; }
 SSAMD_API void ssamd_gemm_set_skinny(int v) { g_skinny = v; }
+SSAMD_API void ssamd_gemm_set_skinny_maxm(int v) { g_skinny_maxm = v; }
 SSAMD_API void ssamd_gemm_set_ring_maxn(int v) { g_ring_maxn = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
@@ -2708,8 +2711,8 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   if (g_gemm_variant < 0 && g_ring_maxk > 0 && N >= 256 && N <= g_ring_maxn && g.K <= g_ring_maxk &&
       Cin % BK == 0)
     variant = 2;
-  // Skinny M (<= 64 rows): 16 x 16 output tiles, k split over the block's waves (skinny_gemm_kernel)
-  if (g_skinny && g.M <= 64 && Cin % 32 == 0 && N % 16 == 0 && !g.ksplit && !bnh && !ex.mask_out && !ex.mask_in &&
+  // Skinny M (<= g_skinny_maxm rows): 16 x 16 output tiles, k split over the block's waves (skinny_gemm_kernel)
+  if (g_skinny && g.M <= g_skinny_maxm && Cin % 32 == 0 && N % 16 == 0 && !bnh && !ex.mask_out && !ex.mask_in &&
       act >= 0 && (ex.post_act == 0 || ex.post_act == ACT_LRELU) && (!out_f32 || !(ex.acc || ex.y2 || ex.post_act ||
       ex.scale != 1.f))) {
     hipLaunchKernelGGL(skinny_gemm_kernel, dim3(N / 16, (g.M + 15) / 16), dim3(256), 0, s, X, W, bias, aux, resid,

@@ -82,7 +82,8 @@ KNOBS: Dict[str, tuple] = {
     "gemm_ring_maxk": (0, int, "GEMMs with K <= this on the 256x128 ring kernel at any tile count (0: only <= 64 "
                                "big tiles)"),
     "gemm_ring_maxn": (256, int, "widest N of gemm_ring_maxk"),
-    "gemm_skinny": (True, _bool, "GEMMs of <= 64 rows on the skinny 16 x 16-tile kernel"),
+    "gemm_skinny": (True, _bool, "small-M GEMMs on the skinny 16 x 16-tile kernel"),
+    "gemm_skinny_maxm": (1024, int, "row limit of gemm_skinny"),
     "bn_fuse": (True, _bool, "PostNet BatchNorm backward started in the data-gradient GEMM's epilogue"),
     "defer_release": (False, _bool, "hand the side-stream weight-gradient inputs back to the trainer, freed "
                                     "during the next forward (holds a step's activations into it)"),
@@ -98,7 +99,8 @@ KNOBS: Dict[str, tuple] = {
 # switch -> kernel-library setter it drives (applied by apply_kernel_switches)
 KERNEL_SWITCHES = {"gemm_stg": "ssamd_gemm_set_stg", "gemm_mask_pre": "ssamd_gemm_set_mask_pre",
                    "gemm_bnh_stg": "ssamd_gemm_set_bnh_stg", "gemm_ring_maxk": "ssamd_gemm_set_ring_maxk",
-                   "gemm_ring_maxn": "ssamd_gemm_set_ring_maxn", "gemm_skinny": "ssamd_gemm_set_skinny"}
+                   "gemm_ring_maxn": "ssamd_gemm_set_ring_maxn", "gemm_skinny": "ssamd_gemm_set_skinny",
+                   "gemm_skinny_maxm": "ssamd_gemm_set_skinny_maxm"}
 
 _values: Dict[str, Any] = {}
 _parsed = [False]

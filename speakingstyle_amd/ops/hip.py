@@ -48,6 +48,7 @@ _SIGS = {
     "ssamd_gemm_set_splitk_tiny": [I],
     "ssamd_gemm_set_ring_maxk": [I],
     "ssamd_gemm_set_skinny": [I],
+    "ssamd_gemm_set_skinny_maxm": [I],
     "ssamd_gemm_set_ring_maxn": [I],
     "ssamd_gemm_set_prio": [I],
     "ssamd_gemm_set_ngrp": [I],

@@ -1582,18 +1582,20 @@ def test_relu_bitmask_epilogue_gpu():
     b = torch.randn(H, device=DEV) * 0.1
     mask = torch.empty(B * L, H // 8, device=DEV, dtype=torch.uint8)
     h = hip.conv_gemm_mask_raw(x, w, b, B, L, C, ks, 4, H, 1, mask_out=mask)
-    hip.lib().ssamd_gemm_set_splitk(0)  # same (unsplit) kernel: bitwise comparable
+    hip.lib().ssamd_gemm_set_splitk(0)  # same (unsplit, tile) kernel: bitwise comparable
+    hip.lib().ssamd_gemm_set_skinny(0)
     try:
         h_ref = hip.conv_gemm_raw(x, w, b, B, L, C, ks, 1, 4, H, 1)
+        bits = ((mask.view(B * L, H // 8, 1).int() >> torch.arange(8, device=DEV)) & 1).view(B, L, H).bool()
+        dz = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
+        w2 = (torch.randn(H, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16)  # dgrad image [H][1][C]
+        d_mask = hip.conv_gemm_mask_raw(dz, w2, None, B, L, C, 1, 0, H, 0, mask_in=mask)
+        d_aux = hip.conv_gemm_raw(dz, w2, None, B, L, C, 1, 1, 0, H, 0, aux=h)
     finally:
         hip.lib().ssamd_gemm_set_splitk(-1)
+        hip.lib().ssamd_gemm_set_skinny(1)
     assert torch.equal(h, h_ref)
-    bits = ((mask.view(B * L, H // 8, 1).int() >> torch.arange(8, device=DEV)) & 1).view(B, L, H).bool()
     assert torch.equal(bits, h > 0)
-    dz = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
-    w2 = (torch.randn(H, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16)  # dgrad image [H][1][C]
-    d_mask = hip.conv_gemm_mask_raw(dz, w2, None, B, L, C, 1, 0, H, 0, mask_in=mask)
-    d_aux = hip.conv_gemm_raw(dz, w2, None, B, L, C, 1, 1, 0, H, 0, aux=h)
     assert torch.equal(d_mask, d_aux)
     # the EPI_MASK instantiation (mask bytes prefetched before the prologue drain) == the generic epilogue;
     # K = 256 (double buffer) and K = 1024 (staggered loop), ragged row count
@@ -1646,8 +1648,8 @@ def test_splitk_gemm_vs_reference(act, use_bias, use_res, packed):
 @pytest.mark.parametrize("dual,post,inplace", [(False, None, True), (True, "lrelu", True), (False, "lrelu", False)])
 def test_splitk_gemm_epix_vs_reference(dual, post, inplace):
     """Split-K with the inference EpiX tail in the reduce (accumulate in place, scale, leaky-ReLU copy, post
-    activation): a tile-poor vocoder conv (904 rows, C = 256, k = 11) vs fp32 torch, forced S = 3 and the auto
-    choice, and bitwise-equal slices order across two runs."""
+    activation): a tile-poor vocoder conv (904 rows, C = 256, k = 11; skinny kernel off) vs fp32 torch, forced
+    S = 3 and the auto choice, and bitwise-equal slices order across two runs."""
     torch.manual_seed(36)
     L, C, ks, dil = 904, 256, 11, 3
     pad = dil * (ks - 1) // 2
@@ -1660,24 +1662,27 @@ def test_splitk_gemm_epix_vs_reference(dual, post, inplace):
     v = (v + a0.float()) * 0.5
     y2_ref = F.leaky_relu(v, 0.1)
     y_ref = F.leaky_relu(v, 0.1) if post else v
-    for S in (3, -1, 3):
-        hip.lib().ssamd_gemm_set_splitk(S)
-        try:
+    first = None
+    hip.lib().ssamd_gemm_set_skinny(0)
+    try:
+        for S in (3, -1, 3):
+            hip.lib().ssamd_gemm_set_splitk(S)
             acc = a0.clone()
             out = hip.conv1d_infer(x, w, b, pad, dil, acc=acc if inplace else a0.clone(), scale=0.5, post_act=post,
                                    dual_lrelu=dual)
-        finally:
-            hip.lib().ssamd_gemm_set_splitk(-1)
-        y, y2 = out if dual else (out, None)
-        assert _rel(y, y_ref) < 1e-2, S
-        if dual:
-            assert _rel(y2, y2_ref) < 1e-2, S
-        if inplace:
-            assert y.data_ptr() == acc.data_ptr()
-        if S == 3:
-            if "first" in locals():
-                assert torch.equal(y, first)
-            first = y.clone()
+            y, y2 = out if dual else (out, None)
+            assert _rel(y, y_ref) < 1e-2, S
+            if dual:
+                assert _rel(y2, y2_ref) < 1e-2, S
+            if inplace:
+                assert y.data_ptr() == acc.data_ptr()
+            if S == 3:
+                if first is not None:
+                    assert torch.equal(y, first)
+                first = y.clone()
+    finally:
+        hip.lib().ssamd_gemm_set_splitk(-1)
+        hip.lib().ssamd_gemm_set_skinny(1)
 
 
 @pytest.mark.gpu
@@ -1695,10 +1700,12 @@ def test_splitk_tiny_tiles_vs_reference(L, ks):
     ys = {}
     for tiny in (3, 0):
         hip.lib().ssamd_gemm_set_splitk_tiny(tiny)
+        hip.lib().ssamd_gemm_set_skinny(0)  # the tile kernels' split-K path, not the skinny kernel
         try:
             ys[tiny] = hip.conv1d_infer(x, w, b, pad, 1, act="relu")
         finally:
             hip.lib().ssamd_gemm_set_splitk_tiny(3)
+            hip.lib().ssamd_gemm_set_skinny(1)
         assert _rel(ys[tiny], y_ref) < 1e-2, tiny
 
 
