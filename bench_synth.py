@@ -44,6 +44,8 @@ def parse():
                     help="row count from which the C = 256 MRF uses the tall per-layer kernel (A/B; default 65536)")
     ap.add_argument("--splitk", type=int, default=None, help="GEMM split-K: -1 auto, 0 off, S forced (A/B)")
     ap.add_argument("--no-skinny", action="store_true", help="GEMMs of <= 64 rows on the tile kernels (A/B)")
+    ap.add_argument("--gemm-addln-rows", type=int, default=None,
+                    help="inference FFT blocks: GEMM + residual + LayerNorm as one kernel up to this many rows (A/B)")
     ap.add_argument("--skinny-maxm", type=int, default=None, help="row limit of the skinny GEMM kernel (A/B)")
     ap.add_argument("--splitk-tiny", type=int, default=None,
                     help="min k-steps per split-K slice for <= 8 GEMM tiles (0: general rule only) (A/B)")
@@ -99,6 +101,10 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.lib().ssamd_gemm_set_skinny(0)
+    if args.gemm_addln_rows is not None and cuda:
+        from speakingstyle_amd.ops import hip
+
+        hip.GEMM_ADDLN_MAX_ROWS = args.gemm_addln_rows
     if args.skinny_maxm is not None and cuda:
         from speakingstyle_amd.ops import hip
 

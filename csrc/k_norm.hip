@@ -431,3 +431,138 @@ SSAMD_API int ssamd_addln_wb_reduce(const float* ws, int B, int L, int C, int fi
 }
 
 SSAMD_DROP_SALT_LOADER(norm)
+
+// ---------------------------------------------------------------- inference: skinny GEMM + residual + LayerNorm
+// out = FiLM(LN(X W^T + bias + res)) with the pad mask, C = 256, for <= 1024 rows (batch-1 serving: the FFT
+// blocks' output projection / second FFN conv followed by their post-LN are two tiny launches each).  A block owns
+// 16 complete rows (below); MFMA fragments straight from global memory.  No dropout (inference), no statistics.
+constexpr int GLN_C = 256;
+constexpr int GLN_P = GLN_C + 4;  // LDS row pitch (floats)
+
+// the wave's k-steps st = kq + 4 i: every operand load issued before the first MFMA when the count is a
+// compile-time SPW (one memory round trip per wave), a 2-deep loop otherwise
+template <int SPW>
+__device__ __forceinline__ void gln_mma(const bf16_t* xrow, const bf16_t* wrow, bool rv, int K, int kq, int nk,
+                                        float4v (&acc)[4]) {
+  if constexpr (SPW > 0) {
+    constexpr int CH = SPW < 4 ? SPW : 4;  // steps per load round (4 x 5 fragments: 80 VGPRs at 128 per lane)
+#pragma unroll
+    for (int c = 0; c < SPW; c += CH) {
+      short8 a[CH], b[CH][4];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int k0 = (kq + 4 * (c + i)) * 32;
+        a[i] = rv ? *reinterpret_cast<const short8*>(xrow + k0) : short8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[i][j] = *reinterpret_cast<const short8*>(wrow + (long)j * 16 * K + k0);
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[i][j], acc[j], 0, 0, 0);
+    }
+  } else {
+#pragma unroll 2
+    for (int st = kq; st < nk; st += 4) {
+      const short8 a = rv ? *reinterpret_cast<const short8*>(xrow + st * 32) : short8{0, 0, 0, 0, 0, 0, 0, 0};
+      short8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const short8*>(wrow + (long)j * 16 * K + st * 32);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[j], 0, 0, 0);
+    }
+  }
+}
+
+// 16 waves own 16 complete rows: wave w computes columns 64 (w & 3) .. +64 over a quarter of the k-steps (w >> 2);
+// the quarters meet in LDS in a fixed order ((2 + 0) and (3 + 1), then the two sums), then wave w normalises row w.
+__global__ void __launch_bounds__(1024) gemm_addln_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          const float* __restrict__ bias, const bf16_t* __restrict__ res,
+                                                          const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                          const float* __restrict__ fg, const float* __restrict__ fb,
+                                                          const float* __restrict__ s_g, const float* __restrict__ s_b,
+                                                          const int64_t* __restrict__ lens,
+                                                          const int64_t* __restrict__ cu, int B, int L, long M, int K,
+                                                          bf16_t* __restrict__ out, float eps) {
+  __shared__ float part[2][16][GLN_P];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cg = wave & 3, kq = wave >> 2;
+  const long m0 = (long)blockIdx.x * 16;
+  const long r = m0 + (lane & 15);
+  const int ks8 = 8 * (lane >> 4);
+  const bf16_t* xrow = X + (r < M ? r : 0) * K + ks8;
+  const bf16_t* wrow = W + (long)(cg * 64 + (lane & 15)) * K + ks8;
+  float4v acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const int nk = K / 32;
+  if (nk == 8) gln_mma<2>(xrow, wrow, r < M, K, kq, nk, acc);
+  else if (nk == 32) gln_mma<8>(xrow, wrow, r < M, K, kq, nk, acc);
+  else gln_mma<0>(xrow, wrow, r < M, K, kq, nk, acc);
+  auto put = [&](int slot, bool add) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float& d = part[slot][4 * (lane >> 4) + i][cg * 64 + j * 16 + (lane & 15)];
+        d = add ? d + acc[j][i] : acc[j][i];
+      }
+  };
+  if (kq >= 2) put(kq - 2, false);
+  __syncthreads();
+  if (kq < 2) put(kq, true);
+  __syncthreads();
+  const int c0 = lane * 4;
+  const int row = wave;
+  const long m = m0 + row;
+  if (m >= M) return;
+  // sequence / position of row m: padded rows b = m / L; packed rows search cu (B is small at these sizes)
+  int b = 0;
+  bool valid = true;
+  if (cu) {
+    valid = false;
+    for (int bb = 0; bb < B; ++bb)
+      if (m >= cu[bb] && m < cu[bb] + lens[bb]) {
+        b = bb;
+        valid = true;
+      }
+  } else {
+    b = (int)(m / L);
+    if (lens) valid = m - (long)b * L < lens[b];
+  }
+  float h[4];
+  const short4v rv = *reinterpret_cast<const short4v*>(res + m * GLN_C + c0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    h[q] = part[0][row][c0 + q] + part[1][row][c0 + q] + (bias ? bias[c0 + q] : 0.f) + bf2f((bf16_t)rv[q]);
+  float s = h[0] + h[1] + h[2] + h[3];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mu = s * (1.f / GLN_C);
+  float v2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v2 += (h[q] - mu) * (h[q] - mu);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v2 += __shfl_xor(v2, o, 64);
+  const float rs = rsqrtf(v2 * (1.f / GLN_C) + eps);
+  short4v o4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float y = (h[q] - mu) * rs * lnw[c0 + q] + lnb[c0 + q];
+    if (fg) y = (*s_g * fg[(long)b * GLN_C + c0 + q] + 1.f) * y + *s_b * fb[(long)b * GLN_C + c0 + q];
+    o4[q] = (short)f2bf(valid ? y : 0.f);
+  }
+  *reinterpret_cast<short4v*>(out + m * GLN_C + c0) = o4;
+}
+
+// X [M][K] bf16 (K % 32 == 0), W [256][K] bf16 image, res / out [M][256] bf16; lens / cu as ssamd_addln_fwd
+// (padded rows of B sequences of L, or packed rows with offsets cu).  M <= 1024.
+SSAMD_API int ssamd_gemm_addln(const bf16_t* X, const bf16_t* W, const float* bias, const bf16_t* res, const float* lnw,
+                               const float* lnb, const float* fg, const float* fb, const float* s_g, const float* s_b,
+                               const int64_t* lens, const int64_t* cu, int B, int L, long M, int K, bf16_t* out,
+                               float eps, hipStream_t s) {
+  if (K % 32 || K <= 0 || M > 1024 || !res || !lnw || !lnb || (cu && !lens) || (fg && (!fb || !s_g || !s_b)))
+    return -2;
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(gemm_addln_kernel, dim3(cdiv(M, 16L)), dim3(1024), 0, s, X, W, bias, res, lnw, lnb, fg, fb, s_g,
+                     s_b, lens, cu, B, L, M, K, out, eps);
+  return (int)hipGetLastError();
+}

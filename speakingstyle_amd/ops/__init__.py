@@ -172,6 +172,25 @@ def add_layernorm(a, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, mail
     return ref.add_layernorm(a, residual, ln_w, ln_b, **kw)
 
 
+def needs_grad(*tensors) -> bool:
+    """Whether autograd will record an op on these tensors (grad mode on and any of them requires grad): the
+    inference-only kernel paths (folded BatchNorm, fused GEMM + LayerNorm) are taken when it does not."""
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
+
+
+def linear_add_layernorm(x, w, b, residual, ln_w, ln_b, pack: Optional[PackInfo] = None, **kw):
+    """add_layernorm(linear(x, w, b), residual, ...) -- ``w`` a Linear [C, K] or a k = 1 Conv1d [C, K, 1] weight.
+    Inference (no grad, not training) on the GPU runs it as ONE kernel for small row counts (``hip.gemm_addln``:
+    batch-1 serving); everything else is the two ops."""
+    if use_hip(x) and not kw.get("training", False) and not needs_grad(x, w, b, residual, ln_w, ln_b):
+        y = _hip().gemm_addln(x, w, b, residual, ln_w, ln_b, film_params=kw.get("film_params"),
+                              lengths=kw.get("lengths"), pack=pack, eps=kw.get("eps", 1e-5))
+        if y is not None:
+            return y
+    a = linear(x, w, b) if w.dim() == 2 else conv1d(x, w, b, pack=pack)
+    return add_layernorm(a, residual, ln_w, ln_b, pack=pack, **kw)
+
+
 def length_regulate(x, durations, max_len, mel_len=None):
     if use_hip(x):
         return _hip().length_regulate(x, durations, max_len, mel_len=mel_len)

@@ -1209,6 +1209,48 @@ def add_layernorm(a, residual, ln_w, ln_b, *, pre_drop=0.0, post_drop=0.0, train
     return out
 
 
+_SIGS["ssamd_gemm_addln"] = [P, P, P, P, P, P, P, P, P, P, P, P, I, I, L_, I, P, F, P]
+# Off (0): measured slower at batch 1 -- 1.82 / 1.83 ms vs 1.74 / 1.74 ms with skinny GEMM + add_layernorm
+# (profiles/r6_b1_latency.txt): one block owns whole rows, so a 14-row encoder step streams the whole weight through
+# ONE CU, where the skinny GEMM spreads it over 16-64.  Kept for A/B (bench_synth --gemm-addln-rows) and tested.
+GEMM_ADDLN_MAX_ROWS = 0
+
+
+def gemm_addln(x, w, b, residual, ln_w, ln_b, *, film_params=None, lengths=None, pack=None, eps=1e-5):
+    """Inference LN(x W^T + b + residual) (+ FiLM, pad mask) in ONE kernel (``ssamd_gemm_addln``) for C = 256 and
+    <= GEMM_ADDLN_MAX_ROWS rows; returns None when the shapes do not qualify (the caller runs linear +
+    add_layernorm).  ``w``: Linear [256, K] or Conv1d [256, K, 1]."""
+    C = w.shape[0]
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    if (C != 256 or K % 32 or rows > GEMM_ADDLN_MAX_ROWS or (w.dim() == 3 and w.shape[2] != 1)
+            or residual is None or tuple(residual.shape) != tuple(x.shape[:-1]) + (C,) or x.dim() != 3
+            or not has("ssamd_gemm_addln")):
+        return None
+    B, L = x.shape[0], x.shape[1]
+    xc = x.to(torch.bfloat16).contiguous()
+    res = residual.to(torch.bfloat16).contiguous()
+    wi = weight_fwd(w)
+    bf = None if b is None else b.detach().float().contiguous()
+    g = bt = sg = sb = None
+    if film_params is not None:
+        g, bt, sg, sb = film_params
+        g, bt = _f32_view(g), _f32_view(bt)  # the style's gamma / beta may be bf16 or column views
+    cu = None
+    if pack is not None:
+        assert B == 1 and L == pack.R, "packed gemm_addln expects [1, R, K]"
+        lens, cu, nb = pack.lens, pack.cu, pack.B
+    else:
+        lens = None if lengths is None else lengths.to(torch.int64).contiguous()
+        nb = B
+    out = torch.empty(B, L, C, device=x.device, dtype=torch.bfloat16)
+    rc = lib().ssamd_gemm_addln(_ptr(xc), _ptr(wi), _ptr(bf), _ptr(res), _ptr(ln_w), _ptr(ln_b), _ptr(g), _ptr(bt),
+                                _ptr(sg), _ptr(sb), _ptr(lens), _ptr(cu), nb, L, rows, K, _ptr(out), float(eps),
+                                _stream())
+    _check(rc, "ssamd_gemm_addln")
+    return out
+
+
 def _ln_bwd_strided(dout, a, a_off, lda, w, b, mean, rstd, dh, dh_off, B, L, C, post_p, seed, relu_in):
     """One LayerNorm backward over a column slice (row stride ``lda``) of ``a`` / ``dh``: the dense dout,
     no residual / pre-dropout / FiLM / mask.  -> (dw, db), written into the parameters' arena slots when

@@ -28,3 +28,18 @@ def test_gst_folded_eval_matches_unfolded():
         ref2 = m.reference_embedding(mel, lens)
     torch.testing.assert_close(got2, ref2.detach(), rtol=1e-4, atol=1e-5)
     assert not any("_fold" in k for k in m.state_dict())
+
+
+def test_fft_block_inference_path_matches_training_path():
+    """Inference (eval, no grad) FFT blocks take the fused linear + residual + LayerNorm route (one kernel on the
+    GPU): on the CPU reference ops it must equal the eval forward with gradients enabled."""
+    from speakingstyle_amd.models.layers import FFTBlock
+
+    torch.manual_seed(2)
+    blk = FFTBlock(256, 2, 128, 128, 1024, (9, 1), dropout=0.1).eval()
+    x = torch.randn(2, 23, 256)
+    lens = torch.tensor([23, 15])
+    ref = blk(x, lens).detach()
+    with torch.no_grad():
+        got = blk(x, lens)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)

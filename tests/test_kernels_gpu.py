@@ -1884,3 +1884,51 @@ def test_skinny_gemm_epix():
     y, y2 = hip.conv1d_infer(x, w, b, 3, 1, acc=acc, scale=0.5, post_act="lrelu", dual_lrelu=True)
     assert y.data_ptr() == acc.data_ptr()
     assert _rel(y, F.leaky_relu(v, 0.1)) < 1e-2 and _rel(y2, F.leaky_relu(v, 0.1)) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,K,film,packed", [(1, 14, 256, False, False), (3, 40, 1024, True, False),
+                                               (1, 113, 1024, True, True), (2, 300, 256, False, True)])
+def test_gemm_addln_vs_reference(B, L, K, film, packed):
+    """Inference LN(x W^T + b + res) (+ FiLM, pad mask) as one kernel (ssamd_gemm_addln) vs fp32 torch: padded rows
+    with lengths, packed rows with offsets."""
+    from speakingstyle_amd.ops.packing import PackInfo
+
+    torch.manual_seed(41)
+    C = 256
+    x = torch.randn(B, L, K, device=DEV).to(torch.bfloat16)
+    res = torch.randn(B, L, C, device=DEV).to(torch.bfloat16)
+    w = torch.randn(C, K, device=DEV) / K ** 0.5
+    b = torch.randn(C, device=DEV) * 0.1
+    lw, lb = 1 + 0.1 * torch.randn(C, device=DEV), 0.1 * torch.randn(C, device=DEV)
+    nb = 2 if packed else B
+    fp = None
+    if film:  # bf16 column views of one [B, 2C] projection, as the style encoders produce them
+        gb = torch.randn(nb, 2 * C, device=DEV).to(torch.bfloat16)
+        fp = (gb[:, :C], gb[:, C:], torch.tensor([0.3], device=DEV), torch.tensor([0.2], device=DEV))
+    h = x.float() @ w.to(torch.bfloat16).float().t() + b + res.float()
+    y = F.layer_norm(h, (C,), lw, lb, 1e-5)
+    pack = lens = None
+    if packed:
+        ln = torch.tensor([L - L // 3, L // 3], device=DEV) if B == 1 else torch.tensor([L, L - 7], device=DEV)
+        R = int(ln.sum())
+        x, res, y = x.reshape(1, -1, K)[:, :R].contiguous(), res.reshape(1, -1, C)[:, :R].contiguous(), None
+        h = x.float() @ w.to(torch.bfloat16).float().t() + b + res.float()
+        y = F.layer_norm(h, (C,), lw, lb, 1e-5)
+        pack = PackInfo.build(ln, int(ln.max()), R)
+        seq = torch.repeat_interleave(torch.arange(2, device=DEV), ln)
+        if film:
+            y = (fp[2] * fp[0].float()[seq] + 1) * y + fp[3] * fp[1].float()[seq]
+    else:
+        lens = torch.tensor([L - 3 * i for i in range(B)], device=DEV)
+        if film:
+            y = (fp[2] * fp[0].float()[:, None] + 1) * y + fp[3] * fp[1].float()[:, None]
+        y = y * (torch.arange(L, device=DEV)[None, :, None] < lens[:, None, None])
+    rows = hip.GEMM_ADDLN_MAX_ROWS
+    hip.GEMM_ADDLN_MAX_ROWS = 1024  # off by default (A/B switch): the kernel itself is tested here
+    try:
+        out = hip.gemm_addln(x, w, b, res, lw, lb, film_params=fp, lengths=lens, pack=pack)
+    finally:
+        hip.GEMM_ADDLN_MAX_ROWS = rows
+    assert out is not None
+    assert _rel(out, y) < 1e-2

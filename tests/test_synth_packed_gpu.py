@@ -17,16 +17,20 @@ def _rel(a, b):
 
 @pytest.fixture
 def pinned_gemm():
-    """The GEMM kernel choice depends on the row count (skinny kernel <= 64 rows, split-K for few tiles), so a
-    batch-1 run and the packed batch accumulate in different orders; the bucketized pitch / energy embeddings turn
-    such rounding differences into bucket flips.  The packing semantics are compared with one kernel family."""
+    """The GEMM kernel choice depends on the row count (skinny kernel, fused GEMM + LayerNorm and split-K for few
+    rows / tiles), so a batch-1 run and the packed batch accumulate in different orders; the bucketized pitch /
+    energy embeddings turn such rounding differences into bucket flips.  The packing semantics are compared with
+    one kernel family."""
     from speakingstyle_amd.ops import hip
 
     hip.lib().ssamd_gemm_set_skinny(0)
     hip.lib().ssamd_gemm_set_splitk(0)
+    rows = hip.GEMM_ADDLN_MAX_ROWS
+    hip.GEMM_ADDLN_MAX_ROWS = 0
     yield
     hip.lib().ssamd_gemm_set_skinny(1)
     hip.lib().ssamd_gemm_set_splitk(-1)
+    hip.GEMM_ADDLN_MAX_ROWS = rows
 
 
 @pytest.mark.parametrize("config", ["BC2013_GST", "LJSpeech"])
