@@ -595,10 +595,10 @@ class Generator(nn.Module):
 
 # the C = 256 MRF (K = 3 / 7 branches) on the tall per-layer ResBlock kernel instead of two GEMMs per layer pair
 _RB256 = [True]
-# row count from which the C = 256 MRF takes the kernel path: every size since the split-K GEMM alternative measured
-# slower at batch 1 too (904 rows: b1 2.394 / 2.427 ms on the kernel vs 2.436 / 2.458 ms on split-K GEMMs,
-# profiles/r6_b1_latency.txt)
-_RB256_MIN_ROWS = [0]
+# row count from which the C = 256 MRF takes the kernel path: above the skinny GEMM kernel's range (<= 1024 rows,
+# csrc/k_gemm.hip), whose GEMMs beat it at batch 1 (904 rows: b1 1.661 / 1.673 ms vs 1.728 / 1.750 ms); the kernel
+# beat the tile GEMMs at every size (profiles/r6_b1_latency.txt)
+_RB256_MIN_ROWS = [1025]
 # GPU inference with host lengths: the packed, length-exact path (infer_packed) instead of length buckets
 _PACKED = [True]
 # square upsamplers (N = stride * Cout = Cin in {64, 128}) on ``hip.conv3_sq`` instead of the generic GEMM
