@@ -1827,6 +1827,9 @@ def test_multi_copy_one_launch():
     (1, 40, 512, 5, 2, 512, 3, False, False, True),
     (4, 16, 512, 1, 1, 80, 0, False, True, False),
     (1, 64, 1024, 1, 1, 256, 2, True, False, False),
+    (1, 113, 256, 9, 1, 1024, 1, False, False, True),   # the decoder / vocoder row counts of batch-1 serving
+    (3, 301, 256, 7, 3, 256, 2, True, False, False),
+    (1, 300, 512, 5, 1, 80, 0, False, True, False),
 ])
 def test_skinny_gemm_vs_reference(B, L, Cin, ks, dil, N, act, res, f32, packed):
     """GEMMs of <= 64 rows on skinny_gemm_kernel (16 x 16 tiles, k split over the waves): conv taps / dilation,
@@ -1843,9 +1846,9 @@ def test_skinny_gemm_vs_reference(B, L, Cin, ks, dil, N, act, res, f32, packed):
     wq = w.to(torch.bfloat16).float()
     ri, lens = None, None
     if packed:
-        ln = torch.tensor([23, 17], device=DEV)
-        ri = PackInfo.build(ln, 23, L).rinfo
-        xs = [x[:, :23].float(), x[:, 23:].float()]
+        ln = torch.tensor([L - L // 3, L // 3], device=DEV)
+        ri = PackInfo.build(ln, int(ln[0]), L).rinfo
+        xs = [x[:, : int(ln[0])].float(), x[:, int(ln[0]):].float()]
     else:
         lens = torch.tensor([L - (i % 3) for i in range(B)], device=DEV)
         xs = [x.float()]
