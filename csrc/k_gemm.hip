@@ -2327,13 +2327,15 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
 // (bias, activation, ReLU-aux mask, residual, row validity, fp32 out, EpiX tail).  Grid = N/16 x M/16 blocks.
 // Requires Cin % 32 == 0 (a k-step never straddles a tap) and N % 16 == 0.  A ConvTranspose 3-tap form (ksplit) is
 // computed in full: its zero tap adds exact zeros, so the result is bitwise the same with or without the skip.
-__global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
-                                                          const float* __restrict__ bias,
-                                                          const bf16_t* __restrict__ aux,
-                                                          const bf16_t* __restrict__ resid,
-                                                          const int64_t* __restrict__ lens, void* Y, int out_f32,
-                                                          ConvGeom g, int act, int ldy, EpiX ex) {
-  __shared__ float red[4][64][4];
+template <int NWV>
+__global__ void __launch_bounds__(64 * NWV) skinny_gemm_kernel(const bf16_t* __restrict__ X,
+                                                               const bf16_t* __restrict__ W,
+                                                               const float* __restrict__ bias,
+                                                               const bf16_t* __restrict__ aux,
+                                                               const bf16_t* __restrict__ resid,
+                                                               const int64_t* __restrict__ lens, void* Y, int out_f32,
+                                                               ConvGeom g, int act, int ldy, EpiX ex) {
+  __shared__ float red[NWV][64][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
   const int r = m0 + (lane & 15), ks8 = 8 * (lane >> 4);
@@ -2343,7 +2345,7 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16_t* __restri
   const bf16_t* wrow = W + (long)(n0 + (lane & 15)) * K + ks8;
   float4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-  for (int st = wave; st < nk; st += 4) {
+  for (int st = wave; st < nk; st += NWV) {
     const int k0 = st * 32, tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
     const int sp = rp.x + tap * g.dil - g.pad;  // source position in the row's sequence
     short8 a = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -2355,11 +2357,14 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16_t* __restri
 #pragma unroll
   for (int i = 0; i < 4; ++i) red[wave][lane][i] = acc[i];
   __syncthreads();
+  if (tid >= 256) return;
   // thread t: output (row 4 * (t >> 6) + (t & 3), col (t >> 2) & 15) -- i.e. lane L = (t >> 2) & 15 | (t >> 6) << 4
   const int L = ((tid >> 2) & 15) | ((tid >> 6) << 4), i = tid & 3;
   const int m = m0 + 4 * (L >> 4) + i, n = n0 + (L & 15);
   if (m >= g.M) return;
-  float v = red[0][L][i] + red[1][L][i] + red[2][L][i] + red[3][L][i];
+  float v = 0.f;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) v += red[w][L][i];
   if (bias) v += bias[n];
   if (act == ACT_RELU) v = fmaxf(v, 0.f);
   else if (act == ACT_LRELU) v = v > 0.f ? v : 0.1f * v;
@@ -2592,6 +2597,9 @@ static int g_splitk = -1;        // -1 auto, 0 off, S > 1 forced slices (big64 s
 static int g_ring_maxk = 0, g_ring_maxn = 256;  // 0: the 256x128 ring only for <= 64 big tiles (A/B knob)
 static int g_splitk_tiny = 3;    // min k-steps per slice for <= 8 tiles (0: the general rule only)
 static int g_skinny = 1;         // skinny_gemm_kernel for M <= g_skinny_maxm rows (0: off, A/B)
+// 8-wave skinny blocks from this many k-steps (0: always 4 waves).  Batch 1: 4 waves 1.674 / 1.676 ms, 8 from 16
+// steps 1.625 / 1.624 / 1.605, from 8 steps 1.613 / 1.618; 16 waves from 32 or 64 steps no better (r6_b1_latency.txt)
+static int g_skinny_w8 = 16;
 static int g_skinny_maxm = 1024;  // measured at batch 1: 64 -> 2.19 ms, 128 -> 1.80, 1024 -> 1.76 (r6_b1_latency.txt)
 static int g_num_cus_gemm = 256;
 // Split-K fp32 partials: one workspace per (device, stream).  A process-global buffer would hand a
@@ -2641,6 +2649,7 @@ SSAMD_API void ssamd_gemm_set_splitk_tiny(int v) { g_splitk_tiny = v; }
 SSAMD_API void ssamd_gemm_set_ring_maxk(int v) { g_ring_maxk = v; }
 SSAMD_API void ssamd_gemm_set_skinny(int v) { g_skinny = v; }
 SSAMD_API void ssamd_gemm_set_skinny_maxm(int v) { g_skinny_maxm = v; }
+SSAMD_API void ssamd_gemm_set_skinny_w8(int v) { g_skinny_w8 = v; }
 SSAMD_API void ssamd_gemm_set_ring_maxn(int v) { g_ring_maxn = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
@@ -2715,8 +2724,12 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
   if (g_skinny && g.M <= g_skinny_maxm && Cin % 32 == 0 && N % 16 == 0 && !bnh && !ex.mask_out && !ex.mask_in &&
       act >= 0 && (ex.post_act == 0 || ex.post_act == ACT_LRELU) && (!out_f32 || !(ex.acc || ex.y2 || ex.post_act ||
       ex.scale != 1.f))) {
-    hipLaunchKernelGGL(skinny_gemm_kernel, dim3(N / 16, (g.M + 15) / 16), dim3(256), 0, s, X, W, bias, aux, resid,
-                       lens, Y, out_f32, g, act, ldy, ex);
+    if (g_skinny_w8 > 0 && g.K / 32 >= g_skinny_w8)  // long K: 8 waves split it (shorter per-wave chains)
+      hipLaunchKernelGGL(skinny_gemm_kernel<8>, dim3(N / 16, (g.M + 15) / 16), dim3(512), 0, s, X, W, bias, aux,
+                         resid, lens, Y, out_f32, g, act, ldy, ex);
+    else
+      hipLaunchKernelGGL(skinny_gemm_kernel<4>, dim3(N / 16, (g.M + 15) / 16), dim3(256), 0, s, X, W, bias, aux,
+                         resid, lens, Y, out_f32, g, act, ldy, ex);
     return (int)hipGetLastError();
   }
   // Split-K for few 256x256 tiles with a long K (encoder-sized M, k = 9 data gradients, K = 9216):
