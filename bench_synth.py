@@ -48,6 +48,8 @@ def parse():
                     help="inference FFT blocks: GEMM + residual + LayerNorm as one kernel up to this many rows (A/B)")
     ap.add_argument("--skinny-maxm", type=int, default=None, help="row limit of the skinny GEMM kernel (A/B)")
     ap.add_argument("--skinny-w8", type=int, default=None, help="8-wave skinny blocks from this many k-steps (A/B)")
+    ap.add_argument("--addln-small-rows", type=int, default=None,
+                    help="rows at or below which add_layernorm runs one row iteration per wave (A/B; 0: off)")
     ap.add_argument("--splitk-tiny", type=int, default=None,
                     help="min k-steps per split-K slice for <= 8 GEMM tiles (0: general rule only) (A/B)")
     ap.add_argument("--rb-whole-extra", action="store_true",
@@ -110,6 +112,10 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.lib().ssamd_gemm_set_skinny_w8(args.skinny_w8)
+    if args.addln_small_rows is not None and cuda:
+        from speakingstyle_amd.ops import hip
+
+        hip.lib().ssamd_addln_set_small_rows(args.addln_small_rows)
     if args.skinny_maxm is not None and cuda:
         from speakingstyle_amd.ops import hip
 

@@ -85,7 +85,7 @@ __device__ __forceinline__ void raw_to_f(const RawRow<EPL>& r, float* v) {
     for (int i = 0; i < 8; ++i) v[8 * j + i] = bf2f((bf16_t)r.x[j][i]);
 }
 
-template <int EPL, int LPR, bool RES>
+template <int EPL, int LPR, bool RES, int RPWV = ROWS_PER_WAVE>
 __global__ void __launch_bounds__(256) addln_fwd_kernel(
     const bf16_t* __restrict__ a, const bf16_t* __restrict__ res, const float* __restrict__ w,
     const float* __restrict__ bias, const float* __restrict__ fg, const float* __restrict__ fb,
@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
   // packed variable-length rows (cu = row offsets): sequence b owns rows cu[b] .. cu[b]+len-1
   const long rowb = cu ? (long)cu[b] : (long)b * L;
   const int Lb = cu ? len : L;
-  if (blockIdx.x * ROWS_PER_BLOCK >= Lb) return;
+  if (blockIdx.x * (WAVES * RPWV) >= Lb) return;
   float wv[EPL], bv[EPL], G[EPL], Bt[EPL];
 #pragma unroll
   for (int i = 0; i < EPL; ++i) {
@@ -123,10 +123,10 @@ __global__ void __launch_bounds__(256) addln_fwd_kernel(
   // straight-line code: a half-wave past the sequence end recomputes and rewrites the last row (identical
   // bytes) instead of branching, and the per-row statistics are stored after the loop, so the waitcnt pass
   // never merges paths with different outstanding stores (which turns every wait into a full drain).
-  constexpr int NR = ROWS_PER_WAVE / RPW;
+  constexpr int NR = RPWV / RPW;
   RawRow<EPL> ra[2], rr[2];
   float mus[NR], rss[NR];
-  auto t_of = [&](int r) { return min(blockIdx.x * ROWS_PER_BLOCK + (r * WAVES + wave) * RPW + sub, Lb - 1); };
+  auto t_of = [&](int r) { return min(blockIdx.x * (WAVES * RPWV) + (r * WAVES + wave) * RPW + sub, Lb - 1); };
   auto fetch = [&](int r, int q) {
     const long row = rowb + t_of(r);
     load_raw<EPL>(a + row * lda + c0, ra[q]);
@@ -346,6 +346,9 @@ __global__ void __launch_bounds__(256) addln_bwd_kernel(
     default: return -1;                                                            \
   }
 
+static int g_addln_small_rows = 1024;  // B * L at or below which the forward runs one row iteration per wave
+SSAMD_API void ssamd_addln_set_small_rows(int v) { g_addln_small_rows = v; }
+
 SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w, const float* bias, const float* fg,
                               const float* fb, const float* s_g, const float* s_b, const int64_t* lens,
                               const int64_t* cu, bf16_t* out,
@@ -355,6 +358,21 @@ SSAMD_API int ssamd_addln_fwd(const bf16_t* a, const bf16_t* res, const float* w
   if (lda == 0) lda = C;
   if (lda < C || lda % 8) return -2;
   if (B == 0 || L == 0) return 0;
+  if ((long)B * L <= g_addln_small_rows) {
+    // few rows (batch-1 serving): one row iteration per wave, more blocks -- the 16-row loop of a wave would
+    // mostly recompute the sequence's last row (t_of clamps) and serialise its loads
+    DISPATCH_EPL(C, {
+      constexpr int RW = 64 / LPR;
+      dim3 grid_s(cdiv(L, WAVES * RW), B);
+      if (res)
+        hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR, true, RW>), grid_s, dim3(256), 0, stream, a, res, w, bias, fg,
+                           fb, s_g, s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps, lda);
+      else
+        hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR, false, RW>), grid_s, dim3(256), 0, stream, a, res, w, bias, fg,
+                           fb, s_g, s_b, lens, cu, out, mean, rstd, L, C, pre_p, post_p, (uint64_t)seed, eps, lda);
+    });
+    return (int)hipGetLastError();
+  }
   dim3 grid(cdiv(L, ROWS_PER_BLOCK), B);
   if (res) {
     DISPATCH_EPL(C, hipLaunchKernelGGL((addln_fwd_kernel<EPL, LPR, true>), grid, dim3(256), 0, stream, a, res, w, bias, fg, fb, s_g,
