@@ -48,6 +48,7 @@ def parse():
                     help="inference FFT blocks: GEMM + residual + LayerNorm as one kernel up to this many rows (A/B)")
     ap.add_argument("--skinny-maxm", type=int, default=None, help="row limit of the skinny GEMM kernel (A/B)")
     ap.add_argument("--skinny-w8", type=int, default=None, help="8-wave skinny blocks from this many k-steps (A/B)")
+    ap.add_argument("--skinny-cin32", action="store_true", help="skinny GEMMs only for Cin % 32 == 0 (A/B)")
     ap.add_argument("--addln-small-rows", type=int, default=None,
                     help="rows at or below which add_layernorm runs one row iteration per wave (A/B; 0: off)")
     ap.add_argument("--splitk-tiny", type=int, default=None,
@@ -112,6 +113,10 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.lib().ssamd_gemm_set_skinny_w8(args.skinny_w8)
+    if args.skinny_cin32 and cuda:
+        from speakingstyle_amd.ops import hip
+
+        hip.lib().ssamd_gemm_set_skinny_any_cin(0)
     if args.addln_small_rows is not None and cuda:
         from speakingstyle_amd.ops import hip
 

@@ -2325,9 +2325,10 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
 // straight from global memory in the MFMA fragment layout (no LDS staging: the A rows are a few KiB, every weight
 // fragment is read once), the four partial tiles summed in LDS in a fixed order, then the conv_gemm epilogue
 // (bias, activation, ReLU-aux mask, residual, row validity, fp32 out, EpiX tail).  Grid = N/16 x M/16 blocks.
-// Requires Cin % 32 == 0 (a k-step never straddles a tap) and N % 16 == 0.  A ConvTranspose 3-tap form (ksplit) is
+// Cin % 32 == 0: a k-step never straddles a tap; otherwise (Cin % 8 == 0) each lane finds the tap of its 8-channel
+// chunk and K is padded to the k-step with zeros.  N % 16 == 0.  A ConvTranspose 3-tap form (ksplit) is
 // computed in full: its zero tap adds exact zeros, so the result is bitwise the same with or without the skip.
-template <int NWV>
+template <int NWV, bool AL = true>  // AL: Cin % 32 == 0 (k-steps never straddle a tap); else per-lane taps, K padded
 __global__ void __launch_bounds__(64 * NWV) skinny_gemm_kernel(const bf16_t* __restrict__ X,
                                                                const bf16_t* __restrict__ W,
                                                                const float* __restrict__ bias,
@@ -2339,19 +2340,31 @@ __global__ void __launch_bounds__(64 * NWV) skinny_gemm_kernel(const bf16_t* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
   const int r = m0 + (lane & 15), ks8 = 8 * (lane >> 4);
-  const int K = g.K, nk = K / 32;
+  const int K = g.K, nk = AL ? K / 32 : (K + 31) / 32;
   int2 rp = make_int2(0, 0);
   if (r < g.M) rp = row_pos(g, r);
   const bf16_t* wrow = W + (long)(n0 + (lane & 15)) * K + ks8;
   float4v acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
   for (int st = wave; st < nk; st += NWV) {
-    const int k0 = st * 32, tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
-    const int sp = rp.x + tap * g.dil - g.pad;  // source position in the row's sequence
-    short8 a = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r < g.M && sp >= 0 && sp < rp.y)
-      a = *reinterpret_cast<const short8*>(X + (long)(r + sp - rp.x) * g.Cin + c0 + ks8);
-    const short8 b = *reinterpret_cast<const short8*>(wrow + k0);
+    const int k0 = st * 32;
+    short8 a = {0, 0, 0, 0, 0, 0, 0, 0}, b = {0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (AL) {
+      const int tap = k0 / g.Cin, c0 = k0 - tap * g.Cin;
+      const int sp = rp.x + tap * g.dil - g.pad;  // source position in the row's sequence
+      if (r < g.M && sp >= 0 && sp < rp.y)
+        a = *reinterpret_cast<const short8*>(X + (long)(r + sp - rp.x) * g.Cin + c0 + ks8);
+      b = *reinterpret_cast<const short8*>(wrow + k0);
+    } else {  // Cin % 8 == 0: the lane's 8-channel chunk lies within one tap; chunks past K are zero
+      const int k = k0 + ks8;
+      if (k < K) {
+        const int tap = k / g.Cin, c = k - tap * g.Cin;
+        const int sp = rp.x + tap * g.dil - g.pad;
+        if (r < g.M && sp >= 0 && sp < rp.y)
+          a = *reinterpret_cast<const short8*>(X + (long)(r + sp - rp.x) * g.Cin + c);
+        b = *reinterpret_cast<const short8*>(wrow + k0);
+      }
+    }
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
   }
 #pragma unroll
@@ -2600,7 +2613,8 @@ static int g_skinny = 1;         // skinny_gemm_kernel for M <= g_skinny_maxm ro
 // 8-wave skinny blocks from this many k-steps (0: always 4 waves).  Batch 1: 4 waves 1.674 / 1.676 ms, 8 from 16
 // steps 1.625 / 1.624 / 1.605, from 8 steps 1.613 / 1.618; 16 waves from 32 or 64 steps no better (r6_b1_latency.txt)
 static int g_skinny_w8 = 16;
-static int g_skinny_maxm = 1024;  // measured at batch 1: 64 -> 2.19 ms, 128 -> 1.80, 1024 -> 1.76 (r6_b1_latency.txt)
+static int g_skinny_maxm = 1024;
+static int g_skinny_any_cin = 1;  // the skinny kernel also for Cin % 32 != 0 (per-lane taps; 0: tile kernels, A/B)  // measured at batch 1: 64 -> 2.19 ms, 128 -> 1.80, 1024 -> 1.76 (r6_b1_latency.txt)
 static int g_num_cus_gemm = 256;
 // Split-K fp32 partials: one workspace per (device, stream).  A process-global buffer would hand a
 // foreign-device pointer to a second GPU and let GEMMs on two streams race on the same partials.
@@ -2650,6 +2664,7 @@ SSAMD_API void ssamd_gemm_set_ring_maxk(int v) { g_ring_maxk = v; }
 SSAMD_API void ssamd_gemm_set_skinny(int v) { g_skinny = v; }
 SSAMD_API void ssamd_gemm_set_skinny_maxm(int v) { g_skinny_maxm = v; }
 SSAMD_API void ssamd_gemm_set_skinny_w8(int v) { g_skinny_w8 = v; }
+SSAMD_API void ssamd_gemm_set_skinny_any_cin(int v) { g_skinny_any_cin = v; }
 SSAMD_API void ssamd_gemm_set_ring_maxn(int v) { g_ring_maxn = v; }
 
 SSAMD_API void ssamd_gemm_set_epilogue(int lds_staged) { g_force_lds_epilogue = lds_staged != 0; }
@@ -2721,15 +2736,26 @@ static int conv_gemm_impl(const bf16_t* X, const bf16_t* W, const float* bias, c
       Cin % BK == 0)
     variant = 2;
   // Skinny M (<= g_skinny_maxm rows): 16 x 16 output tiles, k split over the block's waves (skinny_gemm_kernel)
-  if (g_skinny && g.M <= g_skinny_maxm && Cin % 32 == 0 && N % 16 == 0 && !bnh && !ex.mask_out && !ex.mask_in &&
+  if (g_skinny && g.M <= g_skinny_maxm && (Cin % 32 == 0 || g_skinny_any_cin) && N % 16 == 0 && !bnh && !ex.mask_out && !ex.mask_in &&
       act >= 0 && (ex.post_act == 0 || ex.post_act == ACT_LRELU) && (!out_f32 || !(ex.acc || ex.y2 || ex.post_act ||
       ex.scale != 1.f))) {
-    if (g_skinny_w8 > 0 && g.K / 32 >= g_skinny_w8)  // long K: 8 waves split it (shorter per-wave chains)
-      hipLaunchKernelGGL(skinny_gemm_kernel<8>, dim3(N / 16, (g.M + 15) / 16), dim3(512), 0, s, X, W, bias, aux,
-                         resid, lens, Y, out_f32, g, act, ldy, ex);
-    else
-      hipLaunchKernelGGL(skinny_gemm_kernel<4>, dim3(N / 16, (g.M + 15) / 16), dim3(256), 0, s, X, W, bias, aux,
-                         resid, lens, Y, out_f32, g, act, ldy, ex);
+    const dim3 grid(N / 16, (g.M + 15) / 16);
+    const bool w8 = g_skinny_w8 > 0 && g.K / 32 >= g_skinny_w8;  // long K: 8 waves split it (shorter chains)
+    if (Cin % 32 == 0) {
+      if (w8)
+        hipLaunchKernelGGL((skinny_gemm_kernel<8, true>), grid, dim3(512), 0, s, X, W, bias, aux, resid, lens, Y,
+                           out_f32, g, act, ldy, ex);
+      else
+        hipLaunchKernelGGL((skinny_gemm_kernel<4, true>), grid, dim3(256), 0, s, X, W, bias, aux, resid, lens, Y,
+                           out_f32, g, act, ldy, ex);
+    } else {  // Cin % 8 == 0 (conv_pre / PostNet conv 0 over 80 mel channels, the GST's first im2col layer)
+      if (w8)
+        hipLaunchKernelGGL((skinny_gemm_kernel<8, false>), grid, dim3(512), 0, s, X, W, bias, aux, resid, lens, Y,
+                           out_f32, g, act, ldy, ex);
+      else
+        hipLaunchKernelGGL((skinny_gemm_kernel<4, false>), grid, dim3(256), 0, s, X, W, bias, aux, resid, lens, Y,
+                           out_f32, g, act, ldy, ex);
+    }
     return (int)hipGetLastError();
   }
   // Split-K for few 256x256 tiles with a long K (encoder-sized M, k = 9 data gradients, K = 9216):

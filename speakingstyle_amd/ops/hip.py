@@ -50,6 +50,7 @@ _SIGS = {
     "ssamd_gemm_set_skinny": [I],
     "ssamd_gemm_set_skinny_maxm": [I],
     "ssamd_gemm_set_skinny_w8": [I],
+    "ssamd_gemm_set_skinny_any_cin": [I],
     "ssamd_addln_set_small_rows": [I],
     "ssamd_gemm_set_ring_maxn": [I],
     "ssamd_gemm_set_prio": [I],

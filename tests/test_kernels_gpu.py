@@ -1830,6 +1830,9 @@ def test_multi_copy_one_launch():
     (1, 113, 256, 9, 1, 1024, 1, False, False, True),   # the decoder / vocoder row counts of batch-1 serving
     (3, 301, 256, 7, 3, 256, 2, True, False, False),
     (1, 300, 512, 5, 1, 80, 0, False, True, False),
+    (1, 113, 80, 7, 1, 512, 0, False, False, False),    # Cin % 32 != 0: per-lane taps (vocoder conv_pre)
+    (1, 60, 80, 5, 1, 512, 3, False, False, True),      # (PostNet conv 0, packed)
+    (1, 500, 16, 1, 1, 32, 1, False, False, False),     # (the GST's first im2col layer: K = 16)
 ])
 def test_skinny_gemm_vs_reference(B, L, Cin, ks, dil, N, act, res, f32, packed):
     """GEMMs of <= 64 rows on skinny_gemm_kernel (16 x 16 tiles, k split over the waves): conv taps / dilation,
