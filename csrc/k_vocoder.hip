@@ -467,6 +467,10 @@ template <int C, int K>
 constexpr bool has_half() {
   return has_tall<C, K>() && C <= 128;
 }
+// the 64-row tile (one row block per wave): twice the workgroups of the 128-row tile for batch-1 utterances whose
+// whole stage is a few dozen 128-row tiles (halo recompute 16-19 % instead of 8-9 %)
+template <int C, int K>
+using RBS = RB<C, K, 1>;
 
 template <class R>
 int launch_rb(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2, const float* b2,
@@ -1130,6 +1134,7 @@ int rb_bm_kind(int kind) {  // 3: the tall per-layer tile's BM, 4: the 128-row t
   }
   if constexpr (!tall_only<C>()) {
     if (kind == 4) return RB<C, K>::BM;
+    if (kind == 5) return RBS<C, K>::BM;
   }
   return 0;
 }
@@ -1150,7 +1155,7 @@ SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2
   } else if (kind == 2) {
     if (C == 128) return C3<128>::BM;
     if (C == 64) return C3<64>::BM;
-  } else if (kind == 3 || kind == 4) {  // 3: the tall per-layer tile, 4: the 128-row one (0: no such instance)
+  } else if (kind >= 3 && kind <= 5) {  // 3: the tall per-layer tile, 4: the 128-row one, 5: the 64-row one
 #define VT_RB2(CC, KK) \
   if (C == CC && K == KK) return rb_bm_kind<CC, KK>(kind);
     VT_RB2(32, 3) VT_RB2(32, 7) VT_RB2(32, 11) VT_RB2(64, 3) VT_RB2(64, 7) VT_RB2(64, 11) VT_RB2(128, 3)
@@ -1199,8 +1204,8 @@ SSAMD_API int ssamd_resblock_layer_pk(const bf16_t* x, const bf16_t* w1, const f
 }
 
 // ssamd_resblock_layer_pk with the tile chosen by the caller (tall = 1: the tall tile, 0: the 128-row tile) -- the
-// packed vocoder picks per call from the tile count (ssamd_voc_tile_rows kinds 3 / 4): a batch-1 utterance gets
-// twice the workgroups from the shorter tile, a batch of 256 the tall tile's fewer LDS reads per MFMA
+// packed vocoder picks per call from the tile count (ssamd_voc_tile_rows kinds 3 / 4 / 5; tall = 1 / 0 / -1): a
+// batch-1 utterance gets more workgroups from the shorter tiles, a batch of 256 the tall tile's fewer LDS reads per MFMA
 SSAMD_API int ssamd_resblock_layer_pk2(const bf16_t* x, const bf16_t* w1, const float* b1, const bf16_t* w2,
                                        const float* b2, const bf16_t* acc_in, bf16_t* out, const int* tt, int ntt, int C,
                                        int K, int d, float slope, float out_scale, int post_lrelu, int tall,
@@ -1211,16 +1216,19 @@ SSAMD_API int ssamd_resblock_layer_pk2(const bf16_t* x, const bf16_t* w1, const 
 #define RBK2_CASE(CC, KK)                                                                                          \
   if (C == CC && K == KK) {                                                                                        \
     if constexpr (has_half<CC, KK>()) {                                                                            \
-      if (tall && g_rb_tall == 2)                                                                                  \
+      if (tall > 0 && g_rb_tall == 2)                                                                                  \
         return launch_rb<RBH<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, \
                                       ntt);                                                                        \
     }                                                                                                              \
     if constexpr (has_tall<CC, KK>()) {                                                                            \
-      if (tall)                                                                                                    \
+      if (tall > 0)                                                                                                \
         return launch_rb<RBT<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, \
                                       ntt);                                                                        \
     }                                                                                                              \
     if constexpr (!tall_only<CC>()) {                                                                              \
+      if (tall == -1)                                                                                              \
+        return launch_rb<RBS<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4, \
+                                      ntt);                                                                        \
       if (!tall)                                                                                                   \
         return launch_rb<RB<CC, KK>>(x, w1, b1, w2, b2, acc_in, out, 1, 0, d, slope, out_scale, post_lrelu, s, t4,  \
                                      ntt);                                                                         \

@@ -2475,21 +2475,25 @@ def conv1d_infer_packed(x, vp, rate, w, b, pad, dil, act=None, resid=None, acc=N
     return (y, y2) if dual_lrelu else y
 
 
-_TALL_MIN_TILES = [512]  # packed per-layer ResBlock: the tall tile only when it still yields >= this many tiles
+_TALL_MIN_TILES = [512]
+_SMALL_MAX_TILES = [192]  # the 64-row tile below this many 128-row tiles (3/4 of the CUs; 0: never)  # packed per-layer ResBlock: the tall tile only when it still yields >= this many tiles
 
 
 def rb_layer_tile(C: int, K: int, lens, rate: int):
-    """(tall, tile rows) of the per-layer ResBlock kernel for a packed batch: the tall tile (fewer LDS reads per
-    MFMA, ``csrc/k_vocoder.hip`` RBT) when the batch gives it at least ``_TALL_MIN_TILES`` tiles (two per CU),
-    else the 128-row tile (twice the workgroups: batch-1 latency).  Deterministic in (C, K, lengths, rate), so the
-    tile tables and the launch agree."""
+    """(tile mode, tile rows) of the per-layer ResBlock kernel for a packed batch: 1 = the tall tile (fewer LDS
+    reads per MFMA, ``csrc/k_vocoder.hip`` RBT) when the batch gives it at least ``_TALL_MIN_TILES`` tiles (two per
+    CU), 0 = the 128-row tile, -1 = the 64-row tile (RBS) when even the 128-row tile gives fewer than
+    ``_SMALL_MAX_TILES`` workgroups (batch-1 latency).  Deterministic in (C, K, lengths, rate), so the tile tables
+    and the launch agree."""
     bt, br = voc_tile_rows(3, C, K), voc_tile_rows(4, C, K)
     if not br:
-        return True, bt
-    if not bt or not _TALL[0]:
-        return False, br
-    tiles = sum(-(-int(L) * rate // bt) for L in lens)
-    return (True, bt) if tiles >= _TALL_MIN_TILES[0] else (False, br)
+        return 1, bt
+    if bt and _TALL[0] and sum(-(-int(L) * rate // bt) for L in lens) >= _TALL_MIN_TILES[0]:
+        return 1, bt
+    bs = voc_tile_rows(5, C, K)
+    if bs and sum(-(-int(L) * rate // br) for L in lens) < _SMALL_MAX_TILES[0]:
+        return -1, bs
+    return 0, br
 
 
 _TALL = [True]

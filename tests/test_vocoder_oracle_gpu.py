@@ -186,6 +186,29 @@ def test_packed_vocoding_equals_each_utterance_alone():
     assert H._PACKED[0]
 
 
+def test_packed_resblock_tile_modes_bitwise():
+    """The per-layer ResBlock kernel's three packed tile heights (tall, 128-row, 64-row: hip.rb_layer_tile picks one
+    from the tile count) compute every output row with the same tap / chunk order: a batch-1 utterance vocoded with
+    each forced mode is bitwise the same."""
+    from speakingstyle_amd.ops import hip
+
+    g = _generator(10)
+    torch.manual_seed(6)
+    mel = torch.randn(1, 113, 80, device=DEV) * 2 - 5
+    outs, modes = [], []
+    saved = (hip._SMALL_MAX_TILES[0], hip._TALL_MIN_TILES[0])
+    try:
+        for small, tall in ((1 << 30, 1 << 30), (0, 1 << 30), (0, 0)):  # 64-row, 128-row, tall where instantiated
+            hip._SMALL_MAX_TILES[0], hip._TALL_MIN_TILES[0] = small, tall
+            modes.append(hip.rb_layer_tile(128, 7, [113], 64)[0])
+            with torch.no_grad():
+                outs.append(g.infer_packed(mel, [113]))
+    finally:
+        hip._SMALL_MAX_TILES[0], hip._TALL_MIN_TILES[0] = saved
+    assert modes == [-1, 0, 1], modes
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
 def test_bucketed_vocoding_matches_padded_batch():
     """Length buckets (each group truncated at max_len + receptive radius) vs the padded batch on
     the same HIP kernels: the valid samples agree (the GEMMs are row-independent; only a different
