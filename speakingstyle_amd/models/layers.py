@@ -104,7 +104,8 @@ class MultiHeadAttention(nn.Module):
         o = ops.attention(qkv, lengths, self.n_head, pack)
         # LN(dropout(fc(o)) + x), then the FFT block's pad mask-fill (Layers.py:27-28): one addln kernel
         kw = dict(pre_drop=self.dropout, training=self.training, lengths=lengths, pack=pack)
-        if mb is None and not self.training and not ops.needs_grad(x, self.fc.weight, self.layer_norm.weight):
+        if mb is None and not self.training and not ops.needs_grad(x, *self.fc.parameters(),
+                                                                    *self.layer_norm.parameters()):
             # inference: output projection + residual + LayerNorm as one fused kernel for small batches
             return ops.linear_add_layernorm(o, self.fc.weight, self.fc.bias, x, self.layer_norm.weight,
                                             self.layer_norm.bias, **kw)
@@ -127,7 +128,7 @@ class PositionwiseFeedForward(nn.Module):
         mb = ops.residual_mailbox(x)  # d(residual x) joins the first conv's data gradient
         kw = dict(pre_drop=self.dropout, training=self.training, film_params=film_params, lengths=lengths, pack=pack)
         if (mb is None and not self.training and self.k[1] == 1
-                and not ops.needs_grad(x, self.w_1.weight, self.w_2.weight, self.layer_norm.weight)):
+                and not ops.needs_grad(x, *self.parameters(), *(film_params or ()))):
             # inference: conv -> ReLU, then the second conv + residual + LN (+ FiLM) as one kernel for small batches
             h = ops.conv1d(x, self.w_1.weight, self.w_1.bias, (self.k[0] - 1) // 2, 1, "relu", pack=pack)
             return ops.linear_add_layernorm(h, self.w_2.weight, self.w_2.bias, x, self.layer_norm.weight,

@@ -148,7 +148,7 @@ class GlobalStyleTokens(nn.Module):
         x = mel.unsqueeze(-1)
         if not ops.use_hip(x):
             x = x.float()
-        if not self.training and not ops.needs_grad(mel, self.convs[0].weight, self.bns[0].weight):
+        if not self.training and not ops.needs_grad(mel, *self.convs.parameters(), *self.bns.parameters()):
             # eval BatchNorm is a per-channel affine: folded into the conv, ReLU in its GEMM epilogue
             for prep in self.folded_convs():
                 x = ops.conv2d_s2_infer(x, prep, "relu")

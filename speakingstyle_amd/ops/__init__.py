@@ -182,7 +182,9 @@ def linear_add_layernorm(x, w, b, residual, ln_w, ln_b, pack: Optional[PackInfo]
     """add_layernorm(linear(x, w, b), residual, ...) -- ``w`` a Linear [C, K] or a k = 1 Conv1d [C, K, 1] weight.
     Inference (no grad, not training) on the GPU runs it as ONE kernel for small row counts (``hip.gemm_addln``:
     batch-1 serving); everything else is the two ops."""
-    if use_hip(x) and not kw.get("training", False) and not needs_grad(x, w, b, residual, ln_w, ln_b):
+    fp = kw.get("film_params")
+    if (use_hip(x) and not kw.get("training", False)
+            and not needs_grad(x, w, b, residual, ln_w, ln_b, *(fp if fp is not None else ()))):
         y = _hip().gemm_addln(x, w, b, residual, ln_w, ln_b, film_params=kw.get("film_params"),
                               lengths=kw.get("lengths"), pack=pack, eps=kw.get("eps", 1e-5))
         if y is not None:
