@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--skinny-maxm", type=int, default=None, help="row limit of the skinny GEMM kernel (A/B)")
     ap.add_argument("--skinny-w8", type=int, default=None, help="8-wave skinny blocks from this many k-steps (A/B)")
     ap.add_argument("--skinny-cin32", action="store_true", help="skinny GEMMs only for Cin % 32 == 0 (A/B)")
+    ap.add_argument("--rf-short-tiles", type=int, default=None,
+                    help="whole-ResBlock short tile below this many regular tiles (A/B; 0: never)")
     ap.add_argument("--rb-small-tiles", type=int, default=None,
                     help="per-layer ResBlock 64-row tile below this many 128-row tiles (A/B; 0: never)")
     ap.add_argument("--addln-small-rows", type=int, default=None,
@@ -115,6 +117,10 @@ def run(args):
         from speakingstyle_amd.ops import hip
 
         hip.lib().ssamd_gemm_set_skinny_w8(args.skinny_w8)
+    if args.rf_short_tiles is not None and cuda:
+        from speakingstyle_amd.ops import hip
+
+        hip._RF_SHORT_MAX_TILES[0] = args.rf_short_tiles
     if args.rb_small_tiles is not None and cuda:
         from speakingstyle_amd.ops import hip
 

@@ -708,7 +708,7 @@ struct RFW {
   int d[3];
 };
 
-template <int C, int K>
+template <int C, int K, int S = 0>  // S = 1: the short tile for tile-poor packed batches (batch-1 serving)
 struct RF {
   // RING: the weights stream per (tap, 32-deep chunk) through a 3-slot LDS ring (one barrier per step)
   // instead of a whole image per conv -- the wide / long-kernel instances, whose whole image would
@@ -725,7 +725,9 @@ struct RF {
   // recompute) that lets two workgroups overlap each other's phases (1.41 -> 1.18 ms per ResBlock).
   // (C = 64 / K = 3 measured: the 8-block tile at two per CU is 12 % slower than 24 blocks at one)
   static constexpr int OCC = K == 3 && C == 32 ? 2 : 1;
-  static constexpr int NB = K == 3 && C == 32 ? 16 : C == 32 ? 40 : (C == 64 ? 24 : 12);
+  // S = 1: about a third to a half of the rows (more halo recompute, 2-4x the workgroups of a batch-1 stage)
+  static constexpr int NB = S ? (C == 32 ? (K == 3 ? 8 : 16) : C == 64 ? 12 : 8)
+                              : (K == 3 && C == 32 ? 16 : C == 32 ? 40 : (C == 64 ? 24 : 12));
   static constexpr int R0 = NB * 16;
   static constexpr int LDC = C + 16;               // bf16 pitch: 2 (mod 4) 16-B units (see RB)
   static constexpr int ROWS = R0 + 2 * MG;
@@ -752,10 +754,10 @@ struct RF {
 // profiles/r3_v7_rb_pairs_lost.jsonl; the 16-bit scattered stores stay.)
 // acc[j][s] = conv over the wave's row blocks blk = wr + WR*j (all NB blocks of the tile are computed:
 // straight-line MFMA code; rows outside the conv's valid region are don't-care).
-template <int C, int K>
+template <int C, int K, int S>
 __device__ __forceinline__ void conv_rf(const bf16_t* __restrict__ src, int step, const char* Ws, int wr, int wc,
-                                        int col, int quad, float4v (&acc)[RF<C, K>::MAXRB][RF<C, K>::NSW]) {
-  using R = RF<C, K>;
+                                        int col, int quad, float4v (&acc)[RF<C, K, S>::MAXRB][RF<C, K, S>::NSW]) {
+  using R = RF<C, K, S>;
 #pragma unroll
   for (int j = 0; j < R::MAXRB; ++j)
 #pragma unroll
@@ -786,7 +788,7 @@ __device__ __forceinline__ void conv_rf(const bf16_t* __restrict__ src, int step
 // RING form of conv_rf: weight slices [C][32] (tap, chunk) DMA'd three steps ahead into a 3-slot ring
 // (same source-side chunk swizzle and pipeline as conv_tile), fragments of step+1 read while step's
 // MFMAs run, one barrier per step.
-template <int C, int K>
+template <int C, int K, int S>
 __device__ __forceinline__ void stage_ring(const bf16_t* __restrict__ w, int step, char* slot, int tid, int wave) {
   if (wave * 64 < C * 4) {  // wave-uniform: C*4 16-B chunks per slice
     constexpr int KC = C / 32;
@@ -797,20 +799,20 @@ __device__ __forceinline__ void stage_ring(const bf16_t* __restrict__ w, int ste
   }
 }
 
-template <int C, int K>
+template <int C, int K, int S>
 __device__ __forceinline__ void conv_rf_ring(const bf16_t* __restrict__ src, int step_d, const bf16_t* __restrict__ w,
                                              char* ring, int tid, int wave, int wr, int wc, int col, int quad,
-                                             float4v (&acc)[RF<C, K>::MAXRB][RF<C, K>::NSW]) {
-  using R = RF<C, K>;
+                                             float4v (&acc)[RF<C, K, S>::MAXRB][RF<C, K, S>::NSW]) {
+  using R = RF<C, K, S>;
   constexpr int STEPS = K * R::KC;
   constexpr int SLOT = R::SLOT;
 #pragma unroll
   for (int j = 0; j < R::MAXRB; ++j)
 #pragma unroll
     for (int s = 0; s < R::NSW; ++s) acc[j][s] = float4v{0.f, 0.f, 0.f, 0.f};
-  stage_ring<C, K>(w, 0, ring, tid, wave);
-  if (STEPS > 1) stage_ring<C, K>(w, 1, ring + SLOT, tid, wave);
-  if (STEPS > 2) stage_ring<C, K>(w, 2, ring + 2 * SLOT, tid, wave);
+  stage_ring<C, K, S>(w, 0, ring, tid, wave);
+  if (STEPS > 1) stage_ring<C, K, S>(w, 1, ring + SLOT, tid, wave);
+  if (STEPS > 2) stage_ring<C, K, S>(w, 2, ring + 2 * SLOT, tid, wave);
   if (STEPS > 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if (STEPS > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -841,7 +843,7 @@ __device__ __forceinline__ void conv_rf_ring(const bf16_t* __restrict__ src, int
       if (st + 2 < STEPS) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (st + 3 < STEPS) stage_ring<C, K>(w, st + 3, ring + (st % 3) * SLOT, tid, wave);
+      if (st + 3 < STEPS) stage_ring<C, K, S>(w, st + 3, ring + (st % 3) * SLOT, tid, wave);
       load(st + 1, cur ^ 1);
     }
 #pragma unroll
@@ -852,13 +854,13 @@ __device__ __forceinline__ void conv_rf_ring(const bf16_t* __restrict__ src, int
   }
 }
 
-template <int C, int K>
-__global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fused_kernel(const bf16_t* __restrict__ x, RFW p,
+template <int C, int K, int S>
+__global__ void __launch_bounds__((RF<C, K, S>::NT), (RF<C, K, S>::OCC)) resblock_fused_kernel(const bf16_t* __restrict__ x, RFW p,
                                                                         const bf16_t* acc_in, bf16_t* out, int Tp,
                                                                         int tiles, int HT, float slope,
                                                                         float out_scale, int post_lrelu,
                                                                         const int4* __restrict__ tt) {
-  using R = RF<C, K>;
+  using R = RF<C, K, S>;
   constexpr int NT = R::NT;
   constexpr int CH = C / 8;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -964,10 +966,10 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
     }
     // conv 2pp = conv1 (dilation d) of lrelu(x_p) -> T = lrelu(. + b1), zero outside [0, T)
     if constexpr (R::RING) {
-      conv_rf_ring<C, K>(As, d, p.w[2 * pp], Ws, tid, wave, wr, wc, col, quad, acc);
+      conv_rf_ring<C, K, S>(As, d, p.w[2 * pp], Ws, tid, wave, wr, wc, col, quad, acc);
     } else {
       if (pp < 2) wload(wr0, p.w[2 * pp + 2]);  // in flight during two convs
-      conv_rf<C, K>(As, d, Ws, wr, wc, col, quad, acc);
+      conv_rf<C, K, S>(As, d, Ws, wr, wc, col, quad, acc);
     }
     {
 #pragma unroll
@@ -1001,8 +1003,8 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
         if (j < BM && t < T) ar[it] = *reinterpret_cast<const short8*>(ab + (long)t * C + c0);
       }
     }
-    if constexpr (R::RING) conv_rf_ring<C, K>(Ts, 1, p.w[2 * pp + 1], Ws, tid, wave, wr, wc, col, quad, acc);
-    else conv_rf<C, K>(Ts, 1, Ws, wr, wc, col, quad, acc);
+    if constexpr (R::RING) conv_rf_ring<C, K, S>(Ts, 1, p.w[2 * pp + 1], Ws, tid, wave, wr, wc, col, quad, acc);
+    else conv_rf<C, K, S>(Ts, 1, Ws, wr, wc, col, quad, acc);
     {
 #pragma unroll
       for (int s = 0; s < R::NSW; ++s) {
@@ -1074,23 +1076,23 @@ __global__ void __launch_bounds__((RF<C, K>::NT), (RF<C, K>::OCC)) resblock_fuse
   }
 }
 
-template <int C, int K>
+template <int C, int K, int S>
 int launch_rf(const bf16_t* x, const RFW& p, const bf16_t* acc_in, bf16_t* out, int B, int T, float slope,
               float out_scale, int post_lrelu, hipStream_t s, const int4* tt = nullptr, int ntt = 0) {
-  using R = RF<C, K>;
+  using R = RF<C, K, S>;
   const int HT = R::H2 * (p.d[0] + p.d[1] + p.d[2] + 3);
   const int BM = R::R0 - 2 * HT;
   if (BM < 16) return -2;
   static bool lds_set = false;
   if (!lds_set) {
-    allow_lds(resblock_fused_kernel<C, K>, R::LDS);
+    allow_lds(resblock_fused_kernel<C, K, S>, R::LDS);
     lds_set = true;
   }
   const int tiles = tt ? 1 : (T + BM - 1) / BM;
   const long nblk = tt ? (long)ntt : (long)B * tiles;
   if (nblk > 0x7fffffffL) return -2;
   if (nblk == 0) return 0;
-  hipLaunchKernelGGL((resblock_fused_kernel<C, K>), dim3(nblk), dim3(R::NT), R::LDS, s, x, p, acc_in,
+  hipLaunchKernelGGL((resblock_fused_kernel<C, K, S>), dim3(nblk), dim3(R::NT), R::LDS, s, x, p, acc_in,
                      out, T, tiles, HT, slope, out_scale, post_lrelu, tt);
   return (int)hipGetLastError();
 }
@@ -1152,6 +1154,11 @@ SSAMD_API int ssamd_voc_tile_rows(int kind, int C, int K, int d0, int d1, int d2
     VT_RB(128, 11) VT_RB(256, 3) VT_RB(256, 7)
   } else if (kind == 1) {
     VT_RF(32, 3) VT_RF(32, 7) VT_RF(32, 11) VT_RF(64, 3) VT_RF(64, 7) VT_RF(128, 3) VT_RF(64, 11) VT_RF(128, 7)
+  } else if (kind == 6) {  // the whole-ResBlock kernel's short tile (RF S = 1)
+#define VT_RFS(CC, KK) \
+  if (C == CC && K == KK) return RF<CC, KK, 1>::R0 - 2 * (RF<CC, KK, 1>::H2 * (d0 + d1 + d2 + 3));
+    VT_RFS(32, 3) VT_RFS(32, 7) VT_RFS(32, 11) VT_RFS(64, 3) VT_RFS(64, 7) VT_RFS(128, 3)
+#undef VT_RFS
   } else if (kind == 2) {
     if (C == 128) return C3<128>::BM;
     if (C == 64) return C3<64>::BM;
@@ -1246,7 +1253,7 @@ SSAMD_API int ssamd_resblock_fused_pk(const bf16_t* x, const bf16_t* w0, const b
                                       const float* b1, const float* b2, const float* b3, const float* b4,
                                       const float* b5, const bf16_t* acc_in, bf16_t* out, const int* tt, int ntt, int C,
                                       int K, int d0, int d1, int d2, float slope, float out_scale, int post_lrelu,
-                                      hipStream_t s) {
+                                      int short_tile, hipStream_t s) {
   const int dd[3] = {d0, d1, d2};
   for (int i = 0; i < 3; ++i)
     if (dd[i] < 1 || dd[i] > MAXD) return -2;
@@ -1254,11 +1261,19 @@ SSAMD_API int ssamd_resblock_fused_pk(const bf16_t* x, const bf16_t* w0, const b
   if (ntt <= 0) return 0;
   const int4* t4 = reinterpret_cast<const int4*>(tt);
   RFW p = {{w0, w1, w2, w3, w4, w5}, {b0, b1, b2, b3, b4, b5}, {d0, d1, d2}};
+  // short_tile: the tile table was built for the short tile (ssamd_voc_tile_rows kind 6)
 #define RFK_CASE(CC, KK) \
-  if (C == CC && K == KK) return launch_rf<CC, KK>(x, p, acc_in, out, 1, 1, slope, out_scale, post_lrelu, s, t4, ntt);
+  if (C == CC && K == KK) return launch_rf<CC, KK, 0>(x, p, acc_in, out, 1, 1, slope, out_scale, post_lrelu, s, t4, ntt);
+#define RFS_CASE(CC, KK) \
+  if (C == CC && K == KK) return launch_rf<CC, KK, 1>(x, p, acc_in, out, 1, 1, slope, out_scale, post_lrelu, s, t4, ntt);
+  if (short_tile) {
+    RFS_CASE(32, 3) RFS_CASE(32, 7) RFS_CASE(32, 11) RFS_CASE(64, 3) RFS_CASE(64, 7) RFS_CASE(128, 3)
+    return -2;
+  }
   RFK_CASE(32, 3) RFK_CASE(32, 7) RFK_CASE(32, 11) RFK_CASE(64, 3) RFK_CASE(64, 7) RFK_CASE(128, 3)
   RFK_CASE(64, 11) RFK_CASE(128, 7)
 #undef RFK_CASE
+#undef RFS_CASE
   return -2;
 }
 
@@ -1299,14 +1314,14 @@ SSAMD_API int ssamd_resblock_fused(const bf16_t* x, const bf16_t* w0, const bf16
   if ((long)B * T == 0) return 0;
   if (x == out) return -2;
   RFW p = {{w0, w1, w2, w3, w4, w5}, {b0, b1, b2, b3, b4, b5}, {d0, d1, d2}};
-  if (C == 32 && K == 3) return launch_rf<32, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
-  if (C == 32 && K == 7) return launch_rf<32, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
-  if (C == 32 && K == 11) return launch_rf<32, 11>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
-  if (C == 64 && K == 3) return launch_rf<64, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
-  if (C == 64 && K == 7) return launch_rf<64, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
-  if (C == 128 && K == 3) return launch_rf<128, 3>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
-  if (C == 64 && K == 11) return launch_rf<64, 11>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
-  if (C == 128 && K == 7) return launch_rf<128, 7>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 32 && K == 3) return launch_rf<32, 3, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 32 && K == 7) return launch_rf<32, 7, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 32 && K == 11) return launch_rf<32, 11, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 64 && K == 3) return launch_rf<64, 3, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 64 && K == 7) return launch_rf<64, 7, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 128 && K == 3) return launch_rf<128, 3, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 64 && K == 11) return launch_rf<64, 11, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
+  if (C == 128 && K == 7) return launch_rf<128, 7, 0>(x, p, acc_in, out, B, T, slope, out_scale, post_lrelu, s);
   return -2;
 }
 

@@ -236,7 +236,7 @@ class ResBlock1(nn.Module):
             return []
         if (_WHOLE_BLOCK[0] and len(self.convs1) == 3 and hip.resblock_fusable(C, self.kernel_size)
                 and (C, self.kernel_size) not in _WHOLE_SKIP):
-            return [(rate, hip.voc_tile_rows(1, C, self.kernel_size, self.dilation))]
+            return [(rate, hip.rf_tile(C, self.kernel_size, self.dilation, lens, rate)[1])]
         return [(rate, hip.rb_layer_tile(C, self.kernel_size, lens, rate)[1])]
 
 

@@ -2337,7 +2337,7 @@ _SIGS.update({"ssamd_gemm_retain_workspaces": [I],
               "ssamd_voc_pack": [P, I, P, I, I, I, P, P],
               "ssamd_resblock_layer_pk": [P, P, P, P, P, P, P, P, I, I, I, I, F, F, I, P],
               "ssamd_resblock_layer_pk2": [P, P, P, P, P, P, P, P, I, I, I, I, F, F, I, I, P],
-              "ssamd_resblock_fused_pk": [P] * 16 + [I, I, I, I, I, I, F, F, I, P],
+              "ssamd_resblock_fused_pk": [P] * 16 + [I, I, I, I, I, I, F, F, I, I, P],
               "ssamd_conv3_sq_pk": [P, P, P, P, P, I, I, P],
               "ssamd_conv_post_pk": [P, P, P, P, I, I, F, F, P, P, L_, P],
               "ssamd_conv_post_tile_rows": [],
@@ -2517,6 +2517,20 @@ def resblock_layer_packed(x, vp, rate, c1, c2, d, slope, acc=None, out_scale=1.0
     return out
 
 
+_RF_SHORT_MAX_TILES = [128]  # whole-ResBlock kernel: the short tile below this many regular tiles (0: never)
+
+
+def rf_tile(C: int, K: int, dilations, lens, rate: int):
+    """(short, tile rows) of the whole-ResBlock kernel for a packed batch: its short tile (RF S = 1: 2-4x the
+    workgroups, more halo recompute) when the regular tile gives fewer than ``_RF_SHORT_MAX_TILES`` tiles (a batch-1
+    stage runs 40-125 regular tiles on 256 CUs).  Deterministic in its arguments: table and launch agree."""
+    bm = voc_tile_rows(1, C, K, tuple(dilations))
+    bs = voc_tile_rows(6, C, K, tuple(dilations))
+    if bs and sum(-(-int(L) * rate // bm) for L in lens) < _RF_SHORT_MAX_TILES[0]:
+        return True, bs
+    return False, bm
+
+
 def resblock_fused_packed(x, vp, rate, convs1, convs2, dilations, slope, acc=None, out_scale=1.0, post_lrelu=False):
     """``resblock_fused`` on packed rows x [R*rate, C]."""
     _need(x, torch.bfloat16, "resblock.x")
@@ -2529,10 +2543,11 @@ def resblock_fused_packed(x, vp, rate, convs1, convs2, dilations, slope, acc=Non
             bs.append(c.bias.detach().float().contiguous())
     out = acc if acc is not None else torch.empty_like(x)
     d0, d1, d2 = (int(v) for v in dilations)
-    tt, n = vp.tiles(rate, voc_tile_rows(1, C, K, (d0, d1, d2)))
+    short, bm = rf_tile(C, K, (d0, d1, d2), vp.lens, rate)
+    tt, n = vp.tiles(rate, bm)
     rc = lib().ssamd_resblock_fused_pk(_ptr(x), *[_ptr(w) for w in ws], *[_ptr(b) for b in bs], _ptr(acc), _ptr(out),
                                        _ptr(tt), n, C, K, d0, d1, d2, float(slope), float(out_scale),
-                                       int(bool(post_lrelu)), _stream())
+                                       int(bool(post_lrelu)), int(short), _stream())
     _check(rc, "ssamd_resblock_fused_pk")
     return out
 

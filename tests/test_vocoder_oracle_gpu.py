@@ -209,6 +209,32 @@ def test_packed_resblock_tile_modes_bitwise():
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
 
 
+def test_packed_whole_resblock_short_tile_bitwise():
+    """The whole-ResBlock kernel's short tile (RF S = 1, picked by hip.rf_tile for tile-poor packed batches) and its
+    regular tile recompute each tile's halo from the same inputs in the same order: a batch-1 utterance is bitwise
+    the same either way, and both agree with the utterance's fp32 oracle."""
+    from speakingstyle_amd.ops import hip
+
+    g = _generator(11)
+    torch.manual_seed(7)
+    mel = torch.randn(1, 113, 80, device=DEV) * 2 - 5
+    saved = hip._RF_SHORT_MAX_TILES[0]
+    outs, picks = [], []
+    try:
+        for v in (1 << 30, 0):
+            hip._RF_SHORT_MAX_TILES[0] = v
+            picks.append(hip.rf_tile(64, 7, (1, 3, 5), [113], 128)[0])
+            with torch.no_grad():
+                outs.append(g.infer_packed(mel, [113]))
+    finally:
+        hip._RF_SHORT_MAX_TILES[0] = saved
+    assert picks == [True, False], picks
+    assert torch.equal(outs[0], outs[1])
+    with torch_fp32_only(), torch.no_grad():
+        ref = g(mel.transpose(1, 2)).reshape(-1)
+    assert _rel(outs[0][0], ref) < 5e-2
+
+
 def test_bucketed_vocoding_matches_padded_batch():
     """Length buckets (each group truncated at max_len + receptive radius) vs the padded batch on
     the same HIP kernels: the valid samples agree (the GEMMs are row-independent; only a different
