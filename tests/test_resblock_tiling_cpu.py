@@ -18,6 +18,7 @@ from speakingstyle_amd.models.hifigan import LRELU_SLOPE, ResBlock1
 # (C, K) -> NB of struct RF (16-row blocks per tile)
 RF_NB = {(32, 3): 16, (32, 7): 40, (32, 11): 40, (64, 3): 24, (64, 7): 24, (128, 3): 12}
 RF_NB_EXTRA = {(64, 11): 24, (128, 7): 12}  # behind ssamd_resblock_set_whole_extra (measured slower, off)
+RF_NB_SHORT = {(32, 3): 8, (32, 7): 16, (32, 11): 16, (64, 3): 12, (64, 7): 12, (128, 3): 8}  # RF<C, K, 1>
 MAXD = 5
 
 
@@ -84,10 +85,10 @@ def _block(C, K, seed=0):
     return blk.eval()
 
 
-@pytest.mark.parametrize("C,K", sorted(RF_NB))
-def test_whole_block_tiling_matches_resblock(C, K):
+@pytest.mark.parametrize("C,K,short", [(C, K, s) for (C, K) in sorted(RF_NB) for s in (False, True)])
+def test_whole_block_tiling_matches_resblock(C, K, short):
     blk = _block(C, K)
-    NB = RF_NB[(C, K)]
+    NB = (RF_NB_SHORT if short else RF_NB)[(C, K)]
     HT = (K - 1) // 2 * (1 + 3 + 5 + 3)
     BM = 16 * NB - 2 * HT
     for T in (3, BM - 1, BM, 2 * BM + 7):
@@ -141,8 +142,8 @@ def test_tile_constants_mirror_the_kernel():
     import re
 
     src = open(os.path.join(os.path.dirname(__file__), "..", "csrc", "k_vocoder.hip")).read()
-    m = re.search(r"static constexpr int NB = (.+?);", src[src.index("struct RF {"):])
-    expr = m.group(1)
+    m = re.search(r"static constexpr int NB = (.+?);", src[src.index("struct RF {"):], re.S)
+    expr = " ".join(m.group(1).split())
 
     def ev(e, C, K):  # right-associative C ternary chain -> value
         e = e.strip()
@@ -156,7 +157,7 @@ def test_tile_constants_mirror_the_kernel():
                 q = i
                 break
         if q < 0:
-            return eval(e.replace("&&", " and ").replace("||", " or "), {"C": C, "K": K})
+            return eval(e.replace("&&", " and ").replace("||", " or "), {"C": C, "K": K, "S": S})
         depth, nest = 0, 0
         for i in range(q + 1, len(e)):
             ch = e[i]
@@ -170,7 +171,11 @@ def test_tile_constants_mirror_the_kernel():
                 nest -= 1
         raise ValueError(e)
 
+    S = 0  # the regular tile (RF_NB); the short tile (S = 1) only changes NB: the schedule proof above is per NB
     for (C, K), nb in list(RF_NB.items()) + list(RF_NB_EXTRA.items()):
+        assert ev(expr, C, K) == nb, (C, K, expr)
+    S = 1
+    for (C, K), nb in RF_NB_SHORT.items():  # the short tiles (RF S = 1) simulated above
         assert ev(expr, C, K) == nb, (C, K, expr)
     fus = re.search(r"int ssamd_resblock_fusable\(int C, int K\) \{\s*return (.+?);", src, re.S).group(1)
     fus = " ".join(fus.replace("&&", " and ").replace("||", " or ").split())
