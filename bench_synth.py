@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--rb256-min-rows", type=int, default=None,
                     help="row count from which the C = 256 MRF uses the tall per-layer kernel (A/B; default 65536)")
     ap.add_argument("--splitk", type=int, default=None, help="GEMM split-K: -1 auto, 0 off, S forced (A/B)")
-    ap.add_argument("--no-skinny", action="store_true", help="GEMMs of <= 64 rows on the tile kernels (A/B)")
+    ap.add_argument("--no-skinny", action="store_true", help="small-M GEMMs (<= 1024 rows) on the tile kernels instead of the skinny kernel (A/B)")
     ap.add_argument("--gemm-addln-rows", type=int, default=None,
                     help="inference FFT blocks: GEMM + residual + LayerNorm as one kernel up to this many rows (A/B)")
     ap.add_argument("--skinny-maxm", type=int, default=None, help="row limit of the skinny GEMM kernel (A/B)")

@@ -2319,12 +2319,14 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_reg_kernel(const bf16_t* __r
       }
 }
 
-// Skinny-M implicit-GEMM conv (M <= 64 rows: a batch-1 utterance's phonemes, per-utterance style vectors): the
-// tile machinery above pays a 256-row prologue / epilogue for a handful of rows and leaves most CUs idle.  Here a
-// 4-wave block owns a 16-row x 16-column output tile and splits the k-steps (32 deep) over its waves, operands
-// straight from global memory in the MFMA fragment layout (no LDS staging: the A rows are a few KiB, every weight
-// fragment is read once), the four partial tiles summed in LDS in a fixed order, then the conv_gemm epilogue
-// (bias, activation, ReLU-aux mask, residual, row validity, fp32 out, EpiX tail).  Grid = N/16 x M/16 blocks.
+// Skinny-M implicit-GEMM conv (M <= g_skinny_maxm = 1024 rows: a batch-1 utterance's phonemes and frames, the first
+// vocoder stages, per-utterance style vectors): the tile machinery above pays a 256-row prologue / epilogue for a
+// handful of rows and leaves most CUs idle.  Here a block of NWV waves owns a 16-row x 16-column output tile and
+// splits the k-steps (32 deep) over its waves, operands straight from global memory in the MFMA fragment layout
+// (no LDS staging: the A rows are a few KiB, every weight fragment is read once per row block), the partial tiles
+// summed in LDS in a fixed order, then the conv_gemm epilogue (bias, activation, ReLU-aux mask, residual, row
+// validity, fp32 out, EpiX tail).  Grid = N/16 x M/16 blocks.  (A 32 x 64 tile per block -- fewer fragment loads
+// per MFMA -- measured slower: fewer blocks; profiles/r6_b1_latency.txt.)
 // Cin % 32 == 0: a k-step never straddles a tap; otherwise (Cin % 8 == 0) each lane finds the tap of its 8-channel
 // chunk and K is padded to the k-step with zeros.  N % 16 == 0.  A ConvTranspose 3-tap form (ksplit) is
 // computed in full: its zero tap adds exact zeros, so the result is bitwise the same with or without the skip.
